@@ -1,0 +1,36 @@
+"""EBCDIC code pages (CP/parser/encoding/codepage/CodePage.scala:59-68) and their UTF-8 LUT form.
+
+The GPU kernels take each code page as a 256 x 4-byte table: byte b -> (UTF-8 length, up to 3
+UTF-8 bytes) of the code point the reference maps b to, plus a "trimmable" flag (code point
+<= U+0020, the Java `String.trim` predicate).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+
+from .codepages_data import CODE_PAGES
+
+
+def lut_for(name: str) -> List[int]:
+    """Code-page table by name (CodePage.getCodePageByName)."""
+    if name not in CODE_PAGES:
+        raise ValueError(f"The code page '{name}' is not one of the builtin EBCDIC code pages.")
+    return CODE_PAGES[name]
+
+
+def utf8_lut(table: List[int]) -> np.ndarray:
+    """uint32[256]: bits 0-23 UTF-8 bytes (first byte lowest), bits 24-25 length, bit 31 trimmable."""
+    out = np.zeros(256, dtype=np.uint32)
+    for b, cp in enumerate(table):
+        enc = chr(cp).encode("utf-8")
+        assert 1 <= len(enc) <= 3, (b, cp)
+        v = 0
+        for i, x in enumerate(enc):
+            v |= x << (8 * i)
+        v |= len(enc) << 24
+        if cp <= 0x20:
+            v |= 1 << 31
+        out[b] = v
+    return out
