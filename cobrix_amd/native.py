@@ -1,0 +1,127 @@
+"""ctypes binding of libcobrix_hip.so (include/cobrix_hip.h).
+
+This is the Python counterpart of the JNI / Panama FFM stub a JVM host would use
+(INTEGRATION.md).  There is no fallback: if the HIP library is missing, every product call
+raises `NativeLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcobrix_hip.so")
+
+CBX_MAX_DIMS = 4
+CBX_MAX_SEG_KEYS = 32
+CBX_MAX_SEG_KEY_LEN = 32
+
+# kinds / out types / flags (keep in sync with include/cobrix_hip.h)
+K_STRING, K_STRING_ASCII, K_HEX, K_RAW, K_BCD, K_BINARY, K_ZONED = 1, 2, 3, 4, 5, 6, 7
+K_FLOAT, K_DOUBLE, K_RECORD_ID, K_FILE_ID = 9, 10, 11, 12
+O_I32, O_I64, O_DEC64, O_DEC128, O_F32, O_F64, O_STRING, O_BINARY = 1, 2, 3, 4, 5, 6, 7, 8
+F_SIGNED, F_BIG_ENDIAN, F_EXPLICIT_DOT, F_INTEGRAL, F_IBM, F_LITTLE_ENDIAN_FP, F_DEPENDEE = (
+    0x1, 0x2, 0x4, 0x8, 0x10, 0x20, 0x40)
+TRIM = {"none": 1, "left": 2, "right": 3, "both": 4}
+
+CBX_OK, CBX_E_ARGUMENT, CBX_E_STATE, CBX_E_CAPACITY, CBX_E_HIP, CBX_E_UNSUPPORTED = 0, -1, -2, -3, -4, -5
+
+OUT_WIDTH = {O_I32: 4, O_I64: 8, O_DEC64: 8, O_DEC128: 16, O_F32: 4, O_F64: 8}
+
+# every symbol include/cobrix_hip.h declares
+EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx_plan_destroy",
+                    "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
+                    "cbx_string_sizes_var", "cbx_frame_rdw", "cbx_plan_set_profiling",
+                    "cbx_plan_last_kernel_ms")
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class CbxError(RuntimeError):
+    """Structural error reported by the library (IllegalArgument/IllegalState in the reference)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"cbx error {code}: {msg}")
+        self.code = code
+
+
+class CbxField(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("out_type", ctypes.c_int32), ("offset", ctypes.c_int32),
+                ("size", ctypes.c_int32), ("precision", ctypes.c_int32), ("scale", ctypes.c_int32),
+                ("scale_factor", ctypes.c_int32), ("out_precision", ctypes.c_int32),
+                ("out_scale", ctypes.c_int32), ("flags", ctypes.c_int32), ("trim", ctypes.c_int32),
+                ("n_dims", ctypes.c_int32), ("dim_count", ctypes.c_int32 * CBX_MAX_DIMS),
+                ("dim_stride", ctypes.c_int32 * CBX_MAX_DIMS), ("dim_array", ctypes.c_int32 * CBX_MAX_DIMS),
+                ("segment", ctypes.c_int32), ("column", ctypes.c_int32)]
+
+
+class CbxArray(ctypes.Structure):
+    _fields_ = [("max_count", ctypes.c_int32), ("min_count", ctypes.c_int32), ("dependee", ctypes.c_int32),
+                ("segment", ctypes.c_int32), ("count_column", ctypes.c_int32), ("n_dims", ctypes.c_int32),
+                ("parent", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class CbxSegmentMap(ctypes.Structure):
+    _fields_ = [("field_offset", ctypes.c_int32), ("field_size", ctypes.c_int32), ("n_keys", ctypes.c_int32),
+                ("key_len", ctypes.c_int32 * CBX_MAX_SEG_KEYS),
+                ("key", (ctypes.c_uint16 * CBX_MAX_SEG_KEY_LEN) * CBX_MAX_SEG_KEYS),
+                ("key_segment", ctypes.c_int32 * CBX_MAX_SEG_KEYS)]
+
+
+class CbxPlanOptions(ctypes.Structure):
+    _fields_ = [("n_columns", ctypes.c_int32), ("file_id", ctypes.c_int32), ("has_segments", ctypes.c_int32),
+                ("window_bytes", ctypes.c_int32), ("segment_column", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 3), ("lut", ctypes.c_uint32 * 256),
+                ("segments", CbxSegmentMap)]
+
+
+class CbxColumn(ctypes.Structure):
+    _fields_ = [("values", ctypes.c_void_p), ("validity", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("data", ctypes.c_void_p), ("data_capacity", ctypes.c_int64), ("data_size", ctypes.c_int64)]
+
+
+class CbxRdwParams(ctypes.Structure):
+    _fields_ = [("big_endian", ctypes.c_int32), ("adjustment", ctypes.c_int32),
+                ("file_header_bytes", ctypes.c_int32), ("file_footer_bytes", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def lib_path() -> str:
+    return LIB_PATH
+
+
+def load():
+    """Load the HIP library; raises NativeLibraryError if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    try:
+        L = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    P, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    L.cbx_abi_version.restype = i32
+    L.cbx_last_error.restype = ctypes.c_char_p
+    L.cbx_plan_create.argtypes = [P, i32, P, i32, P, ctypes.POINTER(P)]
+    L.cbx_plan_destroy.argtypes = [P]
+    L.cbx_plan_destroy.restype = None
+    L.cbx_string_sizes_fixed.argtypes = [P, P, i64, i32, i32, P, P]
+    L.cbx_decode_fixed.argtypes = [P, P, i64, i32, i32, i64, P, P]
+    L.cbx_decode_var.argtypes = [P, P, i64, P, P, i64, i32, i64, P, P]
+    L.cbx_string_sizes_var.argtypes = [P, P, i64, P, P, i64, i32, P, P]
+    L.cbx_frame_rdw.argtypes = [P, i64, P, i32, P, P, P, i64, P, P]
+    L.cbx_plan_set_profiling.argtypes = [P, i32]
+    L.cbx_plan_last_kernel_ms.argtypes = [P, P, P, P]
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != CBX_OK:
+        raise CbxError(rc, load().cbx_last_error().decode(errors="replace"))

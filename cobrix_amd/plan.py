@@ -1,0 +1,286 @@
+"""Flatten a Cobrix copybook AST into the descriptor tables of the HIP library.
+
+This is what the JVM host does once per query before calling libcobrix_hip.so: walk the
+`Copybook` AST in `extractRecord` order (CP/reader/extractors/record/RecordExtractors.scala:
+139-172) and emit one `cbx_field` per decoded Primitive (every REDEFINES alternative, every
+OCCURS element as a "slot"), one `cbx_array` per OCCURS node with its DEPENDING ON source, and
+the segment-redefine selection map (FixedLenNestedRowIterator.scala:64-99).
+
+Output columns: one per field, one int32 element-count column per OCCURS node, optionally one
+int32 "active segment" column, plus generated File_Id / Record_Id.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from . import copybook as cbk
+from . import native as N
+from .codepages import lut_for, utf8_lut
+from .schema import (ST_BINARY, ST_DECIMAL, ST_DOUBLE, ST_FLOAT, ST_INT, ST_LONG, ST_STRING,
+                     spark_type)
+
+
+class UnsupportedLayout(ValueError):
+    """The layout uses a feature outside the GPU path (reported, never silently degraded)."""
+
+
+@dataclass
+class ColumnInfo:
+    index: int
+    kind: str                      # "value" | "count" | "segment" | "record_id" | "file_id"
+    out_type: int
+    n_slots: int = 1
+    node: Optional[cbk.Statement] = None
+    stype: Tuple[int, int, int] = (0, 0, 0)
+    hidden: bool = False           # decoded for a dependency only (e.g. FILLER dependee)
+
+
+@dataclass
+class DecodePlan:
+    copybook: cbk.Copybook
+    fields: List[N.CbxField]
+    arrays: List[N.CbxArray]
+    columns: List[ColumnInfo]
+    options: N.CbxPlanOptions
+    field_of_node: Dict[int, int] = field(default_factory=dict)     # id(Primitive) -> field index
+    array_of_node: Dict[int, int] = field(default_factory=dict)     # id(Statement) -> array index
+    segment_groups: List[cbk.Group] = field(default_factory=list)
+    segment_column: int = -1
+    record_id_column: int = -1
+    file_id_column: int = -1
+
+    @property
+    def n_columns(self) -> int:
+        return len(self.columns)
+
+
+def _out_type(st) -> int:
+    t, p, _ = st
+    if t == ST_INT:
+        return N.O_I32
+    if t == ST_LONG:
+        return N.O_I64
+    if t == ST_DECIMAL:
+        return N.O_DEC64 if p <= 18 else N.O_DEC128
+    if t == ST_FLOAT:
+        return N.O_F32
+    if t == ST_DOUBLE:
+        return N.O_F64
+    if t == ST_STRING:
+        return N.O_STRING
+    if t == ST_BINARY:
+        return N.O_BINARY
+    raise UnsupportedLayout(f"unknown spark type {t}")
+
+
+def _kind_and_flags(p: cbk.Primitive, cb: cbk.Copybook) -> Tuple[int, int]:
+    d = p.dtype
+    flags = 0
+    if isinstance(d, cbk.AlphaNumeric):
+        kind = {cbk.EBCDIC: N.K_STRING, cbk.ASCII: N.K_STRING_ASCII, cbk.HEX: N.K_HEX,
+                cbk.RAW: N.K_RAW}.get(d.enc)
+        if kind is None:
+            raise UnsupportedLayout(f"{p.name}: {d.enc} strings are not on the GPU path yet")
+        return kind, 0
+    if d.sign_position is not None:
+        flags |= N.F_SIGNED
+    if isinstance(d, cbk.Integral):
+        flags |= N.F_INTEGRAL
+    if isinstance(d, cbk.Decimal) and d.explicit_decimal:
+        flags |= N.F_EXPLICIT_DOT
+    if p.is_dependee:
+        flags |= N.F_DEPENDEE
+    if d.compact is None:
+        if d.enc != cbk.EBCDIC:
+            raise UnsupportedLayout(f"{p.name}: ASCII DISPLAY numbers are not on the GPU path yet")
+        return N.K_ZONED, flags
+    if d.compact == cbk.COMP3:
+        return N.K_BCD, flags
+    if d.compact in (cbk.COMP4, cbk.COMP5):
+        return N.K_BINARY, flags | N.F_BIG_ENDIAN
+    if d.compact == cbk.COMP9:
+        return N.K_BINARY, flags
+    if d.compact in (cbk.COMP1, cbk.COMP2):
+        if isinstance(d, cbk.Integral):
+            raise UnsupportedLayout(f"{p.name}: COMP-1/COMP-2 is incorrect for an integral number")
+        fp = cb.floating_point_format
+        if fp in ("IBM", "IBM_LE"):
+            flags |= N.F_IBM
+        if fp in ("IBM_LE", "IEEE754_LE"):
+            flags |= N.F_LITTLE_ENDIAN_FP
+        return (N.K_FLOAT if d.compact == cbk.COMP1 else N.K_DOUBLE), flags
+    raise UnsupportedLayout(f"{p.name}: usage {d.compact}")
+
+
+def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
+               segment_redefine_map: Optional[Dict[str, str]] = None, generate_record_id: bool = False,
+               file_id: int = 0, window_bytes: int = 0) -> DecodePlan:
+    fields: List[N.CbxField] = []
+    arrays: List[N.CbxArray] = []
+    columns: List[ColumnInfo] = []
+    field_of_node: Dict[int, int] = {}
+    array_of_node: Dict[int, int] = {}
+    seg_groups: List[cbk.Group] = cb.all_segment_redefines()
+    seg_index = {id(g): i for i, g in enumerate(seg_groups)}
+    trim = N.TRIM[cb.string_trimming]
+    pending_arrays: List[Tuple[int, cbk.Statement]] = []
+    walk_order: Dict[int, int] = {}
+    counter = [0]
+
+    def add_column(**kw) -> int:
+        ci = ColumnInfo(index=len(columns), **kw)
+        columns.append(ci)
+        return ci.index
+
+    def visit(st: cbk.Statement, dims: List[Tuple[int, int, int]], segment: int, in_array: bool):
+        counter[0] += 1
+        walk_order[id(st)] = counter[0]
+        if isinstance(st, cbk.Group) and st.is_segment_redefine:
+            segment = seg_index[id(st)]
+        my_dims = list(dims)
+        if st.is_array:
+            ai = len(arrays)
+            ar = N.CbxArray()
+            ar.max_count = st.array_max_size
+            ar.min_count = st.array_min_size
+            ar.dependee = -1
+            ar.segment = segment
+            ar.n_dims = len(dims)
+            ar.parent = dims[-1][2] if dims else -1
+            arrays.append(ar)
+            array_of_node[id(st)] = ai
+            ar.count_column = add_column(kind="count", out_type=N.O_I32, node=st)
+            pending_arrays.append((ai, st))
+            my_dims.append((st.array_max_size, st.data_size, ai))
+            if len(my_dims) > N.CBX_MAX_DIMS:
+                raise UnsupportedLayout(f"{st.name}: more than {N.CBX_MAX_DIMS} nested OCCURS levels")
+        if isinstance(st, cbk.Group):
+            for c in st.children:
+                visit(c, my_dims, segment, in_array or st.is_array)
+            return
+        p: cbk.Primitive = st  # type: ignore[assignment]
+        if p.is_filler and not p.is_dependee:
+            return
+        kind, flags = _kind_and_flags(p, cb)
+        stp = spark_type(p)
+        f = N.CbxField()
+        f.kind, f.out_type, f.offset, f.size = kind, _out_type(stp), p.offset, p.data_size
+        d = p.dtype
+        if not isinstance(d, cbk.AlphaNumeric):
+            f.precision = d.precision
+            if isinstance(d, cbk.Decimal):
+                f.scale, f.scale_factor = d.scale, d.scale_factor
+        f.out_precision, f.out_scale = stp[1], stp[2]
+        f.flags, f.trim = flags, trim
+        f.n_dims = len(my_dims)
+        n_slots = 1
+        for k, (cnt, stride, ai) in enumerate(my_dims):
+            f.dim_count[k], f.dim_stride[k], f.dim_array[k] = cnt, stride, ai
+            n_slots *= cnt
+        f.segment = segment
+        f.column = add_column(kind="value", out_type=f.out_type, n_slots=n_slots, node=p, stype=stp,
+                              hidden=p.is_filler)
+        field_of_node[id(p)] = len(fields)
+        fields.append(f)
+        p_in_array = in_array or p.is_array
+        if p.is_dependee:
+            p.__dict__["_cbx_in_array"] = p_in_array
+
+    for rec in cb.ast.children:
+        visit(rec, [], -1, False)
+
+    # DEPENDING ON sources (RecordExtractors.scala:64, 72, 126-134)
+    prims = [st for st in _iter_prims(cb.ast)]
+    for ai, st in pending_arrays:
+        if st.depending_on is None:
+            continue
+        cand = [q for q in prims if q.is_dependee and q.name == st.depending_on]
+        if not cand:
+            continue  # the name never registers -> always arrayMaxSize
+        q = cand[0]
+        if walk_order[id(q)] > walk_order[id(st)]:
+            continue  # decoded after the array -> not yet in dependFields -> arrayMaxSize
+        if q.__dict__.get("_cbx_in_array"):
+            raise UnsupportedLayout(f"{st.name}: DEPENDING ON {q.name} inside an OCCURS is not on the GPU path yet")
+        if not isinstance(q.dtype, cbk.Integral) or q.dtype.precision > 18:
+            raise UnsupportedLayout(f"{st.name}: DEPENDING ON a non-integral field (occurs_mappings) is not on the GPU path yet")
+        arrays[ai].dependee = field_of_node[id(q)]
+
+    opts = N.CbxPlanOptions()
+    seg_col = -1
+    if segment_field is not None and segment_redefine_map:
+        sf = cb.get_field_by_name(segment_field)
+        if not isinstance(sf, cbk.Primitive) or not isinstance(sf.dtype, cbk.AlphaNumeric) or sf.dtype.enc != cbk.EBCDIC:
+            raise UnsupportedLayout("segment field must be an EBCDIC alphanumeric field")
+        if len(segment_redefine_map) > N.CBX_MAX_SEG_KEYS:
+            raise UnsupportedLayout("too many segment ids")
+        opts.has_segments = 1
+        sm = opts.segments
+        sm.field_offset, sm.field_size, sm.n_keys = sf.offset, sf.actual_size, len(segment_redefine_map)
+        for k, (key, grp) in enumerate(segment_redefine_map.items()):
+            u = [ord(c) for c in key]
+            if len(u) > N.CBX_MAX_SEG_KEY_LEN:
+                raise UnsupportedLayout("segment id too long")
+            for j, x in enumerate(u):
+                sm.key[k][j] = x
+            sm.key_len[k] = len(u)
+            gname = cbk._transform_identifier(grp).upper()
+            matches = [i for i, g in enumerate(seg_groups) if g.name.upper() == gname]
+            sm.key_segment[k] = matches[0] if matches else -1
+        seg_col = add_column(kind="segment", out_type=N.O_I32)
+    rid_col = fid_col = -1
+    if generate_record_id:
+        fid_col = add_column(kind="file_id", out_type=N.O_I32)
+        f = N.CbxField()
+        f.kind, f.out_type, f.segment, f.column = N.K_FILE_ID, N.O_I32, -1, fid_col
+        fields.append(f)
+        rid_col = add_column(kind="record_id", out_type=N.O_I64)
+        f = N.CbxField()
+        f.kind, f.out_type, f.segment, f.column = N.K_RECORD_ID, N.O_I64, -1, rid_col
+        fields.append(f)
+    opts.n_columns = len(columns)
+    opts.file_id = file_id
+    opts.window_bytes = window_bytes
+    opts.segment_column = seg_col
+    lut = utf8_lut(lut_for(cb.code_page))
+    for i in range(256):
+        opts.lut[i] = int(lut[i])
+    return DecodePlan(cb, fields, arrays, columns, opts, field_of_node, array_of_node, seg_groups,
+                      seg_col, rid_col, fid_col)
+
+
+def _iter_prims(g: cbk.Group):
+    for c in g.children:
+        if isinstance(c, cbk.Group):
+            yield from _iter_prims(c)
+        else:
+            yield c
+
+
+class NativePlan:
+    """Owns a `cbx_plan*` built from a DecodePlan."""
+
+    def __init__(self, plan: DecodePlan):
+        L = N.load()
+        self.plan = plan
+        self._fields = (N.CbxField * len(plan.fields))(*plan.fields)
+        self._arrays = (N.CbxArray * max(1, len(plan.arrays)))(*plan.arrays) if plan.arrays else None
+        h = ctypes.c_void_p()
+        rc = L.cbx_plan_create(ctypes.addressof(self._fields), len(plan.fields),
+                               ctypes.addressof(self._arrays) if self._arrays is not None else None,
+                               len(plan.arrays), ctypes.byref(plan.options), ctypes.byref(h))
+        N.check(rc)
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            N.load().cbx_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,362 @@
+"""Reader facade mirroring Cobrix's `FixedLenNestedReader` / `VarLenNestedReader` over the GPU path.
+
+Reference interfaces (CP = cobol-parser/src/main/scala/za/co/absa/cobrix/cobol/):
+  * FixedLenNestedReader  CP/reader/FixedLenNestedReader.scala:43-144  (getRecordSize,
+    checkBinaryDataValidity, getRecordIterator -> one extractRecord per record)
+  * VarLenNestedReader    CP/reader/VarLenNestedReader.scala:46-310   (generateIndex,
+    getRecordIterator over a SimpleStream with RDW headers)
+  * ReaderParameters      CP/reader/parameters/ReaderParameters.scala:65-103
+The GPU decodes a whole batch (split / partition) per call instead of one record per call;
+`DecodedBatch` holds the columnar result and can rebuild the reference's nested rows.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from decimal import Context, Decimal
+from typing import Any, Dict, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import copybook as cbk
+from . import native as N
+from .plan import DecodePlan, NativePlan, build_plan
+from .schema import ST_DECIMAL, spark_schema
+
+_CTX = Context(prec=200)
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise N.NativeLibraryError("the Cobrix GPU path needs a ROCm device (torch.cuda.is_available() is False)")
+    return torch
+
+
+@dataclass
+class ReaderParameters:
+    """Subset of ReaderParameters (ReaderParameters.scala:65-103) that shapes the decode path."""
+    is_ebcdic: bool = True
+    ebcdic_code_page: str = "common"
+    floating_point_format: str = "IBM"
+    variable_size_occurs: bool = False
+    record_length: Optional[int] = None
+    is_record_sequence: bool = False
+    is_rdw_big_endian: bool = False
+    is_rdw_part_rec_length: bool = False
+    rdw_adjustment: int = 0
+    input_split_records: Optional[int] = None
+    input_split_size_mb: Optional[int] = None
+    start_offset: int = 0
+    end_offset: int = 0
+    file_start_offset: int = 0
+    file_end_offset: int = 0
+    generate_record_id: bool = False
+    schema_policy: str = "keep_original"          # or "collapse_root"
+    string_trimming_policy: str = "both"
+    segment_field: Optional[str] = None
+    segment_id_redefine_map: Dict[str, str] = field(default_factory=dict)
+    segment_id_filter: Optional[List[str]] = None
+    drop_group_fillers: bool = False
+    drop_value_fillers: bool = True
+    non_terminals: Sequence[str] = ()
+    occurs_mappings: Dict[str, Dict[str, int]] = field(default_factory=dict)
+    window_bytes: int = 0
+
+
+@dataclass
+class SparseIndexEntry:
+    """SparseIndexEntry (CP/reader/index/entry/SparseIndexEntry.scala:19)."""
+    offset_from: int
+    offset_to: int
+    file_id: int
+    record_index: int
+
+
+class DecodedBatch:
+    """Columnar decode of a batch of records (device tensors) + row reconstruction."""
+
+    def __init__(self, plan: DecodePlan, n_rec: int, cols: List[Dict[str, Any]], first_record_id: int,
+                 collapse_root: bool, generate_record_id: bool):
+        self.plan, self.n_rec, self.cols = plan, n_rec, cols
+        self.first_record_id = first_record_id
+        self.collapse_root = collapse_root
+        self.generate_record_id = generate_record_id
+
+    # ---- host views
+    def host_column(self, ci: int) -> Dict[str, Any]:
+        c = self.cols[ci]
+        info = self.plan.columns[ci]
+        n = self.n_rec * info.n_slots
+        pitch = (self.n_rec + 63) // 64
+        out: Dict[str, Any] = {"validity": None, "values": None}
+        vb = c["validity"].cpu().numpy().view(np.uint64)
+        bits = np.unpackbits(vb.view(np.uint8), bitorder="little").reshape(info.n_slots, pitch * 64)
+        out["validity"] = bits[:, :self.n_rec].astype(bool)
+        if c.get("offsets") is not None:
+            off = c["offsets"].cpu().numpy()[: n + 1]
+            data = c["data"][: max(1, int(c["data_size"]))].cpu().numpy().tobytes()
+            out["offsets"] = off
+            out["data"] = data
+        else:
+            v = c["values"].cpu().numpy()
+            if info.out_type == N.O_DEC128:
+                v = v.reshape(-1, 2)
+            out["values"] = v
+        return out
+
+    def to_rows(self) -> List[dict]:
+        """Rebuild nested rows (RecordHandler.create + applyRecordPostProcessing)."""
+        plan = self.plan
+        cache: Dict[int, Dict[str, Any]] = {}
+
+        def col(ci):
+            if ci not in cache:
+                cache[ci] = self.host_column(ci)
+            return cache[ci]
+
+        def value(ci: int, slot: int, r: int):
+            c = col(ci)
+            info = plan.columns[ci]
+            if not c["validity"][slot, r]:
+                return None
+            v = slot * self.n_rec + r
+            ot = info.out_type
+            if ot in (N.O_STRING, N.O_BINARY):
+                b = c["data"][int(c["offsets"][v]):int(c["offsets"][v + 1])]
+                return b.decode("utf-8") if ot == N.O_STRING else b
+            x = c["values"][v]
+            if ot == N.O_I32:
+                return int(np.int32(x))
+            if ot == N.O_I64:
+                return int(np.int64(x))
+            if ot == N.O_F32:
+                return np.uint32(x).view(np.float32)
+            if ot == N.O_F64:
+                return np.uint64(x).view(np.float64)
+            if ot == N.O_DEC64:
+                u = int(np.int64(x))
+            else:
+                u = (int(np.int64(x[1])) << 64) | int(np.uint64(x[0]))
+            return Decimal(u).scaleb(-info.stype[2], context=_CTX)
+
+        seg_col = plan.segment_column
+
+        def walk(g: cbk.Group, r: int, idx: List[Tuple[int, int]]) -> dict:
+            d = {}
+            for c in g.children:
+                if c.is_array:
+                    ai = plan.array_of_node[id(c)]
+                    cnt_col = col(plan.arrays[ai].count_column)
+                    cnt = int(np.int32(cnt_col["values"][r]))
+                    vals = []
+                    for i in range(cnt):
+                        sub = idx + [(i, c.array_max_size)]
+                        if isinstance(c, cbk.Group):
+                            vals.append(walk(c, r, sub))
+                        else:
+                            vals.append(prim(c, r, sub))
+                    val: Any = vals
+                elif isinstance(c, cbk.Group):
+                    if c.is_segment_redefine and seg_col >= 0:
+                        si = plan.segment_groups.index(c)
+                        active = int(np.int32(col(seg_col)["values"][r]))
+                        val = walk(c, r, idx) if active == si else None
+                    elif c.is_segment_redefine:
+                        val = None
+                    else:
+                        val = walk(c, r, idx)
+                else:
+                    val = prim(c, r, idx)
+                if not c.is_filler and not c.is_child_segment:
+                    d[c.name] = val
+            return d
+
+        def prim(p: cbk.Primitive, r: int, idx):
+            fi = plan.field_of_node.get(id(p))
+            if fi is None:
+                return None
+            slot = 0
+            for i, m in idx:
+                slot = slot * m + i
+            return value(plan.fields[fi].column, slot, r)
+
+        rows = []
+        for r in range(self.n_rec):
+            recs = [(g.name, walk(g, r, [])) for g in plan.copybook.ast.children if isinstance(g, cbk.Group)]
+            row: Dict[str, Any] = {}
+            if self.generate_record_id:
+                row["File_Id"] = value(plan.file_id_column, 0, r)
+                row["Record_Id"] = value(plan.record_id_column, 0, r)
+            if self.collapse_root:
+                for _, v in recs:
+                    row.update(v)
+            else:
+                row.update({k: v for k, v in recs})
+            rows.append(row)
+        return rows
+
+
+def _alloc_columns(plan: DecodePlan, n_rec: int, string_sizes: Optional[Sequence[int]], device) -> Tuple[List[Dict[str, Any]], ctypes.Array]:
+    torch = _torch()
+    pitch_words = (n_rec + 63) // 64
+    cols: List[Dict[str, Any]] = []
+    cstructs = (N.CbxColumn * plan.n_columns)()
+    for ci, info in enumerate(plan.columns):
+        n = n_rec * info.n_slots
+        c: Dict[str, Any] = {"validity": torch.zeros(max(1, info.n_slots * pitch_words), dtype=torch.int64, device=device)}
+        if info.out_type in (N.O_STRING, N.O_BINARY):
+            cap = int(string_sizes[ci]) if string_sizes is not None else n * info.node.data_size * 3
+            c["offsets"] = torch.zeros(n + 1, dtype=torch.int64, device=device)
+            c["data"] = torch.empty(max(1, cap), dtype=torch.uint8, device=device)
+            c["data_size"] = 0
+            cstructs[ci].offsets = c["offsets"].data_ptr()
+            cstructs[ci].data = c["data"].data_ptr()
+            cstructs[ci].data_capacity = cap
+        else:
+            w = N.OUT_WIDTH[info.out_type]
+            dt = {4: torch.int32, 8: torch.int64, 16: torch.int64}[w]
+            c["values"] = torch.empty(max(1, n * (2 if w == 16 else 1)), dtype=dt, device=device)
+            cstructs[ci].values = c["values"].data_ptr()
+        cstructs[ci].validity = c["validity"].data_ptr()
+        cols.append(c)
+    return cols, cstructs
+
+
+class _BaseReader:
+    def __init__(self, copybook_contents: str, params: ReaderParameters):
+        self.params = params
+        segment_redefines = sorted(set(params.segment_id_redefine_map.values()))
+        self.copybook = cbk.parse_copybook(
+            copybook_contents, data_encoding=cbk.EBCDIC if params.is_ebcdic else cbk.ASCII,
+            drop_group_fillers=params.drop_group_fillers, drop_value_fillers=params.drop_value_fillers,
+            segment_redefines=segment_redefines, string_trimming=params.string_trimming_policy,
+            code_page=params.ebcdic_code_page, floating_point_format=params.floating_point_format,
+            non_terminals=params.non_terminals, occurs_handlers=params.occurs_mappings)
+        if params.variable_size_occurs:
+            raise N.CbxError(N.CBX_E_UNSUPPORTED, "variable_size_occurs=true is not on the GPU path yet")
+        self.plan = build_plan(self.copybook, segment_field=params.segment_field,
+                               segment_redefine_map=params.segment_id_redefine_map or None,
+                               generate_record_id=params.generate_record_id, window_bytes=params.window_bytes)
+        self.native = NativePlan(self.plan)
+
+    @property
+    def collapse_root(self) -> bool:
+        return self.params.schema_policy == "collapse_root"
+
+    def spark_schema(self):
+        return spark_schema(self.copybook, self.collapse_root, self.params.generate_record_id)
+
+    def close(self):
+        self.native.close()
+
+
+class FixedLenNestedReader(_BaseReader):
+    """GPU drop-in for FixedLenNestedReader (CP/reader/FixedLenNestedReader.scala:43-144)."""
+
+    def get_record_size(self) -> int:
+        # FixedLenNestedReader.getRecordSize (:60-63)
+        inner = self.params.record_length if self.params.record_length is not None else self.copybook.record_size
+        return inner + self.params.start_offset + self.params.end_offset
+
+    def check_binary_data_validity(self, n_bytes: int) -> None:
+        # FixedLenNestedReader.checkBinaryDataValidity (:71-90) applied to a whole split
+        p = self.params
+        if p.start_offset < 0:
+            raise ValueError(f"Invalid record start offset = {p.start_offset}. A record start offset cannot be negative.")
+        if p.end_offset < 0:
+            raise ValueError(f"Invalid record end offset = {p.end_offset}. A record end offset cannot be negative.")
+        if p.record_length is not None:
+            if p.record_length < 1:
+                raise ValueError(f"The specified record size {p.record_length} cannot be used. "
+                                 "The record length should be greater then zero.")
+        else:
+            exp = self.copybook.record_size + p.start_offset + p.end_offset
+            if n_bytes < exp:
+                raise ValueError(f"Binary record too small. Expected binary record size = {exp}, got {n_bytes} ")
+            if n_bytes % exp > 0:
+                raise ValueError(f"Binary record size {exp} does not divide data size {n_bytes}.")
+
+    def decode_device(self, d_data, n_bytes: int, first_record_id: int = 0, stream=None) -> DecodedBatch:
+        """Decode a split already resident in HBM (d_data: uint8 CUDA tensor)."""
+        torch = _torch()
+        stride = self.get_record_size()
+        n_rec = n_bytes // stride
+        st = stream if stream is not None else torch.cuda.current_stream()
+        L = N.load()
+        sizes = (ctypes.c_int64 * self.plan.n_columns)()
+        N.check(L.cbx_string_sizes_fixed(self.native.handle, d_data.data_ptr(), n_rec, stride,
+                                         self.params.start_offset, sizes, ctypes.c_void_p(st.cuda_stream)))
+        cols, cs = _alloc_columns(self.plan, n_rec, list(sizes), d_data.device)
+        N.check(L.cbx_decode_fixed(self.native.handle, d_data.data_ptr(), n_rec, stride, self.params.start_offset,
+                                   first_record_id, cs, ctypes.c_void_p(st.cuda_stream)))
+        for ci, c in enumerate(cols):
+            if "data" in c:
+                c["data_size"] = cs[ci].data_size
+        return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, self.params.generate_record_id)
+
+    def decode(self, data: bytes, first_record_id: int = 0) -> DecodedBatch:
+        torch = _torch()
+        self.check_binary_data_validity(len(data))
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda") if len(data) else torch.zeros(16, dtype=torch.uint8, device="cuda")
+        return self.decode_device(t, len(data), first_record_id)
+
+    def get_row_iterator(self, data: bytes) -> Iterator[dict]:
+        return iter(self.decode(data).to_rows())
+
+
+class VarLenNestedReader(_BaseReader):
+    """GPU drop-in for VarLenNestedReader (CP/reader/VarLenNestedReader.scala:46-310), RDW framing."""
+
+    def rdw_params(self) -> N.CbxRdwParams:
+        p = self.params
+        r = N.CbxRdwParams()
+        r.big_endian = int(p.is_rdw_big_endian)
+        r.adjustment = (-4 if p.is_rdw_part_rec_length else 0) + p.rdw_adjustment
+        r.file_header_bytes = p.file_start_offset
+        r.file_footer_bytes = p.file_end_offset
+        return r
+
+    def frame(self, d_data, n_bytes: int, seeds: Optional[Sequence[int]] = None, stream=None):
+        """GPU RDW walk -> (rec_off, rec_len) device tensors of the valid records."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream()
+        seeds = list(seeds) if seeds else [0]
+        cap = max(1, n_bytes // 5 + 1)
+        off = torch.empty(cap, dtype=torch.int64, device=d_data.device)
+        ln = torch.empty(cap, dtype=torch.int32, device=d_data.device)
+        sd = (ctypes.c_int64 * len(seeds))(*seeds)
+        n = ctypes.c_int64(0)
+        prm = self.rdw_params()
+        N.check(N.load().cbx_frame_rdw(d_data.data_ptr(), n_bytes, sd, len(seeds), ctypes.byref(prm),
+                                        off.data_ptr(), ln.data_ptr(), cap, ctypes.byref(n),
+                                        ctypes.c_void_p(st.cuda_stream)))
+        return off[: n.value], ln[: n.value]
+
+    def decode_device(self, d_data, n_bytes: int, rec_off, rec_len, first_record_id: int = 0,
+                      stream=None) -> DecodedBatch:
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream()
+        n_rec = int(rec_off.numel())
+        L = N.load()
+        sizes = (ctypes.c_int64 * self.plan.n_columns)()
+        N.check(L.cbx_string_sizes_var(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(),
+                                       rec_len.data_ptr(), n_rec, self.params.start_offset, sizes,
+                                       ctypes.c_void_p(st.cuda_stream)))
+        cols, cs = _alloc_columns(self.plan, n_rec, list(sizes), d_data.device)
+        N.check(L.cbx_decode_var(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(),
+                                 rec_len.data_ptr(), n_rec, self.params.start_offset, first_record_id, cs,
+                                 ctypes.c_void_p(st.cuda_stream)))
+        for ci, c in enumerate(cols):
+            if "data" in c:
+                c["data_size"] = cs[ci].data_size
+        return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, self.params.generate_record_id)
+
+    def decode(self, data: bytes, seeds: Optional[Sequence[int]] = None, first_record_id: int = 0) -> DecodedBatch:
+        torch = _torch()
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda") if len(data) else torch.zeros(16, dtype=torch.uint8, device="cuda")
+        off, ln = self.frame(t, len(data), seeds)
+        return self.decode_device(t, len(data), off, ln, first_record_id)
+
+    def get_row_iterator(self, data: bytes) -> Iterator[dict]:
+        return iter(self.decode(data).to_rows())

@@ -1,0 +1,206 @@
+/*
+ * cobrix_hip.h -- C ABI of the MI355X (gfx950) Cobrix record decoder (libcobrix_hip.so).
+ *
+ * Drop-in boundary: replaces, per BATCH of records, the per-record
+ *   RecordExtractors.extractRecord(ast, data, offsetBytes, ...)            (CP/reader/extractors/record/RecordExtractors.scala:49-183)
+ *   + Primitive.decodeTypeValue / DecoderSelector decoder closures        (CP/parser/ast/Primitive.scala:102-128,
+ *                                                                            CP/parser/decoders/DecoderSelector.scala:54-290)
+ * that sit under
+ *   FixedLenReader.getRowIterator(binaryData)                              (SC/reader/FixedLenReader.scala:23-25)
+ *   VarLenReader.getRowIterator(stream, startingFileOffset, fileNumber, startingRecordIndex)
+ *                                                                          (SC/reader/VarLenReader.scala:44-60)
+ * and, for RDW files, the sequential header walk of
+ *   VRLRecordReader.fetchRecordUsingRdwHeaders / RecordHeaderParserRDW     (CP/reader/iterator/VRLRecordReader.scala:151-186,
+ *                                                                            CP/parser/headerparsers/RecordHeaderParserRDW.scala:44-85)
+ *   IndexGenerator.sparseIndexGenerator                                   (CP/reader/index/IndexGenerator.scala:33-127)
+ * (CP = cobol-parser/src/main/scala/za/co/absa/cobrix/cobol/, SC = spark-cobol/src/main/scala/za/co/absa/cobrix/spark/cobol/)
+ *
+ * The JVM side flattens the parsed `Copybook` AST into the cbx_field / cbx_array tables below
+ * (what the Scala/Python host does in cobrix_amd/plan.py) and calls this library through
+ * JNI or Panama FFM with device (or pinned host) pointers.  Plain C types only.
+ *
+ * Error convention (mirrors the reference): data errors never fail a call -- a malformed value
+ * decodes to null (validity bit 0), as DecoderSelector.scala:283-290 does.  Structural errors
+ * return a negative status: CBX_E_ARGUMENT ~ IllegalArgumentException, CBX_E_STATE ~
+ * IllegalStateException (bad RDW), with the detail in cbx_last_error().
+ */
+#ifndef COBRIX_HIP_H
+#define COBRIX_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CBX_ABI_VERSION 1
+
+/* status codes */
+#define CBX_OK 0
+#define CBX_E_ARGUMENT (-1)   /* IllegalArgumentException */
+#define CBX_E_STATE (-2)      /* IllegalStateException (e.g. RDW length 0 or > 100 MiB) */
+#define CBX_E_CAPACITY (-3)   /* caller buffer too small; required size reported */
+#define CBX_E_HIP (-4)        /* HIP runtime failure */
+#define CBX_E_UNSUPPORTED (-5)
+
+/* field decode kinds (one per DecoderSelector branch) */
+enum cbx_kind {
+    CBX_K_STRING = 1,      /* EBCDIC string via code page, trimmed   StringDecoders.decodeEbcdicString */
+    CBX_K_STRING_ASCII = 2,/* ASCII string                            StringDecoders.decodeAsciiString  */
+    CBX_K_HEX = 3,         /* debug HEX string                        StringDecoders.decodeHex          */
+    CBX_K_RAW = 4,         /* debug RAW bytes                         StringDecoders.decodeRaw          */
+    CBX_K_BCD = 5,         /* COMP-3                                  BCDNumberDecoders                 */
+    CBX_K_BINARY = 6,      /* COMP / COMP-4 / COMP-5 / COMP-9         BinaryNumberDecoders, BinaryUtils */
+    CBX_K_ZONED = 7,       /* EBCDIC DISPLAY numeric                  StringDecoders.decodeEbcdicNumber */
+    CBX_K_FLOAT = 9,       /* COMP-1                                  FloatingPointDecoders             */
+    CBX_K_DOUBLE = 10,     /* COMP-2                                  FloatingPointDecoders             */
+    CBX_K_RECORD_ID = 11,  /* generated Record_Id (long)              RecordExtractors.scala:409-451    */
+    CBX_K_FILE_ID = 12     /* generated File_Id (int)                                                   */
+};
+
+/* output (Spark) types -- SC/schema/CobolSchema.scala:144-173 */
+enum cbx_out {
+    CBX_O_I32 = 1, CBX_O_I64 = 2, CBX_O_DEC64 = 3, CBX_O_DEC128 = 4,
+    CBX_O_F32 = 5, CBX_O_F64 = 6, CBX_O_STRING = 7, CBX_O_BINARY = 8
+};
+
+/* cbx_field.flags */
+#define CBX_F_SIGNED 0x1        /* PIC has a sign (signPosition.isDefined) */
+#define CBX_F_BIG_ENDIAN 0x2    /* binary: COMP/COMP-4/COMP-5 (COMP-9 is little-endian) */
+#define CBX_F_EXPLICIT_DOT 0x4  /* DISPLAY with explicit decimal point */
+#define CBX_F_INTEGRAL 0x8      /* AST type is Integral (else Decimal) */
+#define CBX_F_IBM 0x10          /* COMP-1/2 in IBM hex float (else IEEE-754) */
+#define CBX_F_LITTLE_ENDIAN_FP 0x20
+#define CBX_F_DEPENDEE 0x40     /* an OCCURS DEPENDING ON source (isDependee) */
+
+/* string trimming (StringTrimmingPolicy) */
+#define CBX_TRIM_NONE 1
+#define CBX_TRIM_LEFT 2
+#define CBX_TRIM_RIGHT 3
+#define CBX_TRIM_BOTH 4
+
+#define CBX_MAX_DIMS 4
+
+/* One decoded leaf (a Primitive of the AST, each OCCURS element flattened into "slots").
+ * Offsets are static (variable_size_occurs = false): element (i0..ik) of the field lives at
+ *   offset + sum_k i_k * dim_stride[k]  relative to the record decode base. */
+typedef struct {
+    int32_t kind;          /* cbx_kind */
+    int32_t out_type;      /* cbx_out */
+    int32_t offset;        /* binaryProperties.offset */
+    int32_t size;          /* binaryProperties.dataSize (bytes per element) */
+    int32_t precision, scale, scale_factor;   /* AST type */
+    int32_t out_precision, out_scale;         /* Spark DecimalType(p, s) */
+    int32_t flags;
+    int32_t trim;          /* CBX_TRIM_* for strings */
+    int32_t n_dims;        /* enclosing OCCURS levels, outermost first */
+    int32_t dim_count[CBX_MAX_DIMS];   /* arrayMaxSize per level */
+    int32_t dim_stride[CBX_MAX_DIMS];  /* bytes per element of that level */
+    int32_t dim_array[CBX_MAX_DIMS];   /* index into the cbx_array table per level */
+    int32_t segment;       /* segment-redefine group this field is under, -1 if none */
+    int32_t column;        /* output column */
+} cbx_field;
+
+/* One OCCURS node. Element count per record (extractArray, RecordExtractors.scala:66-114):
+ *   dependee < 0 ? max : (dependee value v valid && min <= v <= max ? v : max) */
+typedef struct {
+    int32_t max_count, min_count;
+    int32_t dependee;      /* index into the field table, -1 for a fixed OCCURS */
+    int32_t segment;       /* segment of the array node, -1 if none */
+    int32_t count_column;  /* output column receiving the per-record element count (int32) */
+    int32_t n_dims;        /* enclosing OCCURS levels (outer arrays of this array) */
+    int32_t parent;        /* enclosing array index or -1 */
+    int32_t reserved;
+} cbx_array;
+
+/* Segment-redefine selection (FixedLenNestedRowIterator.getSegmentId + redefine map):
+ * the trimmed value of the segment-id field (an EBCDIC string field) is compared with each
+ * key; a match activates segment `segment`; no match leaves every segment group null. */
+#define CBX_MAX_SEG_KEYS 32
+#define CBX_MAX_SEG_KEY_LEN 32
+typedef struct {
+    int32_t field_offset, field_size;   /* segment-id field (relative to decode base) */
+    int32_t n_keys;
+    int32_t key_len[CBX_MAX_SEG_KEYS];
+    uint16_t key[CBX_MAX_SEG_KEYS][CBX_MAX_SEG_KEY_LEN];  /* UTF-16 code units */
+    int32_t key_segment[CBX_MAX_SEG_KEYS];
+} cbx_segment_map;
+
+typedef struct {
+    int32_t n_columns;      /* value columns + count columns */
+    int32_t file_id;        /* File_Id value for CBX_K_FILE_ID */
+    int32_t has_segments;   /* segment map valid */
+    int32_t window_bytes;   /* LDS window per record (0 = default) */
+    int32_t segment_column; /* column receiving the active segment index per record, -1 none */
+    int32_t reserved[3];
+    uint32_t lut[256];      /* code page: UTF-8 bytes (0-23), length (24-25), trimmable (31) */
+    cbx_segment_map segments;
+} cbx_plan_options;
+
+/* Output column buffers (caller-owned, device memory).  Column c holds n_slots(c) x n_rec
+ * values laid out slot-major: value (slot s, record r) is element s * n_rec + r.  Validity is
+ * an Arrow bitmap per slot row with a 64-bit-aligned pitch: bit r of row s is
+ *   validity[(s * pitch_words + r / 64)] >> (r % 64), pitch_words = ceil(n_rec / 64).
+ * Strings/binary: offsets[v] .. offsets[v+1] (int64, v = s * n_rec + r) into data. */
+typedef struct {
+    void* values;          /* fixed-width values (NULL for strings) */
+    uint64_t* validity;
+    int64_t* offsets;      /* strings: n_values + 1 entries */
+    uint8_t* data;         /* strings: UTF-8 payload */
+    int64_t data_capacity;
+    int64_t data_size;     /* out: payload bytes written */
+} cbx_column;
+
+typedef struct cbx_plan cbx_plan;
+
+int32_t cbx_abi_version(void);
+const char* cbx_last_error(void);
+
+/* Build a plan from the flattened copybook.  Copies the tables to device memory. */
+int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const cbx_array* arrays,
+                    int32_t n_arrays, const cbx_plan_options* opts, cbx_plan** out_plan);
+void cbx_plan_destroy(cbx_plan* plan);
+
+/* Exact string payload sizes per column for a batch (first pass of the two-pass string
+ * output); out_sizes[n_columns] (0 for non-string columns). */
+int cbx_string_sizes_fixed(cbx_plan* plan, const uint8_t* d_records, int64_t n_rec,
+                           int32_t rec_stride, int32_t start_offset, int64_t* out_sizes, void* stream);
+
+/* Fixed-length batch: record i occupies d_records[i*rec_stride, (i+1)*rec_stride) and is
+ * decoded at +start_offset (CobolScanners.buildScanForFixedLength; record_start_offset).
+ * Bounds rules of Primitive.decodeTypeValue apply against rec_stride. */
+int cbx_decode_fixed(cbx_plan* plan, const uint8_t* d_records, int64_t n_rec, int32_t rec_stride,
+                     int32_t start_offset, int64_t first_record_id, cbx_column* columns, void* stream);
+
+/* Variable-length batch: record i is d_data[rec_off[i], rec_off[i] + rec_len[i]) (payload
+ * without RDW), decoded at +start_offset; shorter records yield null numerics / truncated strings. */
+int cbx_decode_var(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                   const int32_t* d_rec_len, int64_t n_rec, int32_t start_offset,
+                   int64_t first_record_id, cbx_column* columns, void* stream);
+int cbx_string_sizes_var(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                         const int32_t* d_rec_len, int64_t n_rec, int32_t start_offset,
+                         int64_t* out_sizes, void* stream);
+
+/* Optional per-call kernel timing with HIP events on the call's stream (bench / profiling):
+ * when enabled, the last decode call's sizing-pass, scan and decode-pass durations (ms). */
+int cbx_plan_set_profiling(cbx_plan* plan, int32_t enable);
+int cbx_plan_last_kernel_ms(const cbx_plan* plan, float* sizes_ms, float* scan_ms, float* decode_ms);
+
+/* RDW header walk on the GPU (RecordHeaderParserRDW + VRLRecordReader), seeded by sparse-index
+ * entry points: seeds[k] is a known record-header offset (offsetFrom of an index entry), the
+ * chain from seeds[k] is walked up to seeds[k+1] (or n_bytes).  Writes payload offsets/lengths
+ * of valid records in file order; *n_records receives the count. */
+typedef struct {
+    int32_t big_endian;         /* is_rdw_big_endian */
+    int32_t adjustment;         /* rdw_adjustment (+ -4 if is_rdw_part_of_record_length) */
+    int32_t file_header_bytes;  /* file_start_offset */
+    int32_t file_footer_bytes;  /* file_end_offset */
+} cbx_rdw_params;
+
+int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,
+                  const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len,
+                  int64_t capacity, int64_t* n_records, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

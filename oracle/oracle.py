@@ -379,3 +379,37 @@ def rows(res: OracleResult, collapse_root: bool = True) -> List[dict]:
             row = {k: v for k, v in recs}
         out.append(row)
     return out
+
+
+def _iter_leaves(g):
+    """Primitive nodes in AST (walk) order."""
+    for c in g.children:
+        if isinstance(c, cbk.Group):
+            yield from _iter_leaves(c)
+        else:
+            yield c
+
+
+def columns(res: OracleResult) -> Dict[int, Dict[str, np.ndarray]]:
+    """Per-leaf columnar view of the event stream (slot-major like the GPU output).
+
+    Returns {node id: {"rec", "slot", "valid", "lo", "hi", "bytes"}} for every primitive node that
+    emitted values, and {node id: {"rec", "slot", "count"}} for OCCURS nodes."""
+    ev = res.events
+    out: Dict[int, Dict[str, np.ndarray]] = {}
+    vals = ev[ev["kind"] == EV_VALUE]
+    arrs = ev[ev["kind"] == EV_ARRAY]
+    order = np.argsort(vals["node"], kind="stable")
+    vals = vals[order]
+    nodes, starts = np.unique(vals["node"], return_index=True)
+    ends = list(starts[1:]) + [len(vals)]
+    for nid, s, e in zip(nodes, starts, ends):
+        v = vals[s:e]
+        d = {"rec": v["rec"].astype(np.int64), "slot": v["slot"].astype(np.int64),
+             "valid": v["isnull"] == 0, "lo": v["lo"], "hi": v["hi"], "stype": v["stype"]}
+        out[int(nid)] = d
+    for nid in np.unique(arrs["node"]):
+        a = arrs[arrs["node"] == nid]
+        out[int(nid)] = {"rec": a["rec"].astype(np.int64), "slot": a["slot"].astype(np.int64),
+                         "count": a["lo"]}
+    return out

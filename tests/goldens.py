@@ -15,6 +15,16 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "data")
 
 
+def java_trim(s: str) -> str:
+    """java.lang.String.trim: strip code points <= U+0020."""
+    b, e = 0, len(s)
+    while b < e and s[b] <= " ":
+        b += 1
+    while e > b and s[e - 1] <= " ":
+        e -= 1
+    return s[b:e]
+
+
 def path(*p: str) -> str:
     return os.path.join(GOLDEN, *p)
 

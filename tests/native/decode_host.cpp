@@ -1,0 +1,29 @@
+// TEST SHIM: runs the device field decoders (cobrix_amd/csrc/cbx_decode.h) on the host so the
+// exact GPU arithmetic can be fuzzed against the C oracle without a GPU.  Built by
+// tests/native/Makefile with hipcc (host path of __host__ __device__ functions); never part of
+// the product library.
+#include "cbx_decode.h"
+
+using namespace cbx;
+
+extern "C" int cbxh_decode(const cbx_field* cf, const uint8_t* p, int n_avail, const uint32_t* lut,
+                           uint64_t* lo, uint64_t* hi, uint8_t* sbuf, int32_t* slen) {
+    Field f = make_field(*cf);
+    *lo = *hi = 0;
+    *slen = 0;
+    const bool is_str = f.out_type == CBX_O_STRING || f.out_type == CBX_O_BINARY;
+    if (!is_str) {
+        if (n_avail < f.size) return 0;  // Primitive.decodeTypeValue numeric bounds
+        Val v = decode_numeric(f, p);
+        *lo = v.lo;
+        *hi = v.hi;
+        return v.valid ? 1 : 0;
+    }
+    if (n_avail < 0) return 0;
+    int n = f.size < n_avail ? f.size : n_avail;
+    auto lutf = [&](uint32_t b) -> uint32_t { return f.kind == CBX_K_STRING_ASCII ? ascii_lut(b) : lut[b]; };
+    StrSpan s = string_span(f, p, n, lutf);
+    string_write(f, p, s, sbuf, lutf);
+    *slen = s.utf8_len;
+    return 1;
+}

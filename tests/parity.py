@@ -1,0 +1,90 @@
+"""GPU-vs-oracle column comparison (bit-exact for every integer, decimal, float and string)."""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+
+from cobrix_amd import native as N
+from oracle import oracle as O
+
+
+def compare_batch(batch, res: "O.OracleResult", max_report: int = 10) -> List[str]:
+    plan = batch.plan
+    ocols = O.columns(res)
+    errs: List[str] = []
+    n_rec = batch.n_rec
+    if n_rec != res.n_rec:
+        return [f"record count {n_rec} != oracle {res.n_rec}"]
+    for ci, info in enumerate(plan.columns):
+        if info.kind not in ("value", "count") or info.hidden:
+            continue
+        nid = res.ast.node_of(info.node)
+        g = batch.host_column(ci)
+        o = ocols.get(nid)
+        if info.kind == "count":
+            got = g["values"][:n_rec].astype(np.int64)
+            if o is None:
+                continue
+            # count of the top-level occurrence (slot 0 of the enclosing arrays)
+            sel = o["slot"] == 0
+            exp = np.full(n_rec, -1, dtype=np.int64)
+            exp[o["rec"][sel]] = o["count"][sel]
+            known = exp >= 0
+            bad = np.nonzero(known & (got != exp))[0]
+            if len(bad):
+                errs.append(f"{info.node.name} counts differ at records {bad[:5]}: {got[bad[:5]]} vs {exp[bad[:5]]}")
+            continue
+        exp_valid = np.zeros((info.n_slots, n_rec), dtype=bool)
+        if o is not None:
+            exp_valid[o["slot"], o["rec"]] = o["valid"]
+        gv = g["validity"]
+        bad = np.argwhere(gv != exp_valid)
+        if len(bad):
+            s, r = bad[0]
+            errs.append(f"{info.node.name}: validity differs at {len(bad)} values, first slot {s} record {r}: "
+                        f"gpu {gv[s, r]} oracle {exp_valid[s, r]}")
+            continue
+        if o is None:
+            continue
+        m = o["valid"]
+        rec, slot = o["rec"][m], o["slot"][m]
+        v = slot * n_rec + rec
+        ot = info.out_type
+        if ot in (N.O_STRING, N.O_BINARY):
+            off = g["offsets"]
+            data = g["data"]
+            heap = res.heap
+            lo, hi = o["lo"][m], o["hi"][m]
+            nbad = 0
+            for k in range(len(v)):
+                a = data[int(off[v[k]]):int(off[v[k] + 1])]
+                b = heap[int(lo[k]):int(lo[k]) + int(hi[k])]
+                if a != b:
+                    nbad += 1
+                    if nbad <= 3:
+                        errs.append(f"{info.node.name}: string differs at record {rec[k]} slot {slot[k]}: {a!r} vs {b!r}")
+            continue
+        vals = g["values"]
+        lo = o["lo"][m].astype(np.int64)
+        hi = o["hi"][m].astype(np.int64)
+        if ot == N.O_I32:
+            got = vals[v].astype(np.int64)
+            exp = lo.astype(np.int32).astype(np.int64)
+            diff = got != exp
+        elif ot in (N.O_I64, N.O_DEC64):
+            diff = vals[v].astype(np.int64) != lo
+        elif ot == N.O_DEC128:
+            diff = (vals[v, 0].astype(np.int64) != lo) | (vals[v, 1].astype(np.int64) != hi)
+        elif ot == N.O_F32:
+            diff = (vals[v].astype(np.int64) & 0xFFFFFFFF) != (lo & 0xFFFFFFFF)
+        else:
+            diff = vals[v].astype(np.int64) != lo
+        idx = np.nonzero(diff)[0]
+        if len(idx):
+            k = idx[0]
+            errs.append(f"{info.node.name}: {len(idx)} values differ, first record {rec[k]} slot {slot[k]}: "
+                        f"gpu {vals[v[k]]} oracle lo={lo[k]} hi={hi[k]}")
+        if len(errs) >= max_report:
+            break
+    return errs

@@ -1,0 +1,198 @@
+"""CPU fuzz: the device field decoders (cbx_decode.h, executed on the host through the test
+shim tests/native/libcbx_decode_host.so) against the oracle restatement, value by value.
+
+This pins the GPU arithmetic (COMP-3 nibbles, binary widths, zoned overpunch/sign/dot rules,
+IBM/IEEE floats, Spark HALF_UP/overflow conversion, string trimming + UTF-8) without a GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from cobrix_amd import copybook as cbk
+from cobrix_amd import native as N
+from cobrix_amd.codepages import lut_for, utf8_lut
+from cobrix_amd.plan import build_plan
+from oracle import oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SHIM = os.path.join(HERE, "native", "libcbx_decode_host.so")
+
+FUZZ_COPYBOOK = """
+       01  R.
+           05  S1    PIC X(12).
+           05  S2    PIC X(3).
+           05  A1    PIC A(5).
+           05  Z01   PIC 9(1).
+           05  Z02   PIC 9(4).
+           05  Z03   PIC S9(4).
+           05  Z04   PIC 9(9).
+           05  Z05   PIC S9(9).
+           05  Z06   PIC 9(10).
+           05  Z07   PIC S9(18).
+           05  Z08   PIC 9(20).
+           05  Z09   PIC S9(37).
+           05  Z10   PIC 99V9.
+           05  Z11   PIC S9(5)V99.
+           05  Z12   PIC S9(13)V9(5).
+           05  Z13   PIC 9(16)V9(10).
+           05  Z14   PIC S9(3).99.
+           05  Z15   PIC 9(4),9(2).
+           05  Z16   PIC SPPP9(5).
+           05  Z17   PIC S9(5)PPP.
+           05  Z18   PIC +9(6)V99.
+           05  Z19   PIC Z(6)VZZ-.
+           05  Z20   PIC 9(6).99-.
+           05  Z21   PIC S9(7) SIGN LEADING SEPARATE.
+           05  Z22   PIC S9(5)V99 SIGN TRAILING SEPARATE.
+           05  Z23   PIC SV9(7) SIGN LEADING.
+           05  Z24   PIC Z(8)-.
+           05  Z25   PIC 9(3)PP.
+           05  Z26   PIC SVPP9(3).
+           05  B01   PIC 9(1) COMP.
+           05  B02   PIC S9(4) COMP.
+           05  B03   PIC 9(4) COMP.
+           05  B04   PIC 9(9) COMP.
+           05  B05   PIC S9(9) COMP.
+           05  B06   PIC 9(18) COMP.
+           05  B07   PIC S9(18) COMP.
+           05  B08   PIC 9(20) COMP.
+           05  B09   PIC S9(38) COMP.
+           05  B10   PIC S9(3)V99 COMP.
+           05  B11   PIC 9(7)V99 COMP.
+           05  B12   PIC S9(15)V9(3) COMP.
+           05  B13   PIC 9(16)V99 COMP.
+           05  B14   PIC SPPP9(5) COMP.
+           05  B15   PIC S9(5)PPP COMP.
+           05  B16   PIC S9(2) COMP-5.
+           05  B17   PIC S9(20)V9(5) COMP.
+           05  B18   PIC SPPP9 COMP.
+           05  P01   PIC 9(1) COMP-3.
+           05  P02   PIC S9(4) COMP-3.
+           05  P03   PIC 9(9) COMP-3.
+           05  P04   PIC S9(10) COMP-3.
+           05  P05   PIC S9(18) COMP-3.
+           05  P06   PIC 9(19) COMP-3.
+           05  P07   PIC S9(20) COMP-3.
+           05  P08   PIC S9(37) COMP-3.
+           05  P09   PIC S9(13)V99 COMP-3.
+           05  P10   PIC S9(3)V9(6) COMP-3.
+           05  P11   PIC 9(2)V9(2) COMP-3.
+           05  P12   PIC S9(18)V9(10) COMP-3.
+           05  P13   PIC SV9(5) COMP-3.
+           05  P14   PIC PPP9(5) COMP-3.
+           05  P15   PIC SPP9(4) COMP-3.
+           05  P16   PIC 9(5)PPP COMP-3.
+           05  P17   PIC S9(38) COMP-3.
+           05  F01   COMP-1.
+           05  F02   COMP-2.
+"""
+
+ZONED_ALPHABET = np.array(list(range(0xF0, 0xFA)) * 6 + list(range(0xC0, 0xCA)) + list(range(0xD0, 0xDA))
+                          + [0x40] * 8 + [0x00] * 2 + [0x4B, 0x6B, 0x60, 0x4E] * 2 + [0xC1, 0x81, 0x5B, 0xFA, 0xAB],
+                          dtype=np.uint8)
+STRING_ALPHABET = np.array([0x40] * 10 + [0x00, 0x05, 0x15, 0x41, 0x25, 0x0D] + list(range(0xC1, 0xCA)) +
+                           list(range(0x81, 0x8A)) + list(range(0xF0, 0xFA)) + [0x4B, 0x6B, 0x5B, 0x9F, 0xFF, 0x74, 0xA1],
+                           dtype=np.uint8)
+
+
+def _shim():
+    if not os.path.exists(SHIM):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(SHIM)], check=True)
+    L = ctypes.CDLL(SHIM)
+    P = ctypes.c_void_p
+    L.cbxh_decode.argtypes = [P, P, ctypes.c_int, P, P, P, P, P]
+    return L
+
+
+def _random_bytes(rng, p: cbk.Primitive, n: int) -> bytes:
+    d = p.dtype
+    if isinstance(d, cbk.AlphaNumeric):
+        return bytes(rng.choice(STRING_ALPHABET, n))
+    if d.compact is None:
+        if rng.random() < 0.5:
+            # mostly well-formed: digits with optional sign/overpunch/dot/spaces
+            b = bytearray(rng.choice(np.arange(0xF0, 0xFA, dtype=np.uint8), n))
+            for _ in range(rng.integers(0, 3)):
+                b[rng.integers(0, n)] = int(rng.choice(ZONED_ALPHABET))
+            return bytes(b)
+        return bytes(rng.choice(ZONED_ALPHABET, n))
+    if d.compact == cbk.COMP3:
+        digits = rng.integers(0, 10, 2 * n)
+        if rng.random() < 0.1:
+            digits[rng.integers(0, 2 * n)] = rng.integers(10, 16)
+        sign = int(rng.choice([0xC, 0xD, 0xF, 0xC, 0xD, 0xA, 0xB, 0xE, 0x0, 0x5]))
+        b = bytearray(n)
+        for i in range(n):
+            hi_n = int(digits[2 * i])
+            lo_n = int(digits[2 * i + 1]) if i < n - 1 else sign
+            b[i] = (hi_n << 4) | lo_n
+        if rng.random() < 0.05:
+            b = bytearray(rng.integers(0, 256, n, dtype=np.uint8))
+        return bytes(b)
+    if rng.random() < 0.2:
+        return bytes([0] * (n - 1) + [int(rng.integers(0, 256))])
+    return bytes(rng.integers(0, 256, n, dtype=np.uint8))
+
+
+@pytest.mark.parametrize("fmt", ["IBM", "IEEE754", "IBM_LE"])
+@pytest.mark.parametrize("code_page,trim", [("common", "both"), ("cp037", "both"), ("cp037_extended", "left"),
+                                            ("cp875", "right"), ("common", "none")])
+def test_field_decoders_match_oracle(fmt, code_page, trim):
+    if fmt != "IBM" and (code_page, trim) != ("common", "both"):
+        pytest.skip("float formats only vary float fields")
+    cb = cbk.parse_copybook(FUZZ_COPYBOOK, floating_point_format=fmt, code_page=code_page, string_trimming=trim)
+    plan = build_plan(cb)
+    ast = O.OracleAst(cb)
+    lut = np.array(utf8_lut(lut_for(code_page)), dtype=np.uint32)
+    L = _shim()
+    OL = O.lib()
+    rng = np.random.default_rng(20261015)
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    sbuf = (ctypes.c_uint8 * 4096)()
+    slen = ctypes.c_int32()
+    heap = np.zeros(1 << 16, dtype=np.uint8)
+    ev = np.zeros(1, dtype=O.EVENT_DTYPE)
+    hl = ctypes.c_int64()
+    mismatches = []
+    n_checked = 0
+    for p in O._iter_leaves(cb.ast):
+        fi = plan.field_of_node[id(p)]
+        cf = plan.fields[fi]
+        node = ast.nodes[ast.node_of(p)]
+        for _ in range(400):
+            b = _random_bytes(rng, p, p.data_size)
+            buf = np.frombuffer(b, dtype=np.uint8)
+            valid = L.cbxh_decode(ctypes.byref(cf), buf.ctypes.data, len(b), lut.ctypes.data,
+                                  ctypes.byref(lo), ctypes.byref(hi), sbuf, ctypes.byref(slen))
+            hl.value = 0
+            rc = OL.ora_decode_field(ctypes.byref(node), ctypes.byref(ast.opts), buf.ctypes.data, len(b),
+                                     ev.ctypes.data, heap.ctypes.data, len(heap), ctypes.byref(hl))
+            assert rc == 0
+            e = ev[0]
+            exp_valid = not e["isnull"]
+            ok = exp_valid == bool(valid)
+            if ok and exp_valid:
+                if cf.out_type in (N.O_STRING, N.O_BINARY):
+                    got = bytes(sbuf[: slen.value])
+                    want = heap[int(e["lo"]): int(e["lo"]) + int(e["hi"])].tobytes()
+                    ok = got == want
+                elif cf.out_type == N.O_I32:
+                    ok = np.int32(np.uint64(lo.value).astype(np.uint32).view(np.int32)) == np.int32(int(e["lo"]) & 0xFFFFFFFF if int(e["lo"]) >= 0 else int(e["lo"]))
+                elif cf.out_type in (N.O_I64, N.O_DEC64):
+                    ok = np.uint64(lo.value) == np.uint64(int(e["lo"]) & 0xFFFFFFFFFFFFFFFF)
+                elif cf.out_type == N.O_DEC128:
+                    ok = (lo.value == (int(e["lo"]) & 0xFFFFFFFFFFFFFFFF)) and (hi.value == (int(e["hi"]) & 0xFFFFFFFFFFFFFFFF))
+                elif cf.out_type == N.O_F32:
+                    ok = (lo.value & 0xFFFFFFFF) == (int(e["lo"]) & 0xFFFFFFFF)
+                elif cf.out_type == N.O_F64:
+                    ok = lo.value == (int(e["lo"]) & 0xFFFFFFFFFFFFFFFF)
+            n_checked += 1
+            if not ok:
+                mismatches.append((p.name, b.hex(), bool(valid), lo.value, hi.value, exp_valid, int(e["lo"]), int(e["hi"])))
+    assert n_checked > 20000
+    assert not mismatches, f"{len(mismatches)} mismatches, first: {mismatches[:8]}"
