@@ -64,6 +64,7 @@ struct cbx_plan {
     int64_t* d_block_sums = nullptr;
     int64_t block_sums_cap = 0;
     int num_cus = 256;
+    int contig_max_bytes = 20 * 1024;   // LDS span budget for contiguous fixed-length staging
     // profiling
     bool profiling = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -305,9 +306,15 @@ static KernelArgs make_args(cbx_plan* P, const uint8_t* data, int64_t data_len, 
     return a;
 }
 
-static int launch_decode(cbx_plan* P, const KernelArgs& a, hipStream_t st) {
+static int launch_decode(cbx_plan* P, KernelArgs a, hipStream_t st) {
     if (a.n_tiles == 0) return CBX_OK;
-    size_t lds = 1024 + ((a.n_arrays * kWave * 4 + 15) & ~15) + (size_t)kWave * P->max_pitch;
+    // fixed-length records short enough to stage a whole 64-record span: contiguous mode
+    size_t rows = (size_t)kWave * P->max_pitch;
+    if (a.mode == 0 && !a.rec_off && a.stride > 0 && (size_t)kWave * a.stride + 32 <= (size_t)P->contig_max_bytes) {
+        a.contig = 1;
+        rows = std::max(rows, (size_t)kWave * a.stride + 32);
+    }
+    size_t lds = 1024 + ((a.n_arrays * kWave * 4 + 15) & ~15) + rows + 16;
     if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "LDS window too large");
     // one wave per block; enough blocks to cover every CU several times, grid-stride the rest
     int per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / std::max<size_t>(lds, 1)));

@@ -265,33 +265,10 @@ CBX_HD Val decode_binary(const Field& f, const uint8_t* p) {
 // ------------------------------------------------------------------------------------------
 // EBCDIC DISPLAY numbers (decodeEbcdicNumber + the Int/Long/BigNumber/BigDecimal wrappers)
 // ------------------------------------------------------------------------------------------
-CBX_HD Val decode_zoned(const Field& f, const uint8_t* p) {
-    const int n = f.size;
-    bool malformed = false;
-    int sign = 0;  // 0 none, 1 '+', 2 '-'
-    int nd = 0, ndots = 0, after = 0, sig = 0;
-    U128 D = u128(0);
-    bool ovf = false;
-    for (int i = 0; i < n; i++) {
-        uint32_t c = p[i];
-        uint32_t hi = c >> 4, lo = c & 15;
-        bool dig = lo <= 9 && (hi == 0xF || (sign == 0 && (hi == 0xC || hi == 0xD)));
-        bool sch = sign == 0 && (c == 0x60 || c == 0x4E);
-        bool dot = c == 0x4B || c == 0x6B;
-        bool spc = c == 0x40 || c == 0;
-        if (sign == 0 && dig && hi != 0xF) sign = hi == 0xD ? 2 : 1;
-        if (sch) sign = c == 0x60 ? 2 : 1;
-        malformed |= !(dig || sch || dot || spc);
-        if (dig) {
-            nd++;
-            after += ndots > 0;
-            bool s = sig > 0 || lo != 0;
-            sig += s;
-            if (sig <= 38) u128_muladd(D, 10, lo);
-            else ovf = true;
-        }
-        ndots += dot;
-    }
+// Java-level result of decodeEbcdicNumber summarised: sign (0 none, 1 '+', 2 '-'), digit count,
+// dot count, digits after the first dot, digit magnitude (38 significant digits max, ovf beyond).
+CBX_HD Val zoned_finish(const Field& f, bool malformed, int sign, int nd, int ndots, int after, U128 D,
+                        bool ovf) {
     const bool neg = sign == 2;
     if (malformed || (neg && !(f.flags & CBX_F_SIGNED))) return null_val();
     if (f.flags & CBX_F_INTEGRAL) {
@@ -326,6 +303,36 @@ CBX_HD Val decode_zoned(const Field& f, const uint8_t* p) {
     return finalize_decimal(D, ovf, -f.sf + nd, neg, f);
 }
 
+CBX_HD Val decode_zoned(const Field& f, const uint8_t* p) {
+    const int n = f.size;
+    bool malformed = false;
+    int sign = 0;  // 0 none, 1 '+', 2 '-'
+    int nd = 0, ndots = 0, after = 0, sig = 0;
+    U128 D = u128(0);
+    bool ovf = false;
+    for (int i = 0; i < n; i++) {
+        uint32_t c = p[i];
+        uint32_t hi = c >> 4, lo = c & 15;
+        bool dig = lo <= 9 && (hi == 0xF || (sign == 0 && (hi == 0xC || hi == 0xD)));
+        bool sch = sign == 0 && (c == 0x60 || c == 0x4E);
+        bool dot = c == 0x4B || c == 0x6B;
+        bool spc = c == 0x40 || c == 0;
+        if (sign == 0 && dig && hi != 0xF) sign = hi == 0xD ? 2 : 1;
+        if (sch) sign = c == 0x60 ? 2 : 1;
+        malformed |= !(dig || sch || dot || spc);
+        if (dig) {
+            nd++;
+            after += ndots > 0;
+            bool s = sig > 0 || lo != 0;
+            sig += s;
+            if (sig <= 38) u128_muladd(D, 10, lo);
+            else ovf = true;
+        }
+        ndots += dot;
+    }
+    return zoned_finish(f, malformed, sign, nd, ndots, after, D, ovf);
+}
+
 // ------------------------------------------------------------------------------------------
 // COMP-1 / COMP-2
 // ------------------------------------------------------------------------------------------
@@ -337,7 +344,11 @@ CBX_HD uint32_t ibm_single_bits(uint32_t mant) {
     int32_t expo = (m & (int32_t)0x80000000) >> 22;
     if (frac == 0) return 0u;
     int32_t top = frac & 0x00F00000;
-    while (top == 0) { frac <<= 4; expo -= 4; top = frac & 0x00F00000; }
+    if (top == 0) {
+        // leading zero nibbles of the 24-bit fraction (the reference's shift-by-4 loop)
+        int zn = (__builtin_clz((uint32_t)frac << 8)) >> 2;
+        frac <<= 4 * zn; expo -= 4 * zn; top = frac & 0x00F00000;
+    }
     int32_t lz = (int32_t)((0x000055AFu >> (top >> 19)) & 3);
     frac <<= lz;
     int32_t ce = expo + 131 - lz;
@@ -359,7 +370,10 @@ CBX_HD uint64_t ibm_double_bits(uint64_t m) {
     int64_t expo = (int64_t)((m & 0x7F00000000000000ull) >> 54);
     if (frac == 0) return 0ull;
     int64_t top = frac & 0x00F0000000000000ll;
-    while (top == 0) { frac <<= 4; expo -= 4; top = frac & 0x00F0000000000000ll; }
+    if (top == 0) {
+        int zn = (__builtin_clzll((uint64_t)frac << 8)) >> 2;
+        frac <<= 4 * zn; expo -= 4 * zn; top = frac & 0x00F0000000000000ll;
+    }
     int64_t lz = (int64_t)((0x000055AFull >> (top >> 51)) & 3);
     frac <<= lz;
     int64_t ce = expo + 765 - lz;
@@ -391,6 +405,213 @@ CBX_HD Val decode_numeric(const Field& f, const uint8_t* p) {
     case CBX_K_ZONED: return decode_zoned(f, p);
     case CBX_K_FLOAT: return decode_float(f, p);
     case CBX_K_DOUBLE: return decode_double(f, p);
+    default: return null_val();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Width-specialised decoders over field bytes held in registers (the hot path).
+// FB<N>: byte j of the field sits in bits 8*(j&3) of w[j>>2]; loaded from the LDS image with
+// dword reads + alignbyte, so a field costs ceil((N+6)/4) ds_read_b32 whatever its alignment.
+// ------------------------------------------------------------------------------------------
+template <int N>
+struct FB {
+    uint32_t w[(N + 3) / 4];
+    CBX_HD uint32_t byte(int j) const { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; }
+};
+
+CBX_HD uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (sh & 3)));
+#endif
+}
+
+// buf: LDS image (or any byte buffer) with >= 8 readable bytes past the field
+template <int N>
+CBX_HD FB<N> load_field(const uint8_t* buf, uint32_t addr) {
+    constexpr int NW = (N + 3) / 4;
+    const uint32_t* p = (const uint32_t*)(buf + (addr & ~3u));
+    const uint32_t sh = addr & 3u;
+    uint32_t r[NW + 1];
+#pragma unroll
+    for (int k = 0; k <= NW; k++) r[k] = p[k];
+    FB<N> b;
+#pragma unroll
+    for (int k = 0; k < NW; k++) b.w[k] = align_bytes(r[k + 1], r[k], sh);
+    return b;
+}
+
+// big-endian value of bytes [i, i + k), k <= 8 (i, k compile-time after unrolling)
+template <int N>
+CBX_HD uint64_t fb_be(const FB<N>& b, int i, int k) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        if (j < k) v = (v << 8) | b.byte(i + j);
+    return v;
+}
+
+// 8 valid packed-BCD digits -> binary
+CBX_HD uint32_t bcd8_bin(uint32_t x) {
+    uint32_t t1 = ((x >> 4) & 0x0F0F0F0Fu) * 10u + (x & 0x0F0F0F0Fu);
+    uint32_t t2 = ((t1 >> 8) & 0x00FF00FFu) * 100u + (t1 & 0x00FF00FFu);
+    return (t2 >> 16) * 10000u + (t2 & 0xFFFFu);
+}
+CBX_HD uint64_t bcd16_bin(uint64_t x) {
+    return (uint64_t)bcd8_bin((uint32_t)(x >> 32)) * 100000000ull + bcd8_bin((uint32_t)x);
+}
+// every nibble of x is a decimal digit
+CBX_HD bool bcd_ok(uint64_t x) {
+    uint64_t lo = x & 0x0F0F0F0F0F0F0F0Full, hi = (x >> 4) & 0x0F0F0F0F0F0F0F0Full;
+    return (((lo + 0x0606060606060606ull) | (hi + 0x0606060606060606ull)) & 0x1010101010101010ull) == 0;
+}
+
+template <int N>
+CBX_HD Val decode_bcd_n(const Field& f, const FB<N>& b) {
+    constexpr int NL = N < 8 ? N : 8;      // bytes in the low part (carries the sign nibble)
+    constexpr int NH = N - NL;             // leading bytes (digits only)
+    const uint64_t lo = fb_be(b, NH, NL);
+    const uint32_t sn = (uint32_t)lo & 15u;
+    const uint64_t dlo = lo >> 4;          // 2*NL - 1 digits
+    bool ok = bcd_ok(dlo) && (sn == 0xC || sn == 0xD || sn == 0xF);
+    uint64_t hi = 0;
+    if (NH > 0) { hi = fb_be(b, 0, NH); ok &= bcd_ok(hi); }
+    if (!ok) return null_val();
+    const bool neg = sn == 0xD;
+    U128 M = u128(bcd16_bin(dlo));
+    if (NH > 0) {
+        // M = hi_value * 10^15 + lo_value
+        uint64_t hv = bcd16_bin(hi);
+        const uint64_t P15 = 1000000000000000ull;
+        uint64_t plo = hv * P15, phi = mulhi64(hv, P15);
+        uint64_t s = plo + M.lo;
+        M.hi = phi + (s < plo);
+        M.lo = s;
+    }
+    if ((f.flags & CBX_F_INTEGRAL) && f.precision <= 18) {
+        uint64_t v = neg ? (uint64_t)0 - M.lo : M.lo;  // Java long arithmetic wraps
+        return Val{v, (uint64_t)((int64_t)v >> 63), true};
+    }
+    if (f.flags & CBX_F_INTEGRAL) return finalize_decimal(M, false, 0, neg, f);
+    if (f.sf == 0) return finalize_decimal(M, false, f.scale, neg, f);
+    if (f.sf > 0) {
+        bool okm = u128_mul_pow10(M, f.sf);
+        return finalize_decimal(M, !okm, 0, neg, f);
+    }
+    return finalize_decimal(M, false, -f.sf + 2 * N - 1, neg, f);
+}
+
+template <int N>
+CBX_HD Val decode_binary_n(const Field& f, const FB<N>& b) {
+    const bool be = (f.flags & CBX_F_BIG_ENDIAN) != 0;
+    const bool sgn = (f.flags & CBX_F_SIGNED) != 0;
+    U128 v = u128(0);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        uint32_t x = be ? b.byte(i) : b.byte(N - 1 - i);
+        v.hi = (v.hi << 8) | (v.lo >> 56);
+        v.lo = (v.lo << 8) | x;
+    }
+    const uint32_t top = be ? b.byte(0) : b.byte(N - 1);
+    bool neg = false;
+    if (sgn && (top & 0x80)) {
+        if (8 * N < 64) { v.lo |= ~(uint64_t)0 << (8 * N); v.hi = ~(uint64_t)0; }
+        else if (8 * N < 128) v.hi |= ~(uint64_t)0 << (8 * N - 64);
+        neg = true;
+    }
+    if (f.flags & CBX_F_INTEGRAL) {
+        if (N == 1 || N == 2 || N == 4) {
+            if (!sgn && N == 4 && (v.lo & 0x80000000u)) return null_val();
+            return Val{v.lo, v.hi, true};
+        }
+        if (N == 8) {
+            if (!sgn && (v.lo >> 63)) return null_val();
+            return Val{v.lo, (uint64_t)((int64_t)v.lo >> 63), true};
+        }
+        U128 M = neg ? u128_neg(v) : v;
+        return finalize_decimal(M, false, 0, neg, f);
+    }
+    U128 M = neg ? u128_neg(v) : v;
+    if (f.sf == 0) return finalize_decimal(M, false, f.scale, neg, f);
+    if (f.sf > 0) {
+        bool ok = u128_mul_pow10(M, f.sf);
+        return finalize_decimal(M, !ok, 0, neg, f);
+    }
+    return finalize_decimal(M, false, -f.sf + u128_ndigits(M), neg, f);
+}
+
+// Zoned: fast path for the common layout (F-zone digits, last byte optionally C/D overpunch);
+// anything else (spaces, separate signs, dots, malformed bytes) takes the general state machine.
+template <int N>
+CBX_HD Val decode_zoned_n(const Field& f, const FB<N>& b, const uint8_t* buf, uint32_t addr) {
+    bool fast = true;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        uint32_t c = b.byte(j);
+        uint32_t lo = c & 15u, hi = c >> 4;
+        fast &= lo <= 9u;
+        if (j + 1 < N) fast &= hi == 0xFu;
+        else fast &= hi == 0xFu || hi == 0xCu || hi == 0xDu;
+        acc = acc * 10u + lo;
+    }
+    if (fast) {
+        uint32_t last = b.byte(N - 1) >> 4;
+        int sign = last == 0xD ? 2 : (last == 0xC ? 1 : 0);
+        // digits are all significant-or-leading-zero; N <= 18 keeps acc exact
+        return zoned_finish(f, false, sign, N, 0, 0, u128(acc), false);
+    }
+    Field g = f;
+    g.size = N;
+    return decode_zoned(g, buf + addr);
+}
+
+template <int N>
+CBX_HD Val decode_float_n(const Field& f, const FB<N>& b) {
+    const bool le = (f.flags & CBX_F_LITTLE_ENDIAN_FP) != 0;
+    if (N == 4) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) w = (w << 8) | b.byte(le ? 3 - i : i);
+        return Val{(f.flags & CBX_F_IBM) ? ibm_single_bits(w) : w, 0, true};
+    }
+    uint64_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) w = (w << 8) | b.byte(le ? 7 - i : i);
+    return Val{(f.flags & CBX_F_IBM) ? ibm_double_bits(w) : w, 0, true};
+}
+
+#define CBX_SIZE_CASES_16(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16)
+#define CBX_SIZE_CASES_18(M) CBX_SIZE_CASES_16(M) M(17) M(18)
+
+// Numeric field whose bytes start at buf[addr] (bounds already checked by the caller).
+CBX_HD Val decode_numeric_at(const Field& f, const uint8_t* buf, uint32_t addr) {
+    switch (f.kind) {
+    case CBX_K_BCD:
+        switch (f.size) {
+#define CBX_BCD_CASE(n) case n: return decode_bcd_n<n>(f, load_field<n>(buf, addr));
+            CBX_SIZE_CASES_16(CBX_BCD_CASE)
+#undef CBX_BCD_CASE
+        default: return decode_bcd(f, buf + addr);
+        }
+    case CBX_K_BINARY:
+        switch (f.size) {
+#define CBX_BIN_CASE(n) case n: return decode_binary_n<n>(f, load_field<n>(buf, addr));
+            CBX_SIZE_CASES_16(CBX_BIN_CASE)
+#undef CBX_BIN_CASE
+        default: return decode_binary(f, buf + addr);
+        }
+    case CBX_K_ZONED:
+        switch (f.size) {
+#define CBX_ZON_CASE(n) case n: return decode_zoned_n<n>(f, load_field<n>(buf, addr), buf, addr);
+            CBX_SIZE_CASES_18(CBX_ZON_CASE)
+#undef CBX_ZON_CASE
+        default: return decode_zoned(f, buf + addr);
+        }
+    case CBX_K_FLOAT: return decode_float_n<4>(f, load_field<4>(buf, addr));
+    case CBX_K_DOUBLE: return decode_float_n<8>(f, load_field<8>(buf, addr));
     default: return null_val();
     }
 }

@@ -64,7 +64,7 @@ struct KernelArgs {
     int64_t* tile_sums;              // sizes pass: written; decode pass: exclusive scan (read)
     int64_t n_tiles;
     int32_t max_pitch;         // LDS bytes per row of the widest window
-    int32_t pad;
+    int32_t contig;            // fixed-length: stage each tile's contiguous byte span (all windows at once)
 };
 
 }  // namespace cbx

@@ -127,7 +127,46 @@ __global__ __launch_bounds__(64) void decode_kernel(KernelArgs a) {
             }
         }
 
-        // ---- windows
+        // ---- stage record bytes into the wave's LDS image
+        uint32_t contig_addr = 0;
+        if (a.contig) {
+            // fixed-length tile: one contiguous span [t0b, t0b + nrec * stride), 16-byte chunks,
+            // consecutive lanes on consecutive chunks (1 KiB per wave-instruction)
+            const int64_t t0b = a.base_shift + tile * kWave * (int64_t)a.stride;
+            const int64_t left = a.n_rec - tile * kWave;
+            const int nrec_tile = left < kWave ? (int)left : kWave;
+            const int64_t a0 = t0b & ~(int64_t)15;
+            const int mis = (int)(t0b - a0);
+            const int nch = (int)((t0b + (int64_t)nrec_tile * a.stride - a0 + 15) >> 4);
+            for (int c0 = 0; c0 < nch; c0 += 8 * kWave) {
+                uint4 buf[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int c = c0 + u * kWave + lane;
+                    const int64_t ga = a0 + 16 * (int64_t)c;
+                    buf[u] = make_uint4(0, 0, 0, 0);
+                    if (c < nch) {
+                        if (ga + 16 <= a.data_len) {
+                            buf[u] = *(const uint4*)(a.data + ga);
+                        } else {
+                            uint32_t wv[4] = {0, 0, 0, 0};
+                            for (int j = 0; j < 16; j++)
+                                if (ga + j < a.data_len) wv[j >> 2] |= (uint32_t)a.data[ga + j] << (8 * (j & 3));
+                            buf[u] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int c = c0 + u * kWave + lane;
+                    if (c < nch) *(uint4*)(s_rows + 16 * c) = buf[u];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            contig_addr = (uint32_t)(mis + lane * a.stride + a.start_off);
+        }
         for (int wi = 0; wi < a.n_windows; wi++) {
             const Window& w = a.windows[wi];
             if (sizes && !w.has_strings) continue;
@@ -138,7 +177,7 @@ __global__ __launch_bounds__(64) void decode_kernel(KernelArgs a) {
             const int64_t my_g = base + a.start_off + w.lo;
             const int my_mis = (int)(my_g & 15);
             // stage: flattened (record, chunk) -> lane, 4 chunks in flight per lane
-            const int total = kWave * nch;
+            const int total = a.contig ? 0 : kWave * nch;
             for (int t0 = 0; t0 < total; t0 += 4 * kWave) {
                 uint4 buf[4];
                 int rr[4], kk[4];
@@ -175,11 +214,14 @@ __global__ __launch_bounds__(64) void decode_kernel(KernelArgs a) {
                     }
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-            const uint8_t* my_bytes = my_row + my_mis - w.lo;  // + element offset (relative to decode base)
+            if (!a.contig) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            // LDS byte address of the record's decode base (element offset eo is added per field)
+            const uint32_t rec_addr = a.contig ? contig_addr : (uint32_t)(lane * pitch + my_mis - w.lo);
+            (void)my_row;
             for (int ri = w.run_begin; ri < w.run_end; ri++) {
                 const Run run = a.runs[ri];
                 const Field& f = a.fields[run.field];
@@ -199,11 +241,12 @@ __global__ __launch_bounds__(64) void decode_kernel(KernelArgs a) {
                     }
                     const int o = a.start_off + eo;
                     const int64_t v = (int64_t)s * a.n_rec + rec;
-                    const uint8_t* p = my_bytes + eo;
+                    const uint32_t addr = rec_addr + (uint32_t)eo;
+                    const uint8_t* p = s_rows + addr;
                     if (!is_str) {
                         bool ok = el && o + f.size <= avail;
                         Val x = null_val();
-                        if (ok) x = decode_numeric(f, p);
+                        if (ok) x = decode_numeric_at(f, s_rows, addr);
                         if (active) store_value(col, f.out_type, v, x);
                         uint64_t m = __ballot(x.valid);
                         if (lane == 0) col.validity[(int64_t)s * a.n_tiles + tile] = m;

@@ -14,7 +14,12 @@ extern "C" int cbxh_decode(const cbx_field* cf, const uint8_t* p, int n_avail, c
     const bool is_str = f.out_type == CBX_O_STRING || f.out_type == CBX_O_BINARY;
     if (!is_str) {
         if (n_avail < f.size) return 0;  // Primitive.decodeTypeValue numeric bounds
-        Val v = decode_numeric(f, p);
+        // the kernels' path: width-specialised decoders reading a (padded) byte image
+        uint8_t img[64 + 16] = {0};
+        for (int i = 0; i < f.size && i < 64; i++) img[i + 3] = p[i];
+        Val v = f.size <= 64 ? decode_numeric_at(f, img, 3) : decode_numeric(f, p);
+        Val g = decode_numeric(f, p);   // generic byte-loop decoder must agree
+        if (g.valid != v.valid || (v.valid && (g.lo != v.lo || g.hi != v.hi))) return -1;
         *lo = v.lo;
         *hi = v.hi;
         return v.valid ? 1 : 0;

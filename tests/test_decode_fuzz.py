@@ -169,6 +169,7 @@ def test_field_decoders_match_oracle(fmt, code_page, trim):
             buf = np.frombuffer(b, dtype=np.uint8)
             valid = L.cbxh_decode(ctypes.byref(cf), buf.ctypes.data, len(b), lut.ctypes.data,
                                   ctypes.byref(lo), ctypes.byref(hi), sbuf, ctypes.byref(slen))
+            assert valid != -1, f"{p.name}: width-specialised decoder disagrees with the byte loop on {b.hex()}"
             hl.value = 0
             rc = OL.ora_decode_field(ctypes.byref(node), ctypes.byref(ast.opts), buf.ctypes.data, len(b),
                                      ev.ctypes.data, heap.ctypes.data, len(heap), ctypes.byref(hl))
