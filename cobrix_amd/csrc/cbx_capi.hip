@@ -2,11 +2,14 @@
 //
 // The plan turns the flattened copybook (cbx_field / cbx_array tables produced by the JVM or
 // the Python host from the Cobrix AST) into the device layout the kernels walk:
-//   * per-field constants (10^precision bounds, slot counts),
-//   * LDS windows: greedy packing of every field element [offset, offset + size) sorted by
-//     offset into byte ranges of at most `window_bytes`, then grouped into (field, slot range)
-//     runs so a window's decode loop is wave-uniform,
+//   * per-field constants (decoder variant, 10^precision bounds, slot counts, string sequences),
+//   * two window sets: one window holding every field (contiguous fixed-length staging) and a
+//     greedy packing of every field element [offset, offset + size) into byte ranges of at most
+//     `window_bytes` (windowed staging), each grouped into (field, slot range) runs so a
+//     window's decode loop is wave-uniform,
 //   * the UTF-8 code-page LUT and the segment-redefine keys.
+// Every decode call is asynchronous on the caller's stream: one kernel launch (plus memsets of
+// the look-back workspace); device-side data errors are reported by cbx_plan_check.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,40 +39,62 @@ struct cbx_plan {
     std::vector<cbx_field> hfields;
     std::vector<Field> dfields_h;
     std::vector<cbx_array> harrays;
-    std::vector<Window> hwindows, hswindows;   // decode pass / string sizing pass
-    std::vector<Run> hruns, hsruns;
-    std::vector<int32_t> global_fields;
+    // window sets (contiguous fixed-length staging: one window / windowed staging), each with
+    // its own op tables in window order
+    struct OpSet {
+        std::vector<Window> win;
+        std::vector<NumOp> nops;
+        std::vector<Batch> batches;
+        std::vector<StrOp> sops;
+        std::vector<GenOp> gops;
+        Window* d_win = nullptr;
+        NumOp* d_nops = nullptr;
+        Batch* d_batches = nullptr;
+        StrOp* d_sops = nullptr;
+        GenOp* d_gops = nullptr;
+        int max_str_items = 0;   // string elements in the fullest window
+    } cset, wset;
+    bool contig_ok = true;       // every string element fits the single contiguous window
+    int str_stage = 16;          // LDS payload staging bytes per wave
     cbx_plan_options opts;
     int n_columns = 0;
     int seg_col = -1;
-    int max_pitch = 0;
-    int n_string_cols = 0;
+    int max_pitch = 0;           // widest row of the windowed set
+    int n_seq = 0;               // string sequences (column, slot)
+    std::vector<DeferSeq> hdefer;        // deferral sequences (numeric field, slot)
     std::vector<int32_t> col_is_string;   // per column: 1 if string/binary
     std::vector<int32_t> col_slots;       // per column: slots
+    std::vector<int32_t> col_max_bytes;   // per column: max payload bytes per value
     // device copies
     Field* d_fields = nullptr;
-    Window* d_windows = nullptr;
-    Run* d_runs = nullptr;
-    Window* d_swindows = nullptr;
-    Run* d_sruns = nullptr;
+    DeferSeq* d_defer = nullptr;
+    uint64_t* d_defer_bits = nullptr;
+    int64_t defer_bits_cap = 0;
     cbx_array* d_arrays = nullptr;
-    int32_t* d_global_fields = nullptr;
     cbx_segment_map* d_segmap = nullptr;
     uint32_t* d_lut = nullptr;
     DevColumn* d_cols = nullptr;
-    int64_t* d_seq_base = nullptr;
+    std::vector<DevColumn> h_cols;         // host staging of the per-call column table
     // workspace
-    int64_t* d_tile_sums = nullptr;
-    int64_t tile_sums_cap = 0;
-    int64_t* d_block_sums = nullptr;
-    int64_t block_sums_cap = 0;
+    uint64_t* d_lookback = nullptr;
+    int64_t lookback_cap = 0;
+    int64_t* d_seq_totals = nullptr;
+    uint32_t* d_ticket = nullptr;
+    int32_t* d_status = nullptr;
     int num_cus = 256;
-    int contig_max_bytes = 20 * 1024;   // LDS span budget for contiguous fixed-length staging
-    // profiling
+    // profiling: HIP events around the decode and fixup kernels of every call (no sync)
     bool profiling = false;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    float last_ms[3] = {0, 0, 0};
+    std::vector<hipEvent_t> ev_pool;     // free events
+    struct CallEvents { hipEvent_t e[3]; };
+    std::vector<CallEvents> ev_calls;    // recorded, not yet read
 };
+
+static hipEvent_t take_event(cbx_plan* P) {
+    if (!P->ev_pool.empty()) { hipEvent_t e = P->ev_pool.back(); P->ev_pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
 
 extern "C" int32_t cbx_abi_version(void) { return CBX_ABI_VERSION; }
 extern "C" const char* cbx_last_error(void) { return g_err.c_str(); }
@@ -84,48 +109,157 @@ static int upload(T** dst, const T* src, size_t n) {
     return CBX_OK;
 }
 
-// Greedy LDS window packing: every element [offset, offset + size) sorted by offset, cut into
-// byte ranges of at most wmax, each window's elements regrouped into (field, slot range) runs.
-static void build_windows(cbx_plan* P, int wmax, bool strings_only, std::vector<Window>& wins,
-                          std::vector<Run>& runs) {
-    struct Elem { int lo, hi, field, slot; };
+static bool is_generated(const Field& d) { return d.variant == V_RECORD_ID || d.variant == V_FILE_ID; }
+
+// One element (slot) of a field: static offset and its OCCURS DEPENDING ON conditions.
+struct Elem {
+    int field, slot, eo, size;
+    bool str;
+    int n_odo;
+    int16_t odo_arr[CBX_MAX_DIMS], odo_idx[CBX_MAX_DIMS];
+};
+
+static std::vector<Elem> field_elements(const cbx_plan* P, int fi) {
+    const Field& d = P->dfields_h[fi];
+    std::vector<Elem> out;
+    out.reserve(d.n_slots);
+    for (int s = 0; s < d.n_slots; s++) {
+        Elem e{};
+        e.field = fi; e.slot = s; e.size = d.size; e.str = is_string_out(d.out_type);
+        int eo = d.offset, rem = s;
+        int idx[CBX_MAX_DIMS] = {0, 0, 0, 0};
+        for (int k = d.n_dims - 1; k >= 0; k--) { idx[k] = rem % d.dim_count[k]; rem /= d.dim_count[k]; eo += idx[k] * d.dim_stride[k]; }
+        e.eo = eo;
+        for (int k = 0; k < d.n_dims; k++) {
+            const cbx_array& ar = P->harrays[d.dim_array[k]];
+            if (ar.dependee >= 0) { e.odo_arr[e.n_odo] = (int16_t)d.dim_array[k]; e.odo_idx[e.n_odo] = (int16_t)idx[k]; e.n_odo++; }
+        }
+        out.push_back(e);
+    }
+    return out;
+}
+
+static StrOp make_strop(const Field& d, const Elem& e) {
+    StrOp o{};
+    o.eo = e.eo; o.size = d.size; o.kind = (uint8_t)d.kind; o.trim = (uint8_t)d.trim; o.n_odo = (uint8_t)e.n_odo;
+    o.column = d.column; o.slot = e.slot; o.seq = d.seq + e.slot; o.segment = d.segment;
+    for (int j = 0; j < CBX_MAX_DIMS; j++) { o.odo_arr[j] = e.odo_arr[j]; o.odo_idx[j] = e.odo_idx[j]; }
+    return o;
+}
+
+// Append one window holding `els` (any order) to set S.
+static int out_width(int out_type) {
+    return out_type == CBX_O_I32 || out_type == CBX_O_F32 ? 4 : out_type == CBX_O_DEC128 ? 16 : 8;
+}
+
+static void push_window(cbx_plan* P, cbx_plan::OpSet& S, std::vector<Elem> els, int lo, int hi, bool global,
+                        const std::vector<int>& gen) {
+    // numerics grouped by (variant, output width) so each batch runs a specialised loop;
+    // inside a batch, field then slot order (ascending record offsets, output columns)
+    auto key = [&](const Elem& e) {
+        const Field& d = P->dfields_h[e.field];
+        return (e.n_odo > 0 ? 1024 : 0) + (global ? 0 : d.variant * 32 + out_width(d.out_type));
+    };
+    std::stable_sort(els.begin(), els.end(), [&](const Elem& a, const Elem& b) {
+        const int ka = key(a), kb = key(b);
+        if (ka != kb) return ka < kb;
+        return a.field != b.field ? a.field < b.field : a.slot < b.slot;
+    });
+    Window w{};
+    w.lo = lo; w.hi = hi; w.global = global ? 1 : 0;
+    w.nop_begin = (int)S.nops.size();
+    w.sop_begin = (int)S.sops.size();
+    for (const Elem& e : els) {
+        const Field& d = P->dfields_h[e.field];
+        if (e.str) S.sops.push_back(make_strop(d, e));
+        else S.nops.push_back(make_numop(d, e.slot, e.eo, e.odo_arr, e.odo_idx, e.n_odo));
+    }
+    w.nop_end = (int)S.nops.size();
+    w.sop_end = (int)S.sops.size();
+    w.batch_begin = (int)S.batches.size();
+    for (int i = w.nop_begin; i < w.nop_end;) {
+        const int v = global ? (int)V_GENERIC : S.nops[i].variant, wd = out_width(S.nops[i].out_type);
+        const bool odo = S.nops[i].n_odo > 0;
+        int j = i + 1;
+        while (j < w.nop_end && (global || S.nops[j].variant == v) && out_width(S.nops[j].out_type) == wd &&
+               (S.nops[j].n_odo > 0) == odo)
+            j++;
+        S.batches.push_back(Batch{v, wd, i, j, odo ? 1 : 0, 0});
+        i = j;
+    }
+    w.batch_end = (int)S.batches.size();
+    w.gen_begin = (int)S.gops.size();
+    for (int fi : gen) {
+        const Field& d = P->dfields_h[fi];
+        S.gops.push_back(GenOp{d.kind, d.column, d.out_type, 0});
+    }
+    w.gen_end = (int)S.gops.size();
+    int nch = (hi - lo + 15 + 15) >> 4;
+    w.pitch = global ? 0 : 16 * nch + 4;   // 4 * nch + 1 dwords: odd
+    S.max_str_items = std::max(S.max_str_items, w.sop_end - w.sop_begin);
+    if (global) P->max_pitch = P->max_pitch;  // global windows are never staged
+    else if (&S == &P->wset) P->max_pitch = std::max(P->max_pitch, w.pitch);
+    S.win.push_back(w);
+}
+
+// Contiguous set: one window holding every element + a global window with generated columns.
+static void build_contig(cbx_plan* P) {
     std::vector<Elem> els;
+    std::vector<int> gen;
+    int items = 0;
+    for (int i = 0; i < (int)P->dfields_h.size(); i++) {
+        if (is_generated(P->dfields_h[i])) { gen.push_back(i); continue; }
+        for (const Elem& e : field_elements(P, i)) { items += e.str; els.push_back(e); }
+    }
+    if (items > kMaxStrItems) P->contig_ok = false;
+    if (!els.empty()) push_window(P, P->cset, els, 0, 0, false, {});
+    if (!gen.empty()) push_window(P, P->cset, {}, 0, 0, true, gen);
+}
+
+// Windowed set: every element [eo, eo + size) sorted by offset, cut into byte ranges of at most
+// wmax (and at most kMaxStrItems string elements); oversized fields and generated columns go
+// to the global window.
+static void build_windowed(cbx_plan* P, int wmax) {
+    std::vector<Elem> els, big;
+    std::vector<int> gen;
     for (int i = 0; i < (int)P->dfields_h.size(); i++) {
         const Field& d = P->dfields_h[i];
-        if (d.kind == CBX_K_RECORD_ID || d.kind == CBX_K_FILE_ID || d.size > wmax) continue;
-        if (strings_only && !is_string_out(d.out_type)) continue;
-        for (int s = 0; s < d.n_slots; s++) {
-            int eo = d.offset, rem = s;
-            for (int k = d.n_dims - 1; k >= 0; k--) { int idx = rem % d.dim_count[k]; rem /= d.dim_count[k]; eo += idx * d.dim_stride[k]; }
-            els.push_back(Elem{eo, eo + d.size, i, s});
-        }
+        if (is_generated(d)) { gen.push_back(i); continue; }
+        std::vector<Elem> fe = field_elements(P, i);
+        if (d.size > wmax) big.insert(big.end(), fe.begin(), fe.end());
+        else els.insert(els.end(), fe.begin(), fe.end());
     }
-    std::stable_sort(els.begin(), els.end(), [](const Elem& a, const Elem& b) { return a.lo < b.lo; });
+    std::stable_sort(els.begin(), els.end(), [](const Elem& a, const Elem& b) { return a.eo < b.eo; });
     size_t e0 = 0;
     while (e0 < els.size()) {
-        int lo = els[e0].lo, hi = els[e0].hi;
+        int lo = els[e0].eo, hi = els[e0].eo + els[e0].size;
+        int items = els[e0].str ? 1 : 0;
         size_t e1 = e0 + 1;
-        while (e1 < els.size() && std::max(hi, els[e1].hi) - lo <= wmax) { hi = std::max(hi, els[e1].hi); e1++; }
-        std::vector<Elem> win(els.begin() + e0, els.begin() + e1);
-        std::stable_sort(win.begin(), win.end(), [](const Elem& a, const Elem& b) {
-            return a.field != b.field ? a.field < b.field : a.slot < b.slot;
-        });
-        Window w{};
-        w.lo = lo; w.hi = hi;
-        w.run_begin = (int)runs.size();
-        for (size_t j = 0; j < win.size();) {
-            size_t k = j + 1;
-            while (k < win.size() && win[k].field == win[j].field && win[k].slot == win[k - 1].slot + 1) k++;
-            runs.push_back(Run{win[j].field, win[j].slot, win[k - 1].slot + 1, 0});
-            if (is_string_out(P->dfields_h[win[j].field].out_type)) w.has_strings = 1;
-            j = k;
+        while (e1 < els.size() && std::max(hi, els[e1].eo + els[e1].size) - lo <= wmax && items + (els[e1].str ? 1 : 0) <= kMaxStrItems) {
+            hi = std::max(hi, els[e1].eo + els[e1].size);
+            items += els[e1].str ? 1 : 0;
+            e1++;
         }
-        w.run_end = (int)runs.size();
-        int nch = (hi - lo + 15 + 15) >> 4;
-        w.pitch = 16 * nch + 4;
-        wins.push_back(w);
+        push_window(P, P->wset, std::vector<Elem>(els.begin() + e0, els.begin() + e1), lo, hi, false, {});
         e0 = e1;
     }
+    if (!big.empty() || !gen.empty()) push_window(P, P->wset, big, 0, 0, true, gen);
+}
+
+template <typename T>
+static int upload_vec(T** dst, const std::vector<T>& v) { return upload(dst, v.data(), v.size()); }
+
+static int upload_set(cbx_plan::OpSet& S) {
+    int r;
+    if ((r = upload_vec(&S.d_win, S.win)) || (r = upload_vec(&S.d_nops, S.nops)) || (r = upload_vec(&S.d_batches, S.batches)) ||
+        (r = upload_vec(&S.d_sops, S.sops)) ||
+        (r = upload_vec(&S.d_gops, S.gops)))
+        return r;
+    return CBX_OK;
+}
+
+static void free_set(cbx_plan::OpSet& S) {
+    (void)hipFree(S.d_win); (void)hipFree(S.d_nops); (void)hipFree(S.d_batches); (void)hipFree(S.d_sops); (void)hipFree(S.d_gops);
 }
 
 extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const cbx_array* arrays,
@@ -135,26 +269,41 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     cbx_plan* P = new cbx_plan();
     P->opts = *opts;
     P->n_columns = opts->n_columns;
+    if (P->n_columns <= 0) { delete P; return fail(CBX_E_ARGUMENT, "cbx_plan_create: n_columns must be positive"); }
     P->hfields.assign(fields, fields + n_fields);
     if (n_arrays) P->harrays.assign(arrays, arrays + n_arrays);
     P->col_is_string.assign(P->n_columns, 0);
     P->col_slots.assign(P->n_columns, 1);
+    P->col_max_bytes.assign(P->n_columns, 0);
+
+    // widest UTF-8 expansion of the code page
+    int lut_max = 1;
+    for (int i = 0; i < 256; i++) lut_max = std::max(lut_max, (int)((opts->lut[i] >> 24) & 3));
 
     // ---- fields
     for (int i = 0; i < n_fields; i++) {
         const cbx_field& f = fields[i];
-        if (f.n_dims < 0 || f.n_dims > CBX_MAX_DIMS) { delete P; return fail(CBX_E_ARGUMENT, "field " + std::to_string(i) + ": bad n_dims"); }
+        const std::string fi = "field " + std::to_string(i);
+        if (f.n_dims < 0 || f.n_dims > CBX_MAX_DIMS) { delete P; return fail(CBX_E_ARGUMENT, fi + ": bad n_dims"); }
         for (int k = 0; k < f.n_dims; k++)
             if (f.dim_count[k] <= 0 || f.dim_array[k] < 0 || f.dim_array[k] >= n_arrays) {
-                delete P; return fail(CBX_E_ARGUMENT, "field " + std::to_string(i) + ": bad dimension");
+                delete P; return fail(CBX_E_ARGUMENT, fi + ": bad dimension");
             }
         Field d = make_field(f);
-        if (f.column < 0 || f.column >= P->n_columns) { delete P; return fail(CBX_E_ARGUMENT, "field " + std::to_string(i) + ": bad column"); }
-        bool generated = f.kind == CBX_K_RECORD_ID || f.kind == CBX_K_FILE_ID;
-        if (!generated && f.size <= 0) { delete P; return fail(CBX_E_ARGUMENT, "field " + std::to_string(i) + ": bad size"); }
-        if (f.kind == CBX_K_BINARY && f.size > 16) { delete P; return fail(CBX_E_UNSUPPORTED, "field " + std::to_string(i) + ": binary wider than 16 bytes"); }
+        if (f.column < 0 || f.column >= P->n_columns) { delete P; return fail(CBX_E_ARGUMENT, fi + ": bad column"); }
+        if (!is_generated(d) && (f.size <= 0 || f.offset < 0)) { delete P; return fail(CBX_E_ARGUMENT, fi + ": bad offset/size"); }
+        if (f.kind == CBX_K_BINARY && f.size > 16) { delete P; return fail(CBX_E_UNSUPPORTED, fi + ": binary wider than 16 bytes"); }
         if ((f.out_type == CBX_O_DEC64 || f.out_type == CBX_O_DEC128) && (f.out_precision < 1 || f.out_precision > 38)) {
-            delete P; return fail(CBX_E_UNSUPPORTED, "field " + std::to_string(i) + ": decimal precision outside 1..38");
+            delete P; return fail(CBX_E_UNSUPPORTED, fi + ": decimal precision outside 1..38");
+        }
+        if (d.variant == V_STRING) {
+            if (f.kind == CBX_K_STRING) d.max_utf8 = lut_max;
+            d.seq = P->n_seq;
+            P->n_seq += d.n_slots;
+            P->col_max_bytes[f.column] = f.size * d.max_utf8;
+        } else if (d.variant == V_ZONED16 || d.variant == V_GENERIC) {
+            d.defer = (int)P->hdefer.size();
+            for (int s = 0; s < d.n_slots; s++) P->hdefer.push_back(DeferSeq{i, s});
         }
         P->dfields_h.push_back(d);
         P->col_is_string[f.column] = is_string_out(f.out_type);
@@ -172,20 +321,14 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     P->seg_col = opts->segment_column;
     if (P->seg_col >= P->n_columns) { delete P; return fail(CBX_E_ARGUMENT, "bad segment column"); }
 
-    // ---- LDS windows: all fields (decode pass) and string fields only (sizing pass)
+    // ---- window sets + op tables
     int wmax = opts->window_bytes > 0 ? opts->window_bytes : 256;
     if (wmax > kMaxWindowBytes) wmax = kMaxWindowBytes;
-    for (int i = 0; i < n_fields; i++) {
-        const Field& d = P->dfields_h[i];
-        if (d.kind == CBX_K_RECORD_ID || d.kind == CBX_K_FILE_ID || d.size > wmax) P->global_fields.push_back(i);
-    }
-    build_windows(P, wmax, false, P->hwindows, P->hruns);
-    build_windows(P, wmax, true, P->hswindows, P->hsruns);
-    for (const Window& w : P->hwindows) P->max_pitch = std::max(P->max_pitch, w.pitch);
-    for (const Window& w : P->hswindows) P->max_pitch = std::max(P->max_pitch, w.pitch);
-
-    // ---- string column sequence bases (per column: n_slots * n_tiles entries; filled per call)
-    for (int c = 0; c < P->n_columns; c++) P->n_string_cols += P->col_is_string[c];
+    build_contig(P);
+    build_windowed(P, wmax);
+    for (const Field& d : P->dfields_h)
+        if (d.variant == V_STRING) P->str_stage = std::max(P->str_stage, kWave * d.size * d.max_utf8);
+    P->str_stage = std::min(P->str_stage, kStrStageBytes);
 
     // ---- segment map: keys to UTF-8
     cbx_segment_map sm = opts->segments;
@@ -206,22 +349,21 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
 
     int r;
     if ((r = upload(&P->d_fields, P->dfields_h.data(), P->dfields_h.size())) ||
-        (r = upload(&P->d_windows, P->hwindows.data(), P->hwindows.size())) ||
-        (r = upload(&P->d_runs, P->hruns.data(), P->hruns.size())) ||
-        (r = upload(&P->d_swindows, P->hswindows.data(), P->hswindows.size())) ||
-        (r = upload(&P->d_sruns, P->hsruns.data(), P->hsruns.size())) ||
+        (r = upload_set(P->cset)) || (r = upload_set(P->wset)) ||
         (r = upload(&P->d_arrays, P->harrays.data(), P->harrays.size())) ||
-        (r = upload(&P->d_global_fields, P->global_fields.data(), P->global_fields.size())) ||
+        (r = upload(&P->d_defer, P->hdefer.data(), P->hdefer.size())) ||
         (r = upload(&P->d_lut, opts->lut, 256))) {
         cbx_plan_destroy(P);
         return r;
     }
     if (opts->has_segments && (r = upload(&P->d_segmap, &sm, 1))) { cbx_plan_destroy(P); return r; }
-    if ((r = upload(&P->d_cols, (DevColumn*)nullptr, 0)) != CBX_OK) { cbx_plan_destroy(P); return r; }
-    (void)hipFree(P->d_cols);
-    P->d_cols = nullptr;
-    HIP_CHECK(hipMalloc((void**)&P->d_cols, sizeof(DevColumn) * std::max(1, P->n_columns)));
-    HIP_CHECK(hipMalloc((void**)&P->d_seq_base, sizeof(int64_t) * std::max(1, P->n_columns)));
+    if (hipMalloc((void**)&P->d_cols, sizeof(DevColumn) * P->n_columns) != hipSuccess ||
+        hipMalloc((void**)&P->d_seq_totals, sizeof(int64_t) * std::max(1, P->n_seq)) != hipSuccess ||
+        hipMalloc((void**)&P->d_ticket, 64) != hipSuccess || hipMalloc((void**)&P->d_status, 64) != hipSuccess ||
+        hipMemset(P->d_status, 0, 64) != hipSuccess) {
+        cbx_plan_destroy(P);
+        return fail(CBX_E_HIP, "cbx_plan_create: device allocation failed");
+    }
     int dev = 0;
     (void)hipGetDevice(&dev);
     hipDeviceProp_t prop;
@@ -232,189 +374,211 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
 
 extern "C" void cbx_plan_destroy(cbx_plan* P) {
     if (!P) return;
-    (void)hipFree(P->d_fields); (void)hipFree(P->d_windows); (void)hipFree(P->d_runs);
-    (void)hipFree(P->d_swindows); (void)hipFree(P->d_sruns); (void)hipFree(P->d_arrays);
-    (void)hipFree(P->d_global_fields); (void)hipFree(P->d_segmap); (void)hipFree(P->d_lut); (void)hipFree(P->d_cols);
-    (void)hipFree(P->d_seq_base); (void)hipFree(P->d_tile_sums); (void)hipFree(P->d_block_sums);
-    for (auto& e : P->ev) if (e) (void)hipEventDestroy(e);
+    (void)hipFree(P->d_fields); (void)hipFree(P->d_defer); (void)hipFree(P->d_defer_bits);
+    free_set(P->cset); free_set(P->wset); (void)hipFree(P->d_arrays);
+    (void)hipFree(P->d_segmap); (void)hipFree(P->d_lut); (void)hipFree(P->d_cols);
+    (void)hipFree(P->d_lookback); (void)hipFree(P->d_seq_totals); (void)hipFree(P->d_ticket); (void)hipFree(P->d_status);
+    for (auto& e : P->ev_pool) (void)hipEventDestroy(e);
+    for (auto& c : P->ev_calls) for (auto& e : c.e) if (e) (void)hipEventDestroy(e);
     delete P;
 }
 
-// Column pointers and string-sequence bases for one call.
-static int prepare_call(cbx_plan* P, int64_t n_rec, const cbx_column* columns, hipStream_t st,
-                        int64_t* n_seq_out) {
-    const int64_t n_tiles = (n_rec + kWave - 1) / kWave;
-    std::vector<DevColumn> cols(P->n_columns);
-    std::vector<int64_t> seq(P->n_columns, -1);
-    int64_t n_seq = 0;
-    for (int c = 0; c < P->n_columns; c++) {
-        cols[c].values = columns ? columns[c].values : nullptr;
-        cols[c].validity = columns ? columns[c].validity : nullptr;
-        cols[c].offsets = columns ? columns[c].offsets : nullptr;
-        cols[c].data = columns ? columns[c].data : nullptr;
-        if (P->col_is_string[c]) {
-            seq[c] = n_seq;
-            n_seq += (int64_t)P->col_slots[c] * n_tiles;
-        }
-    }
-    HIP_CHECK(hipMemcpyAsync(P->d_cols, cols.data(), sizeof(DevColumn) * P->n_columns, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipMemcpyAsync(P->d_seq_base, seq.data(), sizeof(int64_t) * P->n_columns, hipMemcpyHostToDevice, st));
-    if (n_seq > P->tile_sums_cap) {
-        HIP_CHECK(hipStreamSynchronize(st));
-        (void)hipFree(P->d_tile_sums);
-        HIP_CHECK(hipMalloc((void**)&P->d_tile_sums, sizeof(int64_t) * (n_seq + 1)));
-        P->tile_sums_cap = n_seq;
-        int64_t nb = (n_seq + kScanTile - 1) / kScanTile + 1;
-        (void)hipFree(P->d_block_sums);
-        HIP_CHECK(hipMalloc((void**)&P->d_block_sums, sizeof(int64_t) * nb));
-        P->block_sums_cap = nb;
-    }
-    *n_seq_out = n_seq;
+extern "C" int cbx_string_bound(const cbx_plan* P, int64_t n_rec, int64_t* out_bytes) {
+    if (!P || n_rec < 0 || !out_bytes) return fail(CBX_E_ARGUMENT, "cbx_string_bound: invalid arguments");
+    for (int c = 0; c < P->n_columns; c++) out_bytes[c] = P->col_is_string[c] ? n_rec * (int64_t)P->col_max_bytes[c] : 0;
     return CBX_OK;
 }
 
-static KernelArgs make_args(cbx_plan* P, const uint8_t* data, int64_t data_len, const int64_t* rec_off,
-                            const int32_t* rec_len, int64_t n_rec, int32_t stride, int32_t start_off,
-                            int64_t first_record_id, int mode) {
+struct CallShape {
+    const uint8_t* data; int64_t data_len; const int64_t* rec_off; const int32_t* rec_len;
+    int64_t n_rec; int32_t stride; int32_t start_off; int64_t first_record_id;
+};
+
+static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, int mode, hipStream_t st) {
+    const int64_t n_tiles = (c.n_rec + kWave - 1) / kWave;
     KernelArgs a{};
-    uintptr_t addr = (uintptr_t)data;
+    uintptr_t addr = (uintptr_t)c.data;
     a.base_shift = (int64_t)(addr & 15);
     a.data = (const uint8_t*)(addr & ~(uintptr_t)15);
-    a.data_len = data_len + a.base_shift;
-    a.rec_off = rec_off;
-    a.rec_len = rec_len;
-    a.n_rec = n_rec;
-    a.stride = stride;
-    a.start_off = start_off;
-    a.first_record_id = first_record_id;
+    a.data_len = c.data_len + a.base_shift;
+    a.rec_off = c.rec_off;
+    a.rec_len = c.rec_len;
+    a.n_rec = c.n_rec;
+    a.n_tiles = n_tiles;
+    a.stride = c.stride;
+    a.start_off = c.start_off;
+    a.first_record_id = c.first_record_id;
     a.file_id = P->opts.file_id;
     a.mode = mode;
-    a.fields = P->d_fields;
-    a.windows = mode == 1 ? P->d_swindows : P->d_windows;
-    a.n_windows = (int)(mode == 1 ? P->hswindows.size() : P->hwindows.size());
-    a.runs = mode == 1 ? P->d_sruns : P->d_runs;
-    a.arrays = P->d_arrays;
+    // staging mode
+    const int sdw = c.stride / 4;
+    const bool contig = !c.rec_off && P->contig_ok && c.stride > 0 && c.stride % 4 == 0 && a.base_shift % 4 == 0 &&
+                        (3 + kWave * sdw + 3) / 4 <= 16 * kWave;
+    a.contig = contig ? 1 : 0;
+    const cbx_plan::OpSet& S = contig ? P->cset : P->wset;
+    if (contig) {
+        a.stride_dw = sdw;
+        a.cpitch = 4 * ((sdw & 1) ? sdw : sdw + 1);
+        a.inv_stride_dw = 1.0f / (float)sdw;
+        a.lds_rows = kGuard + kWave * a.cpitch + 16 + kGuard;
+    } else {
+        a.lds_rows = kGuard + kWave * std::max(P->max_pitch, 16) + kGuard;
+    }
+    a.windows = (const CBX_CONST Window*)S.d_win;
+    a.n_windows = (int)S.win.size();
+    a.nops = (const CBX_CONST NumOp*)S.d_nops;
+    a.batches = (const CBX_CONST Batch*)S.d_batches;
+    a.sops = (const CBX_CONST StrOp*)S.d_sops;
+    a.gops = (const CBX_CONST GenOp*)S.d_gops;
+    a.lds_rows = (a.lds_rows + 15) & ~15;
+    a.lds_counts = ((int)P->harrays.size() * kWave * 4 + 15) & ~15;
+    a.lds_agg = (S.max_str_items * 4 + 15) & ~15;
+    a.str_stage = S.max_str_items > 0 ? P->str_stage : 0;
+    a.lds_wave = a.lds_rows + a.lds_counts + kWave * 8 + a.lds_agg + a.str_stage + 16;
+    a.lds_wave = (a.lds_wave + 15) & ~15;
+    a.fields = (const CBX_CONST Field*)P->d_fields;
+    a.arrays = (const CBX_CONST cbx_array*)P->d_arrays;
     a.n_arrays = (int)P->harrays.size();
     a.seg_col = P->seg_col;
-    a.segmap = P->opts.has_segments ? P->d_segmap : nullptr;
+    a.segmap = P->opts.has_segments ? (const CBX_CONST cbx_segment_map*)P->d_segmap : nullptr;
     a.lut = P->d_lut;
-    a.cols = P->d_cols;
-    a.str_seq_base = P->d_seq_base;
-    a.tile_sums = P->d_tile_sums;
-    a.n_tiles = (n_rec + kWave - 1) / kWave;
-    a.max_pitch = P->max_pitch;
-    return a;
-}
+    a.cols = (const CBX_CONST DevColumn*)P->d_cols;
+    a.n_seq = P->n_seq;
+    a.seq_totals = P->d_seq_totals;
+    a.ticket = P->d_ticket;
+    a.status = P->d_status;
+    if (n_tiles == 0) return CBX_OK;
 
-static int launch_decode(cbx_plan* P, KernelArgs a, hipStream_t st) {
-    if (a.n_tiles == 0) return CBX_OK;
-    // fixed-length records short enough to stage a whole 64-record span: contiguous mode
-    size_t rows = (size_t)kWave * P->max_pitch;
-    if (a.mode == 0 && !a.rec_off && a.stride > 0 && (size_t)kWave * a.stride + 32 <= (size_t)P->contig_max_bytes) {
-        a.contig = 1;
-        rows = std::max(rows, (size_t)kWave * a.stride + 32);
-    }
-    size_t lds = 1024 + ((a.n_arrays * kWave * 4 + 15) & ~15) + rows + 16;
-    if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "LDS window too large");
-    // one wave per block; enough blocks to cover every CU several times, grid-stride the rest
-    int per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / std::max<size_t>(lds, 1)));
-    int64_t grid = std::min<int64_t>(a.n_tiles, (int64_t)P->num_cus * per_cu * 2);
-    if (a.n_windows > 0 || a.n_arrays > 0 || a.seg_col >= 0)
-        hipLaunchKernelGGL(decode_kernel, dim3((unsigned)grid), dim3(kWave), lds, st, a);
-    if (!P->global_fields.empty())
-        hipLaunchKernelGGL(decode_global_kernel, dim3((unsigned)grid), dim3(kWave), 1024, st, a,
-                           (const int32_t*)P->d_global_fields, (int32_t)P->global_fields.size());
-    HIP_CHECK(hipGetLastError());
-    return CBX_OK;
-}
-
-static int run_scan(cbx_plan* P, int64_t n, hipStream_t st) {
-    if (n <= 0) return CBX_OK;
-    int64_t nb = (n + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, P->d_tile_sums, n, P->d_block_sums);
-    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, P->d_block_sums, nb);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, P->d_tile_sums, n, P->d_block_sums);
-    HIP_CHECK(hipGetLastError());
-    return CBX_OK;
-}
-
-static int decode_common(cbx_plan* P, const uint8_t* data, int64_t data_len, const int64_t* rec_off,
-                         const int32_t* rec_len, int64_t n_rec, int32_t stride, int32_t start_off,
-                         int64_t first_record_id, cbx_column* columns, int64_t* sizes_only, hipStream_t st) {
-    if (!P || !data || n_rec < 0 || start_off < 0) return fail(CBX_E_ARGUMENT, "invalid decode arguments");
-    if (!sizes_only && !columns) return fail(CBX_E_ARGUMENT, "columns required");
-    int64_t n_seq = 0;
-    int r = prepare_call(P, n_rec, columns, st, &n_seq);
-    if (r) return r;
-    const int64_t n_tiles = (n_rec + kWave - 1) / kWave;
-    const bool prof = P->profiling && !sizes_only;
-    if (prof) HIP_CHECK(hipEventRecord(P->ev[0], st));
-    if (n_seq > 0) {
-        // pass 1: per-(column, slot, tile) UTF-8 totals, then one device-wide exclusive scan
-        KernelArgs a = make_args(P, data, data_len, rec_off, rec_len, n_rec, stride, start_off, first_record_id, 1);
-        if ((r = launch_decode(P, a, st))) return r;
-        if (prof) HIP_CHECK(hipEventRecord(P->ev[1], st));
-        HIP_CHECK(hipMemsetAsync(P->d_tile_sums + n_seq, 0, sizeof(int64_t), st));
-        if ((r = run_scan(P, n_seq + 1, st))) return r;
-        // column payload sizes = scan[next column start] - scan[column start]
-        std::vector<int64_t> idx;
-        int64_t acc = 0;
-        for (int c = 0; c < P->n_columns; c++)
-            if (P->col_is_string[c]) { idx.push_back(acc); acc += (int64_t)P->col_slots[c] * n_tiles; }
-        idx.push_back(n_seq);
-        std::vector<int64_t> vals(idx.size());
-        for (size_t k = 0; k < idx.size(); k++)
-            HIP_CHECK(hipMemcpyAsync(&vals[k], P->d_tile_sums + idx[k], sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        size_t k = 0;
-        for (int c = 0; c < P->n_columns; c++) {
-            if (!P->col_is_string[c]) {
-                if (sizes_only) sizes_only[c] = 0;
-                continue;
-            }
-            int64_t tot = vals[k + 1] - vals[k];
-            k++;
-            if (sizes_only) { sizes_only[c] = tot; continue; }
-            if (columns[c].data_capacity < tot)
-                return fail(CBX_E_CAPACITY, "column " + std::to_string(c) + " needs " + std::to_string(tot) + " payload bytes");
-            columns[c].data_size = tot;
+    // column table: stream-ordered upload from pageable host memory (staged by the runtime)
+    if (mode == 0) {
+        P->h_cols.resize(P->n_columns);
+        for (int i = 0; i < P->n_columns; i++) {
+            DevColumn d{};
+            d.values = columns[i].values;
+            d.validity = columns[i].validity;
+            d.offsets = columns[i].offsets;
+            d.data = columns[i].data;
+            d.capacity = columns[i].data_capacity;
+            d.sizes = columns[i].data_sizes;
+            P->h_cols[i] = d;
         }
-        if (sizes_only) return CBX_OK;
-    } else if (sizes_only) {
-        for (int c = 0; c < P->n_columns; c++) sizes_only[c] = 0;
+        HIP_CHECK(hipMemcpyAsync(P->d_cols, P->h_cols.data(), sizeof(DevColumn) * P->n_columns, hipMemcpyHostToDevice, st));
+    }
+    // string workspace
+    if (P->n_seq > 0) {
+        if (mode == 0) {
+            const int64_t need = n_tiles * (int64_t)P->n_seq;
+            if (need > P->lookback_cap) {
+                HIP_CHECK(hipStreamSynchronize(st));
+                (void)hipFree(P->d_lookback);
+                P->d_lookback = nullptr;
+                HIP_CHECK(hipMalloc((void**)&P->d_lookback, sizeof(uint64_t) * need));
+                P->lookback_cap = need;
+            }
+            HIP_CHECK(hipMemsetAsync(P->d_lookback, 0, sizeof(uint64_t) * need, st));
+            HIP_CHECK(hipMemsetAsync(P->d_ticket, 0, sizeof(uint32_t), st));
+        } else {
+            HIP_CHECK(hipMemsetAsync(P->d_seq_totals, 0, sizeof(int64_t) * P->n_seq, st));
+        }
+    }
+    a.lookback = P->d_lookback;
+    const int n_defer = (int)P->hdefer.size();
+    if (mode == 0 && n_defer > 0) {
+        const int64_t need = n_tiles * (int64_t)n_defer;
+        if (need > P->defer_bits_cap) {
+            HIP_CHECK(hipStreamSynchronize(st));
+            (void)hipFree(P->d_defer_bits);
+            P->d_defer_bits = nullptr;
+            HIP_CHECK(hipMalloc((void**)&P->d_defer_bits, sizeof(uint64_t) * need));
+            P->defer_bits_cap = need;
+        }
+    }
+    a.defer_bits = P->d_defer_bits;
+    const size_t lds = 1024 + (size_t)kWavesPerBlock * a.lds_wave;
+    if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
+    const int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / lds));
+    const int64_t blocks_needed = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t grid = std::min<int64_t>(blocks_needed, (int64_t)P->num_cus * blocks_per_cu);
+    const bool prof = P->profiling && mode == 0;
+    cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};
+    if (prof) {
+        for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
+        HIP_CHECK(hipEventRecord(ce.e[0], st));
+    }
+    hipLaunchKernelGGL(decode_kernel, dim3((unsigned)grid), dim3(kWave * kWavesPerBlock), lds, st, a);
+    HIP_CHECK(hipGetLastError());
+    if (prof) HIP_CHECK(hipEventRecord(ce.e[1], st));
+    if (mode == 0 && n_defer > 0) {
+        const int64_t words = n_tiles * (int64_t)n_defer;
+        hipLaunchKernelGGL(fixup_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, a,
+                           (const CBX_CONST DeferSeq*)P->d_defer, n_defer);
+        HIP_CHECK(hipGetLastError());
+    }
+    if (prof) {
+        HIP_CHECK(hipEventRecord(ce.e[2], st));
+        P->ev_calls.push_back(ce);
+    }
+    return CBX_OK;
+}
+
+static int decode_common(cbx_plan* P, const CallShape& c, cbx_column* columns, int64_t* sizes_only, hipStream_t st) {
+    if (!P || !c.data || c.n_rec < 0 || c.start_off < 0) return fail(CBX_E_ARGUMENT, "invalid decode arguments");
+    if (!sizes_only && !columns) return fail(CBX_E_ARGUMENT, "columns required");
+    if (sizes_only) {
+        for (int i = 0; i < P->n_columns; i++) sizes_only[i] = 0;
+        if (P->n_seq == 0 || c.n_rec == 0) return CBX_OK;
+        int r = launch(P, c, nullptr, 1, st);
+        if (r) return r;
+        std::vector<int64_t> tot(P->n_seq);
+        HIP_CHECK(hipMemcpyAsync(tot.data(), P->d_seq_totals, sizeof(int64_t) * P->n_seq, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        for (const Field& d : P->dfields_h)
+            if (d.seq >= 0)
+                for (int s = 0; s < d.n_slots; s++) sizes_only[d.column] = std::max(sizes_only[d.column], tot[d.seq + s]);
         return CBX_OK;
     }
-    // pass 2: decode every column
-    KernelArgs a = make_args(P, data, data_len, rec_off, rec_len, n_rec, stride, start_off, first_record_id, 0);
-    if (prof) {
-        if (n_seq <= 0) HIP_CHECK(hipEventRecord(P->ev[1], st));
-        HIP_CHECK(hipEventRecord(P->ev[2], st));
-    }
-    r = launch_decode(P, a, st);
-    if (r) return r;
-    if (prof) {
-        HIP_CHECK(hipEventRecord(P->ev[3], st));
-        HIP_CHECK(hipEventSynchronize(P->ev[3]));
-        HIP_CHECK(hipEventElapsedTime(&P->last_ms[0], P->ev[0], P->ev[1]));
-        HIP_CHECK(hipEventElapsedTime(&P->last_ms[1], P->ev[1], P->ev[2]));
-        HIP_CHECK(hipEventElapsedTime(&P->last_ms[2], P->ev[2], P->ev[3]));
+    for (int i = 0; i < P->n_columns; i++)
+        if (P->col_is_string[i] && c.n_rec > 0 && (!columns[i].offsets || (!columns[i].data && columns[i].data_capacity > 0)))
+            return fail(CBX_E_ARGUMENT, "column " + std::to_string(i) + ": string buffers required");
+    return launch(P, c, columns, 0, st);
+}
+
+extern "C" int cbx_plan_check(cbx_plan* P, void* stream) {
+    if (!P) return fail(CBX_E_ARGUMENT, "null plan");
+    hipStream_t st = (hipStream_t)stream;
+    int32_t status = 0;
+    HIP_CHECK(hipMemcpyAsync(&status, P->d_status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (status != 0) {
+        HIP_CHECK(hipMemset(P->d_status, 0, sizeof(int32_t)));
+        return fail(CBX_E_CAPACITY, "a string column's payload exceeded its data_capacity (size it with cbx_string_bound or cbx_string_sizes_*)");
     }
     return CBX_OK;
 }
 
 extern "C" int cbx_plan_set_profiling(cbx_plan* P, int32_t enable) {
     if (!P) return fail(CBX_E_ARGUMENT, "null plan");
-    if (enable && !P->ev[0])
-        for (auto& e : P->ev) HIP_CHECK(hipEventCreate(&e));
     P->profiling = enable != 0;
     return CBX_OK;
 }
 
-extern "C" int cbx_plan_last_kernel_ms(const cbx_plan* P, float* sizes_ms, float* scan_ms, float* decode_ms) {
-    if (!P) return fail(CBX_E_ARGUMENT, "null plan");
-    if (sizes_ms) *sizes_ms = P->last_ms[0];
-    if (scan_ms) *scan_ms = P->last_ms[1];
-    if (decode_ms) *decode_ms = P->last_ms[2];
+extern "C" int cbx_plan_kernel_times(cbx_plan* P, float* decode_ms, float* fixup_ms, int32_t max_calls, int32_t* n_calls) {
+    if (!P || !n_calls || max_calls < 0) return fail(CBX_E_ARGUMENT, "cbx_plan_kernel_times: invalid arguments");
+    int n = 0;
+    for (auto& c : P->ev_calls) {
+        HIP_CHECK(hipEventSynchronize(c.e[2]));
+        if (n < max_calls) {
+            float d = 0, f = 0;
+            HIP_CHECK(hipEventElapsedTime(&d, c.e[0], c.e[1]));
+            HIP_CHECK(hipEventElapsedTime(&f, c.e[1], c.e[2]));
+            if (decode_ms) decode_ms[n] = d;
+            if (fixup_ms) fixup_ms[n] = f;
+            n++;
+        }
+        for (auto& e : c.e) P->ev_pool.push_back(e);
+    }
+    P->ev_calls.clear();
+    *n_calls = n;
     return CBX_OK;
 }
 
@@ -422,31 +586,31 @@ extern "C" int cbx_string_sizes_fixed(cbx_plan* P, const uint8_t* d_records, int
                                       int32_t start_offset, int64_t* out_sizes, void* stream) {
     if (!out_sizes) return fail(CBX_E_ARGUMENT, "out_sizes required");
     if (rec_stride <= 0) return fail(CBX_E_ARGUMENT, "record stride must be positive");
-    return decode_common(P, d_records, n_rec * (int64_t)rec_stride, nullptr, nullptr, n_rec, rec_stride, start_offset,
-                         0, nullptr, out_sizes, (hipStream_t)stream);
+    CallShape c{d_records, n_rec * (int64_t)rec_stride, nullptr, nullptr, n_rec, rec_stride, start_offset, 0};
+    return decode_common(P, c, nullptr, out_sizes, (hipStream_t)stream);
 }
 
 extern "C" int cbx_decode_fixed(cbx_plan* P, const uint8_t* d_records, int64_t n_rec, int32_t rec_stride,
                                 int32_t start_offset, int64_t first_record_id, cbx_column* columns, void* stream) {
     if (rec_stride <= 0) return fail(CBX_E_ARGUMENT, "record stride must be positive");
-    return decode_common(P, d_records, n_rec * (int64_t)rec_stride, nullptr, nullptr, n_rec, rec_stride, start_offset,
-                         first_record_id, columns, nullptr, (hipStream_t)stream);
+    CallShape c{d_records, n_rec * (int64_t)rec_stride, nullptr, nullptr, n_rec, rec_stride, start_offset, first_record_id};
+    return decode_common(P, c, columns, nullptr, (hipStream_t)stream);
 }
 
 extern "C" int cbx_decode_var(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
                               const int32_t* d_rec_len, int64_t n_rec, int32_t start_offset, int64_t first_record_id,
                               cbx_column* columns, void* stream) {
     if (!d_rec_off || !d_rec_len || n_bytes < 0) return fail(CBX_E_ARGUMENT, "record offsets/lengths required");
-    return decode_common(P, d_data, n_bytes, d_rec_off, d_rec_len, n_rec, 0, start_offset, first_record_id,
-                         columns, nullptr, (hipStream_t)stream);
+    CallShape c{d_data, n_bytes, d_rec_off, d_rec_len, n_rec, 0, start_offset, first_record_id};
+    return decode_common(P, c, columns, nullptr, (hipStream_t)stream);
 }
 
 extern "C" int cbx_string_sizes_var(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
                                     const int32_t* d_rec_len, int64_t n_rec, int32_t start_offset,
                                     int64_t* out_sizes, void* stream) {
     if (!d_rec_off || !d_rec_len || !out_sizes || n_bytes < 0) return fail(CBX_E_ARGUMENT, "invalid arguments");
-    return decode_common(P, d_data, n_bytes, d_rec_off, d_rec_len, n_rec, 0, start_offset, 0, nullptr,
-                         out_sizes, (hipStream_t)stream);
+    CallShape c{d_data, n_bytes, d_rec_off, d_rec_len, n_rec, 0, start_offset, 0};
+    return decode_common(P, c, nullptr, out_sizes, (hipStream_t)stream);
 }
 
 extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,

@@ -11,6 +11,14 @@
 //   decimal conversion -> Spark Decimal.toPrecision (HALF_UP, null on overflow)
 // (paths under /root/reference/cobol-parser/src/main/scala/za/co/absa/cobrix/cobol/parser/decoders/)
 //
+// Two layers:
+//   * generic byte-loop decoders (decode_bcd / decode_binary / decode_zoned / decode_float /
+//     decode_double): any width, any flag combination -- the specification the fast paths are
+//     fuzzed against;
+//   * runtime-width SWAR fast paths over an LDS record image (decode_value): a field ending at
+//     image byte `end` is read as the 8 or 16 bytes before `end` (three dword reads + alignbyte
+//     per 8 bytes, whatever the alignment) and decoded with packed-nibble / packed-byte arithmetic.
+//     One code path per (kind, width class) instead of one per width keeps the kernel small.
 // All functions are __host__ __device__ so tests/native can fuzz the exact device arithmetic
 // against the oracle on a CPU; the product only runs them inside the HIP kernels.
 #pragma once
@@ -20,6 +28,7 @@
 #include "cobrix_hip.h"
 
 #define CBX_HD __host__ __device__ __forceinline__
+#define CBX_HD_NOINLINE __host__ __device__ __attribute__((noinline))
 
 namespace cbx {
 
@@ -106,6 +115,20 @@ CBX_HD int u128_ndigits(U128 a) {
 // ------------------------------------------------------------------------------------------
 // Device-side field descriptor (derived from cbx_field by the plan)
 // ------------------------------------------------------------------------------------------
+// decoder variant per field (chosen by the plan from kind / width / flags)
+enum Variant : int32_t {
+    V_GENERIC = 0,   // byte-loop decoder (wide or unusual numerics): deferred to the fixup kernel
+    V_BCD8 = 1,      // COMP-3, 1..8 bytes (<= 15 digits): one 64-bit packed-nibble conversion
+    V_BCD16 = 2,     // COMP-3, 9..16 bytes (<= 31 digits): two conversions, 128-bit result
+    V_BIN8 = 3,      // COMP/COMP-4/5/9 of 1, 2, 4 or 8 bytes (integral, or decimal without P-scaling)
+    V_ZONED16 = 4,   // DISPLAY, <= 16 bytes: SWAR fast path (F-zone digits, last-byte overpunch);
+                     // any other form (spaces, separate signs, dots, bad bytes) is deferred
+    V_FP = 5,        // COMP-1 / COMP-2 (IBM hex or IEEE-754, either byte order)
+    V_STRING = 6,    // EBCDIC / ASCII / HEX / RAW strings
+    V_RECORD_ID = 7, // generated Record_Id
+    V_FILE_ID = 8    // generated File_Id
+};
+
 struct Field {
     int32_t kind, out_type, offset, size;
     int32_t precision, scale, sf, out_p, out_s;
@@ -115,8 +138,15 @@ struct Field {
     int32_t dim_array[CBX_MAX_DIMS];
     int32_t segment, column;
     int32_t n_slots;        // product of dim_count
-    int32_t window;         // LDS window the field (all its elements) is staged in, -1 = global
-    uint64_t lim_lo, lim_hi;  // 10^out_p (decimal overflow bound)
+    int32_t variant;        // Variant
+    int32_t seq;            // strings: index of the (column, slot 0) string sequence, -1 otherwise
+    int32_t max_utf8;       // strings: max output bytes per input byte (LUT width, HEX 2)
+    int32_t defer;          // numerics that may need the byte-loop decoder: first deferral sequence, else -1
+    int32_t fin;            // fast paths: 0 two's-complement integral, 1 decimal (x 10^E after a bound check)
+    int32_t plus_null;      // zoned fast path: a '+' overpunch yields null (addDecimalPoint quirk)
+    int32_t e_mul;          // fast paths: E = Spark scale - raw scale of the decoded digits (0..19)
+    int32_t e_lim;          // fast paths: magnitude bound exponent out_p - E (0..38)
+    uint64_t lim_lo, lim_hi;  // 10^out_p (decimal overflow bound, byte-loop decoders)
 };
 
 // cbx_field (ABI) -> Field (device), host side
@@ -135,7 +165,57 @@ inline Field make_field(const cbx_field& f) {
     unsigned __int128 lim = 1;
     for (int i = 0; i < f.out_precision; i++) lim *= 10;
     d.lim_lo = (uint64_t)lim; d.lim_hi = (uint64_t)(lim >> 64);
-    d.window = -1;
+    d.seq = -1;
+    d.defer = -1;
+    d.max_utf8 = 1;
+    // Fast-path finish: a raw digit magnitude M at raw scale r becomes M * 10^E at the Spark
+    // scale (E = out_s - r) after the bound check M < 10^(out_p - E); E < 0 would need HALF_UP
+    // rounding, so such fields stay on the byte-loop decoder (V_GENERIC, deferred).
+    auto fast_dec = [&](int r) -> bool {
+        const int E = f.out_scale - r;
+        if (E < 0 || E > 19 || f.out_precision - E < 0 || f.out_precision - E > 38) return false;
+        d.fin = 1;
+        d.e_mul = E;
+        d.e_lim = f.out_precision - E;
+        return true;
+    };
+    const bool integral = (f.flags & CBX_F_INTEGRAL) != 0;
+    switch (f.kind) {
+    case CBX_K_BCD:
+        d.variant = f.size <= 8 ? V_BCD8 : (f.size <= 16 ? V_BCD16 : V_GENERIC);
+        if (d.variant != V_GENERIC) {
+            if (integral && f.precision <= 18) d.fin = 0;
+            else if (!fast_dec(integral ? 0 : f.scale_factor == 0 ? f.scale
+                               : f.scale_factor > 0 ? -f.scale_factor : -f.scale_factor + 2 * f.size - 1))
+                d.variant = V_GENERIC;
+        }
+        break;
+    case CBX_K_BINARY:
+        d.variant = (f.size == 1 || f.size == 2 || f.size == 4 || f.size == 8) && (integral || f.scale_factor >= 0) ? V_BIN8 : V_GENERIC;
+        if (d.variant == V_BIN8) {
+            if (integral) d.fin = 0;
+            else if (!fast_dec(f.scale_factor == 0 ? f.scale : -f.scale_factor)) d.variant = V_GENERIC;
+        }
+        break;
+    case CBX_K_ZONED:
+        d.variant = f.size <= 16 && !(f.flags & CBX_F_EXPLICIT_DOT) &&
+                    (!integral || f.size <= (f.precision <= 9 ? 9 : 18)) ? V_ZONED16 : V_GENERIC;
+        if (d.variant == V_ZONED16) {
+            if (integral) d.fin = 0;
+            else if (!fast_dec(f.scale_factor == 0 ? f.scale : f.scale_factor > 0 ? -f.scale_factor : -f.scale_factor + f.size))
+                d.variant = V_GENERIC;
+            d.plus_null = !integral && f.scale_factor == 0 && f.size < f.scale;
+        }
+        break;
+    case CBX_K_FLOAT: case CBX_K_DOUBLE: d.variant = V_FP; break;
+    case CBX_K_STRING: case CBX_K_STRING_ASCII: case CBX_K_HEX: case CBX_K_RAW:
+        d.variant = V_STRING;
+        d.max_utf8 = f.kind == CBX_K_HEX ? 2 : 1;
+        break;
+    case CBX_K_RECORD_ID: d.variant = V_RECORD_ID; break;
+    case CBX_K_FILE_ID: d.variant = V_FILE_ID; break;
+    default: d.variant = V_GENERIC; break;
+    }
     return d;
 }
 
@@ -410,16 +490,10 @@ CBX_HD Val decode_numeric(const Field& f, const uint8_t* p) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Width-specialised decoders over field bytes held in registers (the hot path).
-// FB<N>: byte j of the field sits in bits 8*(j&3) of w[j>>2]; loaded from the LDS image with
-// dword reads + alignbyte, so a field costs ceil((N+6)/4) ds_read_b32 whatever its alignment.
+// Runtime-width fast paths over a record image.  `img` is an LDS (or host) byte image with at
+// least 16 readable guard bytes before and 8 after every field; a field occupies
+// img[addr, addr + size).  Callers have already applied the Primitive.decodeTypeValue bounds rule.
 // ------------------------------------------------------------------------------------------
-template <int N>
-struct FB {
-    uint32_t w[(N + 3) / 4];
-    CBX_HD uint32_t byte(int j) const { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; }
-};
-
 CBX_HD uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
 #if defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
@@ -428,29 +502,23 @@ CBX_HD uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
 #endif
 }
 
-// buf: LDS image (or any byte buffer) with >= 8 readable bytes past the field
-template <int N>
-CBX_HD FB<N> load_field(const uint8_t* buf, uint32_t addr) {
-    constexpr int NW = (N + 3) / 4;
-    const uint32_t* p = (const uint32_t*)(buf + (addr & ~3u));
-    const uint32_t sh = addr & 3u;
-    uint32_t r[NW + 1];
-#pragma unroll
-    for (int k = 0; k <= NW; k++) r[k] = p[k];
-    FB<N> b;
-#pragma unroll
-    for (int k = 0; k < NW; k++) b.w[k] = align_bytes(r[k + 1], r[k], sh);
-    return b;
+// bytes [end - 8, end) as a little-endian u64 (byte end-8 in bits 0..7)
+CBX_HD uint64_t img_le64_ending(const uint8_t* img, uint32_t end) {
+    const uint32_t s = end - 8;
+    const uint32_t* p = (const uint32_t*)(img + (s & ~3u));
+    const uint32_t sh = s & 3u;
+    const uint32_t r0 = p[0], r1 = p[1], r2 = p[2];
+    return ((uint64_t)align_bytes(r2, r1, sh) << 32) | align_bytes(r1, r0, sh);
 }
 
-// big-endian value of bytes [i, i + k), k <= 8 (i, k compile-time after unrolling)
-template <int N>
-CBX_HD uint64_t fb_be(const FB<N>& b, int i, int k) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++)
-        if (j < k) v = (v << 8) | b.byte(i + j);
-    return v;
+// mask keeping the low n bytes (n in 0..8)
+CBX_HD uint64_t low_bytes_mask(int n) { return n >= 8 ? ~0ull : (n <= 0 ? 0ull : ((1ull << (8 * n)) - 1)); }
+// mask keeping the high n bytes (n in 0..8)
+CBX_HD uint64_t high_bytes_mask(int n) { return n >= 8 ? ~0ull : (n <= 0 ? 0ull : ~0ull << (8 * (8 - n))); }
+
+// big-endian unsigned value of the n <= 8 bytes ending at `end`
+CBX_HD uint64_t img_be(const uint8_t* img, uint32_t end, int n) {
+    return __builtin_bswap64(img_le64_ending(img, end)) & low_bytes_mask(n);
 }
 
 // 8 valid packed-BCD digits -> binary
@@ -467,153 +535,272 @@ CBX_HD bool bcd_ok(uint64_t x) {
     uint64_t lo = x & 0x0F0F0F0F0F0F0F0Full, hi = (x >> 4) & 0x0F0F0F0F0F0F0F0Full;
     return (((lo + 0x0606060606060606ull) | (hi + 0x0606060606060606ull)) & 0x1010101010101010ull) == 0;
 }
+// 8 digit bytes (0..9, most significant digit in the LOWEST byte) -> binary
+CBX_HD uint32_t digits8_bin(uint64_t d) {
+    d = d * 10u + (d >> 8);                                                     // byte 2j: pair value
+    d = (d & 0x000000FF000000FFull) * 100u + ((d >> 16) & 0x000000FF000000FFull);  // dword j: quad value
+    return (uint32_t)(d & 0xFFFFu) * 10000u + (uint32_t)((d >> 32) & 0xFFFFu);
+}
 
-template <int N>
-CBX_HD Val decode_bcd_n(const Field& f, const FB<N>& b) {
-    constexpr int NL = N < 8 ? N : 8;      // bytes in the low part (carries the sign nibble)
-    constexpr int NH = N - NL;             // leading bytes (digits only)
-    const uint64_t lo = fb_be(b, NH, NL);
-    const uint32_t sn = (uint32_t)lo & 15u;
-    const uint64_t dlo = lo >> 4;          // 2*NL - 1 digits
-    bool ok = bcd_ok(dlo) && (sn == 0xC || sn == 0xD || sn == 0xF);
-    uint64_t hi = 0;
-    if (NH > 0) { hi = fb_be(b, 0, NH); ok &= bcd_ok(hi); }
-    if (!ok) return null_val();
-    const bool neg = sn == 0xD;
-    U128 M = u128(bcd16_bin(dlo));
-    if (NH > 0) {
-        // M = hi_value * 10^15 + lo_value
-        uint64_t hv = bcd16_bin(hi);
-        const uint64_t P15 = 1000000000000000ull;
-        uint64_t plo = hv * P15, phi = mulhi64(hv, P15);
-        uint64_t s = plo + M.lo;
-        M.hi = phi + (s < plo);
-        M.lo = s;
+// ------------------------------------------------------------------------------------------
+// Numeric ops: one pre-resolved record per (field, slot) -- what the kernels' hot loop reads
+// with a single scalar load (the plan flattens the descriptor tables into them).
+// ------------------------------------------------------------------------------------------
+enum NumFlags : uint32_t {
+    NF_SIGNED = 1, NF_BIG_ENDIAN = 2, NF_INT = 4 /* fin == 0 */, NF_IBM = 8, NF_LE_FP = 16,
+    NF_PLUS_NULL = 32, NF_FLOAT = 64 /* COMP-1 (else COMP-2) */
+};
+
+struct NumOp {
+    int32_t eo;                       // element offset in the record (slot resolved, before start_off)
+    uint8_t variant, size, out_type, flags;
+    uint8_t e_mul, e_lim, n_odo, pad;
+    int32_t column;
+    int32_t slot;
+    int32_t defer;                    // deferral sequence of this element, -1 if never deferred
+    int32_t segment;                  // segment-redefine group, -1 none
+    int16_t odo_arr[CBX_MAX_DIMS];    // OCCURS DEPENDING ON levels: element index odo_idx[j] must be
+    int16_t odo_idx[CBX_MAX_DIMS];    // < the record's count of array odo_arr[j]
+};
+
+inline NumOp make_numop(const Field& d, int slot, int eo, const int16_t* odo_arr, const int16_t* odo_idx, int n_odo) {
+    NumOp o{};
+    o.eo = eo;
+    o.variant = (uint8_t)d.variant;
+    o.size = (uint8_t)(d.size < 255 ? d.size : 255);
+    o.out_type = (uint8_t)d.out_type;
+    uint32_t fl = 0;
+    if (d.flags & CBX_F_SIGNED) fl |= NF_SIGNED;
+    if (d.flags & CBX_F_BIG_ENDIAN) fl |= NF_BIG_ENDIAN;
+    if (d.fin == 0) fl |= NF_INT;
+    if (d.flags & CBX_F_IBM) fl |= NF_IBM;
+    if (d.flags & CBX_F_LITTLE_ENDIAN_FP) fl |= NF_LE_FP;
+    if (d.plus_null) fl |= NF_PLUS_NULL;
+    if (d.kind == CBX_K_FLOAT) fl |= NF_FLOAT;
+    o.flags = (uint8_t)fl;
+    o.e_mul = (uint8_t)d.e_mul;
+    o.e_lim = (uint8_t)d.e_lim;
+    o.n_odo = (uint8_t)n_odo;
+    o.column = d.column;
+    o.slot = slot;
+    o.defer = d.defer >= 0 ? d.defer + slot : -1;
+    o.segment = d.segment;
+    for (int j = 0; j < CBX_MAX_DIMS; j++) {
+        o.odo_arr[j] = j < n_odo ? odo_arr[j] : 0;
+        o.odo_idx[j] = j < n_odo ? odo_idx[j] : 0;
     }
-    if ((f.flags & CBX_F_INTEGRAL) && f.precision <= 18) {
-        uint64_t v = neg ? (uint64_t)0 - M.lo : M.lo;  // Java long arithmetic wraps
+    return o;
+}
+
+// 10^k, k = 0..38, as 128-bit (lo, hi) words
+#if defined(__HIP_DEVICE_COMPILE__)
+__constant__ const uint64_t kPow10Lo[39] = {
+    0x0000000000000001ull, 0x000000000000000aull, 0x0000000000000064ull,
+    0x00000000000003e8ull, 0x0000000000002710ull, 0x00000000000186a0ull,
+    0x00000000000f4240ull, 0x0000000000989680ull, 0x0000000005f5e100ull,
+    0x000000003b9aca00ull, 0x00000002540be400ull, 0x000000174876e800ull,
+    0x000000e8d4a51000ull, 0x000009184e72a000ull, 0x00005af3107a4000ull,
+    0x00038d7ea4c68000ull, 0x002386f26fc10000ull, 0x016345785d8a0000ull,
+    0x0de0b6b3a7640000ull, 0x8ac7230489e80000ull, 0x6bc75e2d63100000ull,
+    0x35c9adc5dea00000ull, 0x19e0c9bab2400000ull, 0x02c7e14af6800000ull,
+    0x1bcecceda1000000ull, 0x161401484a000000ull, 0xdcc80cd2e4000000ull,
+    0x9fd0803ce8000000ull, 0x3e25026110000000ull, 0x6d7217caa0000000ull,
+    0x4674edea40000000ull, 0xc0914b2680000000ull, 0x85acef8100000000ull,
+    0x38c15b0a00000000ull, 0x378d8e6400000000ull, 0x2b878fe800000000ull,
+    0xb34b9f1000000000ull, 0x00f436a000000000ull, 0x098a224000000000ull};
+__constant__ const uint64_t kPow10Hi[39] = {
+    0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000000ull,
+    0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000000ull,
+    0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000000ull,
+    0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000000ull,
+    0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000000ull,
+    0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000000ull,
+    0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000005ull,
+    0x0000000000000036ull, 0x000000000000021eull, 0x000000000000152dull,
+    0x000000000000d3c2ull, 0x0000000000084595ull, 0x000000000052b7d2ull,
+    0x00000000033b2e3cull, 0x00000000204fce5eull, 0x00000001431e0faeull,
+    0x0000000c9f2c9cd0ull, 0x0000007e37be2022ull, 0x000004ee2d6d415bull,
+    0x0000314dc6448d93ull, 0x0001ed09bead87c0ull, 0x0013426172c74d82ull,
+    0x00c097ce7bc90715ull, 0x0785ee10d5da46d9ull, 0x4b3b4ca85a86c47aull};
+CBX_HD U128 pow10_u128(int k) { return U128{kPow10Lo[k], kPow10Hi[k]}; }
+#else
+inline U128 pow10_u128(int k) {
+    unsigned __int128 x = 1;
+    for (int i = 0; i < k; i++) x *= 10;
+    return U128{(uint64_t)x, (uint64_t)(x >> 64)};
+}
+#endif
+
+// Fast-path result typing (DecoderSelector.scala:104-281 + Spark Decimal.toPrecision) for a
+// digit magnitude M: integral -> two's complement (BCD wraps as a Java long, as the reference);
+// decimal -> null past 10^e_lim, else M * 10^e_mul.  Branch-free apart from uniform tests on
+// the op: every lane computes, `valid` selects.
+CBX_HD Val fast_finish(const NumOp& op, U128 M, bool neg, bool valid) {
+    if (op.flags & NF_INT) {
+        const uint64_t v = neg ? (uint64_t)0 - M.lo : M.lo;
+        return Val{v, (uint64_t)((int64_t)v >> 63), valid};
+    }
+    valid &= u128_lt(M, pow10_u128(op.e_lim));
+    const uint64_t mul = pow10_u128(op.e_mul).lo;
+    U128 R;
+    R.lo = M.lo * mul;
+    R.hi = mulhi64(M.lo, mul) + M.hi * mul;
+    if (neg) R = u128_neg(R);
+    return Val{R.lo, R.hi, valid};
+}
+
+CBX_HD Val decode_bcd8(const NumOp& op, const uint8_t* img, uint32_t addr) {
+    const uint64_t be = img_be(img, addr + op.size, op.size);
+    const uint32_t sn = (uint32_t)be & 15u;
+    const uint64_t dg = be >> 4;
+    const bool valid = bcd_ok(dg) && (sn == 0xC || sn == 0xD || sn == 0xF);
+    return fast_finish(op, u128(bcd16_bin(dg)), sn == 0xD, valid);
+}
+
+CBX_HD Val decode_bcd16(const NumOp& op, const uint8_t* img, uint32_t addr) {
+    const uint32_t end = addr + op.size;
+    const uint64_t lo = __builtin_bswap64(img_le64_ending(img, end));
+    const uint64_t hi = img_be(img, end - 8, op.size - 8);
+    const uint32_t sn = (uint32_t)lo & 15u;
+    const uint64_t dlo = lo >> 4;   // 15 digits
+    const bool valid = bcd_ok(dlo) && bcd_ok(hi) && (sn == 0xC || sn == 0xD || sn == 0xF);
+    const uint64_t hv = bcd16_bin(hi);
+    const uint64_t P15 = 1000000000000000ull;
+    const uint64_t plo = hv * P15, phi = mulhi64(hv, P15);
+    U128 M;
+    M.lo = plo + bcd16_bin(dlo);
+    M.hi = phi + (M.lo < plo);
+    return fast_finish(op, M, sn == 0xD, valid);
+}
+
+CBX_HD Val decode_bin8(const NumOp& op, const uint8_t* img, uint32_t addr) {
+    const int n = op.size;
+    const uint64_t le = img_le64_ending(img, addr + n);
+    uint64_t v = (op.flags & NF_BIG_ENDIAN) ? (__builtin_bswap64(le) & low_bytes_mask(n)) : (le >> (64 - 8 * n));
+    bool neg = false;
+    if (op.flags & NF_SIGNED) {
+        const int sh = 64 - 8 * n;
+        v = (uint64_t)((int64_t)(v << sh) >> sh);
+        neg = (int64_t)v < 0;
+    }
+    if (op.flags & NF_INT) {
+        // unsigned 4- and 8-byte values with the top bit set are null (BinaryNumberDecoders.scala:81-82, 111-112)
+        const bool bad = !(op.flags & NF_SIGNED) && ((n == 4 && (v & 0x80000000ull)) || (n == 8 && (v >> 63)));
+        return Val{v, neg ? ~0ull : 0ull, !bad};
+    }
+    // binary decimal (BinaryUtils.decodeBinaryNumber + addDecimalPoint), scale factor >= 0
+    return fast_finish(op, u128(neg ? (uint64_t)0 - v : v), neg, true);
+}
+
+CBX_HD Val decode_zoned16(const NumOp& op, const uint8_t* img, uint32_t addr, bool& defer) {
+    const int n = op.size;
+    const uint32_t end = addr + n;
+    const uint64_t Z = 0xF0F0F0F0F0F0F0F0ull, L = 0x0F0F0F0F0F0F0F0Full;
+    uint64_t b1 = img_le64_ending(img, end);       // field bytes end-8 .. end-1 (last in the top byte)
+    uint64_t b0 = img_le64_ending(img, end - 8);   // end-16 .. end-9
+    // bytes in front of the field read as '0' digits (0xF0): leading zeros change nothing
+    const uint64_t m1 = high_bytes_mask(n), m0 = high_bytes_mask(n - 8);
+    b1 = (b1 & m1) | (Z & ~m1);
+    b0 = (b0 & m0) | (Z & ~m0);
+    const uint32_t lastz = (uint32_t)(b1 >> 60);
+    const uint64_t d0 = b0 & L, d1 = b1 & L;
+    const bool fast = (b0 & Z) == Z && (((b1 & Z) | 0xF000000000000000ull) == Z) &&
+                      (lastz == 0xF || lastz == 0xC || lastz == 0xD) &&
+                      (((d0 + 0x0606060606060606ull) | (d1 + 0x0606060606060606ull)) & 0x1010101010101010ull) == 0;
+    defer = !fast;
+    const bool neg = lastz == 0xD;
+    const bool valid = fast && !(neg && !(op.flags & NF_SIGNED)) && !(lastz == 0xC && (op.flags & NF_PLUS_NULL));
+    const uint64_t v = (uint64_t)digits8_bin(d0) * 100000000ull + digits8_bin(d1);
+    return fast_finish(op, u128(v), neg, valid);
+}
+
+CBX_HD Val decode_fp(const NumOp& op, const uint8_t* img, uint32_t addr) {
+    const uint64_t le = img_le64_ending(img, addr + op.size);
+    const bool lef = (op.flags & NF_LE_FP) != 0;
+    if (op.flags & NF_FLOAT) {
+        uint32_t w = (uint32_t)(le >> 32);
+        if (!lef) w = __builtin_bswap32(w);
+        return Val{(op.flags & NF_IBM) ? ibm_single_bits(w) : w, 0, true};
+    }
+    const uint64_t w = lef ? le : __builtin_bswap64(le);
+    return Val{(op.flags & NF_IBM) ? ibm_double_bits(w) : w, 0, true};
+}
+
+// Numeric element at img[addr, addr + size) (bounds already checked by the caller).  Sets
+// `defer` (result null) when the value needs the byte-loop decoder: the kernels record it in
+// a deferral bitmap and the fixup kernel decodes it with decode_numeric.
+CBX_HD Val decode_value(const NumOp& op, const uint8_t* img, uint32_t addr, bool& defer) {
+    switch (op.variant) {
+    case V_BCD8: return decode_bcd8(op, img, addr);
+    case V_BCD16: return decode_bcd16(op, img, addr);
+    case V_BIN8: return decode_bin8(op, img, addr);
+    case V_ZONED16: { Val x = decode_zoned16(op, img, addr, defer); return x; }
+    case V_FP: return decode_fp(op, img, addr);
+    default: defer = true; return null_val();
+    }
+}
+
+// OCCURS DEPENDING ON source (integral, precision <= 18, RecordExtractors.scala:126-134): the
+// value as a Java long (BCD wraps; zoned follows Integer/Long.parseInt; binary <= 8 bytes).
+CBX_HD Val decode_count_int(const Field& f, const uint8_t* p) {
+    const int n = f.size;
+    if (f.kind == CBX_K_BCD) {
+        uint64_t v = 0;
+        for (int i = 0; i < n; i++) {
+            const uint32_t b = p[i], hi = b >> 4, lo = b & 15;
+            if (hi > 9) return null_val();
+            v = v * 10 + hi;
+            if (i + 1 < n) {
+                if (lo > 9) return null_val();
+                v = v * 10 + lo;
+            }
+        }
+        const uint32_t sn = p[n - 1] & 15;
+        if (!(sn == 0xC || sn == 0xD || sn == 0xF)) return null_val();
+        if (sn == 0xD) v = (uint64_t)0 - v;
         return Val{v, (uint64_t)((int64_t)v >> 63), true};
     }
-    if (f.flags & CBX_F_INTEGRAL) return finalize_decimal(M, false, 0, neg, f);
-    if (f.sf == 0) return finalize_decimal(M, false, f.scale, neg, f);
-    if (f.sf > 0) {
-        bool okm = u128_mul_pow10(M, f.sf);
-        return finalize_decimal(M, !okm, 0, neg, f);
-    }
-    return finalize_decimal(M, false, -f.sf + 2 * N - 1, neg, f);
-}
-
-template <int N>
-CBX_HD Val decode_binary_n(const Field& f, const FB<N>& b) {
-    const bool be = (f.flags & CBX_F_BIG_ENDIAN) != 0;
-    const bool sgn = (f.flags & CBX_F_SIGNED) != 0;
-    U128 v = u128(0);
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-        uint32_t x = be ? b.byte(i) : b.byte(N - 1 - i);
-        v.hi = (v.hi << 8) | (v.lo >> 56);
-        v.lo = (v.lo << 8) | x;
-    }
-    const uint32_t top = be ? b.byte(0) : b.byte(N - 1);
-    bool neg = false;
-    if (sgn && (top & 0x80)) {
-        if (8 * N < 64) { v.lo |= ~(uint64_t)0 << (8 * N); v.hi = ~(uint64_t)0; }
-        else if (8 * N < 128) v.hi |= ~(uint64_t)0 << (8 * N - 64);
-        neg = true;
-    }
-    if (f.flags & CBX_F_INTEGRAL) {
-        if (N == 1 || N == 2 || N == 4) {
-            if (!sgn && N == 4 && (v.lo & 0x80000000u)) return null_val();
-            return Val{v.lo, v.hi, true};
+    if (f.kind == CBX_K_BINARY) {
+        const bool be = (f.flags & CBX_F_BIG_ENDIAN) != 0;
+        uint64_t v = 0;
+        for (int i = 0; i < n && i < 8; i++) v = (v << 8) | p[be ? i : n - 1 - i];
+        if (f.flags & CBX_F_SIGNED) {
+            const int sh = 64 - 8 * n;
+            v = (uint64_t)((int64_t)(v << sh) >> sh);
+        } else if ((n == 4 && (v & 0x80000000ull)) || (n == 8 && (v >> 63))) {
+            return null_val();
         }
-        if (N == 8) {
-            if (!sgn && (v.lo >> 63)) return null_val();
-            return Val{v.lo, (uint64_t)((int64_t)v.lo >> 63), true};
+        return Val{v, (uint64_t)((int64_t)v >> 63), true};
+    }
+    if (f.kind == CBX_K_ZONED) {
+        int sign = 0, nd = 0, ndots = 0;
+        bool malformed = false, big = false;
+        uint64_t v = 0;
+        for (int i = 0; i < n; i++) {
+            const uint32_t c = p[i], hi = c >> 4, lo = c & 15;
+            const bool dig = lo <= 9 && (hi == 0xF || (sign == 0 && (hi == 0xC || hi == 0xD)));
+            const bool sch = sign == 0 && (c == 0x60 || c == 0x4E);
+            const bool dot = c == 0x4B || c == 0x6B;
+            const bool spc = c == 0x40 || c == 0;
+            if (sign == 0 && dig && hi != 0xF) sign = hi == 0xD ? 2 : 1;
+            if (sch) sign = c == 0x60 ? 2 : 1;
+            malformed |= !(dig || sch || dot || spc);
+            if (dig) {
+                nd++;
+                big |= v > 1000000000000000000ull;
+                v = v * 10 + lo;
+            }
+            ndots += dot;
         }
-        U128 M = neg ? u128_neg(v) : v;
-        return finalize_decimal(M, false, 0, neg, f);
+        const bool neg = sign == 2;
+        if (malformed || (neg && !(f.flags & CBX_F_SIGNED)) || ndots != 0 || nd == 0 || big) return null_val();
+        const uint64_t lim = f.precision <= 9 ? (neg ? 0x80000000ull : 0x7FFFFFFFull)
+                                              : (neg ? 0x8000000000000000ull : 0x7FFFFFFFFFFFFFFFull);
+        if (v > lim) return null_val();
+        v = neg ? (uint64_t)0 - v : v;
+        return Val{v, (uint64_t)((int64_t)v >> 63), true};
     }
-    U128 M = neg ? u128_neg(v) : v;
-    if (f.sf == 0) return finalize_decimal(M, false, f.scale, neg, f);
-    if (f.sf > 0) {
-        bool ok = u128_mul_pow10(M, f.sf);
-        return finalize_decimal(M, !ok, 0, neg, f);
-    }
-    return finalize_decimal(M, false, -f.sf + u128_ndigits(M), neg, f);
-}
-
-// Zoned: fast path for the common layout (F-zone digits, last byte optionally C/D overpunch);
-// anything else (spaces, separate signs, dots, malformed bytes) takes the general state machine.
-template <int N>
-CBX_HD Val decode_zoned_n(const Field& f, const FB<N>& b, const uint8_t* buf, uint32_t addr) {
-    bool fast = true;
-    uint64_t acc = 0;
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-        uint32_t c = b.byte(j);
-        uint32_t lo = c & 15u, hi = c >> 4;
-        fast &= lo <= 9u;
-        if (j + 1 < N) fast &= hi == 0xFu;
-        else fast &= hi == 0xFu || hi == 0xCu || hi == 0xDu;
-        acc = acc * 10u + lo;
-    }
-    if (fast) {
-        uint32_t last = b.byte(N - 1) >> 4;
-        int sign = last == 0xD ? 2 : (last == 0xC ? 1 : 0);
-        // digits are all significant-or-leading-zero; N <= 18 keeps acc exact
-        return zoned_finish(f, false, sign, N, 0, 0, u128(acc), false);
-    }
-    Field g = f;
-    g.size = N;
-    return decode_zoned(g, buf + addr);
-}
-
-template <int N>
-CBX_HD Val decode_float_n(const Field& f, const FB<N>& b) {
-    const bool le = (f.flags & CBX_F_LITTLE_ENDIAN_FP) != 0;
-    if (N == 4) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) w = (w << 8) | b.byte(le ? 3 - i : i);
-        return Val{(f.flags & CBX_F_IBM) ? ibm_single_bits(w) : w, 0, true};
-    }
-    uint64_t w = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) w = (w << 8) | b.byte(le ? 7 - i : i);
-    return Val{(f.flags & CBX_F_IBM) ? ibm_double_bits(w) : w, 0, true};
-}
-
-#define CBX_SIZE_CASES_16(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16)
-#define CBX_SIZE_CASES_18(M) CBX_SIZE_CASES_16(M) M(17) M(18)
-
-// Numeric field whose bytes start at buf[addr] (bounds already checked by the caller).
-CBX_HD Val decode_numeric_at(const Field& f, const uint8_t* buf, uint32_t addr) {
-    switch (f.kind) {
-    case CBX_K_BCD:
-        switch (f.size) {
-#define CBX_BCD_CASE(n) case n: return decode_bcd_n<n>(f, load_field<n>(buf, addr));
-            CBX_SIZE_CASES_16(CBX_BCD_CASE)
-#undef CBX_BCD_CASE
-        default: return decode_bcd(f, buf + addr);
-        }
-    case CBX_K_BINARY:
-        switch (f.size) {
-#define CBX_BIN_CASE(n) case n: return decode_binary_n<n>(f, load_field<n>(buf, addr));
-            CBX_SIZE_CASES_16(CBX_BIN_CASE)
-#undef CBX_BIN_CASE
-        default: return decode_binary(f, buf + addr);
-        }
-    case CBX_K_ZONED:
-        switch (f.size) {
-#define CBX_ZON_CASE(n) case n: return decode_zoned_n<n>(f, load_field<n>(buf, addr), buf, addr);
-            CBX_SIZE_CASES_18(CBX_ZON_CASE)
-#undef CBX_ZON_CASE
-        default: return decode_zoned(f, buf + addr);
-        }
-    case CBX_K_FLOAT: return decode_float_n<4>(f, load_field<4>(buf, addr));
-    case CBX_K_DOUBLE: return decode_float_n<8>(f, load_field<8>(buf, addr));
-    default: return null_val();
-    }
+    return null_val();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -632,12 +819,12 @@ CBX_HD uint32_t ascii_lut(uint32_t b) {
 }
 
 template <typename LutFn>
-CBX_HD StrSpan string_span(const Field& f, const uint8_t* p, int n, LutFn lut) {
+CBX_HD StrSpan string_span(int kind, int trim, const uint8_t* p, int n, LutFn lut) {
     StrSpan s{0, n, 0};
-    if (f.kind == CBX_K_HEX) { s.utf8_len = 2 * n; return s; }
-    if (f.kind == CBX_K_RAW) { s.utf8_len = n; return s; }
-    const bool tl = f.trim == CBX_TRIM_LEFT || f.trim == CBX_TRIM_BOTH;
-    const bool tr = f.trim == CBX_TRIM_RIGHT || f.trim == CBX_TRIM_BOTH;
+    if (kind == CBX_K_HEX) { s.utf8_len = 2 * n; return s; }
+    if (kind == CBX_K_RAW) { s.utf8_len = n; return s; }
+    const bool tl = trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH;
+    const bool tr = trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH;
     int b = 0, e = n;
     if (tl) while (b < e && (lut(p[b]) >> 31)) b++;
     if (tr) while (e > b && (lut(p[e - 1]) >> 31)) e--;
@@ -648,8 +835,8 @@ CBX_HD StrSpan string_span(const Field& f, const uint8_t* p, int n, LutFn lut) {
 }
 
 template <typename LutFn>
-CBX_HD void string_write(const Field& f, const uint8_t* p, const StrSpan& s, uint8_t* out, LutFn lut) {
-    if (f.kind == CBX_K_HEX) {
+CBX_HD void string_write(int kind, const uint8_t* p, const StrSpan& s, uint8_t* out, LutFn lut) {
+    if (kind == CBX_K_HEX) {
         const char* H = "0123456789ABCDEF";
         for (int i = s.begin; i < s.end; i++) {
             out[2 * (i - s.begin)] = (uint8_t)H[p[i] >> 4];
@@ -657,7 +844,7 @@ CBX_HD void string_write(const Field& f, const uint8_t* p, const StrSpan& s, uin
         }
         return;
     }
-    if (f.kind == CBX_K_RAW) {
+    if (kind == CBX_K_RAW) {
         for (int i = s.begin; i < s.end; i++) out[i - s.begin] = p[i];
         return;
     }

@@ -6,25 +6,59 @@
 #include "cbx_decode.h"
 #include "cobrix_hip.h"
 
+// Plan tables are read-only for the whole launch: address space 4 ("constant") lets the
+// compiler fetch uniform descriptors with scalar loads (s_load) through the scalar cache
+// instead of vector memory round trips.
+#define CBX_CONST __attribute__((address_space(4)))
+
 namespace cbx {
 
-constexpr int kWave = 64;            // one wave = one 64-record tile
+constexpr int kWave = 64;              // one wave = one tile of 64 consecutive records (lane = record)
+constexpr int kWavesPerBlock = 2;      // waves per workgroup (each works on its own tile)
+constexpr int kGuard = 16;             // LDS guard bytes in front of / behind a record image
 constexpr int kMaxWindowBytes = 1024;  // fields wider than this are read from HBM directly
+constexpr int kStrStageBytes = 4096;   // per-wave LDS staging of one string item's tile payload
+constexpr int kMaxStrItems = 256;      // string (field, slot) items per window (plan splits windows)
 
-// A run of consecutive slots of one field staged in the same LDS window.
-struct Run {
-    int32_t field;
-    int32_t slot_begin, slot_end;
+// One string element (field, slot), pre-resolved by the plan (cf. NumOp in cbx_decode.h).
+struct StrOp {
+    int32_t eo;                       // element offset in the record (before start_off)
+    int32_t size;
+    uint8_t kind, trim, n_odo, pad;
+    int32_t column;
+    int32_t slot;
+    int32_t seq;                      // look-back sequence
+    int32_t segment;
+    int16_t odo_arr[CBX_MAX_DIMS];
+    int16_t odo_idx[CBX_MAX_DIMS];
     int32_t reserved;
 };
 
-// Byte range [lo, hi) of each record (relative to the decode base) staged into LDS together.
+// A run of numeric ops of one window sharing decoder variant and output width: the kernel
+// runs each batch with a loop specialised for that pair.
+struct Batch {
+    int32_t variant, width;           // Variant, output bytes per value (4, 8, 16)
+    int32_t begin, end;               // NumOp range
+    int32_t odo;                      // ops carry OCCURS DEPENDING ON conditions
+    int32_t reserved;
+};
+
+// Generated column (File_Id / Record_Id).
+struct GenOp {
+    int32_t kind, column, out_type, reserved;
+};
+
+// Byte range [lo, hi) of each record (relative to the decode base) staged into LDS together,
+// with the numeric / string ops whose bytes lie inside it.  The window with global != 0 is
+// never staged: its ops read HBM (oversized fields) or are generated.
 struct Window {
     int32_t lo, hi;
-    int32_t run_begin, run_end;
-    int32_t has_strings;   // any string run (needed by the sizing pass)
-    int32_t pitch;         // LDS row pitch in bytes (4 * odd)
-    int32_t reserved[2];
+    int32_t nop_begin, nop_end;
+    int32_t batch_begin, batch_end;
+    int32_t sop_begin, sop_end;
+    int32_t gen_begin, gen_end;
+    int32_t pitch;         // LDS row pitch in bytes (odd number of dwords)
+    int32_t global;
 };
 
 // Per output column device pointers.
@@ -33,7 +67,15 @@ struct DevColumn {
     uint64_t* validity;
     int64_t* offsets;
     uint8_t* data;
+    int64_t capacity;      // strings: bytes per slot region
+    int64_t* sizes;        // strings: per-slot payload bytes (device, may be null)
 };
+
+// Decoupled look-back word: [63:62] state (0 empty, 1 tile aggregate, 2 inclusive prefix),
+// [61:0] byte count.
+constexpr uint64_t kLbAgg = 1ull << 62;
+constexpr uint64_t kLbPrefix = 2ull << 62;
+constexpr uint64_t kLbValue = (1ull << 62) - 1;
 
 struct KernelArgs {
     // input
@@ -43,28 +85,46 @@ struct KernelArgs {
     const int64_t* rec_off;    // var-len: payload offsets (nullptr for fixed)
     const int32_t* rec_len;    // var-len: payload lengths
     int64_t n_rec;
+    int64_t n_tiles;
     int32_t stride;            // fixed: record stride (avail length)
     int32_t start_off;         // record_start_offset
     int64_t first_record_id;
     int32_t file_id;
-    int32_t mode;              // 0 decode, 1 string sizes
+    int32_t mode;              // 0 decode, 1 string sizes only
+    // fixed-length contiguous staging: the tile's byte span is loaded with 16-byte loads and
+    // scattered dword-wise into rows of `cpitch` bytes (odd dword count: conflict-free lanes)
+    int32_t contig;
+    int32_t cpitch;
+    int32_t stride_dw;         // stride / 4
+    float inv_stride_dw;       // 1 / stride_dw
+    int32_t contig_chunks;     // 16-byte chunks per lane held in registers (prefetch depth)
     // plan
-    const Field* fields;
-    const Window* windows;
+    const CBX_CONST Field* fields;
+    const CBX_CONST Window* windows;
     int32_t n_windows;
-    const Run* runs;
-    const cbx_array* arrays;
+    const CBX_CONST NumOp* nops;
+    const CBX_CONST Batch* batches;
+    const CBX_CONST StrOp* sops;
+    const CBX_CONST GenOp* gops;
+    const CBX_CONST cbx_array* arrays;
     int32_t n_arrays;
     int32_t seg_col;           // column receiving the active segment index, -1 none
-    const cbx_segment_map* segmap;  // nullptr if none
+    const CBX_CONST cbx_segment_map* segmap;  // nullptr if none
     const uint32_t* lut;       // 256 entries
-    DevColumn* cols;
-    // string offsets: per string column base of its (slot, tile) sequence in tile_sums/scan
-    const int64_t* str_seq_base;     // [n_columns] index of the column's first (slot,tile) entry, -1 non-string
-    int64_t* tile_sums;              // sizes pass: written; decode pass: exclusive scan (read)
-    int64_t n_tiles;
-    int32_t max_pitch;         // LDS bytes per row of the widest window
-    int32_t contig;            // fixed-length: stage each tile's contiguous byte span (all windows at once)
+    const CBX_CONST DevColumn* cols;
+    // strings
+    int32_t n_seq;             // string sequences = sum over string fields of n_slots
+    uint64_t* lookback;        // [n_tiles][n_seq] look-back words (zeroed per call)
+    int64_t* seq_totals;       // sizes mode: per-sequence totals (zeroed per call)
+    uint32_t* ticket;          // dynamic tile counter (zeroed per call)
+    int32_t* status;           // [0]: capacity overflow flag
+    uint64_t* defer_bits;      // [n_defer][n_tiles] values left to the fixup kernel
+    // LDS layout (bytes, per wave)
+    int32_t lds_rows;          // record image incl. guards
+    int32_t lds_counts;        // OCCURS element counts
+    int32_t lds_agg;           // string element aggregates of a window (4 B each)
+    int32_t str_stage;         // string payload staging bytes
+    int32_t lds_wave;          // total per wave
 };
 
 }  // namespace cbx

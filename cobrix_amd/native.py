@@ -30,9 +30,10 @@ OUT_WIDTH = {O_I32: 4, O_I64: 8, O_DEC64: 8, O_DEC128: 16, O_F32: 4, O_F64: 8}
 
 # every symbol include/cobrix_hip.h declares
 EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx_plan_destroy",
-                    "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
-                    "cbx_string_sizes_var", "cbx_frame_rdw", "cbx_plan_set_profiling",
-                    "cbx_plan_last_kernel_ms")
+                    "cbx_string_bound", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
+                    "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
+                    "cbx_plan_kernel_times")
+ABI_VERSION = 2
 
 
 class NativeLibraryError(RuntimeError):
@@ -79,7 +80,7 @@ class CbxPlanOptions(ctypes.Structure):
 
 class CbxColumn(ctypes.Structure):
     _fields_ = [("values", ctypes.c_void_p), ("validity", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
-                ("data", ctypes.c_void_p), ("data_capacity", ctypes.c_int64), ("data_size", ctypes.c_int64)]
+                ("data", ctypes.c_void_p), ("data_capacity", ctypes.c_int64), ("data_sizes", ctypes.c_void_p)]
 
 
 class CbxRdwParams(ctypes.Structure):
@@ -111,13 +112,17 @@ def load():
     L.cbx_plan_create.argtypes = [P, i32, P, i32, P, ctypes.POINTER(P)]
     L.cbx_plan_destroy.argtypes = [P]
     L.cbx_plan_destroy.restype = None
+    L.cbx_string_bound.argtypes = [P, i64, P]
     L.cbx_string_sizes_fixed.argtypes = [P, P, i64, i32, i32, P, P]
+    L.cbx_plan_check.argtypes = [P, P]
     L.cbx_decode_fixed.argtypes = [P, P, i64, i32, i32, i64, P, P]
     L.cbx_decode_var.argtypes = [P, P, i64, P, P, i64, i32, i64, P, P]
     L.cbx_string_sizes_var.argtypes = [P, P, i64, P, P, i64, i32, P, P]
     L.cbx_frame_rdw.argtypes = [P, i64, P, i32, P, P, P, i64, P, P]
     L.cbx_plan_set_profiling.argtypes = [P, i32]
-    L.cbx_plan_last_kernel_ms.argtypes = [P, P, P, P]
+    L.cbx_plan_kernel_times.argtypes = [P, P, P, i32, P]
+    if L.cbx_abi_version() != ABI_VERSION:
+        raise NativeLibraryError(f"{LIB_PATH}: ABI {L.cbx_abi_version()} != {ABI_VERSION}; rebuild it")
     _lib = L
     return L
 

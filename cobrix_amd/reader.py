@@ -94,10 +94,9 @@ class DecodedBatch:
         bits = np.unpackbits(vb.view(np.uint8), bitorder="little").reshape(info.n_slots, pitch * 64)
         out["validity"] = bits[:, :self.n_rec].astype(bool)
         if c.get("offsets") is not None:
-            off = c["offsets"].cpu().numpy()[: n + 1]
-            data = c["data"][: max(1, int(c["data_size"]))].cpu().numpy().tobytes()
-            out["offsets"] = off
-            out["data"] = data
+            # slot s: offsets[s * (n_rec + 1) .. + n_rec], absolute into data (slot regions)
+            out["offsets"] = c["offsets"].cpu().numpy().reshape(info.n_slots, self.n_rec + 1)
+            out["data"] = c["data"].cpu().numpy().tobytes()
         else:
             v = c["values"].cpu().numpy()
             if info.out_type == N.O_DEC128:
@@ -123,7 +122,8 @@ class DecodedBatch:
             v = slot * self.n_rec + r
             ot = info.out_type
             if ot in (N.O_STRING, N.O_BINARY):
-                b = c["data"][int(c["offsets"][v]):int(c["offsets"][v + 1])]
+                off = c["offsets"][slot]
+                b = c["data"][int(off[r]):int(off[r + 1])]
                 return b.decode("utf-8") if ot == N.O_STRING else b
             x = c["values"][v]
             if ot == N.O_I32:
@@ -197,7 +197,9 @@ class DecodedBatch:
         return rows
 
 
-def _alloc_columns(plan: DecodePlan, n_rec: int, string_sizes: Optional[Sequence[int]], device) -> Tuple[List[Dict[str, Any]], ctypes.Array]:
+def _alloc_columns(plan: DecodePlan, n_rec: int, slot_capacity: Sequence[int], device) -> Tuple[List[Dict[str, Any]], ctypes.Array]:
+    """Caller-owned output buffers (cobrix_hip.h cbx_column): slot-major values, validity
+    bitmaps, and for strings one Arrow large-string array per slot (regions of slot_capacity)."""
     torch = _torch()
     pitch_words = (n_rec + 63) // 64
     cols: List[Dict[str, Any]] = []
@@ -206,13 +208,15 @@ def _alloc_columns(plan: DecodePlan, n_rec: int, string_sizes: Optional[Sequence
         n = n_rec * info.n_slots
         c: Dict[str, Any] = {"validity": torch.zeros(max(1, info.n_slots * pitch_words), dtype=torch.int64, device=device)}
         if info.out_type in (N.O_STRING, N.O_BINARY):
-            cap = int(string_sizes[ci]) if string_sizes is not None else n * info.node.data_size * 3
-            c["offsets"] = torch.zeros(n + 1, dtype=torch.int64, device=device)
-            c["data"] = torch.empty(max(1, cap), dtype=torch.uint8, device=device)
-            c["data_size"] = 0
+            cap = int(slot_capacity[ci])
+            c["offsets"] = torch.zeros(info.n_slots * (n_rec + 1), dtype=torch.int64, device=device)
+            c["data"] = torch.empty(max(1, cap * info.n_slots), dtype=torch.uint8, device=device)
+            c["sizes"] = torch.zeros(info.n_slots, dtype=torch.int64, device=device)
+            c["capacity"] = cap
             cstructs[ci].offsets = c["offsets"].data_ptr()
             cstructs[ci].data = c["data"].data_ptr()
             cstructs[ci].data_capacity = cap
+            cstructs[ci].data_sizes = c["sizes"].data_ptr()
         else:
             w = N.OUT_WIDTH[info.out_type]
             dt = {4: torch.int32, 8: torch.int64, 16: torch.int64}[w]
@@ -221,6 +225,15 @@ def _alloc_columns(plan: DecodePlan, n_rec: int, string_sizes: Optional[Sequence
         cstructs[ci].validity = c["validity"].data_ptr()
         cols.append(c)
     return cols, cstructs
+
+
+def string_capacity(native_plan, n_rec: int, exact: Optional[Sequence[int]] = None) -> List[int]:
+    """Per-column payload bytes per slot: the exact pre-pass result or cbx_string_bound."""
+    if exact is not None:
+        return [int(x) for x in exact]
+    out = (ctypes.c_int64 * native_plan.plan.n_columns)()
+    N.check(N.load().cbx_string_bound(native_plan.handle, n_rec, out))
+    return list(out)
 
 
 class _BaseReader:
@@ -277,22 +290,28 @@ class FixedLenNestedReader(_BaseReader):
             if n_bytes % exp > 0:
                 raise ValueError(f"Binary record size {exp} does not divide data size {n_bytes}.")
 
-    def decode_device(self, d_data, n_bytes: int, first_record_id: int = 0, stream=None) -> DecodedBatch:
-        """Decode a split already resident in HBM (d_data: uint8 CUDA tensor)."""
+    def decode_device(self, d_data, n_bytes: int, first_record_id: int = 0, stream=None,
+                      exact_strings: bool = False) -> DecodedBatch:
+        """Decode a split already resident in HBM (d_data: uint8 CUDA tensor).
+
+        One asynchronous kernel launch; string payloads go to regions sized by the upper bound
+        (or by the exact pre-pass when exact_strings=True).  cbx_plan_check synchronises and
+        raises if a payload overflowed."""
         torch = _torch()
         stride = self.get_record_size()
         n_rec = n_bytes // stride
         st = stream if stream is not None else torch.cuda.current_stream()
         L = N.load()
-        sizes = (ctypes.c_int64 * self.plan.n_columns)()
-        N.check(L.cbx_string_sizes_fixed(self.native.handle, d_data.data_ptr(), n_rec, stride,
-                                         self.params.start_offset, sizes, ctypes.c_void_p(st.cuda_stream)))
-        cols, cs = _alloc_columns(self.plan, n_rec, list(sizes), d_data.device)
+        exact = None
+        if exact_strings:
+            sizes = (ctypes.c_int64 * self.plan.n_columns)()
+            N.check(L.cbx_string_sizes_fixed(self.native.handle, d_data.data_ptr(), n_rec, stride,
+                                             self.params.start_offset, sizes, ctypes.c_void_p(st.cuda_stream)))
+            exact = list(sizes)
+        cols, cs = _alloc_columns(self.plan, n_rec, string_capacity(self.native, n_rec, exact), d_data.device)
         N.check(L.cbx_decode_fixed(self.native.handle, d_data.data_ptr(), n_rec, stride, self.params.start_offset,
                                    first_record_id, cs, ctypes.c_void_p(st.cuda_stream)))
-        for ci, c in enumerate(cols):
-            if "data" in c:
-                c["data_size"] = cs[ci].data_size
+        N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
         return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, self.params.generate_record_id)
 
     def decode(self, data: bytes, first_record_id: int = 0) -> DecodedBatch:
@@ -334,22 +353,23 @@ class VarLenNestedReader(_BaseReader):
         return off[: n.value], ln[: n.value]
 
     def decode_device(self, d_data, n_bytes: int, rec_off, rec_len, first_record_id: int = 0,
-                      stream=None) -> DecodedBatch:
+                      stream=None, exact_strings: bool = False) -> DecodedBatch:
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream()
         n_rec = int(rec_off.numel())
         L = N.load()
-        sizes = (ctypes.c_int64 * self.plan.n_columns)()
-        N.check(L.cbx_string_sizes_var(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(),
-                                       rec_len.data_ptr(), n_rec, self.params.start_offset, sizes,
-                                       ctypes.c_void_p(st.cuda_stream)))
-        cols, cs = _alloc_columns(self.plan, n_rec, list(sizes), d_data.device)
+        exact = None
+        if exact_strings:
+            sizes = (ctypes.c_int64 * self.plan.n_columns)()
+            N.check(L.cbx_string_sizes_var(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(),
+                                           rec_len.data_ptr(), n_rec, self.params.start_offset, sizes,
+                                           ctypes.c_void_p(st.cuda_stream)))
+            exact = list(sizes)
+        cols, cs = _alloc_columns(self.plan, n_rec, string_capacity(self.native, n_rec, exact), d_data.device)
         N.check(L.cbx_decode_var(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(),
                                  rec_len.data_ptr(), n_rec, self.params.start_offset, first_record_id, cs,
                                  ctypes.c_void_p(st.cuda_stream)))
-        for ci, c in enumerate(cols):
-            if "data" in c:
-                c["data_size"] = cs[ci].data_size
+        N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
         return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, self.params.generate_record_id)
 
     def decode(self, data: bytes, seeds: Optional[Sequence[int]] = None, first_record_id: int = 0) -> DecodedBatch:

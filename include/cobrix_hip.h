@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 1
+#define CBX_ABI_VERSION 2
 
 /* status codes */
 #define CBX_OK 0
@@ -140,14 +140,19 @@ typedef struct {
  * values laid out slot-major: value (slot s, record r) is element s * n_rec + r.  Validity is
  * an Arrow bitmap per slot row with a 64-bit-aligned pitch: bit r of row s is
  *   validity[(s * pitch_words + r / 64)] >> (r % 64), pitch_words = ceil(n_rec / 64).
- * Strings/binary: offsets[v] .. offsets[v+1] (int64, v = s * n_rec + r) into data. */
+ * Strings/binary: every slot is its own Arrow large-string array.  Slot s owns the payload
+ * region data[s * data_capacity, (s + 1) * data_capacity) and the n_rec + 1 offsets
+ * offsets[s * (n_rec + 1) .. s * (n_rec + 1) + n_rec] (absolute byte positions in `data`).
+ * data_capacity = cbx_string_bound(...) always suffices; a smaller capacity (e.g. from
+ * cbx_string_sizes_*) is honoured: payload never overflows its region, an overflow is
+ * reported by cbx_plan_check. */
 typedef struct {
     void* values;          /* fixed-width values (NULL for strings) */
     uint64_t* validity;
-    int64_t* offsets;      /* strings: n_values + 1 entries */
-    uint8_t* data;         /* strings: UTF-8 payload */
-    int64_t data_capacity;
-    int64_t data_size;     /* out: payload bytes written */
+    int64_t* offsets;      /* strings: n_slots * (n_rec + 1) entries */
+    uint8_t* data;         /* strings: UTF-8 payload, n_slots regions of data_capacity bytes */
+    int64_t data_capacity; /* strings: bytes per slot region */
+    int64_t* data_sizes;   /* strings: device array [n_slots] receiving each slot's payload bytes (may be NULL) */
 } cbx_column;
 
 typedef struct cbx_plan cbx_plan;
@@ -160,14 +165,19 @@ int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const cbx_array* 
                     int32_t n_arrays, const cbx_plan_options* opts, cbx_plan** out_plan);
 void cbx_plan_destroy(cbx_plan* plan);
 
-/* Exact string payload sizes per column for a batch (first pass of the two-pass string
- * output); out_sizes[n_columns] (0 for non-string columns). */
+/* Upper bound of a string column's payload per slot for n_rec records (n_rec * field size *
+ * widest UTF-8 expansion of the code page); out_bytes[n_columns] (0 for non-string columns). */
+int cbx_string_bound(const cbx_plan* plan, int64_t n_rec, int64_t* out_bytes);
+
+/* Exact payload sizes (optional pre-pass, synchronous): out_sizes[n_columns] receives, per
+ * string column, the largest slot payload of the batch (0 for non-string columns). */
 int cbx_string_sizes_fixed(cbx_plan* plan, const uint8_t* d_records, int64_t n_rec,
                            int32_t rec_stride, int32_t start_offset, int64_t* out_sizes, void* stream);
 
 /* Fixed-length batch: record i occupies d_records[i*rec_stride, (i+1)*rec_stride) and is
  * decoded at +start_offset (CobolScanners.buildScanForFixedLength; record_start_offset).
- * Bounds rules of Primitive.decodeTypeValue apply against rec_stride. */
+ * Bounds rules of Primitive.decodeTypeValue apply against rec_stride.  Asynchronous on
+ * `stream` (one kernel launch); calls on one plan must be issued in order on one stream. */
 int cbx_decode_fixed(cbx_plan* plan, const uint8_t* d_records, int64_t n_rec, int32_t rec_stride,
                      int32_t start_offset, int64_t first_record_id, cbx_column* columns, void* stream);
 
@@ -180,10 +190,16 @@ int cbx_string_sizes_var(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes,
                          const int32_t* d_rec_len, int64_t n_rec, int32_t start_offset,
                          int64_t* out_sizes, void* stream);
 
-/* Optional per-call kernel timing with HIP events on the call's stream (bench / profiling):
- * when enabled, the last decode call's sizing-pass, scan and decode-pass durations (ms). */
+/* Synchronise `stream` and report device-side errors of the plan's earlier decode calls
+ * (CBX_E_CAPACITY: a string payload exceeded data_capacity). */
+int cbx_plan_check(cbx_plan* plan, void* stream);
+
+/* Optional kernel timing with HIP events on the call's stream (bench / profiling): while
+ * enabled, every decode call records events around its decode kernel and its fixup kernel
+ * (no synchronisation).  cbx_plan_kernel_times waits for the recorded events, returns up to
+ * max_calls per-call durations in ms (oldest first, *n_calls of them) and clears the record. */
 int cbx_plan_set_profiling(cbx_plan* plan, int32_t enable);
-int cbx_plan_last_kernel_ms(const cbx_plan* plan, float* sizes_ms, float* scan_ms, float* decode_ms);
+int cbx_plan_kernel_times(cbx_plan* plan, float* decode_ms, float* fixup_ms, int32_t max_calls, int32_t* n_calls);
 
 /* RDW header walk on the GPU (RecordHeaderParserRDW + VRLRecordReader), seeded by sparse-index
  * entry points: seeds[k] is a known record-header offset (offsetFrom of an index entry), the

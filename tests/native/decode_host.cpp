@@ -15,10 +15,23 @@ extern "C" int cbxh_decode(const cbx_field* cf, const uint8_t* p, int n_avail, c
     if (!is_str) {
         if (n_avail < f.size) return 0;  // Primitive.decodeTypeValue numeric bounds
         // the kernels' path: width-specialised decoders reading a (padded) byte image
-        uint8_t img[64 + 16] = {0};
-        for (int i = 0; i < f.size && i < 64; i++) img[i + 3] = p[i];
-        Val v = f.size <= 64 ? decode_numeric_at(f, img, 3) : decode_numeric(f, p);
+        alignas(16) uint8_t img[16 + 64 + 16];
+        for (int i = 0; i < (int)sizeof img; i++) img[i] = (uint8_t)(0x5A ^ i);   // guard garbage
+        const int at = 16 + (int)(reinterpret_cast<uintptr_t>(p) & 3);           // vary alignment
+        for (int i = 0; i < f.size && i < 64; i++) img[i + at] = p[i];
+        bool defer = false;
+        const NumOp op = make_numop(f, 0, 0, nullptr, nullptr, 0);
+        Val v = f.size <= 64 ? decode_value(op, img, at, defer) : decode_numeric(f, p);
         Val g = decode_numeric(f, p);   // generic byte-loop decoder must agree
+        if (defer) {
+            if (v.valid) return -1;    // a deferred value is left null for the fixup pass
+            v = g;                     // ... which decodes it with the byte-loop decoder
+        }
+        if (f.flags & CBX_F_DEPENDEE) {   // OCCURS DEPENDING ON decoder must agree as well
+            Val c = decode_count_int(f, p);
+            if (f.precision <= 18 && (f.flags & CBX_F_INTEGRAL) &&
+                (c.valid != g.valid || (g.valid && (int32_t)c.lo != (int32_t)g.lo))) return -1;
+        }
         if (g.valid != v.valid || (v.valid && (g.lo != v.lo || g.hi != v.hi))) return -1;
         *lo = v.lo;
         *hi = v.hi;
@@ -27,8 +40,8 @@ extern "C" int cbxh_decode(const cbx_field* cf, const uint8_t* p, int n_avail, c
     if (n_avail < 0) return 0;
     int n = f.size < n_avail ? f.size : n_avail;
     auto lutf = [&](uint32_t b) -> uint32_t { return f.kind == CBX_K_STRING_ASCII ? ascii_lut(b) : lut[b]; };
-    StrSpan s = string_span(f, p, n, lutf);
-    string_write(f, p, s, sbuf, lutf);
+    StrSpan s = string_span(f.kind, f.trim, p, n, lutf);
+    string_write(f.kind, p, s, sbuf, lutf);
     *slen = s.utf8_len;
     return 1;
 }

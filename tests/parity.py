@@ -58,7 +58,8 @@ def compare_batch(batch, res: "O.OracleResult", max_report: int = 10) -> List[st
             lo, hi = o["lo"][m], o["hi"][m]
             nbad = 0
             for k in range(len(v)):
-                a = data[int(off[v[k]]):int(off[v[k] + 1])]
+                so = off[slot[k]]   # per-slot Arrow offsets (absolute into data)
+                a = data[int(so[rec[k]]):int(so[rec[k] + 1])]
                 b = heap[int(lo[k]):int(lo[k]) + int(hi[k])]
                 if a != b:
                     nbad += 1

@@ -1,27 +1,53 @@
-"""The C-ABI library loads and exports every symbol include/cobrix_hip.h declares (no GPU calls)."""
+"""The C-ABI library loads and exports every symbol include/cobrix_hip.h declares, and the
+ctypes mirror of every ABI struct matches the C layout (no GPU calls)."""
 from __future__ import annotations
 
 import ctypes
 import os
 import re
+import subprocess
+
+import pytest
 
 from cobrix_amd import native as N
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "cobrix_hip.h")
 
 
 def test_header_symbols_exported():
-    hdr = open(os.path.join(ROOT, "include", "cobrix_hip.h")).read()
+    hdr = open(HDR).read()
     declared = set(re.findall(r"\b(cbx_[a-z_0-9]+)\s*\(", hdr))
     assert set(N.EXPORTED_SYMBOLS) == declared
     lib = N.load()
     for s in declared:
         assert getattr(lib, s) is not None
-    assert lib.cbx_abi_version() == 1
+    assert lib.cbx_abi_version() == N.ABI_VERSION
+    assert int(re.search(r"#define CBX_ABI_VERSION (\d+)", hdr).group(1)) == N.ABI_VERSION
 
 
-def test_struct_layout_matches_header():
-    # sizes of the ABI structs as compiled into the library's consumers
-    assert ctypes.sizeof(N.CbxField) == 4 * (12 + 3 * N.CBX_MAX_DIMS + 2)
-    assert ctypes.sizeof(N.CbxArray) == 32
-    assert ctypes.sizeof(N.CbxColumn) == 48
+STRUCTS = {"cbx_field": N.CbxField, "cbx_array": N.CbxArray, "cbx_segment_map": N.CbxSegmentMap,
+           "cbx_plan_options": N.CbxPlanOptions, "cbx_column": N.CbxColumn, "cbx_rdw_params": N.CbxRdwParams}
+
+
+def test_struct_layout_matches_header(tmp_path):
+    """sizeof / offsetof of every ABI struct as a C compiler sees include/cobrix_hip.h."""
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "cobrix_hip.h"', "int main(void) {"]
+    for cname, py in STRUCTS.items():
+        src.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            src.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    src.append("return 0; }")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    try:
+        subprocess.run(["gcc", "-I", os.path.dirname(HDR), "-o", str(exe), str(c)], check=True, capture_output=True)
+    except (OSError, subprocess.CalledProcessError) as e:  # pragma: no cover
+        pytest.skip(f"no C compiler: {e}")
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    for line in filter(None, out):
+        cname, what, val = line.split()
+        py = STRUCTS[cname]
+        got = ctypes.sizeof(py) if what == "sizeof" else getattr(py, what).offset
+        assert got == int(val), f"{cname}.{what}: ctypes {got} != C {val}"

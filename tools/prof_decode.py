@@ -15,17 +15,16 @@ def main():
     a = ap.parse_args()
     import torch
     from cobrix_amd import native as N
-    from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters, _alloc_columns
+    from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters, _alloc_columns, string_capacity
     from cobrix_amd.synth import SYN200_COPYBOOK, syn200
     rec = syn200(a.records, device="cuda").view(-1)
     rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters(window_bytes=a.window))
     L = N.load()
-    st = torch.cuda.current_stream()
-    sizes = (ctypes.c_int64 * rd.plan.n_columns)()
-    N.check(L.cbx_string_sizes_fixed(rd.native.handle, rec.data_ptr(), a.records, 200, 0, sizes, ctypes.c_void_p(st.cuda_stream)))
-    cols, cs = _alloc_columns(rd.plan, a.records, list(sizes), rec.device)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    cols, cs = _alloc_columns(rd.plan, a.records, string_capacity(rd.native, a.records), rec.device)
     for _ in range(a.iters):
-        N.check(L.cbx_decode_fixed(rd.native.handle, rec.data_ptr(), a.records, 200, 0, 0, cs, ctypes.c_void_p(st.cuda_stream)))
+        N.check(L.cbx_decode_fixed(rd.native.handle, rec.data_ptr(), a.records, 200, 0, 0, cs, st))
+    N.check(L.cbx_plan_check(rd.native.handle, st))
     torch.cuda.synchronize()
     print("done", flush=True)
 
