@@ -8,8 +8,9 @@
 //     `window_bytes` (windowed staging), each grouped into (field, slot range) runs so a
 //     window's decode loop is wave-uniform,
 //   * the UTF-8 code-page LUT and the segment-redefine keys.
-// Every decode call is asynchronous on the caller's stream: one kernel launch (plus memsets of
-// the look-back workspace); device-side data errors are reported by cbx_plan_check.
+// Every decode call is asynchronous on the caller's stream: the decode kernel, the fixup kernel
+// for deferred values, and for string columns a scan of per-tile payload totals plus the
+// placement kernel; device-side data errors are reported by cbx_plan_check.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -75,19 +76,44 @@ struct cbx_plan {
     uint32_t* d_lut = nullptr;
     DevColumn* d_cols = nullptr;
     std::vector<DevColumn> h_cols;         // host staging of the per-call column table
-    // workspace
-    uint64_t* d_lookback = nullptr;
-    int64_t lookback_cap = 0;
-    int64_t* d_seq_totals = nullptr;
-    uint32_t* d_ticket = nullptr;
+    std::vector<NumCall> h_ncall;          // per-call op address tables (host staging)
+    std::vector<StrCall> h_scall;
+    NumCall* d_ncall = nullptr;
+    StrCall* d_scall = nullptr;
+    size_t ncall_cap = 0, scall_cap = 0;
+    // string workspace (two-pass placement): per (sequence, tile) totals and their exclusive
+    // scan, tile-local value starts, per-tile payload scratch regions, per-sequence call table
+    std::vector<int32_t> seq_field, seq_slot;   // sequence -> (field, slot)
+    std::vector<int64_t> seq_tile_cap;          // bytes per tile region
+    std::vector<SeqCall> h_seqcall;
+    std::vector<int64_t> h_seq_scratch;         // per-call scratch offset of each sequence
+    SeqCall* d_seqcall = nullptr;
+    uint32_t* d_str_tot = nullptr;  int64_t str_tot_cap = 0;
+    int64_t* d_str_excl = nullptr;  int64_t str_excl_cap = 0;
+    int64_t* d_block_sums = nullptr; int64_t block_sums_cap = 0;
+    uint32_t* d_local = nullptr;    int64_t local_cap = 0;
+    uint8_t* d_scratch = nullptr;   int64_t scratch_cap = 0;
     int32_t* d_status = nullptr;
     int num_cus = 256;
-    // profiling: HIP events around the decode and fixup kernels of every call (no sync)
+    // profiling: HIP events around the decode kernel and the post passes of every call (no sync)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;     // free events
     struct CallEvents { hipEvent_t e[3]; };
     std::vector<CallEvents> ev_calls;    // recorded, not yet read
 };
+
+// grow a device buffer to at least `need` elements (contents not preserved)
+template <typename T>
+static int grow(T** p, int64_t* cap, int64_t need, hipStream_t st) {
+    if (need <= *cap) return CBX_OK;
+    HIP_CHECK(hipStreamSynchronize(st));
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIP_CHECK(hipMalloc((void**)p, sizeof(T) * std::max<int64_t>(need, 1)));
+    *cap = need;
+    return CBX_OK;
+}
 
 static hipEvent_t take_event(cbx_plan* P) {
     if (!P->ev_pool.empty()) { hipEvent_t e = P->ev_pool.back(); P->ev_pool.pop_back(); return e; }
@@ -142,6 +168,7 @@ static std::vector<Elem> field_elements(const cbx_plan* P, int fi) {
 static StrOp make_strop(const Field& d, const Elem& e) {
     StrOp o{};
     o.eo = e.eo; o.size = d.size; o.kind = (uint8_t)d.kind; o.trim = (uint8_t)d.trim; o.n_odo = (uint8_t)e.n_odo;
+    o.pad = (uint8_t)d.max_utf8;
     o.column = d.column; o.slot = e.slot; o.seq = d.seq + e.slot; o.segment = d.segment;
     for (int j = 0; j < CBX_MAX_DIMS; j++) { o.odo_arr[j] = e.odo_arr[j]; o.odo_idx[j] = e.odo_idx[j]; }
     return o;
@@ -300,6 +327,11 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
             if (f.kind == CBX_K_STRING) d.max_utf8 = lut_max;
             d.seq = P->n_seq;
             P->n_seq += d.n_slots;
+            for (int sl = 0; sl < d.n_slots; sl++) {
+                P->seq_field.push_back(i);
+                P->seq_slot.push_back(sl);
+                P->seq_tile_cap.push_back(((int64_t)kWave * f.size * d.max_utf8 + 15) & ~(int64_t)15);
+            }
             P->col_max_bytes[f.column] = f.size * d.max_utf8;
         } else if (d.variant == V_ZONED16 || d.variant == V_GENERIC) {
             d.defer = (int)P->hdefer.size();
@@ -358,8 +390,8 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     }
     if (opts->has_segments && (r = upload(&P->d_segmap, &sm, 1))) { cbx_plan_destroy(P); return r; }
     if (hipMalloc((void**)&P->d_cols, sizeof(DevColumn) * P->n_columns) != hipSuccess ||
-        hipMalloc((void**)&P->d_seq_totals, sizeof(int64_t) * std::max(1, P->n_seq)) != hipSuccess ||
-        hipMalloc((void**)&P->d_ticket, 64) != hipSuccess || hipMalloc((void**)&P->d_status, 64) != hipSuccess ||
+        hipMalloc((void**)&P->d_seqcall, sizeof(SeqCall) * std::max(1, P->n_seq)) != hipSuccess ||
+        hipMalloc((void**)&P->d_status, 64) != hipSuccess ||
         hipMemset(P->d_status, 0, 64) != hipSuccess) {
         cbx_plan_destroy(P);
         return fail(CBX_E_HIP, "cbx_plan_create: device allocation failed");
@@ -376,8 +408,10 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
     if (!P) return;
     (void)hipFree(P->d_fields); (void)hipFree(P->d_defer); (void)hipFree(P->d_defer_bits);
     free_set(P->cset); free_set(P->wset); (void)hipFree(P->d_arrays);
+    (void)hipFree(P->d_ncall); (void)hipFree(P->d_scall);
     (void)hipFree(P->d_segmap); (void)hipFree(P->d_lut); (void)hipFree(P->d_cols);
-    (void)hipFree(P->d_lookback); (void)hipFree(P->d_seq_totals); (void)hipFree(P->d_ticket); (void)hipFree(P->d_status);
+    (void)hipFree(P->d_seqcall); (void)hipFree(P->d_str_tot); (void)hipFree(P->d_str_excl); (void)hipFree(P->d_block_sums);
+    (void)hipFree(P->d_local); (void)hipFree(P->d_scratch); (void)hipFree(P->d_status);
     for (auto& e : P->ev_pool) (void)hipEventDestroy(e);
     for (auto& c : P->ev_calls) for (auto& e : c.e) if (e) (void)hipEventDestroy(e);
     delete P;
@@ -386,6 +420,22 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
 extern "C" int cbx_string_bound(const cbx_plan* P, int64_t n_rec, int64_t* out_bytes) {
     if (!P || n_rec < 0 || !out_bytes) return fail(CBX_E_ARGUMENT, "cbx_string_bound: invalid arguments");
     for (int c = 0; c < P->n_columns; c++) out_bytes[c] = P->col_is_string[c] ? n_rec * (int64_t)P->col_max_bytes[c] : 0;
+    return CBX_OK;
+}
+
+// Exclusive scan (int64) of the per-(sequence, tile) payload totals, sequences concatenated.
+static int string_scan(cbx_plan* P, int64_t n_tiles, hipStream_t st) {
+    const int64_t n = (int64_t)P->n_seq * n_tiles;
+    const int64_t nb = (n + kScanTile - 1) / kScanTile;
+    int r;
+    if ((r = grow(&P->d_str_excl, &P->str_excl_cap, n, st)) || (r = grow(&P->d_block_sums, &P->block_sums_cap, nb, st)))
+        return r;
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)P->d_str_tot, n,
+                       P->d_block_sums);
+    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, P->d_block_sums, nb);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)P->d_str_tot, n,
+                       (const int64_t*)P->d_block_sums, P->d_str_excl);
+    HIP_CHECK(hipGetLastError());
     return CBX_OK;
 }
 
@@ -405,6 +455,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.rec_len = c.rec_len;
     a.n_rec = c.n_rec;
     a.n_tiles = n_tiles;
+    a.pitch = n_tiles * kWave;
     a.stride = c.stride;
     a.start_off = c.start_off;
     a.first_record_id = c.first_record_id;
@@ -418,7 +469,11 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     const cbx_plan::OpSet& S = contig ? P->cset : P->wset;
     if (contig) {
         a.stride_dw = sdw;
-        a.cpitch = 4 * ((sdw & 1) ? sdw : sdw + 1);
+        // pad rows to an odd dword count only when the plain stride would give >= 4-way bank
+        // conflicts on the per-lane dword reads (gcd(stride_dw, 32) >= 4); 2-way is cheaper
+        // than the dword scatter padding costs
+        const int g = std::__gcd(sdw, 32);
+        a.cpitch = 4 * (g >= 4 ? ((sdw & 1) ? sdw : sdw + 1) : sdw);
         a.inv_stride_dw = 1.0f / (float)sdw;
         a.lds_rows = kGuard + kWave * a.cpitch + 16 + kGuard;
     } else {
@@ -432,9 +487,8 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.gops = (const CBX_CONST GenOp*)S.d_gops;
     a.lds_rows = (a.lds_rows + 15) & ~15;
     a.lds_counts = ((int)P->harrays.size() * kWave * 4 + 15) & ~15;
-    a.lds_agg = (S.max_str_items * 4 + 15) & ~15;
     a.str_stage = S.max_str_items > 0 ? P->str_stage : 0;
-    a.lds_wave = a.lds_rows + a.lds_counts + kWave * 8 + a.lds_agg + a.str_stage + 16;
+    a.lds_wave = a.lds_rows + a.lds_counts + a.str_stage + 16;
     a.lds_wave = (a.lds_wave + 15) & ~15;
     a.fields = (const CBX_CONST Field*)P->d_fields;
     a.arrays = (const CBX_CONST cbx_array*)P->d_arrays;
@@ -444,12 +498,21 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.lut = P->d_lut;
     a.cols = (const CBX_CONST DevColumn*)P->d_cols;
     a.n_seq = P->n_seq;
-    a.seq_totals = P->d_seq_totals;
-    a.ticket = P->d_ticket;
     a.status = P->d_status;
     if (n_tiles == 0) return CBX_OK;
 
-    // column table: stream-ordered upload from pageable host memory (staged by the runtime)
+    // column table + per-op address tables: stream-ordered uploads from pageable host memory
+    // (staged by the runtime, so the host vectors are free again when the call returns)
+    const int n_defer_seq = (int)P->hdefer.size();
+    if (mode == 0 && P->n_seq > 0) {
+        int rr;
+        P->h_seq_scratch.resize(P->n_seq);
+        int64_t scratch = 0;
+        for (int q = 0; q < P->n_seq; q++) { P->h_seq_scratch[q] = scratch; scratch += n_tiles * P->seq_tile_cap[q]; }
+        if ((rr = grow(&P->d_local, &P->local_cap, (int64_t)P->n_seq * a.pitch, st)) ||
+            (rr = grow(&P->d_scratch, &P->scratch_cap, scratch, st)))
+            return rr;
+    }
     if (mode == 0) {
         P->h_cols.resize(P->n_columns);
         for (int i = 0; i < P->n_columns; i++) {
@@ -463,40 +526,91 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
             P->h_cols[i] = d;
         }
         HIP_CHECK(hipMemcpyAsync(P->d_cols, P->h_cols.data(), sizeof(DevColumn) * P->n_columns, hipMemcpyHostToDevice, st));
-    }
-    // string workspace
-    if (P->n_seq > 0) {
-        if (mode == 0) {
-            const int64_t need = n_tiles * (int64_t)P->n_seq;
-            if (need > P->lookback_cap) {
+        if (n_defer_seq > 0) {
+            const int64_t need = n_tiles * (int64_t)n_defer_seq;
+            if (need > P->defer_bits_cap) {
                 HIP_CHECK(hipStreamSynchronize(st));
-                (void)hipFree(P->d_lookback);
-                P->d_lookback = nullptr;
-                HIP_CHECK(hipMalloc((void**)&P->d_lookback, sizeof(uint64_t) * need));
-                P->lookback_cap = need;
+                (void)hipFree(P->d_defer_bits);
+                P->d_defer_bits = nullptr;
+                HIP_CHECK(hipMalloc((void**)&P->d_defer_bits, sizeof(uint64_t) * need));
+                P->defer_bits_cap = need;
             }
-            HIP_CHECK(hipMemsetAsync(P->d_lookback, 0, sizeof(uint64_t) * need, st));
-            HIP_CHECK(hipMemsetAsync(P->d_ticket, 0, sizeof(uint32_t), st));
-        } else {
-            HIP_CHECK(hipMemsetAsync(P->d_seq_totals, 0, sizeof(int64_t) * P->n_seq, st));
         }
-    }
-    a.lookback = P->d_lookback;
-    const int n_defer = (int)P->hdefer.size();
-    if (mode == 0 && n_defer > 0) {
-        const int64_t need = n_tiles * (int64_t)n_defer;
-        if (need > P->defer_bits_cap) {
+        P->h_ncall.resize(S.nops.size());
+        for (size_t i = 0; i < S.nops.size(); i++) {
+            const NumOp& op = S.nops[i];
+            const cbx_column& col = columns[op.column];
+            NumCall nc{};
+            nc.values = (uint8_t*)col.values + (int64_t)op.slot * a.pitch * out_width(op.out_type);
+            nc.validity = col.validity + (int64_t)op.slot * n_tiles;
+            nc.defer = op.defer >= 0 ? P->d_defer_bits + (int64_t)op.defer * n_tiles : nullptr;
+            P->h_ncall[i] = nc;
+        }
+        P->h_scall.resize(S.sops.size());
+        for (size_t i = 0; i < S.sops.size(); i++) {
+            const StrOp& op = S.sops[i];
+            const cbx_column& col = columns[op.column];
+            StrCall sc{};
+            sc.validity = col.validity + (int64_t)op.slot * n_tiles;
+            sc.local = P->d_local + (int64_t)op.seq * a.pitch;
+            sc.scratch = P->d_scratch + P->h_seq_scratch[op.seq];
+            sc.tile_cap = P->seq_tile_cap[op.seq];
+            P->h_scall[i] = sc;
+        }
+        P->h_seqcall.resize(P->n_seq);
+        for (int q = 0; q < P->n_seq; q++) {
+            const Field& d = P->dfields_h[P->seq_field[q]];
+            const cbx_column& col = columns[d.column];
+            const int sl = P->seq_slot[q];
+            SeqCall sq{};
+            sq.offsets = col.offsets + (int64_t)sl * (a.pitch + 1);
+            sq.region = (int64_t)sl * col.data_capacity;
+            sq.data = col.data + sq.region;
+            sq.local = P->d_local + (int64_t)q * a.pitch;
+            sq.scratch = P->d_scratch + P->h_seq_scratch[q];
+            sq.size = col.data_sizes ? col.data_sizes + sl : nullptr;
+            sq.capacity = col.data_capacity;
+            sq.tile_cap = (int32_t)P->seq_tile_cap[q];
+            P->h_seqcall[q] = sq;
+        }
+        if (P->n_seq > 0)
+            HIP_CHECK(hipMemcpyAsync(P->d_seqcall, P->h_seqcall.data(), sizeof(SeqCall) * P->n_seq, hipMemcpyHostToDevice, st));
+        if (P->h_ncall.size() > P->ncall_cap) {
             HIP_CHECK(hipStreamSynchronize(st));
-            (void)hipFree(P->d_defer_bits);
-            P->d_defer_bits = nullptr;
-            HIP_CHECK(hipMalloc((void**)&P->d_defer_bits, sizeof(uint64_t) * need));
-            P->defer_bits_cap = need;
+            (void)hipFree(P->d_ncall);
+            P->d_ncall = nullptr;
+            HIP_CHECK(hipMalloc((void**)&P->d_ncall, sizeof(NumCall) * P->h_ncall.size()));
+            P->ncall_cap = P->h_ncall.size();
         }
+        if (P->h_scall.size() > P->scall_cap) {
+            HIP_CHECK(hipStreamSynchronize(st));
+            (void)hipFree(P->d_scall);
+            P->d_scall = nullptr;
+            HIP_CHECK(hipMalloc((void**)&P->d_scall, sizeof(StrCall) * P->h_scall.size()));
+            P->scall_cap = P->h_scall.size();
+        }
+        if (!P->h_ncall.empty())
+            HIP_CHECK(hipMemcpyAsync(P->d_ncall, P->h_ncall.data(), sizeof(NumCall) * P->h_ncall.size(), hipMemcpyHostToDevice, st));
+        if (!P->h_scall.empty())
+            HIP_CHECK(hipMemcpyAsync(P->d_scall, P->h_scall.data(), sizeof(StrCall) * P->h_scall.size(), hipMemcpyHostToDevice, st));
     }
+    a.ncall = (const CBX_CONST NumCall*)P->d_ncall;
+    a.scall = (const CBX_CONST StrCall*)P->d_scall;
+    // string workspace: per (sequence, tile) totals (written by the decode kernel for every tile)
+    int r;
+    if (P->n_seq > 0 && (r = grow(&P->d_str_tot, &P->str_tot_cap, (int64_t)P->n_seq * n_tiles, st))) return r;
+    a.str_tot = P->d_str_tot;
+    const int n_defer = n_defer_seq;
     a.defer_bits = P->d_defer_bits;
     const size_t lds = 1024 + (size_t)kWavesPerBlock * a.lds_wave;
     if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
-    const int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / lds));
+    // resident blocks per CU: the LDS bound and the runtime's occupancy (registers); the grid
+    // never exceeds what can be co-resident, so the static tile order of the look-back holds
+    int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / lds));
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, decode_kernel, kWave * kWavesPerBlock, lds) == hipSuccess &&
+        occ > 0)
+        blocks_per_cu = std::min(blocks_per_cu, occ);
     const int64_t blocks_needed = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t grid = std::min<int64_t>(blocks_needed, (int64_t)P->num_cus * blocks_per_cu);
     const bool prof = P->profiling && mode == 0;
@@ -514,6 +628,16 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                            (const CBX_CONST DeferSeq*)P->d_defer, n_defer);
         HIP_CHECK(hipGetLastError());
     }
+    if (P->n_seq > 0) {
+        if ((r = string_scan(P, n_tiles, st))) return r;
+        if (mode == 0) {
+            const unsigned gx = (unsigned)std::min<int64_t>(n_tiles, 4096);
+            hipLaunchKernelGGL(str_place_kernel, dim3(gx, (unsigned)P->n_seq), dim3(kWave), 0, st,
+                               (const CBX_CONST SeqCall*)P->d_seqcall, (const uint32_t*)P->d_str_tot,
+                               (const int64_t*)P->d_str_excl, n_tiles, c.n_rec, P->d_status);
+            HIP_CHECK(hipGetLastError());
+        }
+    }
     if (prof) {
         HIP_CHECK(hipEventRecord(ce.e[2], st));
         P->ev_calls.push_back(ce);
@@ -529,12 +653,20 @@ static int decode_common(cbx_plan* P, const CallShape& c, cbx_column* columns, i
         if (P->n_seq == 0 || c.n_rec == 0) return CBX_OK;
         int r = launch(P, c, nullptr, 1, st);
         if (r) return r;
-        std::vector<int64_t> tot(P->n_seq);
-        HIP_CHECK(hipMemcpyAsync(tot.data(), P->d_seq_totals, sizeof(int64_t) * P->n_seq, hipMemcpyDeviceToHost, st));
+        // sequence total = excl[last tile] + tot[last tile] - excl[first tile]
+        const int64_t n_tiles = (c.n_rec + kWave - 1) / kWave;
+        std::vector<int64_t> e0(P->n_seq), e1(P->n_seq);
+        std::vector<uint32_t> t1(P->n_seq);
+        for (int q = 0; q < P->n_seq; q++) {
+            HIP_CHECK(hipMemcpyAsync(&e0[q], P->d_str_excl + (int64_t)q * n_tiles, 8, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(&e1[q], P->d_str_excl + (int64_t)q * n_tiles + n_tiles - 1, 8, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(&t1[q], P->d_str_tot + (int64_t)q * n_tiles + n_tiles - 1, 4, hipMemcpyDeviceToHost, st));
+        }
         HIP_CHECK(hipStreamSynchronize(st));
-        for (const Field& d : P->dfields_h)
-            if (d.seq >= 0)
-                for (int s = 0; s < d.n_slots; s++) sizes_only[d.column] = std::max(sizes_only[d.column], tot[d.seq + s]);
+        for (int q = 0; q < P->n_seq; q++) {
+            const int col = P->dfields_h[P->seq_field[q]].column;
+            sizes_only[col] = std::max(sizes_only[col], e1[q] + (int64_t)t1[q] - e0[q]);
+        }
         return CBX_OK;
     }
     for (int i = 0; i < P->n_columns; i++)

@@ -649,18 +649,19 @@ CBX_HD Val fast_finish(const NumOp& op, U128 M, bool neg, bool valid) {
     return Val{R.lo, R.hi, valid};
 }
 
-CBX_HD Val decode_bcd8(const NumOp& op, const uint8_t* img, uint32_t addr) {
-    const uint64_t be = img_be(img, addr + op.size, op.size);
+// The *_raw decoders take the 8 bytes ending at the element's end (r1 = img_le64_ending(img,
+// end)) and, for 16-byte classes, the 8 before them (r0 = img_le64_ending(img, end - 8)).
+CBX_HD Val bcd8_raw(const NumOp& op, uint64_t r1) {
+    const uint64_t be = __builtin_bswap64(r1) & low_bytes_mask(op.size);
     const uint32_t sn = (uint32_t)be & 15u;
     const uint64_t dg = be >> 4;
     const bool valid = bcd_ok(dg) && (sn == 0xC || sn == 0xD || sn == 0xF);
     return fast_finish(op, u128(bcd16_bin(dg)), sn == 0xD, valid);
 }
 
-CBX_HD Val decode_bcd16(const NumOp& op, const uint8_t* img, uint32_t addr) {
-    const uint32_t end = addr + op.size;
-    const uint64_t lo = __builtin_bswap64(img_le64_ending(img, end));
-    const uint64_t hi = img_be(img, end - 8, op.size - 8);
+CBX_HD Val bcd16_raw(const NumOp& op, uint64_t r1, uint64_t r0) {
+    const uint64_t lo = __builtin_bswap64(r1);
+    const uint64_t hi = __builtin_bswap64(r0) & low_bytes_mask(op.size - 8);
     const uint32_t sn = (uint32_t)lo & 15u;
     const uint64_t dlo = lo >> 4;   // 15 digits
     const bool valid = bcd_ok(dlo) && bcd_ok(hi) && (sn == 0xC || sn == 0xD || sn == 0xF);
@@ -673,9 +674,8 @@ CBX_HD Val decode_bcd16(const NumOp& op, const uint8_t* img, uint32_t addr) {
     return fast_finish(op, M, sn == 0xD, valid);
 }
 
-CBX_HD Val decode_bin8(const NumOp& op, const uint8_t* img, uint32_t addr) {
+CBX_HD Val bin8_raw(const NumOp& op, uint64_t le) {
     const int n = op.size;
-    const uint64_t le = img_le64_ending(img, addr + n);
     uint64_t v = (op.flags & NF_BIG_ENDIAN) ? (__builtin_bswap64(le) & low_bytes_mask(n)) : (le >> (64 - 8 * n));
     bool neg = false;
     if (op.flags & NF_SIGNED) {
@@ -692,12 +692,11 @@ CBX_HD Val decode_bin8(const NumOp& op, const uint8_t* img, uint32_t addr) {
     return fast_finish(op, u128(neg ? (uint64_t)0 - v : v), neg, true);
 }
 
-CBX_HD Val decode_zoned16(const NumOp& op, const uint8_t* img, uint32_t addr, bool& defer) {
+CBX_HD Val zoned16_raw(const NumOp& op, uint64_t r1, uint64_t r0, bool& defer) {
     const int n = op.size;
-    const uint32_t end = addr + n;
     const uint64_t Z = 0xF0F0F0F0F0F0F0F0ull, L = 0x0F0F0F0F0F0F0F0Full;
-    uint64_t b1 = img_le64_ending(img, end);       // field bytes end-8 .. end-1 (last in the top byte)
-    uint64_t b0 = img_le64_ending(img, end - 8);   // end-16 .. end-9
+    uint64_t b1 = r1;   // field bytes end-8 .. end-1 (last in the top byte)
+    uint64_t b0 = r0;   // end-16 .. end-9
     // bytes in front of the field read as '0' digits (0xF0): leading zeros change nothing
     const uint64_t m1 = high_bytes_mask(n), m0 = high_bytes_mask(n - 8);
     b1 = (b1 & m1) | (Z & ~m1);
@@ -714,8 +713,7 @@ CBX_HD Val decode_zoned16(const NumOp& op, const uint8_t* img, uint32_t addr, bo
     return fast_finish(op, u128(v), neg, valid);
 }
 
-CBX_HD Val decode_fp(const NumOp& op, const uint8_t* img, uint32_t addr) {
-    const uint64_t le = img_le64_ending(img, addr + op.size);
+CBX_HD Val fp_raw(const NumOp& op, uint64_t le) {
     const bool lef = (op.flags & NF_LE_FP) != 0;
     if (op.flags & NF_FLOAT) {
         uint32_t w = (uint32_t)(le >> 32);
@@ -730,12 +728,13 @@ CBX_HD Val decode_fp(const NumOp& op, const uint8_t* img, uint32_t addr) {
 // `defer` (result null) when the value needs the byte-loop decoder: the kernels record it in
 // a deferral bitmap and the fixup kernel decodes it with decode_numeric.
 CBX_HD Val decode_value(const NumOp& op, const uint8_t* img, uint32_t addr, bool& defer) {
+    const uint32_t end = addr + op.size;
     switch (op.variant) {
-    case V_BCD8: return decode_bcd8(op, img, addr);
-    case V_BCD16: return decode_bcd16(op, img, addr);
-    case V_BIN8: return decode_bin8(op, img, addr);
-    case V_ZONED16: { Val x = decode_zoned16(op, img, addr, defer); return x; }
-    case V_FP: return decode_fp(op, img, addr);
+    case V_BCD8: return bcd8_raw(op, img_le64_ending(img, end));
+    case V_BCD16: return bcd16_raw(op, img_le64_ending(img, end), img_le64_ending(img, end - 8));
+    case V_BIN8: return bin8_raw(op, img_le64_ending(img, end));
+    case V_ZONED16: return zoned16_raw(op, img_le64_ending(img, end), img_le64_ending(img, end - 8), defer);
+    case V_FP: return fp_raw(op, img_le64_ending(img, end));
     default: defer = true; return null_val();
     }
 }
@@ -856,6 +855,83 @@ CBX_HD void string_write(int kind, const uint8_t* p, const StrSpan& s, uint8_t* 
         if (l > 1) out[k + 1] = (uint8_t)(e >> 8);
         if (l > 2) out[k + 2] = (uint8_t)(e >> 16);
         k += l;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Strings of at most kStrFastBytes bytes: the element's bytes are read from the record image
+// as dwords, each byte's LUT entry is looked up once, and trimming / UTF-8 length become bit
+// operations over per-byte masks (ctz / clz / popcount) -- no data-dependent loops.
+// ------------------------------------------------------------------------------------------
+constexpr int kStrFastBytes = 32;
+
+// bytes img[addr, addr + size) as 8 little-endian dwords (size <= 32; reads up to 36 bytes)
+CBX_HD void img_bytes32(const uint8_t* img, uint32_t addr, int size, uint32_t w[8]) {
+    const uint32_t* p = (const uint32_t*)(img + (addr & ~3u));
+    const uint32_t sh = addr & 3u;
+    uint32_t r[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) r[k] = 4 * k < size + 3 ? p[k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = align_bytes(r[k + 1], r[k], sh);
+}
+
+CBX_HD uint32_t ctz32(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
+CBX_HD uint32_t clz32(uint32_t x) { return (uint32_t)__builtin_clz(x); }
+CBX_HD uint32_t popc32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
+CBX_HD uint32_t bits_below(int k) { return k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u); }
+
+// Trimmed span + UTF-8 length (StringDecoders.decodeEbcdicString / decodeAsciiString +
+// StringTools.trim*) of the first n (<= size <= 32) bytes held in w.
+template <typename LutFn>
+CBX_HD StrSpan string_span32(int trim, const uint32_t w[8], int n, int size, LutFn lut) {
+    uint32_t keep = 0, m2 = 0, m3 = 0;   // bit j: byte j not trimmable / 2-byte / 3-byte UTF-8
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++) {
+        if (j < size) {
+            const uint32_t e = lut((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            const uint32_t l = (e >> 24) & 3u;
+            const uint32_t bit = 1u << j;
+            keep |= (e >> 31) ? 0u : bit;
+            m2 |= l == 2 ? bit : 0u;
+            m3 |= l == 3 ? bit : 0u;
+        }
+    }
+    keep &= bits_below(n);
+    const bool tl = trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH;
+    const bool tr = trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH;
+    int b = 0, e = n;
+    if (tl) b = keep ? (int)ctz32(keep) : n;
+    if (tr) e = keep ? 32 - (int)clz32(keep) : b;
+    const uint32_t range = bits_below(e) & ~bits_below(b);
+    StrSpan s;
+    s.begin = b;
+    s.end = e;
+    s.utf8_len = (e - b) + (int)popc32(m2 & range) + 2 * (int)popc32(m3 & range);
+    return s;
+}
+
+// UTF-8 bytes of the span into out[0, utf8_len); writes of bytes outside the span (and of the
+// unused 2nd / 3rd bytes of a character) go to `dump` instead of branching per lane.
+template <typename LutFn>
+CBX_HD void string_write32(const uint32_t w[8], const StrSpan& s, uint8_t* out, uint8_t* dump, int size,
+                           bool multibyte, LutFn lut) {
+    int k = 0;
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++) {
+        if (j < size) {
+            const bool in = j >= s.begin && j < s.end;
+            const uint32_t e = lut((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            *(in ? out + k : dump) = (uint8_t)e;
+            if (multibyte) {
+                const uint32_t l = (e >> 24) & 3u;
+                *(in && l > 1 ? out + k + 1 : dump) = (uint8_t)(e >> 8);
+                *(in && l > 2 ? out + k + 2 : dump) = (uint8_t)(e >> 16);
+                k += in ? (int)l : 0;
+            } else {
+                k += in ? 1 : 0;
+            }
+        }
     }
 }
 

@@ -24,7 +24,7 @@ constexpr int kMaxStrItems = 256;      // string (field, slot) items per window 
 struct StrOp {
     int32_t eo;                       // element offset in the record (before start_off)
     int32_t size;
-    uint8_t kind, trim, n_odo, pad;
+    uint8_t kind, trim, n_odo, pad;   // pad: widest UTF-8 expansion of a byte (1..3)
     int32_t column;
     int32_t slot;
     int32_t seq;                      // look-back sequence
@@ -41,6 +41,22 @@ struct Batch {
     int32_t begin, end;               // NumOp range
     int32_t odo;                      // ops carry OCCURS DEPENDING ON conditions
     int32_t reserved;
+};
+
+// Per-call output addresses of one numeric op (host-resolved column + slot bases).
+struct NumCall {
+    uint8_t* values;          // values of (column, slot): element r at values + r * width
+    uint64_t* validity;       // validity words of (column, slot): word t = tile t
+    uint64_t* defer;          // deferral words of the op's sequence (null if never deferred)
+    uint64_t reserved;
+};
+
+// Per-call addresses of one string op (tile-local pass).
+struct StrCall {
+    uint64_t* validity;       // validity words of (column, slot)
+    uint32_t* local;          // tile-local start of every value of the slot (pitch entries)
+    uint8_t* scratch;         // tile regions of the slot: tile t at scratch + t * tile_cap
+    int64_t tile_cap;         // bytes per tile region (64 * size * widest UTF-8 expansion, 16-aligned)
 };
 
 // Generated column (File_Id / Record_Id).
@@ -71,12 +87,6 @@ struct DevColumn {
     int64_t* sizes;        // strings: per-slot payload bytes (device, may be null)
 };
 
-// Decoupled look-back word: [63:62] state (0 empty, 1 tile aggregate, 2 inclusive prefix),
-// [61:0] byte count.
-constexpr uint64_t kLbAgg = 1ull << 62;
-constexpr uint64_t kLbPrefix = 2ull << 62;
-constexpr uint64_t kLbValue = (1ull << 62) - 1;
-
 struct KernelArgs {
     // input
     const uint8_t* data;
@@ -86,6 +96,7 @@ struct KernelArgs {
     const int32_t* rec_len;    // var-len: payload lengths
     int64_t n_rec;
     int64_t n_tiles;
+    int64_t pitch;             // values per slot row of every output column (64 * n_tiles)
     int32_t stride;            // fixed: record stride (avail length)
     int32_t start_off;         // record_start_offset
     int64_t first_record_id;
@@ -103,8 +114,10 @@ struct KernelArgs {
     const CBX_CONST Window* windows;
     int32_t n_windows;
     const CBX_CONST NumOp* nops;
+    const CBX_CONST NumCall* ncall;
     const CBX_CONST Batch* batches;
     const CBX_CONST StrOp* sops;
+    const CBX_CONST StrCall* scall;
     const CBX_CONST GenOp* gops;
     const CBX_CONST cbx_array* arrays;
     int32_t n_arrays;
@@ -114,15 +127,12 @@ struct KernelArgs {
     const CBX_CONST DevColumn* cols;
     // strings
     int32_t n_seq;             // string sequences = sum over string fields of n_slots
-    uint64_t* lookback;        // [n_tiles][n_seq] look-back words (zeroed per call)
-    int64_t* seq_totals;       // sizes mode: per-sequence totals (zeroed per call)
-    uint32_t* ticket;          // dynamic tile counter (zeroed per call)
+    uint32_t* str_tot;         // [n_seq][n_tiles] payload bytes of every (sequence, tile)
     int32_t* status;           // [0]: capacity overflow flag
     uint64_t* defer_bits;      // [n_defer][n_tiles] values left to the fixup kernel
     // LDS layout (bytes, per wave)
     int32_t lds_rows;          // record image incl. guards
     int32_t lds_counts;        // OCCURS element counts
-    int32_t lds_agg;           // string element aggregates of a window (4 B each)
     int32_t str_stage;         // string payload staging bytes
     int32_t lds_wave;          // total per wave
 };

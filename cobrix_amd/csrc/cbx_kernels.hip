@@ -15,32 +15,34 @@
 //     (record, 16-byte chunk) pairs are spread over the lanes.
 // Validity bits come from one 64-lane ballot per (field, slot).
 //
-// String columns are produced in ONE pass with a decoupled look-back across tiles: a tile
-// publishes its per-sequence UTF-8 byte total (aggregate) before decoding its numeric fields,
-// then resolves its exclusive base from its predecessors' words, publishes its inclusive prefix
-// and writes its payload (staged in LDS, copied out with dword stores).  Tiles are handed out
-// by an atomic ticket so every tile a wave waits on is already owned by a running wave.
+// String columns: the decode kernel computes every value's trimmed span and UTF-8 length, a
+// DPP wave scan gives tile-local positions, and the tile's payload (staged in LDS, copied with
+// dword stores) goes to a per-tile scratch region; a device-wide scan of the per-tile totals
+// and the placement kernel then write the final payload and absolute offsets.  (A single-pass
+// decoupled look-back was measured slower on this chip: device-scope atomics and look-back
+// probes are memory-side round trips, and ~2,500 tiles are in flight at once -- DESIGN.md.)
 #include <hip/hip_runtime.h>
 
 #include "cbx_internal.h"
 
 namespace cbx {
 
-__device__ __forceinline__ int64_t wave_excl_scan(int64_t x, int lane, int64_t* total) {
-    int64_t v = x;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        int64_t y = __shfl_up(v, d, kWave);
-        if (lane >= d) v += y;
-    }
-    *total = __shfl(v, kWave - 1, kWave);
+// Exclusive scan of a 32-bit value over the wave with DPP row shifts (Hillis-Steele inside
+// each 16-lane row) plus the preceding rows' totals read with v_readlane.  All lanes active.
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t x, int lane, uint32_t& total) {
+    uint32_t v = x;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+    const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    const int row = lane >> 4;
+    v += (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+    total = r0 + r1 + r2 + r3;
     return v - x;
-}
-
-__device__ __forceinline__ int32_t wave_sum32(int32_t x) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, kWave);
-    return x;
 }
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -60,13 +62,6 @@ __device__ __forceinline__ T ldc(const CBX_CONST T* p) {
     T r;
     __builtin_memcpy(&r, w, sizeof(T));
     return r;
-}
-
-__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // 16 bytes at data + ga (ga 16-byte aligned); bytes outside [0, len) read as 0.
@@ -148,23 +143,32 @@ __device__ __forceinline__ uint32_t str_lut(int kind, const uint32_t* s_lut, uin
 }
 
 // String element of the current tile: trimmed span + UTF-8 length (StringDecoders / StringTools).
+// Elements of at most kStrFastBytes EBCDIC/ASCII bytes keep their bytes in `w` (register path).
 __device__ __forceinline__ StrSpan sop_span(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
                                             const TileCtx& t, const int32_t* s_cnt, int lane, const uint8_t* src,
-                                            uint32_t rec_addr, const uint32_t* s_lut, bool& ok) {
+                                            uint32_t rec_addr, const uint32_t* s_lut, bool& ok, bool fast, uint32_t w[8]) {
     bool el = t.active && (op.segment < 0 || op.segment == t.seg);
     if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
     const int o = a.start_off + op.eo;
     ok = el && o <= t.avail;
     const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
+    auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
+    if (fast) {
+        img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
+        return string_span32(op.trim, w, n, op.size, lutf);
+    }
     StrSpan sp{0, 0, 0};
-    if (ok) sp = string_span(op.kind, op.trim, src + rec_addr + (uint32_t)op.eo, n,
-                             [&](uint32_t b) { return str_lut(op.kind, s_lut, b); });
+    if (ok) sp = string_span(op.kind, op.trim, src + rec_addr + (uint32_t)op.eo, n, lutf);
     return sp;
 }
 
-// W = output bytes per value; W = 0: width from the op's output type (generic batches)
+__device__ __forceinline__ bool sop_fast(const StrOp& op, bool global) {
+    return !global && op.size <= kStrFastBytes && (op.kind == CBX_K_STRING || op.kind == CBX_K_STRING_ASCII);
+}
+
 template <int W>
 __device__ __forceinline__ void store_w(void* values, int64_t v, const Val& x, int out_type) {
+    // v: element index within the slot row
     const int w = W ? W : (out_type == CBX_O_I32 || out_type == CBX_O_F32 ? 4 : out_type == CBX_O_DEC128 ? 16 : 8);
     if (w == 4) ((uint32_t*)values)[v] = (uint32_t)x.lo;
     else if (w == 8) ((uint64_t*)values)[v] = x.lo;
@@ -176,34 +180,116 @@ __device__ __forceinline__ void store_w(void* values, int64_t v, const Val& x, i
 // conditions only select validity.  The validity (and deferral) word of each op is a wave
 // ballot stored by every lane to the same address.
 template <int V, int W, bool kOdo, bool kGlobal>
+__device__ __forceinline__ void num_one(const KernelArgs& a, const NumOp& op, int i, const TileCtx& t,
+                                        bool ok, uint64_t r1, uint64_t r0, const int32_t* s_cnt, int lane) {
+    if (op.segment >= 0) ok &= op.segment == t.seg;
+    if (kOdo) ok &= odo_present(a.nops + i, op.n_odo, s_cnt, lane);
+    Val x = null_val();
+    bool defer = false;
+    if (kGlobal || V == V_GENERIC) {
+        defer = ok;
+    } else {
+        if (V == V_BCD8) x = bcd8_raw(op, r1);
+        else if (V == V_BCD16) x = bcd16_raw(op, r1, r0);
+        else if (V == V_BIN8) x = bin8_raw(op, r1);
+        else if (V == V_ZONED16) { x = zoned16_raw(op, r1, r0, defer); defer &= ok; }
+        else if (V == V_FP) x = fp_raw(op, r1);
+        x.valid &= ok;
+    }
+    const NumCall c = ldc(a.ncall + i);
+    // every lane stores (slot rows are padded to 64 * n_tiles values): no exec-mask branches
+    store_w<W>(c.values, t.rec, x, op.out_type);
+    const uint64_t m = __ballot(x.valid);
+    c.validity[t.tile] = m;
+    if (V == V_ZONED16 || V == V_GENERIC || kGlobal) {
+        const uint64_t dm = __ballot(defer);
+        if (c.defer) c.defer[t.tile] = dm;
+    }
+}
+
+// One batch of numeric ops (same decoder variant V, output width W), four ops per step: the
+// LDS reads of the four elements are issued before any of them is decoded.  Decoding is
+// branch-free per lane: every lane reads its (clamped) element and computes, the bounds /
+// segment / OCCURS conditions only select validity.  The validity (and deferral) word of each
+// op is a wave ballot stored by every lane to the same address.
+template <int V, int W, bool kOdo, bool kGlobal>
 __device__ __forceinline__ void num_batch(const KernelArgs& a, const Batch& b, const TileCtx& t, const uint8_t* src,
                                           uint32_t rec_addr, const int32_t* s_cnt, int lane) {
+    constexpr bool kWide = V == V_BCD16 || V == V_ZONED16;   // two 8-byte reads per element
+    constexpr bool kRead = !(kGlobal || V == V_GENERIC);
     const int lim = t.active ? t.avail - a.start_off : -1;   // element must end within the record
-    for (int i = b.begin; i < b.end; i++) {
-        const NumOp op = ldc(a.nops + i);
-        bool ok = op.eo + op.size <= lim;
-        if (op.segment >= 0) ok &= op.segment == t.seg;
-        if (kOdo) ok &= odo_present(a.nops + i, op.n_odo, s_cnt, lane);
-        Val x = null_val();
-        bool defer = false;
-        if (kGlobal || V == V_GENERIC) {
-            defer = ok;
-        } else {
-            const uint32_t addr = rec_addr + (ok ? (uint32_t)op.eo : 0u);
-            if (V == V_BCD8) x = decode_bcd8(op, src, addr);
-            else if (V == V_BCD16) x = decode_bcd16(op, src, addr);
-            else if (V == V_BIN8) x = decode_bin8(op, src, addr);
-            else if (V == V_ZONED16) { x = decode_zoned16(op, src, addr, defer); defer &= ok; }
-            else if (V == V_FP) x = decode_fp(op, src, addr);
-            x.valid &= ok;
+    constexpr int U = 4;
+    int i = b.begin;
+    for (; i + U <= b.end; i += U) {
+        NumOp op[U];
+        bool ok[U];
+        uint64_t r1[U], r0[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            op[u] = ldc(a.nops + i + u);
+            ok[u] = op[u].eo + op[u].size <= lim;
+            r1[u] = r0[u] = 0;
+            if (kRead) {
+                const uint32_t end = rec_addr + (ok[u] ? (uint32_t)op[u].eo : 0u) + op[u].size;
+                r1[u] = img_le64_ending(src, end);
+                if (kWide) r0[u] = img_le64_ending(src, end - 8);
+            }
         }
-        const DevColumn col = ldc(a.cols + op.column);
-        if (t.active) store_w<W>(col.values, (int64_t)op.slot * a.n_rec + t.rec, x, op.out_type);
-        const uint64_t m = __ballot(x.valid);
-        col.validity[(int64_t)op.slot * a.n_tiles + t.tile] = m;
-        if (V == V_ZONED16 || V == V_GENERIC || kGlobal) {
-            const uint64_t dm = __ballot(defer);
-            if (op.defer >= 0) a.defer_bits[(int64_t)op.defer * a.n_tiles + t.tile] = dm;
+#pragma unroll
+        for (int u = 0; u < U; u++) num_one<V, W, kOdo, kGlobal>(a, op[u], i + u, t, ok[u], r1[u], r0[u], s_cnt, lane);
+    }
+    for (; i < b.end; i++) {
+        const NumOp op = ldc(a.nops + i);
+        const bool ok = op.eo + op.size <= lim;
+        uint64_t r1 = 0, r0 = 0;
+        if (kRead) {
+            const uint32_t end = rec_addr + (ok ? (uint32_t)op.eo : 0u) + op.size;
+            r1 = img_le64_ending(src, end);
+            if (kWide) r0 = img_le64_ending(src, end - 8);
+        }
+        num_one<V, W, kOdo, kGlobal>(a, op, i, t, ok, r1, r0, s_cnt, lane);
+    }
+}
+
+// One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):
+// span + tile-local scan; the tile's payload is staged contiguously in LDS and copied with
+// dword stores to the tile's scratch region; the tile-local start of every value and the
+// tile's byte total are recorded for the compaction kernel, which places tiles after a
+// device-wide scan of the totals (two-pass string offsets, no cross-tile waiting).
+__device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
+                                            const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
+                                            const uint8_t* src, uint32_t rec_addr, bool global,
+                                            const uint32_t* s_lut, uint8_t* s_str, int lane) {
+    const bool fast = sop_fast(op, global);
+    bool ok;
+    uint32_t wb[8];
+    const StrSpan sp = sop_span(a, op, opp, t, s_cnt, lane, src, rec_addr, s_lut, ok, fast, wb);
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32((uint32_t)sp.utf8_len, lane, tot);
+    if (a.mode == 1) {
+        if (lane == 0) a.str_tot[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
+        return;
+    }
+    c.validity[t.tile] = __ballot(ok);
+    c.local[t.rec] = ex;
+    if (lane == 0) a.str_tot[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
+    auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
+    const uint8_t* sp_src = src + rec_addr + (uint32_t)op.eo;
+    uint32_t* dst32 = (uint32_t*)(c.scratch + t.tile * (int64_t)c.tile_cap);   // 16-byte aligned region
+    if ((int)tot <= a.str_stage) {
+        if (fast) string_write32(wb, sp, s_str + ex, s_str + a.str_stage, op.size, op.pad > 1, lutf);
+        else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
+        wave_sync_lds();
+        const uint32_t* s32 = (const uint32_t*)s_str;
+        for (int q = lane; 4 * q < (int)tot; q += kWave) dst32[q] = s32[q];
+        wave_sync_lds();
+    } else if (ok) {
+        uint8_t* dst = (uint8_t*)dst32 + ex;
+        if (fast) {
+            uint8_t dump[4];
+            string_write32(wb, sp, dst, dump, op.size, op.pad > 1, lutf);
+        } else {
+            string_write(op.kind, sp_src, sp, dst, lutf);
         }
     }
 }
@@ -213,19 +299,13 @@ __device__ __forceinline__ void num_batch(const KernelArgs& a, const Batch& b, c
 template <bool kGlobal>
 __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window& w, const TileCtx& t, const uint8_t* src,
                                               uint32_t rec_addr, const int32_t* s_cnt, const uint32_t* s_lut,
-                                              uint8_t* s_str, uint64_t* s_scr, uint32_t* s_agg, int lane) {
+                                              uint8_t* s_str, int lane) {
     const bool sizes = a.mode == 1;
-    // ---- strings, phase A: per-element tile aggregates (kept in LDS for phase C)
+    // ---- strings (tile-local; placed by the compaction kernel)
     for (int i = w.sop_begin; i < w.sop_end; i++) {
         const StrOp op = ldc(a.sops + i);
-        bool ok;
-        const StrSpan sp = sop_span(a, op, a.sops + i, t, s_cnt, lane, src, rec_addr, s_lut, ok);
-        const int32_t agg = wave_sum32(sp.utf8_len);
-        if (lane == 0) {
-            s_agg[i - w.sop_begin] = (uint32_t)agg;
-            if (sizes) atomicAdd((unsigned long long*)&a.seq_totals[op.seq], (unsigned long long)agg);
-            else lb_store(&a.lookback[t.tile * a.n_seq + op.seq], (t.tile == 0 ? kLbPrefix : kLbAgg) | (uint64_t)agg);
-        }
+        const StrCall c = sizes ? StrCall{} : ldc(a.scall + i);
+        str_element(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
     }
     if (sizes) return;
     // ---- generated columns (File_Id / Record_Id)
@@ -273,84 +353,6 @@ __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window&
 #undef CBX_BATCH
     }
     if (w.sop_begin == w.sop_end) return;
-    wave_sync_lds();
-    // ---- strings, phase C: resolve bases (look-back), write offsets + payload
-    for (int i0 = w.sop_begin; i0 < w.sop_end; i0 += kWave) {
-        const int ni = min(kWave, w.sop_end - i0);
-        // lane k resolves element i0 + k
-        if (lane < ni) {
-            const int seq = a.sops[i0 + lane].seq;
-            uint64_t* me = &a.lookback[t.tile * a.n_seq + seq];
-            uint64_t excl = 0;
-            if (t.tile > 0) {
-                int64_t j = t.tile - 1;
-                while (true) {
-                    const uint64_t wv = lb_load(&a.lookback[j * a.n_seq + seq]);
-                    const uint64_t st = wv >> 62;
-                    if (st == 0) { __builtin_amdgcn_s_sleep(1); continue; }
-                    excl += wv & kLbValue;
-                    if (st == 2) break;
-                    j--;
-                }
-                lb_store(me, kLbPrefix | (excl + s_agg[i0 - w.sop_begin + lane]));
-            }
-            s_scr[lane] = excl;
-        }
-        wave_sync_lds();
-        for (int k = 0; k < ni; k++) {
-            const StrOp op = ldc(a.sops + i0 + k);
-            const DevColumn col = ldc(a.cols + op.column);
-            bool ok;
-            const StrSpan sp = sop_span(a, op, a.sops + i0 + k, t, s_cnt, lane, src, rec_addr, s_lut, ok);
-            int64_t tot;
-            const int64_t ex = wave_excl_scan(sp.utf8_len, lane, &tot);
-            const int64_t tbase = (int64_t)s_scr[k];
-            const int64_t region = (int64_t)op.slot * col.capacity;
-            const bool fits = tbase + tot <= col.capacity;
-            const int64_t ob = (int64_t)op.slot * (a.n_rec + 1);
-            if (t.active) {
-                col.offsets[ob + t.rec] = region + tbase + ex;
-                if (t.rec == a.n_rec - 1) {
-                    col.offsets[ob + a.n_rec] = region + tbase + ex + sp.utf8_len;
-                    if (col.sizes) col.sizes[op.slot] = tbase + ex + sp.utf8_len;
-                }
-            }
-            const uint64_t m = __ballot(ok);
-            if (lane == 0) col.validity[(int64_t)op.slot * a.n_tiles + t.tile] = m;
-            if (!fits) {
-                if (lane == 0) atomicOr(a.status, 1);
-                continue;
-            }
-            auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
-            const uint8_t* sp_src = src + rec_addr + (uint32_t)op.eo;
-            uint8_t* gdst = col.data + region + tbase;
-            if (tot <= a.str_stage) {
-                // stage the tile's payload contiguously in LDS, copy out with dword stores
-                if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
-                wave_sync_lds();
-                const uint64_t g0 = (uint64_t)gdst;
-                const uint64_t A = (g0 + 3) & ~3ull, B = (g0 + tot) & ~3ull;
-                if (A > B) {   // payload inside one dword: byte stores
-                    if (lane < tot) gdst[lane] = s_str[lane];
-                } else {
-                    const int head = (int)(A - g0), tail = (int)(g0 + tot - B);
-                    if (lane < head) gdst[lane] = s_str[lane];
-                    if (lane < tail) gdst[(int)(B - g0) + lane] = s_str[(int)(B - g0) + lane];
-                    const int ndw = (int)((B - A) >> 2);
-                    const uint32_t* s32 = (const uint32_t*)s_str;
-                    uint32_t* d32 = (uint32_t*)A;
-                    for (int q = lane; q < ndw; q += kWave) {
-                        const uint32_t byte = (uint32_t)head + 4u * (uint32_t)q;
-                        const uint32_t lo = s32[byte >> 2], hi = s32[(byte >> 2) + 1];
-                        d32[q] = align_bytes(hi, lo, byte & 3u);
-                    }
-                }
-                wave_sync_lds();
-            } else if (ok) {
-                string_write(op.kind, sp_src, sp, gdst + ex, lutf);
-            }
-        }
-    }
 }
 
 // Contiguous staging of a fixed-length tile: the tile's byte span [t0b, t0b + n * stride) is
@@ -444,21 +446,12 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void decode_kernel(KernelAr
     uint8_t* wbase = smem + 1024 + wid * a.lds_wave;
     uint8_t* s_img = wbase + kGuard;
     int32_t* s_cnt = (int32_t*)(wbase + a.lds_rows);
-    uint64_t* s_scr = (uint64_t*)(wbase + a.lds_rows + a.lds_counts);
-    uint32_t* s_agg = (uint32_t*)(wbase + a.lds_rows + a.lds_counts + kWave * 8);
-    uint8_t* s_str = wbase + a.lds_rows + a.lds_counts + kWave * 8 + a.lds_agg;
+    uint8_t* s_str = wbase + a.lds_rows + a.lds_counts;
     for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lut[i] = a.lut[i];
     __syncthreads();
 
-    const bool dynamic = a.n_seq > 0 && a.mode == 0;
-    int64_t tile;
-    if (dynamic) {
-        uint32_t tk = 0;
-        if (lane == 0) tk = atomicAdd(a.ticket, 1u);
-        tile = __shfl((int)tk, 0, kWave);
-    } else {
-        tile = (int64_t)blockIdx.x * kWavesPerBlock + wid;
-    }
+    // static grid-stride tile order (tiles are independent)
+    int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid;
     const int64_t tstep = (int64_t)gridDim.x * kWavesPerBlock;
 
     while (tile < a.n_tiles) {
@@ -512,29 +505,152 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void decode_kernel(KernelAr
             }
         }
 
-        // ---- next tile (ticket taken early: its owner is this wave, so waiters progress)
-        int64_t next;
-        if (dynamic) {
-            uint32_t tk = 0;
-            if (lane == 0) tk = atomicAdd(a.ticket, 1u);
-            next = __shfl((int)tk, 0, kWave);
-        } else {
-            next = tile + tstep;
-        }
-
         for (int wi = 0; wi < a.n_windows; wi++) {
             const Window w = ldc(a.windows + wi);
             if (a.mode == 1 && w.sop_begin == w.sop_end) continue;
             if (w.global) {
-                decode_window<true>(a, w, t, rp, 0u, s_cnt, s_lut, s_str, s_scr, s_agg, lane);
+                decode_window<true>(a, w, t, rp, 0u, s_cnt, s_lut, s_str, lane);
                 continue;
             }
             const uint32_t rec_addr = a.contig ? stage_contig(a, tile, s_img, lane) : stage_window(a, w, t, s_img, lane);
             wave_sync_lds();
-            decode_window<false>(a, w, t, (const uint8_t*)s_img, rec_addr, s_cnt, s_lut, s_str, s_scr, s_agg, lane);
+            decode_window<false>(a, w, t, (const uint8_t*)s_img, rec_addr, s_cnt, s_lut, s_str, lane);
             wave_sync_lds();
         }
-        tile = next;
+        tile += tstep;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// String placement.  Exclusive scan of the per-(sequence, tile) payload totals (one int64 array
+// over all sequences; a sequence's base is subtracted by the compaction kernel), then one wave
+// per (sequence, tile) copies the tile's payload from its scratch region to its final place and
+// writes the absolute Arrow offsets.
+// ------------------------------------------------------------------------------------------
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanBlock * kScanItems;
+
+__device__ __forceinline__ int64_t block_excl_scan64(int64_t x, int64_t* s_w, int64_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int64_t v = x;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const int64_t y = __shfl_up(v, d, kWave);
+        if (lane >= d) v += y;
+    }
+    if (lane == kWave - 1) s_w[wid] = v;
+    __syncthreads();
+    int64_t pre = 0, all = 0;
+    for (int i = 0; i < kScanBlock / kWave; i++) {
+        if (i < wid) pre += s_w[i];
+        all += s_w[i];
+    }
+    __syncthreads();
+    *total = all;
+    return pre + v - x;
+}
+
+// pass 1: per-block sums of uint32 totals
+__global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t* in, int64_t n, int64_t* block_sums) {
+    __shared__ int64_t s_w[kScanBlock / kWave];
+    const int64_t b0 = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    int64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) sum += b0 + i < n ? in[b0 + i] : 0u;
+    int64_t total;
+    block_excl_scan64(sum, s_w, &total);
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
+}
+
+// pass 2: exclusive scan of the block sums (one block, loops)
+__global__ __launch_bounds__(kScanBlock) void scan_block_sums_kernel(int64_t* block_sums, int64_t nb) {
+    __shared__ int64_t s_w[kScanBlock / kWave];
+    int64_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += kScanBlock) {
+        const int64_t i = b0 + threadIdx.x;
+        const int64_t x = i < nb ? block_sums[i] : 0;
+        int64_t total;
+        const int64_t ex = block_excl_scan64(x, s_w, &total);
+        if (i < nb) block_sums[i] = carry + ex;
+        carry += total;
+    }
+}
+
+// pass 3: exclusive prefix of every element
+__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint32_t* in, int64_t n, const int64_t* block_sums,
+                                                                int64_t* out) {
+    __shared__ int64_t s_w[kScanBlock / kWave];
+    const int64_t b0 = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    int64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        v[i] = b0 + i < n ? in[b0 + i] : 0u;
+        sum += v[i];
+    }
+    int64_t total;
+    int64_t ex = block_excl_scan64(sum, s_w, &total) + block_sums[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        if (b0 + i < n) out[b0 + i] = ex;
+        ex += v[i];
+    }
+}
+
+struct SeqCall {
+    int64_t* offsets;       // slot offsets (pitch + 1 entries)
+    uint8_t* data;          // slot payload region
+    const uint32_t* local;  // tile-local starts of the slot's values
+    const uint8_t* scratch; // tile regions of the slot
+    int64_t* size;          // slot payload bytes (may be null)
+    int64_t region;         // region position in the column's data
+    int64_t capacity;
+    int32_t tile_cap;
+    int32_t reserved;
+};
+
+__global__ __launch_bounds__(kWave) void str_place_kernel(const CBX_CONST SeqCall* seqs, const uint32_t* tot,
+                                                          const int64_t* excl, int64_t n_tiles, int64_t n_rec,
+                                                          int32_t* status) {
+    const int seq = blockIdx.y;
+    const int lane = threadIdx.x;
+    const SeqCall q = ldc(seqs + seq);
+    const int64_t seq0 = excl[(int64_t)seq * n_tiles];
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int64_t base = excl[(int64_t)seq * n_tiles + tile] - seq0;
+        const uint32_t n = tot[(int64_t)seq * n_tiles + tile];
+        const int64_t rec = tile * kWave + lane;
+        q.offsets[rec] = q.region + base + q.local[rec];   // lanes past n_rec write padding entries
+        if (tile == n_tiles - 1 && lane == 0) {
+            q.offsets[n_rec] = q.region + base + n;
+            if (q.size) *q.size = base + n;
+        }
+        if (base + (int64_t)n > q.capacity) {
+            if (lane == 0) atomicOr(status, 1);
+            continue;
+        }
+        // payload: scratch (aligned) -> data + base (any alignment); dword stores in the middle,
+        // byte stores for the unaligned head and tail
+        const uint32_t* src = (const uint32_t*)(q.scratch + tile * (int64_t)q.tile_cap);
+        uint8_t* dst = q.data + base;
+        const uint64_t g0 = (uint64_t)dst;
+        const uint64_t A = (g0 + 3) & ~3ull, B = (g0 + n) & ~3ull;
+        const uint8_t* s8 = (const uint8_t*)src;
+        if (A > B) {
+            if (lane < (int)n) dst[lane] = s8[lane];
+            continue;
+        }
+        const int head = (int)(A - g0), tail = (int)(g0 + n - B);
+        if (lane < head) dst[lane] = s8[lane];
+        if (lane < tail) dst[(int)(B - g0) + lane] = s8[(int)(B - g0) + lane];
+        const int ndw = (int)((B - A) >> 2);
+        uint32_t* d32 = (uint32_t*)A;
+        for (int i = lane; i < ndw; i += kWave) {
+            const uint32_t byte = (uint32_t)head + 4u * (uint32_t)i;
+            const uint32_t lo = src[byte >> 2], hi = src[(byte >> 2) + 1];
+            d32[i] = align_bytes(hi, lo, byte & 3u);
+        }
     }
 }
 
@@ -571,7 +687,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(KernelArgs a, const CBX_CONS
         const int64_t rec = tile * kWave + b;
         const int64_t base = a.base_shift + (a.rec_off ? a.rec_off[rec] : rec * (int64_t)a.stride);
         const Val x = decode_numeric(f, a.data + base + a.start_off + eo);
-        store_value(col, f.out_type, (int64_t)ds.slot * a.n_rec + rec, x);
+        store_value(col, f.out_type, (int64_t)ds.slot * a.pitch + rec, x);
         if (x.valid) vbits |= 1ull << b;
     }
     if (vbits) col.validity[(int64_t)ds.slot * a.n_tiles + tile] |= vbits;

@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_string_bound", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
                     "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
                     "cbx_plan_kernel_times")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class NativeLibraryError(RuntimeError):

@@ -87,20 +87,21 @@ class DecodedBatch:
     def host_column(self, ci: int) -> Dict[str, Any]:
         c = self.cols[ci]
         info = self.plan.columns[ci]
-        n = self.n_rec * info.n_slots
         pitch = (self.n_rec + 63) // 64
         out: Dict[str, Any] = {"validity": None, "values": None}
         vb = c["validity"].cpu().numpy().view(np.uint64)
         bits = np.unpackbits(vb.view(np.uint8), bitorder="little").reshape(info.n_slots, pitch * 64)
         out["validity"] = bits[:, :self.n_rec].astype(bool)
         if c.get("offsets") is not None:
-            # slot s: offsets[s * (n_rec + 1) .. + n_rec], absolute into data (slot regions)
-            out["offsets"] = c["offsets"].cpu().numpy().reshape(info.n_slots, self.n_rec + 1)
+            # slot s: offsets[s * (pitch + 1) .. + n_rec], absolute into data (slot regions)
+            out["offsets"] = c["offsets"].cpu().numpy().reshape(info.n_slots, 64 * pitch + 1)[:, : self.n_rec + 1]
             out["data"] = c["data"].cpu().numpy().tobytes()
         else:
             v = c["values"].cpu().numpy()
             if info.out_type == N.O_DEC128:
-                v = v.reshape(-1, 2)
+                v = v.reshape(info.n_slots, 64 * pitch, 2)[:, : self.n_rec].reshape(-1, 2)
+            else:
+                v = v.reshape(info.n_slots, 64 * pitch)[:, : self.n_rec].reshape(-1)
             out["values"] = v
         return out
 
@@ -202,14 +203,15 @@ def _alloc_columns(plan: DecodePlan, n_rec: int, slot_capacity: Sequence[int], d
     bitmaps, and for strings one Arrow large-string array per slot (regions of slot_capacity)."""
     torch = _torch()
     pitch_words = (n_rec + 63) // 64
+    pitch = 64 * pitch_words          # values per slot row (cobrix_hip.h: padded to whole tiles)
     cols: List[Dict[str, Any]] = []
     cstructs = (N.CbxColumn * plan.n_columns)()
     for ci, info in enumerate(plan.columns):
-        n = n_rec * info.n_slots
+        n = pitch * info.n_slots
         c: Dict[str, Any] = {"validity": torch.zeros(max(1, info.n_slots * pitch_words), dtype=torch.int64, device=device)}
         if info.out_type in (N.O_STRING, N.O_BINARY):
             cap = int(slot_capacity[ci])
-            c["offsets"] = torch.zeros(info.n_slots * (n_rec + 1), dtype=torch.int64, device=device)
+            c["offsets"] = torch.zeros(info.n_slots * (pitch + 1), dtype=torch.int64, device=device)
             c["data"] = torch.empty(max(1, cap * info.n_slots), dtype=torch.uint8, device=device)
             c["sizes"] = torch.zeros(info.n_slots, dtype=torch.int64, device=device)
             c["capacity"] = cap

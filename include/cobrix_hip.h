@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 2
+#define CBX_ABI_VERSION 3
 
 /* status codes */
 #define CBX_OK 0
@@ -136,20 +136,21 @@ typedef struct {
     cbx_segment_map segments;
 } cbx_plan_options;
 
-/* Output column buffers (caller-owned, device memory).  Column c holds n_slots(c) x n_rec
- * values laid out slot-major: value (slot s, record r) is element s * n_rec + r.  Validity is
- * an Arrow bitmap per slot row with a 64-bit-aligned pitch: bit r of row s is
- *   validity[(s * pitch_words + r / 64)] >> (r % 64), pitch_words = ceil(n_rec / 64).
+/* Output column buffers (caller-owned, device memory).  Every column is n_slots(c) slot rows
+ * of pitch = 64 * ceil(n_rec / 64) values (one row per OCCURS element; 1 row without OCCURS):
+ * value (slot s, record r) is element s * pitch + r; elements r >= n_rec are padding the
+ * kernels may overwrite.  Validity is an Arrow bitmap per slot row, 64-bit words:
+ *   bit r of row s = validity[s * (pitch / 64) + r / 64] >> (r % 64).
  * Strings/binary: every slot is its own Arrow large-string array.  Slot s owns the payload
- * region data[s * data_capacity, (s + 1) * data_capacity) and the n_rec + 1 offsets
- * offsets[s * (n_rec + 1) .. s * (n_rec + 1) + n_rec] (absolute byte positions in `data`).
- * data_capacity = cbx_string_bound(...) always suffices; a smaller capacity (e.g. from
- * cbx_string_sizes_*) is honoured: payload never overflows its region, an overflow is
- * reported by cbx_plan_check. */
+ * region data[s * data_capacity, (s + 1) * data_capacity) and the offsets
+ * offsets[s * (pitch + 1) + r], r = 0 .. n_rec (absolute byte positions in `data`; entries past
+ * n_rec are padding).  data_capacity = cbx_string_bound(...) always suffices; a smaller
+ * capacity (e.g. from cbx_string_sizes_*) is honoured: payload never overflows its region, an
+ * overflow is reported by cbx_plan_check. */
 typedef struct {
     void* values;          /* fixed-width values (NULL for strings) */
     uint64_t* validity;
-    int64_t* offsets;      /* strings: n_slots * (n_rec + 1) entries */
+    int64_t* offsets;      /* strings: n_slots * (pitch + 1) entries */
     uint8_t* data;         /* strings: UTF-8 payload, n_slots regions of data_capacity bytes */
     int64_t data_capacity; /* strings: bytes per slot region */
     int64_t* data_sizes;   /* strings: device array [n_slots] receiving each slot's payload bytes (may be NULL) */
@@ -195,11 +196,12 @@ int cbx_string_sizes_var(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes,
 int cbx_plan_check(cbx_plan* plan, void* stream);
 
 /* Optional kernel timing with HIP events on the call's stream (bench / profiling): while
- * enabled, every decode call records events around its decode kernel and its fixup kernel
- * (no synchronisation).  cbx_plan_kernel_times waits for the recorded events, returns up to
- * max_calls per-call durations in ms (oldest first, *n_calls of them) and clears the record. */
+ * enabled, every decode call records events around its decode kernel and around its post
+ * passes (fixup of deferred values, string scan + placement), without synchronising.
+ * cbx_plan_kernel_times waits for the recorded events, returns up to max_calls per-call
+ * durations in ms (oldest first, *n_calls of them) and clears the record. */
 int cbx_plan_set_profiling(cbx_plan* plan, int32_t enable);
-int cbx_plan_kernel_times(cbx_plan* plan, float* decode_ms, float* fixup_ms, int32_t max_calls, int32_t* n_calls);
+int cbx_plan_kernel_times(cbx_plan* plan, float* decode_ms, float* post_ms, int32_t max_calls, int32_t* n_calls);
 
 /* RDW header walk on the GPU (RecordHeaderParserRDW + VRLRecordReader), seeded by sparse-index
  * entry points: seeds[k] is a known record-header offset (offsetFrom of an index entry), the

@@ -42,6 +42,20 @@ extern "C" int cbxh_decode(const cbx_field* cf, const uint8_t* p, int n_avail, c
     auto lutf = [&](uint32_t b) -> uint32_t { return f.kind == CBX_K_STRING_ASCII ? ascii_lut(b) : lut[b]; };
     StrSpan s = string_span(f.kind, f.trim, p, n, lutf);
     string_write(f.kind, p, s, sbuf, lutf);
+    if ((f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII) && f.size <= kStrFastBytes) {
+        // the kernels' register path must agree with the byte loop
+        alignas(16) uint8_t img[16 + 64 + 16];
+        for (int i = 0; i < (int)sizeof img; i++) img[i] = (uint8_t)(0xA5 ^ (3 * i));
+        const int at = 16 + (int)(reinterpret_cast<uintptr_t>(p) & 3);
+        for (int i = 0; i < n; i++) img[at + i] = p[i];
+        uint32_t w[8];
+        img_bytes32(img, at, f.size, w);
+        StrSpan s2 = string_span32(f.trim, w, n, f.size, lutf);
+        if (s2.begin != s.begin || s2.end != s.end || s2.utf8_len != s.utf8_len) return -1;
+        uint8_t out2[4 * kStrFastBytes + 8], dump[4];
+        string_write32(w, s2, out2, dump, f.size, true, lutf);
+        for (int i = 0; i < s.utf8_len; i++) if (out2[i] != sbuf[i]) return -1;
+    }
     *slen = s.utf8_len;
     return 1;
 }
