@@ -40,6 +40,18 @@ def algorithmic_bytes(plan, n_rec: int, record_bytes: int, payload_bytes: int) -
     return total
 
 
+def measured_traffic(n_rec: int):
+    """HBM bytes per decode-kernel launch from the newest committed rocprofv3 FETCH_SIZE/WRITE_SIZE
+    passes of this configuration (tools/gpu_profile.sh -> profiles/<round tag>/traffic_<n_rec>.json)."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_{n_rec}.json")))
+    if not found:
+        return None, None
+    with open(found[-1]) as f:
+        t = json.load(f)
+    return int(t["traffic_bytes"]), os.path.relpath(found[-1], ROOT)
+
+
 def _cpu_baseline(seconds: float = 12.0):
     """Oracle (scalar C restatement of the reference decoders) on a bounded SYN200 sample, 1 core."""
     from cobrix_amd.copybook import parse_copybook
@@ -138,6 +150,7 @@ def main():
     dec_avg_ms = sum(dec[: nc.value]) / max(1, nc.value)
     fix_avg_ms = sum(fix[: nc.value]) / max(1, nc.value)
     achieved = alg / (dec_avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = measured_traffic(n_rec)
     if rank == 0:
         out = {
             "metric": "decoded input GB/s + records/s, fixed-len COMP-3 mix, 1-8 MI355X; % HBM peak",
@@ -164,7 +177,8 @@ def main():
                           "post_kernels (deferred-value fixup, string scan + placement)": round(fix_avg_ms, 4)},
             "roofline": {"bound": "hbm", "kernel": "cbx::decode_kernel", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "algorithmic_bytes_per_launch": alg, "traffic": None},
+                         "algorithmic_bytes_per_launch": alg, "traffic": traffic,
+                         "traffic_source": traffic_src},
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = _cpu_baseline()
