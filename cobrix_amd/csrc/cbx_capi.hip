@@ -93,6 +93,7 @@ struct cbx_plan {
     int64_t* d_block_sums = nullptr; int64_t block_sums_cap = 0;
     uint32_t* d_local = nullptr;    int64_t local_cap = 0;
     uint8_t* d_scratch = nullptr;   int64_t scratch_cap = 0;
+    uint64_t* d_stamps = nullptr;   // diagnostic build only
     int32_t* d_status = nullptr;
     int num_cus = 256;
     // profiling: HIP events around the decode kernel and the post passes of every call (no sync)
@@ -411,7 +412,7 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
     (void)hipFree(P->d_ncall); (void)hipFree(P->d_scall);
     (void)hipFree(P->d_segmap); (void)hipFree(P->d_lut); (void)hipFree(P->d_cols);
     (void)hipFree(P->d_seqcall); (void)hipFree(P->d_str_tot); (void)hipFree(P->d_str_excl); (void)hipFree(P->d_block_sums);
-    (void)hipFree(P->d_local); (void)hipFree(P->d_scratch); (void)hipFree(P->d_status);
+    (void)hipFree(P->d_local); (void)hipFree(P->d_scratch); (void)hipFree(P->d_status); (void)hipFree(P->d_stamps);
     for (auto& e : P->ev_pool) (void)hipEventDestroy(e);
     for (auto& c : P->ev_calls) for (auto& e : c.e) if (e) (void)hipEventDestroy(e);
     delete P;
@@ -499,6 +500,13 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.cols = (const CBX_CONST DevColumn*)P->d_cols;
     a.n_seq = P->n_seq;
     a.status = P->d_status;
+#ifdef CBX_STAMPS
+    if (!P->d_stamps) {
+        HIP_CHECK(hipMalloc((void**)&P->d_stamps, 8 * sizeof(uint64_t)));
+        HIP_CHECK(hipMemset(P->d_stamps, 0, 8 * sizeof(uint64_t)));
+    }
+    a.stamps = P->d_stamps;
+#endif
     if (n_tiles == 0) return CBX_OK;
 
     // column table + per-op address tables: stream-ordered uploads from pageable host memory
@@ -510,7 +518,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         int64_t scratch = 0;
         for (int q = 0; q < P->n_seq; q++) { P->h_seq_scratch[q] = scratch; scratch += n_tiles * P->seq_tile_cap[q]; }
         if ((rr = grow(&P->d_local, &P->local_cap, (int64_t)P->n_seq * a.pitch, st)) ||
-            (rr = grow(&P->d_scratch, &P->scratch_cap, scratch, st)))
+            (rr = grow(&P->d_scratch, &P->scratch_cap, scratch + 16, st)))   // +16: placement reads a dword past a payload end
             return rr;
     }
     if (mode == 0) {
@@ -623,8 +631,8 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     HIP_CHECK(hipGetLastError());
     if (prof) HIP_CHECK(hipEventRecord(ce.e[1], st));
     if (mode == 0 && n_defer > 0) {
-        const int64_t words = n_tiles * (int64_t)n_defer;
-        hipLaunchKernelGGL(fixup_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, a,
+        const unsigned gy = (unsigned)std::min<int64_t>(n_defer, 65535);
+        hipLaunchKernelGGL(fixup_kernel, dim3((unsigned)((n_tiles + 255) / 256), gy), dim3(256), 0, st, a,
                            (const CBX_CONST DeferSeq*)P->d_defer, n_defer);
         HIP_CHECK(hipGetLastError());
     }
@@ -632,9 +640,9 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         if ((r = string_scan(P, n_tiles, st))) return r;
         if (mode == 0) {
             const unsigned gx = (unsigned)std::min<int64_t>(n_tiles, 4096);
-            hipLaunchKernelGGL(str_place_kernel, dim3(gx, (unsigned)P->n_seq), dim3(kWave), 0, st,
+            hipLaunchKernelGGL(str_place_kernel, dim3(gx, (unsigned)std::min<int64_t>(P->n_seq, 65535)), dim3(kWave), 0, st,
                                (const CBX_CONST SeqCall*)P->d_seqcall, (const uint32_t*)P->d_str_tot,
-                               (const int64_t*)P->d_str_excl, n_tiles, c.n_rec, P->d_status);
+                               (const int64_t*)P->d_str_excl, n_tiles, c.n_rec, P->n_seq, P->d_status);
             HIP_CHECK(hipGetLastError());
         }
     }
@@ -693,6 +701,19 @@ extern "C" int cbx_plan_set_profiling(cbx_plan* P, int32_t enable) {
     P->profiling = enable != 0;
     return CBX_OK;
 }
+
+#ifdef CBX_STAMPS
+// Diagnostic build only: per-segment s_memtime sums of the contiguous decode loop since the
+// last call (out[0..5] segments, out[7] waves), then reset.
+extern "C" int cbx_debug_stamps(cbx_plan* P, uint64_t* out) {
+    if (!P || !out) return fail(CBX_E_ARGUMENT, "cbx_debug_stamps: invalid arguments");
+    if (!P->d_stamps) { memset(out, 0, 8 * sizeof(uint64_t)); return CBX_OK; }
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy(out, P->d_stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemset(P->d_stamps, 0, 8 * sizeof(uint64_t)));
+    return CBX_OK;
+}
+#endif
 
 extern "C" int cbx_plan_kernel_times(cbx_plan* P, float* decode_ms, float* fixup_ms, int32_t max_calls, int32_t* n_calls) {
     if (!P || !n_calls || max_calls < 0) return fail(CBX_E_ARGUMENT, "cbx_plan_kernel_times: invalid arguments");

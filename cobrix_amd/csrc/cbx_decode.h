@@ -554,14 +554,23 @@ enum NumFlags : uint32_t {
 struct NumOp {
     int32_t eo;                       // element offset in the record (slot resolved, before start_off)
     uint8_t variant, size, out_type, flags;
-    uint8_t e_mul, e_lim, n_odo, pad;
+    uint8_t n_odo, shift, pad0, pad1; // shift: 64 - 8 * min(size, 8) (binary sign extension)
     int32_t column;
     int32_t slot;
     int32_t defer;                    // deferral sequence of this element, -1 if never deferred
     int32_t segment;                  // segment-redefine group, -1 none
+    int32_t reserved;
+    // plan-time constants of the fast paths (no table lookups or shifts by size in the kernel)
+    uint64_t mask;                    // BCD8 / BIN8: low `size` bytes (after bswap); BCD16: low size-8
+                                      // bytes of the leading word; ZONED16: high min(size, 8) bytes
+    uint64_t mask0;                   // ZONED16: high size-8 bytes of the preceding word
+    uint64_t mul;                     // 10^E (decimal fast finish)
+    uint64_t lim_lo, lim_hi;          // 10^(out_p - E): magnitude bound
+    uint64_t lim64;                   // the bound saturated to 64 bits (magnitudes that fit 64 bits)
     int16_t odo_arr[CBX_MAX_DIMS];    // OCCURS DEPENDING ON levels: element index odo_idx[j] must be
     int16_t odo_idx[CBX_MAX_DIMS];    // < the record's count of array odo_arr[j]
 };
+static_assert(sizeof(NumOp) == 96, "NumOp is a 96-byte scalar-load record");
 
 inline NumOp make_numop(const Field& d, int slot, int eo, const int16_t* odo_arr, const int16_t* odo_idx, int n_odo) {
     NumOp o{};
@@ -578,9 +587,21 @@ inline NumOp make_numop(const Field& d, int slot, int eo, const int16_t* odo_arr
     if (d.plus_null) fl |= NF_PLUS_NULL;
     if (d.kind == CBX_K_FLOAT) fl |= NF_FLOAT;
     o.flags = (uint8_t)fl;
-    o.e_mul = (uint8_t)d.e_mul;
-    o.e_lim = (uint8_t)d.e_lim;
     o.n_odo = (uint8_t)n_odo;
+    const int n8 = d.size < 8 ? d.size : 8;
+    o.shift = (uint8_t)(64 - 8 * n8);
+    switch (d.variant) {
+    case V_BCD16: o.mask = low_bytes_mask(d.size - 8); break;
+    case V_ZONED16: o.mask = high_bytes_mask(d.size); o.mask0 = high_bytes_mask(d.size - 8); break;
+    default: o.mask = low_bytes_mask(d.size); break;
+    }
+    unsigned __int128 mul = 1, lim = 1;
+    for (int i = 0; i < d.e_mul; i++) mul *= 10;
+    for (int i = 0; i < d.e_lim; i++) lim *= 10;
+    o.mul = (uint64_t)mul;
+    o.lim_lo = (uint64_t)lim;
+    o.lim_hi = (uint64_t)(lim >> 64);
+    o.lim64 = o.lim_hi ? ~0ull : o.lim_lo;
     o.column = d.column;
     o.slot = slot;
     o.defer = d.defer >= 0 ? d.defer + slot : -1;
@@ -633,35 +654,44 @@ inline U128 pow10_u128(int k) {
 
 // Fast-path result typing (DecoderSelector.scala:104-281 + Spark Decimal.toPrecision) for a
 // digit magnitude M: integral -> two's complement (BCD wraps as a Java long, as the reference);
-// decimal -> null past 10^e_lim, else M * 10^e_mul.  Branch-free apart from uniform tests on
-// the op: every lane computes, `valid` selects.
+// decimal -> null from 10^(out_p - E) on, else M * 10^E.  Branch-free apart from uniform tests
+// on the op: every lane computes, `valid` selects.  W = output bytes (0: any): for W <= 8 only
+// the low 64 bits are produced (a valid decimal of <= 18 digits fits them).
+template <int W>
 CBX_HD Val fast_finish(const NumOp& op, U128 M, bool neg, bool valid) {
     if (op.flags & NF_INT) {
         const uint64_t v = neg ? (uint64_t)0 - M.lo : M.lo;
         return Val{v, (uint64_t)((int64_t)v >> 63), valid};
     }
-    valid &= u128_lt(M, pow10_u128(op.e_lim));
-    const uint64_t mul = pow10_u128(op.e_mul).lo;
+    if (W == 4 || W == 8) {
+        valid &= M.hi == 0 && M.lo < op.lim64;
+        const uint64_t r = M.lo * op.mul;
+        const uint64_t v = neg ? (uint64_t)0 - r : r;
+        return Val{v, (uint64_t)((int64_t)v >> 63), valid};
+    }
+    valid &= u128_lt(M, U128{op.lim_lo, op.lim_hi});
     U128 R;
-    R.lo = M.lo * mul;
-    R.hi = mulhi64(M.lo, mul) + M.hi * mul;
+    R.lo = M.lo * op.mul;
+    R.hi = mulhi64(M.lo, op.mul) + M.hi * op.mul;
     if (neg) R = u128_neg(R);
     return Val{R.lo, R.hi, valid};
 }
 
 // The *_raw decoders take the 8 bytes ending at the element's end (r1 = img_le64_ending(img,
 // end)) and, for 16-byte classes, the 8 before them (r0 = img_le64_ending(img, end - 8)).
+template <int W>
 CBX_HD Val bcd8_raw(const NumOp& op, uint64_t r1) {
-    const uint64_t be = __builtin_bswap64(r1) & low_bytes_mask(op.size);
+    const uint64_t be = __builtin_bswap64(r1) & op.mask;
     const uint32_t sn = (uint32_t)be & 15u;
     const uint64_t dg = be >> 4;
     const bool valid = bcd_ok(dg) && (sn == 0xC || sn == 0xD || sn == 0xF);
-    return fast_finish(op, u128(bcd16_bin(dg)), sn == 0xD, valid);
+    return fast_finish<W>(op, u128(bcd16_bin(dg)), sn == 0xD, valid);
 }
 
+template <int W>
 CBX_HD Val bcd16_raw(const NumOp& op, uint64_t r1, uint64_t r0) {
     const uint64_t lo = __builtin_bswap64(r1);
-    const uint64_t hi = __builtin_bswap64(r0) & low_bytes_mask(op.size - 8);
+    const uint64_t hi = __builtin_bswap64(r0) & op.mask;
     const uint32_t sn = (uint32_t)lo & 15u;
     const uint64_t dlo = lo >> 4;   // 15 digits
     const bool valid = bcd_ok(dlo) && bcd_ok(hi) && (sn == 0xC || sn == 0xD || sn == 0xF);
@@ -671,36 +701,36 @@ CBX_HD Val bcd16_raw(const NumOp& op, uint64_t r1, uint64_t r0) {
     U128 M;
     M.lo = plo + bcd16_bin(dlo);
     M.hi = phi + (M.lo < plo);
-    return fast_finish(op, M, sn == 0xD, valid);
+    return fast_finish<W>(op, M, sn == 0xD, valid);
 }
 
+template <int W>
 CBX_HD Val bin8_raw(const NumOp& op, uint64_t le) {
-    const int n = op.size;
-    uint64_t v = (op.flags & NF_BIG_ENDIAN) ? (__builtin_bswap64(le) & low_bytes_mask(n)) : (le >> (64 - 8 * n));
+    const int sh = op.shift;
+    uint64_t v = (op.flags & NF_BIG_ENDIAN) ? (__builtin_bswap64(le) & op.mask) : (le >> sh);
     bool neg = false;
     if (op.flags & NF_SIGNED) {
-        const int sh = 64 - 8 * n;
         v = (uint64_t)((int64_t)(v << sh) >> sh);
         neg = (int64_t)v < 0;
     }
     if (op.flags & NF_INT) {
         // unsigned 4- and 8-byte values with the top bit set are null (BinaryNumberDecoders.scala:81-82, 111-112)
+        const int n = op.size;
         const bool bad = !(op.flags & NF_SIGNED) && ((n == 4 && (v & 0x80000000ull)) || (n == 8 && (v >> 63)));
         return Val{v, neg ? ~0ull : 0ull, !bad};
     }
     // binary decimal (BinaryUtils.decodeBinaryNumber + addDecimalPoint), scale factor >= 0
-    return fast_finish(op, u128(neg ? (uint64_t)0 - v : v), neg, true);
+    return fast_finish<W>(op, u128(neg ? (uint64_t)0 - v : v), neg, true);
 }
 
+template <int W>
 CBX_HD Val zoned16_raw(const NumOp& op, uint64_t r1, uint64_t r0, bool& defer) {
-    const int n = op.size;
     const uint64_t Z = 0xF0F0F0F0F0F0F0F0ull, L = 0x0F0F0F0F0F0F0F0Full;
     uint64_t b1 = r1;   // field bytes end-8 .. end-1 (last in the top byte)
     uint64_t b0 = r0;   // end-16 .. end-9
     // bytes in front of the field read as '0' digits (0xF0): leading zeros change nothing
-    const uint64_t m1 = high_bytes_mask(n), m0 = high_bytes_mask(n - 8);
-    b1 = (b1 & m1) | (Z & ~m1);
-    b0 = (b0 & m0) | (Z & ~m0);
+    b1 = (b1 & op.mask) | (Z & ~op.mask);
+    b0 = (b0 & op.mask0) | (Z & ~op.mask0);
     const uint32_t lastz = (uint32_t)(b1 >> 60);
     const uint64_t d0 = b0 & L, d1 = b1 & L;
     const bool fast = (b0 & Z) == Z && (((b1 & Z) | 0xF000000000000000ull) == Z) &&
@@ -710,7 +740,7 @@ CBX_HD Val zoned16_raw(const NumOp& op, uint64_t r1, uint64_t r0, bool& defer) {
     const bool neg = lastz == 0xD;
     const bool valid = fast && !(neg && !(op.flags & NF_SIGNED)) && !(lastz == 0xC && (op.flags & NF_PLUS_NULL));
     const uint64_t v = (uint64_t)digits8_bin(d0) * 100000000ull + digits8_bin(d1);
-    return fast_finish(op, u128(v), neg, valid);
+    return fast_finish<W>(op, u128(v), neg, valid);
 }
 
 CBX_HD Val fp_raw(const NumOp& op, uint64_t le) {
@@ -727,13 +757,14 @@ CBX_HD Val fp_raw(const NumOp& op, uint64_t le) {
 // Numeric element at img[addr, addr + size) (bounds already checked by the caller).  Sets
 // `defer` (result null) when the value needs the byte-loop decoder: the kernels record it in
 // a deferral bitmap and the fixup kernel decodes it with decode_numeric.
+template <int W = 0>
 CBX_HD Val decode_value(const NumOp& op, const uint8_t* img, uint32_t addr, bool& defer) {
     const uint32_t end = addr + op.size;
     switch (op.variant) {
-    case V_BCD8: return bcd8_raw(op, img_le64_ending(img, end));
-    case V_BCD16: return bcd16_raw(op, img_le64_ending(img, end), img_le64_ending(img, end - 8));
-    case V_BIN8: return bin8_raw(op, img_le64_ending(img, end));
-    case V_ZONED16: return zoned16_raw(op, img_le64_ending(img, end), img_le64_ending(img, end - 8), defer);
+    case V_BCD8: return bcd8_raw<W>(op, img_le64_ending(img, end));
+    case V_BCD16: return bcd16_raw<W>(op, img_le64_ending(img, end), img_le64_ending(img, end - 8));
+    case V_BIN8: return bin8_raw<W>(op, img_le64_ending(img, end));
+    case V_ZONED16: return zoned16_raw<W>(op, img_le64_ending(img, end), img_le64_ending(img, end - 8), defer);
     case V_FP: return fp_raw(op, img_le64_ending(img, end));
     default: defer = true; return null_val();
     }

@@ -1,0 +1,642 @@
+// cbx_device.h -- device-side building blocks of the decode hot path, shared by the
+// interpreter kernel (cbx_kernels.hip: plan tables read at run time) and the per-copybook
+// specialised kernels compiled at run time with hipRTC (cbx_jit.cpp: the same functions with the
+// op records as compile-time constants).  See cbx_kernels.hip for the work decomposition.
+#pragma once
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#endif
+
+#include "cbx_internal.h"
+
+namespace cbx {
+
+// Exclusive scan of a 32-bit value over the wave with DPP row shifts (Hillis-Steele inside
+// each 16-lane row) plus the preceding rows' totals read with v_readlane.  All lanes active.
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t x, int lane, uint32_t& total) {
+    uint32_t v = x;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+    const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    const int row = lane >> 4;
+    v += (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+    total = r0 + r1 + r2 + r3;
+    return v - x;
+}
+
+// Plan-table and column pointers are plain (generic) pointers; stores through them would be
+// `flat_*` instructions, which also count in lgkmcnt -- every later LDS / scalar-load wait
+// would then wait for those stores to reach memory.  gp() re-qualifies them as global.
+#define CBX_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ CBX_GLOBAL T* gp(T* p) { return (CBX_GLOBAL T*)p; }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Copy a plan-table entry out of the constant address space (scalar loads when uniform).
+template <typename T>
+__device__ __forceinline__ T ldc(const CBX_CONST T* p) {
+    static_assert(sizeof(T) % 4 == 0, "plan tables are dword structs");
+    int32_t w[sizeof(T) / 4];
+    const CBX_CONST int32_t* q = (const CBX_CONST int32_t*)p;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++) w[i] = q[i];
+    T r;
+    __builtin_memcpy(&r, w, sizeof(T));
+    return r;
+}
+
+// 16 bytes at data + ga (ga 16-byte aligned); bytes outside [0, len) read as 0.
+__device__ __forceinline__ uint4 load16_guarded(const uint8_t* data, int64_t ga, int64_t len) {
+    if (ga >= 0 && ga + 16 <= len) return *(const uint4*)(data + ga);
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int64_t g = ga + j;
+        const uint32_t b = (g >= 0 && g < len) ? data[g] : 0u;
+        w[j >> 2] |= b << (8 * (j & 3));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// FixedLenNestedRowIterator.getSegmentId / VRLRecordReader.getSegmentId:
+// extractPrimitiveField(field).toString.trim, looked up in the segment-redefine map.
+__device__ int segment_of(const KernelArgs& a, const uint32_t* lut, const uint8_t* rec, int avail) {
+    const CBX_CONST cbx_segment_map* m = a.segmap;
+    int o = a.start_off + m->field_offset;
+    int n = m->field_size;
+    if (o > avail) o = avail;
+    if (o + n > avail) n = avail - o;
+    if (n < 0) n = 0;
+    const uint8_t* p = rec + o;
+    int b = 0, e = n;
+    while (b < e && (lut[p[b]] >> 31)) b++;
+    while (e > b && (lut[p[e - 1]] >> 31)) e--;
+    // keys are stored as UTF-8 (key[k][] holds bytes, key_len[k] their count)
+    for (int k = 0; k < m->n_keys; k++) {
+        const CBX_CONST uint16_t* key = m->key[k];
+        int kl = m->key_len[k];
+        int pos = 0;
+        bool eq = true;
+        for (int i = b; i < e && eq; i++) {
+            uint32_t en = lut[p[i]];
+            int l = (en >> 24) & 3;
+            for (int j = 0; j < l; j++) {
+                if (pos >= kl || key[pos] != ((en >> (8 * j)) & 0xFF)) { eq = false; break; }
+                pos++;
+            }
+        }
+        if (eq && pos == kl) return m->key_segment[k];
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void store_value(const DevColumn& c, int out_type, int64_t v, const Val& x) {
+    switch (out_type) {
+    case CBX_O_I32: gp((int32_t*)c.values)[v] = (int32_t)x.lo; break;
+    case CBX_O_F32: gp((uint32_t*)c.values)[v] = (uint32_t)x.lo; break;
+    case CBX_O_DEC128: gp((uint64_t*)c.values)[2 * v] = x.lo; gp((uint64_t*)c.values)[2 * v + 1] = x.hi; break;
+    default: gp((uint64_t*)c.values)[v] = x.lo; break;
+    }
+}
+
+// Per-lane state of the tile being decoded.
+struct TileCtx {
+    int64_t tile;
+    int64_t rec;        // record index of this lane
+    bool active;        // rec < n_rec
+    int64_t base;       // byte offset of the record (relative to a.data) -- decode base minus start_off
+    int avail;          // bytes available in the record (rec_len / stride)
+    int seg;            // active segment-redefine index, -1 none
+};
+
+// OCCURS DEPENDING ON presence of an element: every ODO level's element index is below the
+// record's count (read through the table pointer: a dynamic index into a register copy of
+// the op would force it to scratch).
+template <typename OP>
+__device__ __forceinline__ bool odo_present(const CBX_CONST OP* opp, int n_odo, const int32_t* s_cnt, int lane) {
+    bool el = true;
+    for (int j = 0; j < n_odo; j++) el &= opp->odo_idx[j] < s_cnt[opp->odo_arr[j] * kWave + lane];
+    return el;
+}
+
+__device__ __forceinline__ uint32_t str_lut(int kind, const uint32_t* s_lut, uint32_t b) {
+    return kind == CBX_K_STRING_ASCII ? ascii_lut(b) : s_lut[b];
+}
+
+// String element of the current tile: trimmed span + UTF-8 length (StringDecoders / StringTools).
+// Elements of at most kStrFastBytes EBCDIC/ASCII bytes keep their bytes in `w` (register path).
+__device__ __forceinline__ StrSpan sop_span(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
+                                            const TileCtx& t, const int32_t* s_cnt, int lane, const uint8_t* src,
+                                            uint32_t rec_addr, const uint32_t* s_lut, bool& ok, bool fast, uint32_t w[8]) {
+    bool el = t.active && (op.segment < 0 || op.segment == t.seg);
+    if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
+    const int o = a.start_off + op.eo;
+    ok = el && o <= t.avail;
+    const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
+    auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
+    if (fast) {
+        img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
+        return string_span32(op.trim, w, n, op.size, lutf);
+    }
+    StrSpan sp{0, 0, 0};
+    if (ok) sp = string_span(op.kind, op.trim, src + rec_addr + (uint32_t)op.eo, n, lutf);
+    return sp;
+}
+
+__device__ __forceinline__ bool sop_fast(const StrOp& op, bool global) {
+    return !global && op.size <= kStrFastBytes && (op.kind == CBX_K_STRING || op.kind == CBX_K_STRING_ASCII);
+}
+
+template <int W>
+__device__ __forceinline__ void store_w(void* values, int64_t v, const Val& x, int out_type) {
+    // v: element index within the slot row
+    const int w = W ? W : (out_type == CBX_O_I32 || out_type == CBX_O_F32 ? 4 : out_type == CBX_O_DEC128 ? 16 : 8);
+    if (w == 4) gp((uint32_t*)values)[v] = (uint32_t)x.lo;
+    else if (w == 8) gp((uint64_t*)values)[v] = x.lo;
+    else gp((u32x4*)values)[v] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
+}
+
+// One batch of numeric ops (same decoder variant V, output width W).  Decoding is branch-free
+// per lane: every lane reads its (clamped) element and computes, the bounds / segment / OCCURS
+// conditions only select validity.  The validity (and deferral) word of each op is a wave
+// ballot stored by every lane to the same address.
+template <int V, int W, bool kOdo, bool kGlobal>
+__device__ __forceinline__ void num_one(const KernelArgs& a, const NumOp& op, int i, const TileCtx& t,
+                                        bool ok, uint64_t r1, uint64_t r0, const int32_t* s_cnt, int lane) {
+    if (op.segment >= 0) ok &= op.segment == t.seg;
+    if (kOdo) ok &= odo_present(a.nops + i, op.n_odo, s_cnt, lane);
+    Val x = null_val();
+    bool defer = false;
+    if (kGlobal || V == V_GENERIC) {
+        defer = ok;
+    } else {
+        if (V == V_BCD8) x = bcd8_raw<W>(op, r1);
+        else if (V == V_BCD16) x = bcd16_raw<W>(op, r1, r0);
+        else if (V == V_BIN8) x = bin8_raw<W>(op, r1);
+        else if (V == V_ZONED16) { x = zoned16_raw<W>(op, r1, r0, defer); defer &= ok; }
+        else if (V == V_FP) x = fp_raw(op, r1);
+        x.valid &= ok;
+    }
+    const NumCall c = ldc(a.ncall + i);
+    // every lane stores (slot rows are padded to 64 * n_tiles values): no exec-mask branches
+    store_w<W>(c.values, t.rec, x, op.out_type);
+    const uint64_t m = __ballot(x.valid);
+    gp(c.validity)[t.tile] = m;
+    if (V == V_ZONED16 || V == V_GENERIC || kGlobal) {
+        const uint64_t dm = __ballot(defer);
+        if (c.defer) gp(c.defer)[t.tile] = dm;
+    }
+}
+
+// One batch of numeric ops (same decoder variant V, output width W), four ops per step: the
+// LDS reads of the four elements are issued before any of them is decoded.  Decoding is
+// branch-free per lane: every lane reads its (clamped) element and computes, the bounds /
+// segment / OCCURS conditions only select validity.  The validity (and deferral) word of each
+// op is a wave ballot stored by every lane to the same address.
+template <int V, int W, bool kOdo, bool kGlobal>
+__device__ __forceinline__ void num_batch(const KernelArgs& a, const Batch& b, const TileCtx& t, const uint8_t* src,
+                                          uint32_t rec_addr, const int32_t* s_cnt, int lane) {
+    constexpr bool kWide = V == V_BCD16 || V == V_ZONED16;   // two 8-byte reads per element
+    constexpr bool kRead = !(kGlobal || V == V_GENERIC);
+    const int lim = t.active ? t.avail - a.start_off : -1;   // element must end within the record
+    constexpr int U = 4;
+    int i = b.begin;
+    for (; i + U <= b.end; i += U) {
+        NumOp op[U];
+        bool ok[U];
+        uint64_t r1[U], r0[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            op[u] = ldc(a.nops + i + u);
+            ok[u] = op[u].eo + op[u].size <= lim;
+            r1[u] = r0[u] = 0;
+            if (kRead) {
+                const uint32_t end = rec_addr + (ok[u] ? (uint32_t)op[u].eo : 0u) + op[u].size;
+                r1[u] = img_le64_ending(src, end);
+                if (kWide) r0[u] = img_le64_ending(src, end - 8);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) num_one<V, W, kOdo, kGlobal>(a, op[u], i + u, t, ok[u], r1[u], r0[u], s_cnt, lane);
+    }
+    for (; i < b.end; i++) {
+        const NumOp op = ldc(a.nops + i);
+        const bool ok = op.eo + op.size <= lim;
+        uint64_t r1 = 0, r0 = 0;
+        if (kRead) {
+            const uint32_t end = rec_addr + (ok ? (uint32_t)op.eo : 0u) + op.size;
+            r1 = img_le64_ending(src, end);
+            if (kWide) r0 = img_le64_ending(src, end - 8);
+        }
+        num_one<V, W, kOdo, kGlobal>(a, op, i, t, ok, r1, r0, s_cnt, lane);
+    }
+}
+
+// One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):
+// span + tile-local scan; the tile's payload is staged contiguously in LDS and copied with
+// dword stores to the tile's scratch region; the tile-local start of every value and the
+// tile's byte total are recorded for the compaction kernel, which places tiles after a
+// device-wide scan of the totals (two-pass string offsets, no cross-tile waiting).
+__device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
+                                            const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
+                                            const uint8_t* src, uint32_t rec_addr, bool global,
+                                            const uint32_t* s_lut, uint8_t* s_str, int lane) {
+    const bool fast = sop_fast(op, global);
+    bool ok;
+    uint32_t wb[8];
+    const StrSpan sp = sop_span(a, op, opp, t, s_cnt, lane, src, rec_addr, s_lut, ok, fast, wb);
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32((uint32_t)sp.utf8_len, lane, tot);
+    if (a.mode == 1) {
+        if (lane == 0) gp(a.str_tot)[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
+        return;
+    }
+    gp(c.validity)[t.tile] = __ballot(ok);
+    gp(c.local)[t.rec] = ex;
+    if (lane == 0) gp(a.str_tot)[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
+    auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
+    const uint8_t* sp_src = src + rec_addr + (uint32_t)op.eo;
+    uint32_t* dst32 = (uint32_t*)(c.scratch + t.tile * (int64_t)c.tile_cap);   // 16-byte aligned region
+    if ((int)tot <= a.str_stage) {
+        if (fast) string_write32(wb, sp, s_str + ex, s_str + a.str_stage, op.size, op.pad > 1, lutf);
+        else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
+        wave_sync_lds();
+        const uint32_t* s32 = (const uint32_t*)s_str;
+        for (int q = lane; 4 * q < (int)tot; q += kWave) gp(dst32)[q] = s32[q];
+        wave_sync_lds();
+    } else if (ok) {
+        uint8_t* dst = (uint8_t*)dst32 + ex;
+        if (fast) {
+            uint8_t dump[4];
+            string_write32(wb, sp, dst, dump, op.size, op.pad > 1, lutf);
+        } else {
+            string_write(op.kind, sp_src, sp, dst, lutf);
+        }
+    }
+}
+
+// Generated columns of a window (File_Id / Record_Id).
+__device__ __forceinline__ void decode_generated(const KernelArgs& a, const Window& w, const TileCtx& t, int lane) {
+    if (a.mode == 1) return;
+    for (int i = w.gen_begin; i < w.gen_end; i++) {
+        const GenOp g = ldc(a.gops + i);
+        const DevColumn col = ldc(a.cols + g.column);
+        Val x{g.kind == CBX_K_RECORD_ID ? (uint64_t)(a.first_record_id + t.rec) : (uint64_t)(int64_t)a.file_id, 0, true};
+        if (t.active) store_value(col, g.out_type, t.rec, x);
+        const uint64_t m = __ballot(t.active);
+        if (lane == 0) gp(col.validity)[t.tile] = m;
+    }
+}
+
+// Decode one window of the current tile.  src + rec_addr is the record's decode base (LDS
+// image, or HBM for the global window).
+template <bool kGlobal>
+__device__ __forceinline__ void decode_window(const KernelArgs& a, const Window& w, const TileCtx& t, const uint8_t* src,
+                                              uint32_t rec_addr, const int32_t* s_cnt, const uint32_t* s_lut,
+                                              uint8_t* s_str, int lane) {
+    const bool sizes = a.mode == 1;
+    // ---- strings (tile-local; placed by the compaction kernel)
+    for (int i = w.sop_begin; i < w.sop_end; i++) {
+        const StrOp op = ldc(a.sops + i);
+        const StrCall c = sizes ? StrCall{} : ldc(a.scall + i);
+        str_element(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
+    }
+    if (sizes) return;
+    decode_generated(a, w, t, lane);
+    // ---- numerics (look-back words of earlier tiles land meanwhile), one specialised loop per batch
+    for (int bi = w.batch_begin; bi < w.batch_end; bi++) {
+        const Batch b = ldc(a.batches + bi);
+        if (kGlobal) {
+            if (b.odo) num_batch<V_GENERIC, 8, true, true>(a, b, t, src, rec_addr, s_cnt, lane);
+            else num_batch<V_GENERIC, 8, false, true>(a, b, t, src, rec_addr, s_cnt, lane);
+            continue;
+        }
+        if (b.odo) {   // elements under OCCURS DEPENDING ON: one generic-width loop per variant
+            switch (b.variant) {
+            case V_BCD8: num_batch<V_BCD8, 0, true, false>(a, b, t, src, rec_addr, s_cnt, lane); break;
+            case V_BCD16: num_batch<V_BCD16, 0, true, false>(a, b, t, src, rec_addr, s_cnt, lane); break;
+            case V_BIN8: num_batch<V_BIN8, 0, true, false>(a, b, t, src, rec_addr, s_cnt, lane); break;
+            case V_ZONED16: num_batch<V_ZONED16, 0, true, false>(a, b, t, src, rec_addr, s_cnt, lane); break;
+            case V_FP: num_batch<V_FP, 0, true, false>(a, b, t, src, rec_addr, s_cnt, lane); break;
+            default: num_batch<V_GENERIC, 0, true, false>(a, b, t, src, rec_addr, s_cnt, lane); break;
+            }
+            continue;
+        }
+#define CBX_BATCH(V)                                                                                  \
+    case V:                                                                                           \
+        if (b.width == 4) num_batch<V, 4, false, false>(a, b, t, src, rec_addr, s_cnt, lane);        \
+        else if (b.width == 8) num_batch<V, 8, false, false>(a, b, t, src, rec_addr, s_cnt, lane);   \
+        else num_batch<V, 16, false, false>(a, b, t, src, rec_addr, s_cnt, lane);                    \
+        break;
+        switch (b.variant) {
+            CBX_BATCH(V_BCD8)
+            CBX_BATCH(V_BCD16)
+            CBX_BATCH(V_BIN8)
+            CBX_BATCH(V_ZONED16)
+            CBX_BATCH(V_FP)
+            default: num_batch<V_GENERIC, 0, false, false>(a, b, t, src, rec_addr, s_cnt, lane); break;
+        }
+#undef CBX_BATCH
+    }
+    if (w.sop_begin == w.sop_end) return;
+}
+
+// Contiguous staging of a fixed-length tile: the tile's byte span [t0b, t0b + n * stride) is
+// fetched with 16-byte loads (consecutive lanes on consecutive chunks, 1 KiB per
+// wave-instruction) and written to LDS rows of cpitch bytes (odd dword count when padding pays).
+// A tile span inside the input is loaded in one go into kPre registers per lane, issued one tile
+// ahead (the decode of tile t overlaps the loads of tile t + stride); the last tile (span
+// reaching past the input) is staged synchronously with guarded loads.
+constexpr int kPre = 16;   // 16-byte chunks per lane: a 16 KiB tile span (plan limit for contig)
+
+struct ContigSpan {
+    int64_t a0;      // 16-byte aligned start of the span
+    int mis_dw;      // dwords between a0 and the first record
+    int span_dw;     // dwords of the tile's records
+    int nch;         // 16-byte chunks to load
+    bool inb;        // whole span inside the input
+};
+
+__device__ __forceinline__ ContigSpan contig_span(const KernelArgs& a, int64_t tile) {
+    ContigSpan sp;
+    const int64_t t0b = a.base_shift + tile * kWave * (int64_t)a.stride;
+    const int64_t left = a.n_rec - tile * kWave;
+    const int nrec_tile = left < kWave ? (int)left : kWave;
+    sp.a0 = t0b & ~(int64_t)15;
+    sp.mis_dw = (int)((t0b - sp.a0) >> 2);
+    sp.span_dw = nrec_tile * a.stride_dw;
+    sp.nch = (sp.mis_dw + sp.span_dw + 3) >> 2;
+    sp.inb = sp.a0 + 16 * (int64_t)sp.nch <= a.data_len;
+    return sp;
+}
+
+// Issue the loads of an in-bounds span (no wait): unconditional loads at clamped chunk indices.
+__device__ __forceinline__ void contig_issue(const KernelArgs& a, const ContigSpan& sp, int lane, uint4 (&buf)[kPre]) {
+#pragma unroll
+    for (int u = 0; u < kPre; u++) {
+        if (u * kWave < sp.nch) {   // wave-uniform
+            const int c = u * kWave + lane;
+            buf[u] = *(const uint4*)(a.data + sp.a0 + 16 * (int64_t)(c < sp.nch ? c : sp.nch - 1));
+        }
+    }
+}
+
+// Chunk c (16 bytes at a0 + 16c) into the LDS rows.
+__device__ __forceinline__ void contig_put(const KernelArgs& a, const ContigSpan& sp, int c, uint4 v, uint8_t* s_img) {
+    if (a.cpitch == 4 * a.stride_dw) {
+        *(uint4*)(s_img + 16 * c) = v;
+        return;
+    }
+    uint32_t* img32 = (uint32_t*)s_img;
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int d = 4 * c + k - sp.mis_dw;
+        if (d >= 0 && d < sp.span_dw) {
+            const int r = (int)(((float)d + 0.5f) * a.inv_stride_dw);
+            img32[d + sp.mis_dw + r] = wv[k];
+        }
+    }
+}
+
+__device__ __forceinline__ void contig_store(const KernelArgs& a, const ContigSpan& sp, int lane, const uint4 (&buf)[kPre],
+                                             uint8_t* s_img) {
+    // opaque lane index: keeps the compiler from computing the LDS addresses when the loads
+    // are issued (a tile earlier) and holding them in registers across the decode
+    asm volatile("" : "+v"(lane));
+#pragma unroll
+    for (int u = 0; u < kPre; u++) {
+        const int c = u * kWave + lane;
+        if (u * kWave < sp.nch && c < sp.nch) contig_put(a, sp, c, buf[u], s_img);
+    }
+}
+
+// Synchronous guarded staging (the span reaches past the end of the input).
+__device__ __forceinline__ void contig_stage_guarded(const KernelArgs& a, const ContigSpan& sp, int lane, uint8_t* s_img) {
+    constexpr int kRound = 8;
+    for (int c0 = 0; c0 < sp.nch; c0 += kRound * kWave) {
+        uint4 buf[kRound];
+#pragma unroll
+        for (int u = 0; u < kRound; u++) {
+            const int c = c0 + u * kWave + lane;
+            buf[u] = c < sp.nch ? load16_guarded(a.data, sp.a0 + 16 * (int64_t)c, a.data_len) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kRound; u++) {
+            const int c = c0 + u * kWave + lane;
+            if (c < sp.nch) contig_put(a, sp, c, buf[u], s_img);
+        }
+    }
+}
+
+// Windowed staging: bytes [w.lo, w.hi) of every record of the tile, (record, 16-byte chunk)
+// pairs spread over the lanes, rows of w.pitch bytes.  Returns the lane's record base.
+__device__ __forceinline__ uint32_t stage_window(const KernelArgs& a, const Window& w, const TileCtx& t,
+                                                 uint8_t* s_img, int lane) {
+    const int W = w.hi - w.lo;
+    const int pitch = w.pitch;
+    const int nch = (W + 15 + 15) >> 4;
+    const float inv_nch = 1.0f / (float)nch;
+    const int64_t my_g = t.base + a.start_off + w.lo;
+    const int my_mis = (int)(my_g & 15);
+    const int total = kWave * nch;
+    for (int t0 = 0; t0 < total; t0 += 8 * kWave) {
+        uint4 buf[8];
+        int rr[8], kk[8];
+        bool ld[8];
+        int64_t ga[8];
+        bool slow = a.data_len < 16;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int q = t0 + u * kWave + lane;
+            int r = (int)(((float)q + 0.5f) * inv_nch);
+            r = r < kWave ? r : kWave - 1;
+            const int k = q - r * nch;
+            rr[u] = r; kk[u] = k;
+            const int64_t gb = __shfl(my_g, r, kWave);
+            const bool ract = __shfl((int)t.active, r, kWave) != 0;
+            ld[u] = q < total && ract;
+            ga[u] = (gb & ~(int64_t)15) + 16 * (int64_t)k;
+            slow |= ld[u] && !(ga[u] >= 0 && ga[u] + 16 <= a.data_len);
+        }
+        // loads of a round issue back to back (unconditional; idle lanes read chunk 0) unless a
+        // chunk crosses the end of the input (wave-uniform choice)
+        if (__ballot(slow) == 0) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) buf[u] = *(const uint4*)(a.data + (ld[u] ? ga[u] : 0));
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; u++) buf[u] = ld[u] ? load16_guarded(a.data, ga[u], a.data_len) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (ld[u]) {
+                uint32_t* dst = (uint32_t*)(s_img + rr[u] * pitch + 16 * kk[u]);
+                dst[0] = buf[u].x; dst[1] = buf[u].y; dst[2] = buf[u].z; dst[3] = buf[u].w;
+            }
+        }
+    }
+    return (uint32_t)(lane * pitch + my_mis - w.lo);
+}
+
+// Per-lane tile context: record index, base offset and available bytes.
+__device__ __forceinline__ TileCtx tile_ctx(const KernelArgs& a, int64_t tile, int lane) {
+    TileCtx t;
+    t.tile = tile;
+    t.rec = tile * kWave + lane;
+    t.active = t.rec < a.n_rec;
+    t.base = a.base_shift;
+    t.avail = 0;
+    t.seg = -1;
+    if (a.rec_off) {
+        if (t.active) { t.base += a.rec_off[t.rec]; t.avail = a.rec_len[t.rec]; }
+    } else if (t.active) {
+        t.base += t.rec * (int64_t)a.stride;
+        t.avail = a.stride;
+    }
+    return t;
+}
+
+// Per-record prologue: segment-redefine selection and OCCURS DEPENDING ON element counts
+// (their count columns written here), reading the record at rp (the LDS image in contiguous
+// mode -- no HBM loads in that loop besides the staging loads -- or HBM).
+__device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, const uint8_t* rp, int lane,
+                                              const uint32_t* s_lut, int32_t* s_cnt) {
+    // ---- segment redefine selection
+    if (a.segmap && t.active) t.seg = segment_of(a, s_lut, rp, t.avail);
+    if (a.mode == 0 && a.seg_col >= 0) {
+        const DevColumn c = ldc(a.cols + a.seg_col);
+        if (t.active) gp((int32_t*)c.values)[t.rec] = t.seg;
+        const uint64_t m = __ballot(t.active);
+        if (lane == 0) gp(c.validity)[t.tile] = m;
+    }
+
+    // ---- OCCURS DEPENDING ON element counts (extractArray, RecordExtractors.scala:66-114)
+    for (int ai = 0; ai < a.n_arrays; ai++) {
+        const cbx_array ar = ldc(a.arrays + ai);
+        int cnt = ar.max_count;
+        if (ar.dependee >= 0 && t.active) {
+            const Field df = ldc(a.fields + ar.dependee);
+            const int o = a.start_off + df.offset;
+            const bool seg_ok = df.segment < 0 || df.segment == t.seg;
+            if (seg_ok && o + df.size <= t.avail) {
+                Val dv = decode_count_int(df, rp + o);
+                if (dv.valid) {
+                    const int32_t v = (int32_t)dv.lo;   // Number.intValue
+                    if (v >= ar.min_count && v <= ar.max_count) cnt = v;
+                }
+            }
+        }
+        s_cnt[ai * kWave + lane] = cnt;
+        if (a.mode == 0 && ar.count_column >= 0) {
+            const DevColumn c = ldc(a.cols + ar.count_column);
+            const bool ok = t.active && (ar.segment < 0 || ar.segment == t.seg);
+            if (t.active) gp((int32_t*)c.values)[t.rec] = cnt;
+            const uint64_t m = __ballot(ok);
+            if (lane == 0) gp(c.validity)[t.tile] = m;
+        }
+    }
+}
+
+// Diagnostic build only (-DCBX_STAMPS, tools/stamps.py): s_memtime stamps between the segments
+// of the contiguous tile loop, summed per segment over all waves.  The product build has none.
+struct Stamps {
+#ifdef CBX_STAMPS
+    uint64_t acc[8];
+    unsigned long long last;
+    __device__ __forceinline__ void init() {
+        for (int k = 0; k < 8; k++) acc[k] = 0;
+        last = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    __device__ __forceinline__ void mark(int k) {
+        __builtin_amdgcn_sched_barrier(0);
+        unsigned long long t;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        acc[k] += t - last;
+        last = t;
+    }
+    __device__ __forceinline__ void flush(const KernelArgs& a, int lane) {
+        if (lane == 0 && a.stamps) {
+            for (int k = 0; k < 6; k++) atomicAdd((unsigned long long*)a.stamps + k, (unsigned long long)acc[k]);
+            atomicAdd((unsigned long long*)a.stamps + 7, 1ull);
+        }
+    }
+#else
+    __device__ __forceinline__ void init() {}
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush(const KernelArgs&, int) {}
+#endif
+};
+
+// LDS carve-up of a decode workgroup: the code page LUT, then one region per wave.
+struct WaveLds {
+    uint32_t* lut;
+    uint8_t* img;       // record image (after the front guard)
+    int32_t* cnt;       // OCCURS element counts
+    uint8_t* str;       // string payload staging
+};
+
+__device__ __forceinline__ WaveLds wave_lds(const KernelArgs& a, uint8_t* smem, int wid) {
+    WaveLds l;
+    l.lut = (uint32_t*)smem;
+    uint8_t* wbase = smem + 1024 + wid * a.lds_wave;
+    l.img = wbase + kGuard;
+    l.cnt = (int32_t*)(wbase + a.lds_rows);
+    l.str = wbase + a.lds_rows + a.lds_counts;
+    return l;
+}
+
+// Fixed-length records, the whole tile span staged once per tile, its loads issued one tile
+// ahead.  Nothing else in this loop loads from HBM (prologue and decode read the LDS image), so
+// no wait on the staging loads or on earlier stores sits in the decode.  `body` decodes one
+// staged tile: body(a, t, img, rec_addr, lds, lane, stamps).
+template <typename Body>
+__device__ __forceinline__ void contig_loop(const KernelArgs& a, const WaveLds& l, int64_t tile, int64_t tstep,
+                                            int lane, const Body& body) {
+    uint4 buf[kPre];
+    bool have = false;
+    if (tile < a.n_tiles) {
+        const ContigSpan sp = contig_span(a, tile);
+        if (sp.inb) { contig_issue(a, sp, lane, buf); have = true; }
+    }
+    Stamps st;
+    st.init();
+    while (tile < a.n_tiles) {
+        const ContigSpan sp = contig_span(a, tile);
+        if (have) contig_store(a, sp, lane, buf, l.img);
+        else contig_stage_guarded(a, sp, lane, l.img);
+        wave_sync_lds();
+        st.mark(0);   // staging: wait for the prefetched loads + LDS writes
+        const int64_t next = tile + tstep;
+        have = false;
+        if (next < a.n_tiles) {
+            const ContigSpan sn = contig_span(a, next);
+            if (sn.inb) { contig_issue(a, sn, lane, buf); have = true; }
+        }
+        st.mark(1);   // prefetch issue
+        TileCtx t = tile_ctx(a, tile, lane);
+        const uint32_t rec0 = (uint32_t)(lane * a.cpitch + 4 * sp.mis_dw);   // record start in the image
+        tile_prologue(a, t, l.img + rec0, lane, l.lut, l.cnt);
+        st.mark(2);   // prologue
+        body(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
+        wave_sync_lds();
+        st.mark(5);   // end of tile
+        tile = next;
+    }
+    st.flush(a, lane);
+}
+
+}  // namespace cbx

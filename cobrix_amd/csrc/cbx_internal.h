@@ -1,6 +1,8 @@
 // cbx_internal.h -- device-side plan layout shared by the kernels and the C ABI.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 #include "cbx_decode.h"
@@ -108,7 +110,6 @@ struct KernelArgs {
     int32_t cpitch;
     int32_t stride_dw;         // stride / 4
     float inv_stride_dw;       // 1 / stride_dw
-    int32_t contig_chunks;     // 16-byte chunks per lane held in registers (prefetch depth)
     // plan
     const CBX_CONST Field* fields;
     const CBX_CONST Window* windows;
@@ -135,6 +136,7 @@ struct KernelArgs {
     int32_t lds_counts;        // OCCURS element counts
     int32_t str_stage;         // string payload staging bytes
     int32_t lds_wave;          // total per wave
+    uint64_t* stamps;          // diagnostic build (CBX_STAMPS) only: per-segment wave-cycle sums
 };
 
 }  // namespace cbx

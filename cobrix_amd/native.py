@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcobrix_hip.so")
+# CBX_LIB_VARIANT=stamps selects the diagnostic build (tools/stamps.py); the product library otherwise
+LIB_PATH = os.path.join(_HERE, "libcobrix_hip_%s.so" % os.environ["CBX_LIB_VARIANT"]
+                        if os.environ.get("CBX_LIB_VARIANT") else "libcobrix_hip.so")
 
 CBX_MAX_DIMS = 4
 CBX_MAX_SEG_KEYS = 32

@@ -22,6 +22,12 @@ extern "C" int cbxh_decode(const cbx_field* cf, const uint8_t* p, int n_avail, c
         bool defer = false;
         const NumOp op = make_numop(f, 0, 0, nullptr, nullptr, 0);
         Val v = f.size <= 64 ? decode_value(op, img, at, defer) : decode_numeric(f, p);
+        if (f.size <= 64 && f.out_type != CBX_O_DEC128) {
+            // the kernels' narrow-output (<= 8 bytes) specialisation must agree on the low word
+            bool d8 = false;
+            const Val v8 = decode_value<8>(op, img, at, d8);
+            if (d8 != defer || v8.valid != v.valid || (v.valid && v8.lo != v.lo)) return -1;
+        }
         Val g = decode_numeric(f, p);   // generic byte-loop decoder must agree
         if (defer) {
             if (v.valid) return -1;    // a deferred value is left null for the fixup pass

@@ -6,7 +6,7 @@ import os
 import sys
 
 tag = sys.argv[1]
-root = f"gpurun_out/prof_{tag}"
+root = tag if os.path.isdir(tag) else f"gpurun_out/prof_{tag}"
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 names = {}
 for f in sorted(glob.glob(f"{root}/pmc*/run_counter_collection.csv")):

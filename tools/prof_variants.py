@@ -22,6 +22,17 @@ def variant(cb: str, keep) -> str:
     return "\n".join(out)
 
 
+VARIANTS = {
+    "full": lambda n: True,
+    "no_string": lambda n: n != "NAME",
+    "string_only": lambda n: n == "NAME",
+    "bcd8_only": lambda n: n.startswith("AMT"),
+    "zoned_only": lambda n: n.startswith("ZN") or n.startswith("ZD"),
+    "binary_only": lambda n: n in ("REC-ID", "BR-ID", "ACCT-NO", "CUST-KEY"),
+    "one_field": lambda n: n == "REC-ID",
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=10_000_000)
@@ -35,16 +46,7 @@ def main():
     rec = syn200(a.records, device="cuda").view(-1)
     L = N.load()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    variants = {
-        "full": lambda n: True,
-        "no_string": lambda n: n != "NAME",
-        "string_only": lambda n: n == "NAME",
-        "bcd8_only": lambda n: n.startswith("AMT"),
-        "zoned_only": lambda n: n.startswith("ZN") or n.startswith("ZD"),
-        "binary_only": lambda n: n in ("REC-ID", "BR-ID", "ACCT-NO", "CUST-KEY"),
-        "one_field": lambda n: n == "REC-ID",
-    }
-    for name, keep in variants.items():
+    for name, keep in VARIANTS.items():
         if a.only and name != a.only:
             continue
         rd = FixedLenNestedReader(variant(SYN200_COPYBOOK, keep), ReaderParameters())
