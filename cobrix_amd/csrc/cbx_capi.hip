@@ -94,6 +94,12 @@ struct cbx_plan {
     uint32_t* d_local = nullptr;    int64_t local_cap = 0;
     uint8_t* d_scratch = nullptr;   int64_t scratch_cap = 0;
     uint64_t* d_stamps = nullptr;   // diagnostic build only
+    // copybook-specialised kernel (cbx_jit.h), built on the first large contiguous decode
+    int64_t jit_min = 262144;
+    bool jit_tried[2] = {false, false};      // [windowed, contiguous] op set
+    hipFunction_t jit_fn[2] = {nullptr, nullptr};
+    std::string jit_error;
+    int last_kind = 0;
     int32_t* d_status = nullptr;
     int num_cus = 256;
     // profiling: HIP events around the decode kernel and the post passes of every call (no sync)
@@ -102,6 +108,8 @@ struct cbx_plan {
     struct CallEvents { hipEvent_t e[3]; };
     std::vector<CallEvents> ev_calls;    // recorded, not yet read
 };
+
+#include "cbx_jit.h"
 
 // grow a device buffer to at least `need` elements (contents not preserved)
 template <typename T>
@@ -296,6 +304,9 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
         return fail(CBX_E_ARGUMENT, "cbx_plan_create: invalid arguments");
     cbx_plan* P = new cbx_plan();
     P->opts = *opts;
+    P->jit_min = opts->jit_min_records < 0 ? -1 : (opts->jit_min_records == 0 ? 262144 : opts->jit_min_records);
+    if (const char* e = getenv("CBX_JIT"))
+        if (e[0] == '0') P->jit_min = -1;   // operator switch: table-driven kernel only
     P->n_columns = opts->n_columns;
     if (P->n_columns <= 0) { delete P; return fail(CBX_E_ARGUMENT, "cbx_plan_create: n_columns must be positive"); }
     P->hfields.assign(fields, fields + n_fields);
@@ -614,11 +625,22 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
     // resident blocks per CU: the LDS bound and the runtime's occupancy (registers); the grid
     // never exceeds what can be co-resident, so the static tile order of the look-back holds
+    // copybook-specialised kernel for large contiguous batches (cbx_jit.h)
+    hipFunction_t jfn = nullptr;
+    if (mode == 0 && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
+        const int k = contig ? 1 : 0;
+        if (!P->jit_tried[k]) {
+            P->jit_tried[k] = true;
+            P->jit_fn[k] = jit_get(jit_source(contig, S.win, S.nops, S.batches, S.sops), &P->jit_error);
+        }
+        jfn = P->jit_fn[k];
+    }
+    P->last_kind = jfn ? 1 : 0;
     int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / lds));
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, decode_kernel, kWave * kWavesPerBlock, lds) == hipSuccess &&
-        occ > 0)
-        blocks_per_cu = std::min(blocks_per_cu, occ);
+    const hipError_t oe = jfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, jfn, kWave * kWavesPerBlock, lds)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, decode_kernel, kWave * kWavesPerBlock, lds);
+    if (oe == hipSuccess && occ > 0) blocks_per_cu = std::min(blocks_per_cu, occ);
     const int64_t blocks_needed = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t grid = std::min<int64_t>(blocks_needed, (int64_t)P->num_cus * blocks_per_cu);
     const bool prof = P->profiling && mode == 0;
@@ -627,8 +649,13 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
         HIP_CHECK(hipEventRecord(ce.e[0], st));
     }
-    hipLaunchKernelGGL(decode_kernel, dim3((unsigned)grid), dim3(kWave * kWavesPerBlock), lds, st, a);
-    HIP_CHECK(hipGetLastError());
+    if (jfn) {
+        void* kargs[] = {&a};
+        HIP_CHECK(hipModuleLaunchKernel(jfn, (unsigned)grid, 1, 1, kWave * kWavesPerBlock, 1, 1, (unsigned)lds, st, kargs, nullptr));
+    } else {
+        hipLaunchKernelGGL(decode_kernel, dim3((unsigned)grid), dim3(kWave * kWavesPerBlock), lds, st, a);
+        HIP_CHECK(hipGetLastError());
+    }
     if (prof) HIP_CHECK(hipEventRecord(ce.e[1], st));
     if (mode == 0 && n_defer > 0) {
         const unsigned gy = (unsigned)std::min<int64_t>(n_defer, 65535);
@@ -714,6 +741,31 @@ extern "C" int cbx_debug_stamps(cbx_plan* P, uint64_t* out) {
     return CBX_OK;
 }
 #endif
+
+extern "C" int cbx_plan_specialize(cbx_plan* P, char* source, int64_t source_cap, int64_t* source_len, int32_t compile) {
+    if (!P) return fail(CBX_E_ARGUMENT, "cbx_plan_specialize: invalid arguments");
+    const cbx_plan::OpSet& S = P->contig_ok ? P->cset : P->wset;
+    const std::string src = jit_source(P->contig_ok, S.win, S.nops, S.batches, S.sops);
+    if (source_len) *source_len = (int64_t)src.size();
+    if (source && source_cap > 0) {
+        const size_t n = std::min<size_t>(src.size(), (size_t)source_cap - 1);
+        memcpy(source, src.data(), n);
+        source[n] = 0;
+    }
+    if (compile) {
+        std::vector<char> code;
+        std::string err;
+        if (!jit_compile(src, &code, &err)) return fail(CBX_E_HIP, err);
+    }
+    return CBX_OK;
+}
+
+extern "C" int cbx_plan_kernel_kind(cbx_plan* P, int32_t* kind) {
+    if (!P || !kind) return fail(CBX_E_ARGUMENT, "cbx_plan_kernel_kind: invalid arguments");
+    *kind = P->last_kind;
+    if (!P->last_kind && !P->jit_error.empty()) g_err = P->jit_error;
+    return CBX_OK;
+}
 
 extern "C" int cbx_plan_kernel_times(cbx_plan* P, float* decode_ms, float* fixup_ms, int32_t max_calls, int32_t* n_calls) {
     if (!P || !n_calls || max_calls < 0) return fail(CBX_E_ARGUMENT, "cbx_plan_kernel_times: invalid arguments");

@@ -22,8 +22,10 @@
 // All functions are __host__ __device__ so tests/native can fuzz the exact device arithmetic
 // against the oracle on a CPU; the product only runs them inside the HIP kernels.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif   /* hipRTC (cbx_jit.h) provides the runtime and the fixed-width types */
 
 #include "cobrix_hip.h"
 

@@ -243,6 +243,30 @@ __device__ __forceinline__ void num_batch(const KernelArgs& a, const Batch& b, c
     }
 }
 
+// A group of N <= 4 numeric ops with the op records known at compile time (the specialised
+// kernels of cbx_jit.h): the interpreter's batch step with every descriptor field folded.
+template <int V, int W, bool kOdo, int N>
+__device__ __forceinline__ void num_group(const KernelArgs& a, const NumOp (&op)[N], int i0, const TileCtx& t,
+                                          const uint8_t* src, uint32_t rec_addr, const int32_t* s_cnt, int lane) {
+    constexpr bool kWide = V == V_BCD16 || V == V_ZONED16;
+    constexpr bool kRead = V != V_GENERIC;
+    const int lim = t.active ? t.avail - a.start_off : -1;
+    bool ok[N];
+    uint64_t r1[N], r0[N];
+#pragma unroll
+    for (int u = 0; u < N; u++) {
+        ok[u] = op[u].eo + op[u].size <= lim;
+        r1[u] = r0[u] = 0;
+        if (kRead) {
+            const uint32_t end = rec_addr + (ok[u] ? (uint32_t)op[u].eo : 0u) + op[u].size;
+            r1[u] = img_le64_ending(src, end);
+            if (kWide) r0[u] = img_le64_ending(src, end - 8);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < N; u++) num_one<V, W, kOdo, false>(a, op[u], i0 + u, t, ok[u], r1[u], r0[u], s_cnt, lane);
+}
+
 // One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):
 // span + tile-local scan; the tile's payload is staged contiguously in LDS and copied with
 // dword stores to the tile's scratch region; the tile-local start of every value and the

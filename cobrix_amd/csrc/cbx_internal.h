@@ -2,8 +2,8 @@
 #pragma once
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
-#endif
 #include <stdint.h>
+#endif   /* hipRTC (cbx_jit.h) provides the runtime and the fixed-width types */
 
 #include "cbx_decode.h"
 #include "cobrix_hip.h"

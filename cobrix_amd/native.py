@@ -34,7 +34,7 @@ OUT_WIDTH = {O_I32: 4, O_I64: 8, O_DEC64: 8, O_DEC128: 16, O_F32: 4, O_F64: 8}
 EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx_plan_destroy",
                     "cbx_string_bound", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
                     "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
-                    "cbx_plan_kernel_times")
+                    "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize")
 ABI_VERSION = 3
 
 
@@ -76,7 +76,8 @@ class CbxSegmentMap(ctypes.Structure):
 class CbxPlanOptions(ctypes.Structure):
     _fields_ = [("n_columns", ctypes.c_int32), ("file_id", ctypes.c_int32), ("has_segments", ctypes.c_int32),
                 ("window_bytes", ctypes.c_int32), ("segment_column", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 3), ("lut", ctypes.c_uint32 * 256),
+                ("jit_min_records", ctypes.c_int32), ("reserved", ctypes.c_int32 * 2),
+                ("lut", ctypes.c_uint32 * 256),
                 ("segments", CbxSegmentMap)]
 
 
@@ -123,6 +124,8 @@ def load():
     L.cbx_frame_rdw.argtypes = [P, i64, P, i32, P, P, P, i64, P, P]
     L.cbx_plan_set_profiling.argtypes = [P, i32]
     L.cbx_plan_kernel_times.argtypes = [P, P, P, i32, P]
+    L.cbx_plan_kernel_kind.argtypes = [P, P]
+    L.cbx_plan_specialize.argtypes = [P, P, i64, P, i32]
     if L.cbx_abi_version() != ABI_VERSION:
         raise NativeLibraryError(f"{LIB_PATH}: ABI {L.cbx_abi_version()} != {ABI_VERSION}; rebuild it")
     _lib = L

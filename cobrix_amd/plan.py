@@ -116,7 +116,7 @@ def _kind_and_flags(p: cbk.Primitive, cb: cbk.Copybook) -> Tuple[int, int]:
 
 def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
                segment_redefine_map: Optional[Dict[str, str]] = None, generate_record_id: bool = False,
-               file_id: int = 0, window_bytes: int = 0) -> DecodePlan:
+               file_id: int = 0, window_bytes: int = 0, jit_min_records: int = 0) -> DecodePlan:
     fields: List[N.CbxField] = []
     arrays: List[N.CbxArray] = []
     columns: List[ColumnInfo] = []
@@ -244,6 +244,7 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
     opts.file_id = file_id
     opts.window_bytes = window_bytes
     opts.segment_column = seg_col
+    opts.jit_min_records = jit_min_records
     lut = utf8_lut(lut_for(cb.code_page))
     for i in range(256):
         opts.lut[i] = int(lut[i])

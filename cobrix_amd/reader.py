@@ -62,6 +62,9 @@ class ReaderParameters:
     non_terminals: Sequence[str] = ()
     occurs_mappings: Dict[str, Dict[str, int]] = field(default_factory=dict)
     window_bytes: int = 0
+    # fixed-length batches of at least this many records run a copybook-specialised kernel
+    # (hipRTC, compiled once per layout): 0 = library default, < 0 = never
+    jit_min_records: int = 0
 
 
 @dataclass
@@ -252,7 +255,8 @@ class _BaseReader:
             raise N.CbxError(N.CBX_E_UNSUPPORTED, "variable_size_occurs=true is not on the GPU path yet")
         self.plan = build_plan(self.copybook, segment_field=params.segment_field,
                                segment_redefine_map=params.segment_id_redefine_map or None,
-                               generate_record_id=params.generate_record_id, window_bytes=params.window_bytes)
+                               generate_record_id=params.generate_record_id, window_bytes=params.window_bytes,
+                               jit_min_records=params.jit_min_records)
         self.native = NativePlan(self.plan)
 
     @property

@@ -26,7 +26,18 @@
  */
 #ifndef COBRIX_HIP_H
 #define COBRIX_HIP_H
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#else   /* compiled by hipRTC (the library's copybook-specialised kernels): its fixed-width types */
+typedef __hip_internal::int8_t int8_t;
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::int16_t int16_t;
+typedef __hip_internal::uint16_t uint16_t;
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::int64_t int64_t;
+typedef __hip_internal::uint64_t uint64_t;
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -131,7 +142,10 @@ typedef struct {
     int32_t has_segments;   /* segment map valid */
     int32_t window_bytes;   /* LDS window per record (0 = default) */
     int32_t segment_column; /* column receiving the active segment index per record, -1 none */
-    int32_t reserved[3];
+    int32_t jit_min_records;/* batches of at least this many records run a kernel
+                               specialised for the copybook (compiled once with hipRTC);
+                               0 = default (262144), < 0 = never */
+    int32_t reserved[2];
     uint32_t lut[256];      /* code page: UTF-8 bytes (0-23), length (24-25), trimmable (31) */
     cbx_segment_map segments;
 } cbx_plan_options;
@@ -202,6 +216,19 @@ int cbx_plan_check(cbx_plan* plan, void* stream);
  * durations in ms (oldest first, *n_calls of them) and clears the record. */
 int cbx_plan_set_profiling(cbx_plan* plan, int32_t enable);
 int cbx_plan_kernel_times(cbx_plan* plan, float* decode_ms, float* post_ms, int32_t max_calls, int32_t* n_calls);
+
+/* Which decode kernel the plan's last decode call ran: *kind = 0 the table-driven kernel,
+ * 1 the copybook-specialised kernel.  If specialisation was attempted and failed, *kind = 0 and
+ * the reason is in cbx_last_error() (the call itself succeeded on the table-driven kernel). */
+int cbx_plan_kernel_kind(cbx_plan* plan, int32_t* kind);
+
+/* The copybook-specialised kernel of a plan (its contiguous fixed-length variant when the layout
+ * has one, else the windowed variant): writes its HIP source
+ * (NUL-terminated, truncated to source_cap) and its length; with compile != 0 also compiles it
+ * for gfx950 with hipRTC (no device needed) and reports a failure with the compiler log in
+ * cbx_last_error().  Decode calls build and use it on their own (cbx_plan_options.jit_min_records);
+ * this entry point is for inspection, ahead-of-time warm-up and tests. */
+int cbx_plan_specialize(cbx_plan* plan, char* source, int64_t source_cap, int64_t* source_len, int32_t compile);
 
 /* RDW header walk on the GPU (RecordHeaderParserRDW + VRLRecordReader), seeded by sparse-index
  * entry points: seeds[k] is a known record-header offset (offsetFrom of an index entry), the

@@ -161,3 +161,58 @@ def test_rdw_errors():
     t = torch.frombuffer(bytearray(bad), dtype=torch.uint8).cuda()
     with pytest.raises(CbxError):
         rd.frame(t, len(bad))
+
+
+def _kernel_kind(rd) -> int:
+    import ctypes
+    from cobrix_amd import native as N
+    k = ctypes.c_int32(-1)
+    N.check(N.load().cbx_plan_kernel_kind(rd.native.handle, ctypes.byref(k)))
+    return k.value
+
+
+def _jit_cases():
+    from test_decode_fuzz import FUZZ_COPYBOOK, _random_bytes
+    t1 = (G.read("test1_copybook.cob").decode(), G.read("test1_data", "example.bin"), {}, {})
+    t6 = (G.read("test6_copybook.cob").decode(), G.read("test6_data", "INTEGR.TYPES.NOV28.DATA.dat"), {}, {})
+    syn = (SYN200_COPYBOOK, syn200(100_003, seed=11).numpy().tobytes(), {}, {})
+    cb = cbk.parse_copybook(FUZZ_COPYBOOK, code_page="cp037", string_trimming="left", floating_point_format="IEEE754")
+    rng = np.random.default_rng(9)
+    leaves = list(O._iter_leaves(cb.ast))
+    recs = bytearray()
+    for _ in range(2000):
+        for p in leaves:
+            recs += _random_bytes(rng, p, p.data_size)
+    fz = (FUZZ_COPYBOOK, bytes(recs),
+          dict(ebcdic_code_page="cp037", string_trimming_policy="left", floating_point_format="IEEE754"), {})
+    return {"test1": t1, "test6": t6, "syn200": syn, "fuzz_cp037": fz}
+
+
+@pytest.mark.parametrize("case", ["test1", "test6", "syn200", "fuzz_cp037"])
+def test_specialised_kernel_vs_oracle(case):
+    """The copybook-specialised kernel (hipRTC, cbx_jit.h) gives the oracle's results bit for bit."""
+    cb_text, data, kw, okw = _jit_cases()[case]
+    rd, batch = _fixed(cb_text, data, jit_min_records=1, **kw)
+    assert _kernel_kind(rd) == 1, "specialised kernel did not run"
+    errs = compare_batch(batch, O.decode_fixed(rd.copybook, data, **okw))
+    assert not errs, errs
+    # the table-driven kernel on the same plan layout agrees as well
+    rd2, batch2 = _fixed(cb_text, data, jit_min_records=-1, **kw)
+    assert _kernel_kind(rd2) == 0
+    assert not compare_batch(batch2, O.decode_fixed(rd2.copybook, data, **okw))
+
+
+def test_specialised_kernel_segments_and_offsets():
+    cb_text = G.read("test5_copybook.cob").decode()
+    raw = G.read("test5_data", "COMP.DETAILS.SEP30.DATA.dat")
+    off, ln = O.frame_rdw(raw)
+    cb = cbk.parse_copybook(cb_text)
+    L = cb.record_size
+    recs = b"".join(b"\x00\x11\x22" + (raw[o:o + l] + b"\x40" * L)[:L] + b"\x33" for o, l in zip(off, ln))
+    seg_map = {"C": "STATIC-DETAILS", "P": "CONTACTS"}
+    rd, batch = _fixed(cb_text, recs, segment_field="SEGMENT-ID", segment_id_redefine_map=seg_map,
+                       start_offset=3, end_offset=1, jit_min_records=1)
+    assert _kernel_kind(rd) == 1
+    res = O.decode_fixed(rd.copybook, recs, segment_field="SEGMENT-ID", segment_redefine_map=seg_map,
+                         record_size=L, start_offset=3, end_offset=1)
+    assert not compare_batch(batch, res)

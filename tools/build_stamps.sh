@@ -3,4 +3,4 @@
 set -e
 cd "$(dirname "$0")/.."
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DCBX_STAMPS -Iinclude -Icobrix_amd/csrc \
-    -o cobrix_amd/libcobrix_hip_stamps.so cobrix_amd/csrc/cbx_capi.hip
+    -o cobrix_amd/libcobrix_hip_stamps.so cobrix_amd/csrc/cbx_capi.hip -lhiprtc
