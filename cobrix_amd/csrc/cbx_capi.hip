@@ -529,7 +529,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         int64_t scratch = 0;
         for (int q = 0; q < P->n_seq; q++) { P->h_seq_scratch[q] = scratch; scratch += n_tiles * P->seq_tile_cap[q]; }
         if ((rr = grow(&P->d_local, &P->local_cap, (int64_t)P->n_seq * a.pitch, st)) ||
-            (rr = grow(&P->d_scratch, &P->scratch_cap, scratch + 16, st)))   // +16: placement reads a dword past a payload end
+            (rr = grow(&P->d_scratch, &P->scratch_cap, scratch + 64, st)))   // +64: placement reads up to 20 bytes past a payload end
             return rr;
     }
     if (mode == 0) {
@@ -659,15 +659,15 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     if (prof) HIP_CHECK(hipEventRecord(ce.e[1], st));
     if (mode == 0 && n_defer > 0) {
         const unsigned gy = (unsigned)std::min<int64_t>(n_defer, 65535);
-        hipLaunchKernelGGL(fixup_kernel, dim3((unsigned)((n_tiles + 255) / 256), gy), dim3(256), 0, st, a,
+        hipLaunchKernelGGL(fixup_kernel, dim3((unsigned)((n_tiles + 4 * kWave - 1) / (4 * kWave)), gy), dim3(4 * kWave), 0, st, a,
                            (const CBX_CONST DeferSeq*)P->d_defer, n_defer);
         HIP_CHECK(hipGetLastError());
     }
     if (P->n_seq > 0) {
         if ((r = string_scan(P, n_tiles, st))) return r;
         if (mode == 0) {
-            const unsigned gx = (unsigned)std::min<int64_t>(n_tiles, 4096);
-            hipLaunchKernelGGL(str_place_kernel, dim3(gx, (unsigned)std::min<int64_t>(P->n_seq, 65535)), dim3(kWave), 0, st,
+            const unsigned gx = (unsigned)((n_tiles + kPlaceWaves - 1) / kPlaceWaves);
+            hipLaunchKernelGGL(str_place_kernel, dim3(gx, (unsigned)std::min<int64_t>(P->n_seq, 65535)), dim3(kWave * kPlaceWaves), 0, st,
                                (const CBX_CONST SeqCall*)P->d_seqcall, (const uint32_t*)P->d_str_tot,
                                (const int64_t*)P->d_str_excl, n_tiles, c.n_rec, P->n_seq, P->d_status);
             HIP_CHECK(hipGetLastError());

@@ -179,48 +179,62 @@ struct SeqCall {
     int32_t reserved;
 };
 
-__global__ __launch_bounds__(kWave) void str_place_kernel(const CBX_CONST SeqCall* seqs, const uint32_t* tot,
-                                                          const int64_t* excl, int64_t n_tiles, int64_t n_rec,
-                                                          int32_t n_seq, int32_t* status) {
-    const int lane = threadIdx.x;
+// One wave per (sequence, tile): 4 tiles per workgroup, no grid-stride loop (tiles are ~1 KiB
+// each: many in flight hide the load latency).  The payload moves in 16-byte pieces: each lane
+// reads 5 dwords of the (aligned) scratch region and writes 4 realigned dwords at the
+// destination (any alignment; byte stores at the unaligned ends).
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+constexpr int kPlaceWaves = 4;
+
+__global__ __launch_bounds__(kWave * kPlaceWaves) void str_place_kernel(const CBX_CONST SeqCall* seqs, const uint32_t* tot,
+                                                                         const int64_t* excl, int64_t n_tiles, int64_t n_rec,
+                                                                         int32_t n_seq, int32_t* status) {
+    const int lane = threadIdx.x % kWave;
+    const int64_t tile = (int64_t)blockIdx.x * kPlaceWaves + threadIdx.x / kWave;
+    if (tile >= n_tiles) return;
     for (int seq = blockIdx.y; seq < n_seq; seq += gridDim.y) {
         const SeqCall q = ldc(seqs + seq);
         const int64_t seq0 = excl[(int64_t)seq * n_tiles];
-        CBX_GLOBAL int64_t* offs = gp(q.offsets);
-        const CBX_GLOBAL uint32_t* local = gp(q.local);
-        for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-            const int64_t base = excl[(int64_t)seq * n_tiles + tile] - seq0;
-            const uint32_t n = tot[(int64_t)seq * n_tiles + tile];
-            const int64_t rec = tile * kWave + lane;
-            offs[rec] = q.region + base + local[rec];   // lanes past n_rec write padding entries
-            if (tile == n_tiles - 1 && lane == 0) {
-                offs[n_rec] = q.region + base + n;
-                if (q.size) *gp(q.size) = base + n;
-            }
-            if (base + (int64_t)n > q.capacity) {
-                if (lane == 0) atomicOr(status, 1);
-                continue;
-            }
-            // payload: scratch (aligned) -> data + base (any alignment); dword stores in the middle,
-            // byte stores for the unaligned head and tail
-            const CBX_GLOBAL uint32_t* src = gp((const uint32_t*)(q.scratch + tile * (int64_t)q.tile_cap));
-            CBX_GLOBAL uint8_t* dst = gp(q.data + base);
-            const uint64_t g0 = (uint64_t)(q.data + base);
-            const uint64_t A = (g0 + 3) & ~3ull, B = (g0 + n) & ~3ull;
-            const CBX_GLOBAL uint8_t* s8 = (const CBX_GLOBAL uint8_t*)src;
-            if (A > B) {
-                if (lane < (int)n) dst[lane] = s8[lane];
-                continue;
-            }
-            const int head = (int)(A - g0), tail = (int)(g0 + n - B);
-            if (lane < head) dst[lane] = s8[lane];
-            if (lane < tail) dst[(int)(B - g0) + lane] = s8[(int)(B - g0) + lane];
-            const int ndw = (int)((B - A) >> 2);
-            CBX_GLOBAL uint32_t* d32 = (CBX_GLOBAL uint32_t*)(dst + head);
-            for (int i = lane; i < ndw; i += kWave) {
-                const uint32_t byte = (uint32_t)head + 4u * (uint32_t)i;
-                const uint32_t lo = src[byte >> 2], hi = src[(byte >> 2) + 1];
-                d32[i] = align_bytes(hi, lo, byte & 3u);
+        const int64_t base = excl[(int64_t)seq * n_tiles + tile] - seq0;
+        const uint32_t n = tot[(int64_t)seq * n_tiles + tile];
+        const int64_t rec = tile * kWave + lane;
+        gp(q.offsets)[rec] = q.region + base + gp(q.local)[rec];   // lanes past n_rec write padding entries
+        if (tile == n_tiles - 1 && lane == 0) {
+            gp(q.offsets)[n_rec] = q.region + base + n;
+            if (q.size) *gp(q.size) = base + n;
+        }
+        if (base + (int64_t)n > q.capacity) {
+            if (lane == 0) atomicOr(status, 1);
+            continue;
+        }
+        const CBX_GLOBAL uint32_t* src = gp((const uint32_t*)(q.scratch + tile * (int64_t)q.tile_cap));
+        const CBX_GLOBAL uint8_t* s8 = (const CBX_GLOBAL uint8_t*)src;
+        CBX_GLOBAL uint8_t* dst = gp(q.data + base);
+        const uint32_t g0 = (uint32_t)((uint64_t)(q.data + base) & 3);
+        const uint32_t head = (4 - g0) & 3;                 // bytes before the first aligned dword
+        if (n <= head) {
+            if (lane < (int)n) dst[lane] = s8[lane];
+            continue;
+        }
+        const uint32_t ndw = (n - head) >> 2;               // whole destination dwords
+        const uint32_t tail = (n - head) & 3;
+        if (lane < (int)head) dst[lane] = s8[lane];
+        if (lane < (int)tail) dst[head + 4 * ndw + lane] = s8[head + 4 * ndw + lane];
+        CBX_GLOBAL uint32_t* d32 = (CBX_GLOBAL uint32_t*)(dst + head);
+        const uint32_t sh = head & 3;                       // source byte shift (scratch is 16-aligned)
+        const uint32_t k0 = head >> 2;                      // = 0: head < 4
+        for (uint32_t d = 4u * lane; d < ndw; d += 4u * kWave) {
+            const uint32_t k = k0 + d;
+            const u32x4a v = *(const CBX_GLOBAL u32x4a*)(src + k);
+            const uint32_t e = src[k + 4];
+            const uint32_t w0 = align_bytes(v.y, v.x, sh), w1 = align_bytes(v.z, v.y, sh);
+            const uint32_t w2 = align_bytes(v.w, v.z, sh), w3 = align_bytes(e, v.w, sh);
+            if (d + 4 <= ndw) {
+                *(CBX_GLOBAL u32x4a*)(d32 + d) = u32x4a{w0, w1, w2, w3};
+            } else {
+                d32[d] = w0;
+                if (d + 1 < ndw) d32[d + 1] = w1;
+                if (d + 2 < ndw) d32[d + 2] = w2;
             }
         }
     }
@@ -235,13 +249,17 @@ struct DeferSeq {
     int32_t field, slot;
 };
 
+// One wave per 64 tiles of a deferral sequence: the wave's deferred values (set bits of its 64
+// words, ~0.5 % of the zoned values of SYN200) are enumerated with a wave scan and spread over
+// the lanes one value each, so a word with many deferrals does not serialise its wave.
 __global__ __launch_bounds__(256) void fixup_kernel(KernelArgs a, const CBX_CONST DeferSeq* dseq, int32_t n_defer) {
-    // blockIdx.y (strided) = deferral sequence: the op descriptor is wave-uniform (scalar loads)
-    const int64_t tile = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (tile >= a.n_tiles) return;
+    const int lane = threadIdx.x % kWave;
+    const int64_t tile = ((int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave) * kWave + lane;
     for (int d = blockIdx.y; d < n_defer; d += gridDim.y) {
-        uint64_t bits = a.defer_bits[(int64_t)d * a.n_tiles + tile];
-        if (!__ballot(bits != 0)) continue;
+        const uint64_t bits = tile < a.n_tiles ? a.defer_bits[(int64_t)d * a.n_tiles + tile] : 0ull;
+        uint32_t total;
+        const uint32_t ex = wave_excl_scan32((uint32_t)__popcll(bits), lane, total);
+        if (total == 0) continue;
         const DeferSeq ds = ldc(dseq + d);
         const CBX_CONST Field* fp = a.fields + ds.field;
         const Field f = ldc(fp);
@@ -252,17 +270,28 @@ __global__ __launch_bounds__(256) void fixup_kernel(KernelArgs a, const CBX_CONS
             rem /= dc;
         }
         const DevColumn col = ldc(a.cols + f.column);
-        uint64_t vbits = 0;
-        while (bits) {
-            const int b = __builtin_ctzll(bits);
-            bits &= bits - 1;
-            const int64_t rec = tile * kWave + b;
+        for (uint32_t j = lane; j < total + (kWave - 1) - ((total + kWave - 1) % kWave); j += kWave) {
+            // owner lane: the last lane whose exclusive prefix is <= j (binary search over the wave)
+            int lo = 0;
+#pragma unroll
+            for (int step = kWave / 2; step >= 1; step >>= 1) {
+                const uint32_t e = (uint32_t)__shfl((int)ex, lo + step, kWave);
+                if (e <= j) lo += step;
+            }
+            // every lane takes part in the shuffles (a shuffle from an inactive lane reads 0)
+            const uint64_t wb = __shfl(bits, lo, kWave);
+            const int64_t wt = __shfl(tile, lo, kWave);
+            const uint32_t we = (uint32_t)__shfl((int)ex, lo, kWave);
+            if (j >= total) continue;
+            uint64_t m = wb;
+            for (uint32_t r = j - we; r > 0; r--) m &= m - 1;   // r-th set bit of the owner's word
+            const int b = __builtin_ctzll(m);
+            const int64_t rec = wt * kWave + b;
             const int64_t base = a.base_shift + (a.rec_off ? a.rec_off[rec] : rec * (int64_t)a.stride);
             const Val x = decode_numeric(f, a.data + base + a.start_off + eo);
             store_value(col, f.out_type, (int64_t)ds.slot * a.pitch + rec, x);
-            if (x.valid) vbits |= 1ull << b;
+            if (x.valid) atomicOr((unsigned long long*)(col.validity + (int64_t)ds.slot * a.n_tiles + wt), 1ull << b);
         }
-        if (vbits) gp(col.validity)[(int64_t)ds.slot * a.n_tiles + tile] |= vbits;
     }
 }
 
