@@ -150,6 +150,9 @@ def main():
     dec_avg_ms = sum(dec[: nc.value]) / max(1, nc.value)
     fix_avg_ms = sum(fix[: nc.value]) / max(1, nc.value)
     achieved = alg / (dec_avg_ms * 1e-3) / 1e9
+    kind = ctypes.c_int32(0)
+    N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
+    kname = "cbx_jit_decode (copybook-specialised, hipRTC)" if kind.value == 1 else "cbx::decode_kernel (table-driven)"
     traffic, traffic_src = measured_traffic(n_rec)
     if rank == 0:
         out = {
@@ -175,7 +178,7 @@ def main():
                        "inputs_resident_in_hbm": True},
             "kernel_ms": {"decode_kernel": round(dec_avg_ms, 4),
                           "post_kernels (deferred-value fixup, string scan + placement)": round(fix_avg_ms, 4)},
-            "roofline": {"bound": "hbm", "kernel": "cbx::decode_kernel", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "algorithmic_bytes_per_launch": alg, "traffic": traffic,
                          "traffic_source": traffic_src},

@@ -12,7 +12,7 @@ names = {}
 for f in sorted(glob.glob(f"{root}/pmc*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "cbx::" not in k:
+        if "cbx::" not in k and "cbx_jit" not in k:
             continue
         key = (os.path.basename(os.path.dirname(f)), r["Dispatch_Id"])
         names[key] = k.split("(")[0]

@@ -11,18 +11,21 @@ import json
 import os
 import sys
 
+DECODE_KERNELS = ("cbx::decode_kernel", "cbx_jit_decode")   # table-driven / copybook-specialised
 root, records = sys.argv[1], int(sys.argv[2])
+names = set()
 vals = collections.defaultdict(float)
 for pas, ctr in (("pmc3", "FETCH_SIZE"), ("pmc4", "WRITE_SIZE")):
     rows = list(csv.DictReader(open(os.path.join(root, pas, "run_counter_collection.csv"))))
     per = collections.defaultdict(float)
     for r in rows:
-        if r["Kernel_Name"].startswith("cbx::decode_kernel") and r["Counter_Name"] == ctr:
+        if r["Kernel_Name"].startswith(DECODE_KERNELS) and r["Counter_Name"] == ctr:
             per[r["Dispatch_Id"]] += float(r["Counter_Value"])
+            names.add(r["Kernel_Name"].split("(")[0])
     last = max(per, key=int)          # the measured launch (tools/prof_decode.py --iters 1)
     vals[ctr] = per[last] * 1024.0
 fetch = 2.0 * vals["FETCH_SIZE"]
-out = {"kernel": "cbx::decode_kernel", "records": records, "fetch_bytes_raw": vals["FETCH_SIZE"],
+out = {"kernel": "/".join(sorted(names)), "records": records, "fetch_bytes_raw": vals["FETCH_SIZE"],
        "fetch_bytes": fetch, "write_bytes": vals["WRITE_SIZE"], "traffic_bytes": fetch + vals["WRITE_SIZE"],
        "note": "FETCH_SIZE doubled (gfx950 counts half of 16-B/lane streaming reads)"}
 print(json.dumps(out))
