@@ -824,44 +824,93 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     hipStream_t st = (hipStream_t)stream;
     if (!d_data || n_bytes < 0 || !params || !n_records || (n_seeds > 0 && !seeds))
         return fail(CBX_E_ARGUMENT, "cbx_frame_rdw: invalid arguments");
-    std::vector<int64_t> hseeds;
-    if (n_seeds <= 0) hseeds.push_back(0);
-    else hseeds.assign(seeds, seeds + n_seeds);
-    int ns = (int)hseeds.size();
-    int64_t *d_seeds = nullptr, *d_counts = nullptr, *d_err = nullptr;
-    HIP_CHECK(hipMalloc((void**)&d_seeds, sizeof(int64_t) * ns));
-    HIP_CHECK(hipMalloc((void**)&d_counts, sizeof(int64_t) * ns));
-    HIP_CHECK(hipMalloc((void**)&d_err, sizeof(int64_t) * 2));
-    HIP_CHECK(hipMemcpyAsync(d_seeds, hseeds.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipMemsetAsync(d_err, 0, sizeof(int64_t) * 2, st));
-    RdwArgs a{};
-    a.data = d_data; a.n_bytes = n_bytes; a.seeds = d_seeds; a.n_seeds = ns; a.p = *params;
-    a.counts = d_counts; a.rec_off = d_rec_off; a.rec_len = d_rec_len; a.capacity = capacity; a.error = d_err;
-    int threads = 64, blocks = (ns + threads - 1) / threads;
-    hipLaunchKernelGGL(rdw_walk_kernel, dim3(blocks), dim3(threads), 0, st, a, 0);
-    std::vector<int64_t> cnt(ns);
-    int64_t err[2];
-    HIP_CHECK(hipMemcpyAsync(cnt.data(), d_counts, sizeof(int64_t) * ns, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(err, d_err, sizeof(err), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    int rc = CBX_OK;
-    if (err[0] != 0) {
-        char msg[160];
-        snprintf(msg, sizeof msg, "RDW headers %s at %lld.", err[0] == -2 ? "should never be zero" : "too big (> 100 MiB)",
-                 (long long)err[1]);
-        rc = fail(CBX_E_STATE, msg);
-    } else {
-        int64_t total = 0;
-        for (int k = 0; k < ns; k++) { int64_t c = cnt[k]; cnt[k] = total; total += c; }
-        *n_records = total;
-        if (total > capacity) {
-            rc = fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(total));
-        } else {
-            HIP_CHECK(hipMemcpyAsync(d_counts, cnt.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL(rdw_walk_kernel, dim3(blocks), dim3(threads), 0, st, a, 1);
-            HIP_CHECK(hipStreamSynchronize(st));
+    *n_records = 0;
+    // seed ranges cut into chunks (rdw_spec_kernel / rdw_fix_kernel / rdw_emit_kernel)
+    int64_t chunk = 16 * 1024;
+    if (const char* e = getenv("CBX_RDW_CHUNK_BYTES")) chunk = std::max<int64_t>(8, atoll(e));   // tests: many chunks
+    std::vector<int64_t> hs;
+    if (n_seeds <= 0) hs.push_back(0);
+    else hs.assign(seeds, seeds + n_seeds);
+    std::vector<int64_t> cs, ce, cr;
+    std::vector<uint8_t> ck;
+    for (size_t k = 0; k < hs.size(); k++) {
+        const int64_t r0 = hs[k], r1 = k + 1 < hs.size() ? hs[k + 1] : n_bytes;
+        if (r0 < 0 || r0 > n_bytes || r1 < r0) return fail(CBX_E_ARGUMENT, "cbx_frame_rdw: seeds must be increasing offsets");
+        for (int64_t s0 = r0; s0 < r1 || s0 == r0; s0 += chunk) {
+            cs.push_back(s0);
+            ce.push_back(std::min(s0 + chunk, r1));
+            cr.push_back(r1);
+            ck.push_back(s0 == r0);
+            if (s0 + chunk >= r1) break;
         }
     }
-    (void)hipFree(d_seeds); (void)hipFree(d_counts); (void)hipFree(d_err);
-    return rc;
+    const int64_t n = (int64_t)cs.size();
+    // one device block: start, end, range_end, entry, exit x2, err, base (int64) | count (u32) | known (u8)
+    const size_t bytes = sizeof(int64_t) * (8 * n + 2) + sizeof(uint32_t) * n + n + 64;
+    uint8_t* blk = nullptr;
+    HIP_CHECK(hipMallocAsync((void**)&blk, bytes, st));
+    int64_t* d64 = (int64_t*)blk;
+    RdwChunkArgs c{};
+    int64_t* d_start = d64;
+    int64_t* d_end = d64 + n;
+    int64_t* d_re = d64 + 2 * n;
+    c.entry = d64 + 3 * n;
+    int64_t* exits[2] = {d64 + 4 * n, d64 + 5 * n};
+    c.err = d64 + 6 * n;
+    int64_t* d_base = d64 + 7 * n;
+    unsigned long long* d_first_err = (unsigned long long*)(d64 + 8 * n);
+    c.changed = (int32_t*)(d64 + 8 * n + 1);
+    c.count = (uint32_t*)(d64 + 8 * n + 2);
+    uint8_t* d_known = (uint8_t*)(c.count + n);
+    c.start = d_start; c.end = d_end; c.range_end = d_re; c.known = d_known; c.n = n;
+    HIP_CHECK(hipMemcpyAsync(d_start, cs.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d_end, ce.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d_re, cr.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d_known, ck.data(), n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemsetAsync(d_first_err, 0xFF, sizeof(unsigned long long), st));
+    RdwArgs a{};
+    a.data = d_data; a.n_bytes = n_bytes; a.p = *params;
+    const unsigned threads = 64, blocks = (unsigned)((n + threads - 1) / threads);
+    c.exit_in = nullptr; c.exit_out = exits[0];
+    hipLaunchKernelGGL(rdw_spec_kernel, dim3(blocks), dim3(threads), 0, st, a, c);
+    HIP_CHECK(hipGetLastError());
+    // fix rounds until no entry changes (each round validates at least the next chunk of every
+    // range: bounded by the chunk count)
+    int cur = 0;
+    for (int64_t round = 0; round <= n; round++) {
+        HIP_CHECK(hipMemsetAsync(c.changed, 0, sizeof(int32_t), st));
+        c.exit_in = exits[cur]; c.exit_out = exits[cur ^ 1];
+        hipLaunchKernelGGL(rdw_fix_kernel, dim3(blocks), dim3(threads), 0, st, a, c);
+        HIP_CHECK(hipGetLastError());
+        cur ^= 1;
+        int32_t changed = 0;
+        HIP_CHECK(hipMemcpyAsync(&changed, c.changed, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        if (!changed) break;
+    }
+    // record counts -> bases (host scan of the chunk counts: one value per 16 KiB)
+    std::vector<uint32_t> cnt(n);
+    HIP_CHECK(hipMemcpyAsync(cnt.data(), c.count, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    std::vector<int64_t> base(n);
+    int64_t total = 0;
+    for (int64_t k = 0; k < n; k++) { base[k] = total; total += cnt[k]; }
+    HIP_CHECK(hipMemcpyAsync(d_base, base.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(rdw_emit_kernel, dim3(blocks), dim3(threads), 0, st, a, c, (const int64_t*)d_base, d_rec_off,
+                       d_rec_len, capacity, d_first_err);
+    HIP_CHECK(hipGetLastError());
+    unsigned long long first_err = 0;
+    HIP_CHECK(hipMemcpyAsync(&first_err, d_first_err, sizeof(first_err), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipFreeAsync(blk, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (first_err != ~0ull) {
+        const long long off = (long long)(first_err >> 2);
+        char msg[200];
+        if ((first_err & 3) == 2) snprintf(msg, sizeof msg, "RDW headers should never be zero. Found zero size record at %lld.", off);
+        else snprintf(msg, sizeof msg, "RDW headers too big (length > %lld) at %lld.", 100ll * 1024 * 1024, off);
+        return fail(CBX_E_STATE, msg);
+    }
+    *n_records = total;
+    if (total > capacity) return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(total));
+    return CBX_OK;
 }

@@ -302,55 +302,167 @@ __global__ __launch_bounds__(256) void fixup_kernel(KernelArgs a, const CBX_CONS
 struct RdwArgs {
     const uint8_t* data;
     int64_t n_bytes;
-    const int64_t* seeds;
-    int32_t n_seeds;
     cbx_rdw_params p;
-    int64_t* counts;       // per seed: pass 0 out, pass 1 in (exclusive scan)
-    int64_t* rec_off;
-    int32_t* rec_len;
-    int64_t capacity;
-    int64_t* error;        // [0] = code (0 ok, -2 zero, -3 too big), [1] = offset
 };
 
-__global__ void rdw_walk_kernel(RdwArgs a, int pass) {
-    int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= a.n_seeds) return;
-    int64_t pos = a.seeds[k];
-    const int64_t end = k + 1 < a.n_seeds ? a.seeds[k + 1] : a.n_bytes;
-    int64_t out = pass ? a.counts[k] : 0;
-    int64_t cnt = 0;
-    while (pos < end) {
-        int64_t avail = a.n_bytes - pos;
-        int64_t hl = avail < 4 ? avail : 4;
-        const uint8_t* h = a.data + pos;
-        pos += hl;
-        const int64_t file_offset = pos;
-        int64_t rlen;
-        bool valid;
-        if (a.p.file_header_bytes > 4 && file_offset == 4) {
-            rlen = a.p.file_header_bytes - 4; valid = false;
-        } else if (a.n_bytes > 0 && a.p.file_footer_bytes > 0 && a.n_bytes - file_offset <= a.p.file_footer_bytes) {
-            rlen = a.n_bytes - file_offset; valid = false;
-        } else if (hl < 4) {
-            rlen = -1; valid = false;
-        } else {
-            rlen = a.p.big_endian ? (int64_t)h[1] + 256 * (int64_t)h[0] + a.p.adjustment
-                                  : (int64_t)h[2] + 256 * (int64_t)h[3] + a.p.adjustment;
-            if (rlen <= 0) { atomicCAS((unsigned long long*)a.error, 0ull, (unsigned long long)-2ll); a.error[1] = file_offset; return; }
-            if (rlen > 100ll * 1024 * 1024) { atomicCAS((unsigned long long*)a.error, 0ull, (unsigned long long)-3ll); a.error[1] = file_offset; return; }
-            valid = true;
-        }
-        if (rlen <= 0) break;
-        int64_t rem = a.n_bytes - pos;
-        int64_t got = rlen < rem ? rlen : rem;
-        if (valid) {
-            if (pass && out < a.capacity) { a.rec_off[out] = pos; a.rec_len[out] = (int32_t)got; }
-            out++;
-            cnt++;
-        }
-        pos += got;
+// Header walk step (RecordHeaderParserRDW.getRecordMetadata + VRLRecordReader.fetchRecordUsingRdwHeaders):
+// the header at pos gives the next header position, the payload (off, len) and whether the
+// record is valid (file header / footer records are not).  err: -2 length <= 0, -3 > 100 MiB.
+struct RdwStep {
+    int64_t next, off;
+    int32_t len;
+    bool valid, stop;
+    int32_t err;
+};
+
+__device__ __forceinline__ uint32_t rdw_header(const RdwArgs& a, int64_t pos) {
+    // 4 bytes at any alignment (caller guarantees pos + 4 <= n_bytes)
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) w |= (uint32_t)a.data[pos + j] << (8 * j);
+    return w;
+}
+
+__device__ __forceinline__ int64_t rdw_len(const RdwArgs& a, uint32_t h) {
+    const uint32_t b0 = h & 0xFF, b1 = (h >> 8) & 0xFF, b2 = (h >> 16) & 0xFF, b3 = h >> 24;
+    return (a.p.big_endian ? (int64_t)b1 + 256 * (int64_t)b0 : (int64_t)b2 + 256 * (int64_t)b3) + a.p.adjustment;
+}
+
+__device__ __forceinline__ RdwStep rdw_step(const RdwArgs& a, int64_t pos) {
+    RdwStep s{0, 0, 0, false, false, 0};
+    const int64_t avail = a.n_bytes - pos;
+    const int64_t hl = avail < 4 ? avail : 4;
+    const int64_t fo = pos + hl;   // file offset after the header
+    int64_t rlen;
+    if (a.p.file_header_bytes > 4 && fo == 4) {
+        rlen = a.p.file_header_bytes - 4;
+    } else if (a.n_bytes > 0 && a.p.file_footer_bytes > 0 && a.n_bytes - fo <= a.p.file_footer_bytes) {
+        rlen = a.n_bytes - fo;
+    } else if (hl < 4) {
+        s.stop = true;
+        s.next = a.n_bytes;
+        return s;
+    } else {
+        rlen = rdw_len(a, rdw_header(a, pos));
+        if (rlen <= 0) { s.err = -2; return s; }
+        if (rlen > 100ll * 1024 * 1024) { s.err = -3; return s; }
+        s.valid = true;
     }
-    if (!pass) a.counts[k] = cnt;
+    if (rlen <= 0) { s.stop = true; s.next = a.n_bytes; return s; }
+    const int64_t rem = a.n_bytes - fo;
+    const int64_t got = rlen < rem ? rlen : rem;
+    s.off = fo;
+    s.len = (int32_t)got;
+    s.next = fo + got;
+    return s;
+}
+
+// Chunk-parallel RDW offset discovery.  The byte range of every sparse-
+// index seed is cut into chunks; a chunk holds the records whose header starts in
+// [start, end).  Every chunk walks from a speculated entry (a plausible header chain near its
+// start; the seed itself for a range's first chunk) to its exit (first header position >= end);
+// then rounds of the fix kernel replace each entry with the predecessor's exit and re-walk the
+// chunks that change, until no chunk changes: by induction from the seeds the entries are then
+// exactly the sequential walk's header positions.  A final pass writes (offset, length) of the
+// valid records at each chunk's scanned base.
+struct RdwChunkArgs {
+    const int64_t* start;
+    const int64_t* end;
+    const int64_t* range_end;
+    const uint8_t* known;    // entry known (a seed)
+    int64_t* entry;
+    int64_t* exit_in;
+    int64_t* exit_out;
+    uint32_t* count;         // valid records from the current entry
+    int64_t* err;            // per chunk: (error position << 2 | code) or -1
+    int32_t* changed;
+    int64_t n;
+};
+
+struct RdwWalk {
+    int64_t exit;            // first header position >= end; -2 after an error (dead chain)
+    uint32_t count;
+    int64_t err;
+};
+
+template <bool kEmit>
+__device__ RdwWalk rdw_walk(const RdwArgs& a, int64_t pos, int64_t end, int64_t* rec_off, int32_t* rec_len,
+                            int64_t out, int64_t cap) {
+    RdwWalk w{pos, 0, -1};
+    if (pos < 0) { w.exit = pos; return w; }
+    while (pos < end) {
+        const RdwStep s = rdw_step(a, pos);
+        if (s.err) {
+            w.err = ((pos + 4) << 2) | (s.err == -2 ? 2 : 3);   // reported at the payload offset
+            w.exit = -2;
+            return w;
+        }
+        if (s.stop) { pos = s.next; break; }
+        if (s.valid) {
+            if (kEmit && out < cap) { rec_off[out] = s.off; rec_len[out] = s.len; }
+            out++;
+            w.count++;
+        }
+        pos = s.next;
+    }
+    w.exit = pos;
+    return w;
+}
+
+// A plausible header chain starting at q: kHops headers with lengths in (0, 100 MiB] inside the
+// range (strict: the two bytes that do not carry the length are zero, as RDWs write them).
+__device__ __forceinline__ bool rdw_plausible(const RdwArgs& a, int64_t q, int64_t range_end, bool strict) {
+    constexpr int kHops = 4;
+    int64_t pos = q;
+    for (int k = 0; k < kHops; k++) {
+        if (pos >= range_end || pos + 4 > a.n_bytes) return k > 0;
+        const uint32_t h = rdw_header(a, pos);
+        const int64_t len = rdw_len(a, h);
+        if (len <= 0 || len > 100ll * 1024 * 1024) return false;
+        if (strict && (a.p.big_endian ? (h >> 16) : (h & 0xFFFF)) != 0) return false;
+        pos += 4 + len;
+    }
+    return true;
+}
+
+__global__ void rdw_spec_kernel(RdwArgs a, RdwChunkArgs c) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= c.n) return;
+    const int64_t s = c.start[k], e = c.end[k], re = c.range_end[k];
+    int64_t entry = s;
+    if (!c.known[k]) {
+        bool found = false;
+        for (int strict = 1; strict >= 0 && !found; strict--)
+            for (int64_t q = s; q < e && !found; q++)
+                if (rdw_plausible(a, q, re, strict != 0)) { entry = q; found = true; }
+    }
+    c.entry[k] = entry;
+    const RdwWalk w = rdw_walk<false>(a, entry, e, nullptr, nullptr, 0, 0);
+    c.exit_out[k] = w.exit;
+    c.count[k] = w.count;
+    c.err[k] = w.err;
+}
+
+__global__ void rdw_fix_kernel(RdwArgs a, RdwChunkArgs c) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= c.n) return;
+    if (c.known[k]) { c.exit_out[k] = c.exit_in[k]; return; }
+    const int64_t e = c.exit_in[k - 1];
+    if (e == c.entry[k]) { c.exit_out[k] = c.exit_in[k]; return; }
+    c.entry[k] = e;
+    *c.changed = 1;
+    const RdwWalk w = rdw_walk<false>(a, e, c.end[k], nullptr, nullptr, 0, 0);
+    c.exit_out[k] = w.exit;
+    c.count[k] = w.count;
+    c.err[k] = w.err;
+}
+
+__global__ void rdw_emit_kernel(RdwArgs a, RdwChunkArgs c, const int64_t* base, int64_t* rec_off, int32_t* rec_len,
+                                int64_t cap, unsigned long long* first_err) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= c.n) return;
+    if (c.err[k] >= 0) atomicMin(first_err, (unsigned long long)c.err[k]);
+    rdw_walk<true>(a, c.entry[k], c.end[k], rec_off, rec_len, base[k], cap);
 }
 
 }  // namespace cbx

@@ -118,3 +118,54 @@ def syn200(n: int, seed: int = 20261015, device="cpu", malformed_rate: float = 0
     rec = torch.cat(parts, dim=1)
     assert rec.shape[1] == SYN200_RECORD_SIZE, rec.shape
     return rec.contiguous()
+
+
+# --------------------------------------------------------------------------------------------
+# RDW narrow multisegment file (config C4, exp2_multiseg_narrow / test5 layout): segment 'C'
+# (STATIC-DETAILS, 64-byte payload) or 'P' (CONTACTS, 60-byte payload) behind a 4-byte RDW, so
+# records are 68 / 64 bytes on disk (~65 B per record).
+# --------------------------------------------------------------------------------------------
+RDW_NARROW_COPYBOOK = """
+        01  COMPANY-DETAILS.
+            05  SEGMENT-ID        PIC X(5).
+            05  COMPANY-ID        PIC X(10).
+            05  STATIC-DETAILS.
+               10  COMPANY-NAME      PIC X(15).
+               10  ADDRESS           PIC X(25).
+               10  TAXPAYER.
+                  15  TAXPAYER-TYPE  PIC X(1).
+                  15  TAXPAYER-STR   PIC X(8).
+                  15  TAXPAYER-NUM  REDEFINES TAXPAYER-STR
+                                     PIC 9(8) COMP.
+            05  CONTACTS REDEFINES STATIC-DETAILS.
+               10  PHONE-NUMBER      PIC X(17).
+               10  CONTACT-PERSON    PIC X(28).
+"""
+RDW_NARROW_SEGMENTS = {"C": "STATIC-DETAILS", "P": "CONTACTS"}
+
+
+def rdw_narrow(n: int, seed: int = 20261016, device="cpu", big_endian: bool = False):
+    """n records of the C4 layout with RDW headers -> (bytes [total] uint8, header offsets [n] int64)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    is_c = torch.rand((n,), generator=g, device=device) < 0.35
+    plen = torch.where(is_c, 64, 60).to(torch.int64)
+    hdr = torch.cumsum(plen + 4, 0) - (plen + 4)                     # header offsets
+    total = int((plen + 4).sum().item()) if n else 0
+    alnum = torch.tensor(_CP037_ALNUM, dtype=torch.uint8, device=device)
+    out = alnum[torch.randint(0, len(_CP037_ALNUM), (max(total, 1),), generator=g, device=device)][:total].clone()
+    if n == 0:
+        return out, hdr
+    # RDW: length in bytes 2-3 little-endian (bytes 0-1 zero), or bytes 0-1 big-endian
+    lo, hi = (plen & 0xFF).to(torch.uint8), (plen >> 8).to(torch.uint8)
+    z = torch.zeros_like(lo)
+    for j, col in enumerate((hi, lo, z, z) if big_endian else (z, z, lo, hi)):
+        out[hdr + j] = col
+    # SEGMENT-ID 'C    ' / 'P    ' (cp037 C = 0xC3, P = 0xD7, space 0x40)
+    out[hdr + 4] = torch.where(is_c, 0xC3, 0xD7).to(torch.uint8)
+    for j in range(1, 5):
+        out[hdr + 4 + j] = 0x40
+    # COMPANY-ID: digits
+    for j in range(10):
+        out[hdr + 9 + j] = (0xF0 + torch.randint(0, 10, (n,), generator=g, device=device)).to(torch.uint8)
+    return out, hdr

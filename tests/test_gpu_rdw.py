@@ -1,0 +1,127 @@
+"""GPU RDW offset discovery (cbx_frame_rdw, chunk-parallel speculate / verify / repair) against the
+oracle's sequential walk (RecordHeaderParserRDW.scala:44-85, VRLRecordReader.scala:151-186).
+
+Small CBX_RDW_CHUNK_BYTES values force thousands of chunks per file, so most chunks start inside
+a record and their speculated entries must be checked and repaired.
+"""
+from __future__ import annotations
+
+import re
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from cobrix_amd.native import CbxError  # noqa: E402
+from cobrix_amd.reader import ReaderParameters, VarLenNestedReader  # noqa: E402
+from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _frame(raw: bytes, seeds=None, **kw):
+    rd = VarLenNestedReader(RDW_NARROW_COPYBOOK, ReaderParameters(is_record_sequence=True, **kw))
+    t = torch.frombuffer(bytearray(raw) if raw else bytearray(16), dtype=torch.uint8).cuda()
+    off, ln = rd.frame(t, len(raw), seeds=seeds)
+    return off.cpu().numpy(), ln.cpu().numpy()
+
+
+def _oracle(raw: bytes, **kw):
+    return O.frame_rdw(raw, **kw)
+
+
+def _adversarial(n: int, seed: int, big_endian=False, adjust=0, max_len=3000) -> bytes:
+    """Records of 1..max_len bytes whose payloads are full of zeros and fake plausible headers."""
+    rng = np.random.default_rng(seed)
+    out = bytearray()
+    for _ in range(n):
+        ln = int(rng.integers(1, max_len)) if rng.random() < 0.3 else int(rng.integers(1, 80))
+        hl = ln - adjust
+        h = bytes([hl >> 8, hl & 0xFF, 0, 0]) if big_endian else bytes([0, 0, hl & 0xFF, hl >> 8])
+        body = bytearray(rng.integers(0, 256, ln, dtype=np.uint8).tobytes())
+        for _ in range(ln // 16):   # fake headers inside the payload
+            p = int(rng.integers(0, max(1, ln - 4)))
+            fl = int(rng.integers(1, 200))
+            body[p:p + 4] = bytes([fl >> 8, fl & 0xFF, 0, 0]) if big_endian else bytes([0, 0, fl & 0xFF, fl >> 8])
+        if rng.random() < 0.2:
+            body[:] = bytes(len(body))
+        out += h + bytes(body[:ln])
+    return bytes(out)
+
+
+@pytest.mark.parametrize("chunk", [8, 37, 256, 4096, None])
+@pytest.mark.parametrize("big_endian", [False, True])
+def test_c4_layout_vs_oracle(monkeypatch, chunk, big_endian):
+    if chunk:
+        monkeypatch.setenv("CBX_RDW_CHUNK_BYTES", str(chunk))
+    d, _ = rdw_narrow(20_000, seed=3, big_endian=big_endian)
+    raw = d.numpy().tobytes()
+    eo, el = _oracle(raw, big_endian=big_endian)
+    off, ln = _frame(raw, is_rdw_big_endian=big_endian)
+    assert np.array_equal(off, eo) and np.array_equal(ln, el)
+    seeds = [e[0] for e in O.sparse_index(raw, big_endian=big_endian, records_per_entry=997)]
+    off2, ln2 = _frame(raw, seeds=seeds, is_rdw_big_endian=big_endian)
+    assert np.array_equal(off2, eo) and np.array_equal(ln2, el)
+
+
+@pytest.mark.parametrize("chunk", [8, 64, 1000])
+@pytest.mark.parametrize("case", [dict(), dict(big_endian=True), dict(adjust=-4), dict(header=10, footer=7)])
+def test_adversarial_payloads(monkeypatch, chunk, case):
+    monkeypatch.setenv("CBX_RDW_CHUNK_BYTES", str(chunk))
+    be, adj = case.get("big_endian", False), case.get("adjust", 0)
+    body = _adversarial(800, seed=chunk + 7 * len(case), big_endian=be, adjust=adj)
+    hb, fb = case.get("header", 0), case.get("footer", 0)
+    raw = (bytes([0, 0, 0, 0]) + b"\x11" * (hb - 4) if hb else b"") + body + b"\x22" * fb
+    eo, el = _oracle(raw, big_endian=be, adjustment=adj, file_header_bytes=hb, file_footer_bytes=fb)
+    kw = dict(is_rdw_big_endian=be, rdw_adjustment=adj, file_start_offset=hb, file_end_offset=fb)
+    off, ln = _frame(raw, **kw)
+    assert len(off) == len(eo)
+    assert np.array_equal(off, eo) and np.array_equal(ln, el)
+
+
+def test_record_spanning_many_chunks(monkeypatch):
+    monkeypatch.setenv("CBX_RDW_CHUNK_BYTES", "512")
+    rng = np.random.default_rng(2)
+    raw = bytearray()
+    for ln in (10, 60000, 3, 64000, 5, 17):
+        raw += bytes([0, 0, ln & 0xFF, ln >> 8]) + bytes(rng.integers(0, 256, ln, dtype=np.uint8).tobytes())
+    raw = bytes(raw)
+    eo, el = _oracle(raw)
+    off, ln = _frame(raw)
+    assert np.array_equal(off, eo) and np.array_equal(ln, el)
+
+
+def test_truncated_last_record_and_tiny_inputs():
+    d, _ = rdw_narrow(50, seed=5)
+    raw = d.numpy().tobytes()
+    for cut in (len(raw) - 1, len(raw) - 30, len(raw) - 66, 3, 2, 0):
+        part = raw[:cut]
+        eo, el = _oracle(part)
+        off, ln = _frame(part)
+        assert np.array_equal(off, eo) and np.array_equal(ln, el), cut
+
+
+@pytest.mark.parametrize("chunk", [16, None])
+def test_zero_length_header_is_an_error_at_the_first_occurrence(monkeypatch, chunk):
+    if chunk:
+        monkeypatch.setenv("CBX_RDW_CHUNK_BYTES", str(chunk))
+    d, hdr = rdw_narrow(400, seed=9)
+    raw = bytearray(d.numpy().tobytes())
+    for k in (123, 300):   # two zero-length headers: the first one is reported
+        h = int(hdr[k])
+        raw[h:h + 4] = bytes(4)
+    raw = bytes(raw)
+    with pytest.raises(RuntimeError) as oe:
+        _oracle(raw)
+    with pytest.raises(CbxError) as ge:
+        _frame(raw)
+    want = int(re.search(r"offset (\d+)", str(oe.value)).group(1))
+    assert f"at {want}." in str(ge.value), (str(ge.value), want)
