@@ -34,3 +34,29 @@ def utf8_lut(table: List[int]) -> np.ndarray:
             v |= 1 << 31
         out[b] = v
     return out
+
+
+def ascii_charset_table(name: str) -> List[int]:
+    """AsciiStringDecoderWrapper (CP/parser/decoders/AsciiStringDecoderWrapper.scala:43-67) as a
+    code-page table: bytes 0x00-0x1F become ' ', every other byte is decoded by the single-byte
+    charset `name` (Charset.forName aliases as Python's codec registry knows them; an unmappable
+    byte decodes to U+FFFD, as Java's decoder replaces it).  Multi-byte charsets cannot be a
+    per-byte table and raise ValueError."""
+    import codecs
+    info = codecs.lookup(name)
+    if info.name.startswith(("utf", "ascii")) or "jis" in info.name or info.name in (
+            "cp932", "cp936", "cp949", "cp950", "gb2312", "gbk", "gb18030", "big5", "big5hkscs", "euc_jp",
+            "euc_kr", "johab", "hz", "iso2022_jp", "iso2022_kr"):
+        raise ValueError(f"ascii_charset {name!r} is not a single-byte charset")
+    whole = bytes(range(256)).decode(info.name, errors="replace")
+    if len(whole) != 256:
+        raise ValueError(f"ascii_charset {name!r} is not a single-byte charset")
+    return [0x20 if b < 32 else ord(whole[b]) for b in range(256)]
+
+
+def is_us_ascii(name: str) -> bool:
+    """DecoderSelector.scala:79 -- an empty name or US-ASCII keeps decodeAsciiString."""
+    if not name:
+        return True
+    import codecs
+    return codecs.lookup(name).name == "ascii"

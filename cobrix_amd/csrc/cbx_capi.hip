@@ -331,7 +331,12 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
         Field d = make_field(f);
         if (f.column < 0 || f.column >= P->n_columns) { delete P; return fail(CBX_E_ARGUMENT, fi + ": bad column"); }
         if (!is_generated(d) && (f.size <= 0 || f.offset < 0)) { delete P; return fail(CBX_E_ARGUMENT, fi + ": bad offset/size"); }
+        if (!(f.kind >= CBX_K_STRING && f.kind <= CBX_K_UTF16_LE)) { delete P; return fail(CBX_E_ARGUMENT, fi + ": unknown kind"); }
         if (f.kind == CBX_K_BINARY && f.size > 16) { delete P; return fail(CBX_E_UNSUPPORTED, fi + ": binary wider than 16 bytes"); }
+        if (f.kind == CBX_K_ASCII_NUM && (f.size > kAsciiNumMax || f.scale < 0 || f.scale > 100 || f.scale_factor < -100 ||
+                                          f.scale_factor > 100)) {
+            delete P; return fail(CBX_E_UNSUPPORTED, fi + ": ASCII DISPLAY number wider than 64 bytes");
+        }
         if ((f.out_type == CBX_O_DEC64 || f.out_type == CBX_O_DEC128) && (f.out_precision < 1 || f.out_precision > 38)) {
             delete P; return fail(CBX_E_UNSUPPORTED, fi + ": decimal precision outside 1..38");
         }

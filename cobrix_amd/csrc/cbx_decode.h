@@ -209,10 +209,13 @@ inline Field make_field(const cbx_field& f) {
             d.plus_null = !integral && f.scale_factor == 0 && f.size < f.scale;
         }
         break;
+    case CBX_K_ASCII_NUM: d.variant = V_GENERIC; break;   // byte-loop decoder (fixup kernel)
     case CBX_K_FLOAT: case CBX_K_DOUBLE: d.variant = V_FP; break;
     case CBX_K_STRING: case CBX_K_STRING_ASCII: case CBX_K_HEX: case CBX_K_RAW:
+    case CBX_K_UTF16_BE: case CBX_K_UTF16_LE:
         d.variant = V_STRING;
-        d.max_utf8 = f.kind == CBX_K_HEX ? 2 : 1;
+        // UTF-16: a 2-byte unit -> <= 3 UTF-8 bytes, a 4-byte pair -> 4, a lone tail byte -> U+FFFD (3)
+        d.max_utf8 = f.kind == CBX_K_HEX ? 2 : (f.kind == CBX_K_UTF16_BE || f.kind == CBX_K_UTF16_LE) ? 3 : 1;
         break;
     case CBX_K_RECORD_ID: d.variant = V_RECORD_ID; break;
     case CBX_K_FILE_ID: d.variant = V_FILE_ID; break;
@@ -416,6 +419,155 @@ CBX_HD Val decode_zoned(const Field& f, const uint8_t* p) {
 }
 
 // ------------------------------------------------------------------------------------------
+// ASCII DISPLAY numbers (StringDecoders.decodeAsciiNumber, StringDecoders.scala:221-243, and the
+// decodeAsciiInt / Long / BigNumber / BigDecimal wrappers, :259-361).  decodeAsciiNumber keeps
+// the LAST '+'/'-' byte as the sign (wherever it is), maps '.' and ',' to '.', appends every
+// other byte as a Java char (a signed byte >= 0x80 becomes U+FF80..U+FFFF: no digit, no space)
+// and returns sign + buf.trim.  Integer/Long parsing is streamed; the BigDecimal wrappers build
+// the Java string (<= kAsciiNumMax bytes, a plan limit) and parse it.
+// ------------------------------------------------------------------------------------------
+constexpr int kAsciiNumMax = 64;
+
+// Integer.parseInt / Long.parseLong of decodeAsciiNumber(bytes): after the sign bytes are taken
+// out, the trimmed rest must be one non-empty run of '0'..'9'.
+CBX_HD Val ascii_integral(const Field& f, const uint8_t* p) {
+    const int n = f.size;
+    int sign = 0, phase = 0, nd = 0;   // phase 0 leading spaces, 1 digits, 2 trailing spaces
+    bool bad = false, big = false;
+    uint64_t v = 0;
+    for (int i = 0; i < n; i++) {
+        const uint32_t c = p[i];
+        if (c == '+' || c == '-') { sign = c == '-' ? 2 : 1; continue; }
+        if (c <= 0x20) { phase = phase == 1 ? 2 : phase; continue; }
+        if (phase == 2 || c < '0' || c > '9') { bad = true; continue; }
+        phase = 1;
+        nd++;
+        big |= v > 1844674407370955160ull;
+        v = v * 10 + (c - '0');
+    }
+    const bool neg = sign == 2;
+    if (bad || nd == 0 || big || (neg && !(f.flags & CBX_F_SIGNED))) return null_val();
+    const uint64_t lim = f.precision <= 9 ? (neg ? 0x80000000ull : 0x7FFFFFFFull)
+                                          : (neg ? 0x8000000000000000ull : 0x7FFFFFFFFFFFFFFFull);
+    if (v > lim) return null_val();
+    v = neg ? (uint64_t)0 - v : v;
+    return Val{v, (uint64_t)((int64_t)v >> 63), true};
+}
+
+// Spark Decimal.toPrecision of the exact BigDecimal  (M * 10^-vs), M holding the leading <= 38
+// significant digits and `first_cut` the first digit cut off after them (-1: none cut, vs
+// already counts the cut digits out).  HALF_UP needs only the first dropped digit.
+CBX_HD Val finalize_decimal_wide(U128 M, int64_t vs, int first_cut, bool neg, const Field& f) {
+    const int S = f.out_s;
+    if (u128_is_zero(M) && first_cut <= 0) return Val{0, 0, true};
+    if (vs == S) {
+        if (first_cut >= 5) u128_muladd(M, 1, 1);
+        if (!u128_lt(M, U128{f.lim_lo, f.lim_hi})) return null_val();
+        const U128 v = neg ? u128_neg(M) : M;
+        return Val{v.lo, v.hi, true};
+    }
+    if (vs < S && S - vs > 38) return null_val();      // a non-zero M times >= 10^39
+    if (vs > S && vs - S > 40) return Val{0, 0, true};   // every digit dropped, the first a 0
+    return finalize_decimal(M, false, (int)vs, neg, f);
+}
+
+// java.math.BigDecimal(String) (significand [+-]?digits[.digits] | .digits, exponent [eE][+-]?digits)
+// then the Spark conversion.
+CBX_HD Val parse_java_bigdecimal(const Field& f, const uint8_t* s, int n) {
+    int i = 0;
+    bool neg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+    int nd = 0, sig = 0, cut = 0, first_cut = -1;
+    bool dot = false;
+    int64_t scale = 0;
+    U128 M = u128(0);
+    for (; i < n; i++) {
+        const uint32_t c = s[i];
+        if (c >= '0' && c <= '9') {
+            nd++;
+            scale += dot;
+            if (sig > 0 || c != '0') {
+                if (sig < 38) { u128_muladd(M, 10, c - '0'); sig++; }
+                else { if (cut == 0) first_cut = (int)(c - '0'); cut++; }
+            }
+        } else if (c == '.' && !dot) {
+            dot = true;
+        } else if (c == 'e' || c == 'E') {
+            i++;
+            bool eneg = false;
+            if (i < n && (s[i] == '+' || s[i] == '-')) { eneg = s[i] == '-'; i++; }
+            if (i >= n) return null_val();
+            int64_t ex = 0;
+            int ed = 0;
+            for (; i < n; i++) {
+                if (s[i] < '0' || s[i] > '9') return null_val();
+                ex = ex * 10 + (s[i] - '0');
+                ed += ex > 0;
+                if (ed > 10) return null_val();
+            }
+            scale -= eneg ? -ex : ex;
+            if (scale > 2147483647ll || scale < -2147483648ll) return null_val();
+            break;
+        } else {
+            return null_val();
+        }
+    }
+    if (nd == 0) return null_val();
+    return finalize_decimal_wide(M, scale - cut, first_cut, neg, f);
+}
+
+CBX_HD Val decode_ascii_num(const Field& f, const uint8_t* p) {
+    if ((f.flags & CBX_F_INTEGRAL) && f.precision <= 18) return ascii_integral(f, p);
+    const int n = f.size < kAsciiNumMax ? f.size : kAsciiNumMax;
+    // decodeAsciiNumber -> s = [sign] + buf.trim
+    uint8_t buf[kAsciiNumMax];
+    int bl = 0, sign = 0;
+    for (int i = 0; i < n; i++) {
+        const uint32_t c = p[i];
+        if (c == '+' || c == '-') sign = c == '-' ? 2 : 1;
+        else buf[bl++] = (uint8_t)(c == ',' ? '.' : c >= 0x80 ? 0xFF : c);   // 0xFF: a U+FFxx char
+    }
+    if (sign == 2 && !(f.flags & CBX_F_SIGNED)) return null_val();
+    int b = 0, e = bl;
+    while (b < e && buf[b] <= 0x20) b++;
+    while (e > b && buf[e - 1] <= 0x20) e--;
+    uint8_t s[2 * kAsciiNumMax + 48];
+    int sl = 0;
+    if (sign) s[sl++] = sign == 2 ? '-' : '+';
+    for (int i = b; i < e; i++) s[sl++] = buf[i];
+    if ((f.flags & CBX_F_INTEGRAL) || (f.flags & CBX_F_EXPLICIT_DOT) || (f.scale == 0 && f.sf == 0))
+        return parse_java_bigdecimal(f, s, sl);   // BigDecimal(s) == BigDecimal(addDecimalPoint(s, 0, 0))
+    // BinaryUtils.addDecimalPoint(s, scale, scaleFactor) (BinaryUtils.scala:194-238)
+    uint8_t t[2 * kAsciiNumMax + 48];
+    int tl = 0;
+    const bool is_neg = sl > 0 && s[0] == '-';
+    if (f.sf == 0) {
+        const int sc = f.scale;
+        if (is_neg ? sl - 1 > sc : sl > sc) {
+            for (int i = 0; i < sl - sc; i++) t[tl++] = s[i];
+            t[tl++] = '.';
+            for (int i = sl - sc; i < sl; i++) t[tl++] = s[i];
+        } else {
+            if (is_neg) t[tl++] = '-';
+            t[tl++] = '0';
+            t[tl++] = '.';
+            for (int z = 0; z < sc - sl + (is_neg ? 1 : 0); z++) t[tl++] = '0';
+            for (int i = is_neg ? 1 : 0; i < sl; i++) t[tl++] = s[i];
+        }
+    } else if (f.sf < 0) {
+        if (is_neg) t[tl++] = '-';
+        t[tl++] = '0';
+        t[tl++] = '.';
+        for (int z = 0; z < -f.sf; z++) t[tl++] = '0';
+        for (int i = (sl > 0 && (s[0] == '-' || s[0] == '+')) ? 1 : 0; i < sl; i++) t[tl++] = s[i];
+    } else {
+        for (int i = 0; i < sl; i++) t[tl++] = s[i];
+        for (int z = 0; z < f.sf; z++) t[tl++] = '0';
+    }
+    return parse_java_bigdecimal(f, t, tl);
+}
+
+// ------------------------------------------------------------------------------------------
 // COMP-1 / COMP-2
 // ------------------------------------------------------------------------------------------
 // decodeIbmSingleBigEndian, restated bit for bit (the exponent mask is the sign bit)
@@ -485,6 +637,7 @@ CBX_HD Val decode_numeric(const Field& f, const uint8_t* p) {
     case CBX_K_BCD: return decode_bcd(f, p);
     case CBX_K_BINARY: return decode_binary(f, p);
     case CBX_K_ZONED: return decode_zoned(f, p);
+    case CBX_K_ASCII_NUM: return decode_ascii_num(f, p);
     case CBX_K_FLOAT: return decode_float(f, p);
     case CBX_K_DOUBLE: return decode_double(f, p);
     default: return null_val();
@@ -804,6 +957,7 @@ CBX_HD Val decode_count_int(const Field& f, const uint8_t* p) {
         }
         return Val{v, (uint64_t)((int64_t)v >> 63), true};
     }
+    if (f.kind == CBX_K_ASCII_NUM) return ascii_integral(f, p);
     if (f.kind == CBX_K_ZONED) {
         int sign = 0, nd = 0, ndots = 0;
         bool malformed = false, big = false;
@@ -850,11 +1004,61 @@ CBX_HD uint32_t ascii_lut(uint32_t b) {
     return c | (1u << 24) | (c <= 0x20 ? 0x80000000u : 0u);
 }
 
+// UTF-16 (StringDecoders.decodeUtf16String, StringDecoders.scala:98-114): `new String(bytes,
+// UTF_16BE|LE)` decodes with the JDK UnicodeDecoder under REPLACE -- U+FFFE and an unpaired low
+// surrogate are malformed(2), a high surrogate followed by a non-low unit is malformed(4) (both
+// units), a high surrogate or a lone byte at the end is malformed(rest); each malformed run is
+// one U+FFFD.  One token at byte `pos` of p[0, n): returns its byte length, code point in cp.
+CBX_HD int utf16_token(const uint8_t* p, int pos, int n, bool be, uint32_t& cp) {
+    const int r = n - pos;
+    cp = 0xFFFDu;
+    if (r < 2) return r;
+    const uint32_t u = be ? (uint32_t)p[pos] << 8 | p[pos + 1] : (uint32_t)p[pos + 1] << 8 | p[pos];
+    if (u >= 0xD800u && u <= 0xDBFFu) {
+        if (r < 4) return r;
+        const uint32_t u2 = be ? (uint32_t)p[pos + 2] << 8 | p[pos + 3] : (uint32_t)p[pos + 3] << 8 | p[pos + 2];
+        if (u2 >= 0xDC00u && u2 <= 0xDFFFu) cp = 0x10000u + ((u - 0xD800u) << 10) + (u2 - 0xDC00u);
+        return 4;
+    }
+    if (!(u == 0xFFFEu || (u >= 0xDC00u && u <= 0xDFFFu))) cp = u;
+    return 2;
+}
+CBX_HD int utf8_width(uint32_t cp) { return cp < 0x80u ? 1 : cp < 0x800u ? 2 : cp < 0x10000u ? 3 : 4; }
+
+// Trimmed span (token boundaries) + UTF-8 length of a UTF-16 field; trimming drops chars <= U+0020.
+CBX_HD StrSpan utf16_span(int kind, int trim, const uint8_t* p, int n) {
+    const bool be = kind == CBX_K_UTF16_BE;
+    int pos = 0, first = -1, last_end = 0, run = 0, u8_first = 0, u8_last = 0;
+    while (pos < n) {
+        uint32_t cp;
+        const int len = utf16_token(p, pos, n, be, cp);
+        const int w = utf8_width(cp);
+        if (cp > 0x20u) {
+            if (first < 0) { first = pos; u8_first = run; }
+            last_end = pos + len;
+            u8_last = run + w;
+        }
+        run += w;
+        pos += len;
+    }
+    const bool tl = trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH;
+    const bool tr = trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH;
+    StrSpan s;
+    int u0 = 0, u1 = run;
+    s.begin = 0;
+    s.end = n;
+    if (tl) { s.begin = first < 0 ? n : first; u0 = first < 0 ? run : u8_first; }
+    if (tr) { s.end = first < 0 ? s.begin : last_end; u1 = first < 0 ? u0 : u8_last; }
+    s.utf8_len = u1 - u0;
+    return s;
+}
+
 template <typename LutFn>
 CBX_HD StrSpan string_span(int kind, int trim, const uint8_t* p, int n, LutFn lut) {
     StrSpan s{0, n, 0};
     if (kind == CBX_K_HEX) { s.utf8_len = 2 * n; return s; }
     if (kind == CBX_K_RAW) { s.utf8_len = n; return s; }
+    if (kind == CBX_K_UTF16_BE || kind == CBX_K_UTF16_LE) return utf16_span(kind, trim, p, n);
     const bool tl = trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH;
     const bool tr = trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH;
     int b = 0, e = n;
@@ -878,6 +1082,27 @@ CBX_HD void string_write(int kind, const uint8_t* p, const StrSpan& s, uint8_t* 
     }
     if (kind == CBX_K_RAW) {
         for (int i = s.begin; i < s.end; i++) out[i - s.begin] = p[i];
+        return;
+    }
+    if (kind == CBX_K_UTF16_BE || kind == CBX_K_UTF16_LE) {
+        // s.begin / s.end are token boundaries of the tokenisation over the whole field, so
+        // re-tokenising [begin, end) yields the same tokens
+        int k = 0;
+        for (int pos = s.begin; pos < s.end;) {
+            uint32_t cp;
+            pos += utf16_token(p, pos, s.end, kind == CBX_K_UTF16_BE, cp);
+            if (cp < 0x80u) {
+                out[k++] = (uint8_t)cp;
+            } else if (cp < 0x800u) {
+                out[k++] = (uint8_t)(0xC0u | cp >> 6); out[k++] = (uint8_t)(0x80u | (cp & 63u));
+            } else if (cp < 0x10000u) {
+                out[k++] = (uint8_t)(0xE0u | cp >> 12); out[k++] = (uint8_t)(0x80u | ((cp >> 6) & 63u));
+                out[k++] = (uint8_t)(0x80u | (cp & 63u));
+            } else {
+                out[k++] = (uint8_t)(0xF0u | cp >> 18); out[k++] = (uint8_t)(0x80u | ((cp >> 12) & 63u));
+                out[k++] = (uint8_t)(0x80u | ((cp >> 6) & 63u)); out[k++] = (uint8_t)(0x80u | (cp & 63u));
+            }
+        }
         return;
     }
     int k = 0;

@@ -20,6 +20,7 @@ CBX_MAX_SEG_KEY_LEN = 32
 
 # kinds / out types / flags (keep in sync with include/cobrix_hip.h)
 K_STRING, K_STRING_ASCII, K_HEX, K_RAW, K_BCD, K_BINARY, K_ZONED = 1, 2, 3, 4, 5, 6, 7
+K_ASCII_NUM, K_UTF16_BE, K_UTF16_LE = 8, 13, 14
 K_FLOAT, K_DOUBLE, K_RECORD_ID, K_FILE_ID = 9, 10, 11, 12
 O_I32, O_I64, O_DEC64, O_DEC128, O_F32, O_F64, O_STRING, O_BINARY = 1, 2, 3, 4, 5, 6, 7, 8
 F_SIGNED, F_BIG_ENDIAN, F_EXPLICIT_DOT, F_INTEGRAL, F_IBM, F_LITTLE_ENDIAN_FP, F_DEPENDEE = (
@@ -35,7 +36,7 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_string_bound", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
                     "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
                     "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class NativeLibraryError(RuntimeError):

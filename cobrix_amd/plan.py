@@ -17,7 +17,7 @@ from typing import Dict, List, Optional, Tuple
 
 from . import copybook as cbk
 from . import native as N
-from .codepages import lut_for, utf8_lut
+from .codepages import ascii_charset_table, is_us_ascii, lut_for, utf8_lut
 from .schema import (ST_BINARY, ST_DECIMAL, ST_DOUBLE, ST_FLOAT, ST_INT, ST_LONG, ST_STRING,
                      spark_type)
 
@@ -75,12 +75,20 @@ def _out_type(st) -> int:
     raise UnsupportedLayout(f"unknown spark type {t}")
 
 
+def _charset_strings(cb: cbk.Copybook) -> bool:
+    """ASCII strings decode through AsciiStringDecoderWrapper (a charset other than US-ASCII,
+    DecoderSelector.scala:78-84): the plan's byte table becomes that charset's."""
+    return not is_us_ascii(cb.ascii_charset)
+
+
 def _kind_and_flags(p: cbk.Primitive, cb: cbk.Copybook) -> Tuple[int, int]:
     d = p.dtype
     flags = 0
     if isinstance(d, cbk.AlphaNumeric):
-        kind = {cbk.EBCDIC: N.K_STRING, cbk.ASCII: N.K_STRING_ASCII, cbk.HEX: N.K_HEX,
-                cbk.RAW: N.K_RAW}.get(d.enc)
+        if d.enc == cbk.ASCII and _charset_strings(cb):
+            return N.K_STRING, 0   # an ASCII copybook has no EBCDIC strings to share the table with
+        kind = {cbk.EBCDIC: N.K_STRING, cbk.ASCII: N.K_STRING_ASCII, cbk.HEX: N.K_HEX, cbk.RAW: N.K_RAW,
+                cbk.UTF16: N.K_UTF16_BE if cb.is_utf16_big_endian else N.K_UTF16_LE}.get(d.enc)
         if kind is None:
             raise UnsupportedLayout(f"{p.name}: {d.enc} strings are not on the GPU path yet")
         return kind, 0
@@ -94,7 +102,9 @@ def _kind_and_flags(p: cbk.Primitive, cb: cbk.Copybook) -> Tuple[int, int]:
         flags |= N.F_DEPENDEE
     if d.compact is None:
         if d.enc != cbk.EBCDIC:
-            raise UnsupportedLayout(f"{p.name}: ASCII DISPLAY numbers are not on the GPU path yet")
+            if p.data_size > 64:
+                raise UnsupportedLayout(f"{p.name}: ASCII DISPLAY numbers wider than 64 bytes are not on the GPU path")
+            return N.K_ASCII_NUM, flags
         return N.K_ZONED, flags
     if d.compact == cbk.COMP3:
         return N.K_BCD, flags
@@ -245,7 +255,7 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
     opts.window_bytes = window_bytes
     opts.segment_column = seg_col
     opts.jit_min_records = jit_min_records
-    lut = utf8_lut(lut_for(cb.code_page))
+    lut = utf8_lut(ascii_charset_table(cb.ascii_charset) if _charset_strings(cb) else lut_for(cb.code_page))
     for i in range(256):
         opts.lut[i] = int(lut[i])
     return DecodePlan(cb, fields, arrays, columns, opts, field_of_node, array_of_node, seg_groups,

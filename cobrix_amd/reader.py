@@ -39,6 +39,8 @@ class ReaderParameters:
     is_ebcdic: bool = True
     ebcdic_code_page: str = "common"
     floating_point_format: str = "IBM"
+    is_utf16_big_endian: bool = True
+    ascii_charset: str = ""
     variable_size_occurs: bool = False
     record_length: Optional[int] = None
     is_record_sequence: bool = False
@@ -250,6 +252,7 @@ class _BaseReader:
             drop_group_fillers=params.drop_group_fillers, drop_value_fillers=params.drop_value_fillers,
             segment_redefines=segment_redefines, string_trimming=params.string_trimming_policy,
             code_page=params.ebcdic_code_page, floating_point_format=params.floating_point_format,
+            is_utf16_big_endian=params.is_utf16_big_endian, ascii_charset=params.ascii_charset,
             non_terminals=params.non_terminals, occurs_handlers=params.occurs_mappings)
         if params.variable_size_occurs:
             raise N.CbxError(N.CBX_E_UNSUPPORTED, "variable_size_occurs=true is not on the GPU path yet")

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 3
+#define CBX_ABI_VERSION 4
 
 /* status codes */
 #define CBX_OK 0
@@ -62,10 +62,13 @@ enum cbx_kind {
     CBX_K_BCD = 5,         /* COMP-3                                  BCDNumberDecoders                 */
     CBX_K_BINARY = 6,      /* COMP / COMP-4 / COMP-5 / COMP-9         BinaryNumberDecoders, BinaryUtils */
     CBX_K_ZONED = 7,       /* EBCDIC DISPLAY numeric                  StringDecoders.decodeEbcdicNumber */
+    CBX_K_ASCII_NUM = 8,   /* ASCII DISPLAY numeric                   StringDecoders.decodeAsciiNumber  */
     CBX_K_FLOAT = 9,       /* COMP-1                                  FloatingPointDecoders             */
     CBX_K_DOUBLE = 10,     /* COMP-2                                  FloatingPointDecoders             */
     CBX_K_RECORD_ID = 11,  /* generated Record_Id (long)              RecordExtractors.scala:409-451    */
-    CBX_K_FILE_ID = 12     /* generated File_Id (int)                                                   */
+    CBX_K_FILE_ID = 12,    /* generated File_Id (int)                                                   */
+    CBX_K_UTF16_BE = 13,   /* PIC N, is_utf16_big_endian=true         StringDecoders.decodeUtf16String  */
+    CBX_K_UTF16_LE = 14    /* PIC N, is_utf16_big_endian=false                                          */
 };
 
 /* output (Spark) types -- SC/schema/CobolSchema.scala:144-173 */

@@ -53,6 +53,25 @@ static int parse_bigdecimal(const char* s, jvalue* v) {
         } else if (c == '.') {
             if (dot >= 0) return 0;
             dot = i;
+        } else if (c == 'e' || c == 'E') {
+            /* java.math.BigDecimal(String) exponent: [eE][+-]?digits, scale -= exponent; an
+             * exponent past 10 digits (or a scale outside int) -> NumberFormatException */
+            i++;
+            int eneg = 0;
+            if (i < n && (s[i] == '+' || s[i] == '-')) { eneg = s[i] == '-'; i++; }
+            if (i >= n) return 0;
+            long long ex = 0;
+            int ed = 0;
+            for (; i < n; i++) {
+                if (s[i] < '0' || s[i] > '9') return 0;
+                ex = ex * 10 + (s[i] - '0');
+                if (ex > 0 || s[i] != '0') ed++;
+                if (ed > 10) return 0;
+            }
+            long long sc = (long long)scale - (eneg ? -ex : ex);
+            if (sc > 2147483647LL || sc < -2147483648LL) return 0;
+            scale = (int)sc;
+            break;
         } else {
             return 0;
         }
@@ -117,6 +136,51 @@ static void decode_ascii_string(const uint8_t* b, int n, int trimming, jvalue* v
         int8_t sb = (int8_t)b[i];
         v->str[v->slen++] = sb < 32 ? 0x20 : (uint16_t)sb;
     }
+    apply_trim(v->str, &v->slen, trimming);
+}
+
+/* StringDecoders.decodeUtf16String (StringDecoders.scala:98-114): `new String(bytes, UTF_16BE/LE)`
+ * with the JDK 8 sun.nio.cs.UnicodeDecoder.decodeLoop under CodingErrorAction.REPLACE (what
+ * String(byte[], Charset) uses): U+FFFE, an unpaired low surrogate -> malformed(2); a high
+ * surrogate not followed by a low one -> malformed(4) (both units); a high surrogate or an odd
+ * byte at the end -> underflow, then malformed(remaining) at end of input.  Every malformed run
+ * becomes ONE U+FFFD.  Then String.trim / StringTools.trimLeft / trimRight. */
+static void decode_utf16_string(const uint8_t* b, int n, int trimming, int big_endian, jvalue* v) {
+    v->type = JSTRING;
+    v->slen = 0;
+    int pos = 0;
+    while (pos < n && v->slen < MAXS - 2) {
+        int mark = pos;
+        int malformed = 0;
+        if (n - pos < 2) {
+            malformed = n - pos;                                 /* end of input, odd byte */
+        } else {
+            uint16_t c = big_endian ? (uint16_t)(b[pos] << 8 | b[pos + 1]) : (uint16_t)(b[pos + 1] << 8 | b[pos]);
+            pos += 2;
+            if (c == 0xFFFE) malformed = 2;
+            else if (c >= 0xD800 && c <= 0xDBFF) {
+                if (n - pos < 2) malformed = n - mark;           /* UNDERFLOW -> malformed(remaining) */
+                else {
+                    uint16_t c2 = big_endian ? (uint16_t)(b[pos] << 8 | b[pos + 1]) : (uint16_t)(b[pos + 1] << 8 | b[pos]);
+                    pos += 2;
+                    if (c2 >= 0xDC00 && c2 <= 0xDFFF) { v->str[v->slen++] = c; v->str[v->slen++] = c2; continue; }
+                    malformed = 4;
+                }
+            } else if (c >= 0xDC00 && c <= 0xDFFF) malformed = 2;
+            else { v->str[v->slen++] = c; continue; }
+        }
+        v->str[v->slen++] = 0xFFFD;
+        pos = mark + malformed;
+    }
+    apply_trim(v->str, &v->slen, trimming);
+}
+
+/* AsciiStringDecoderWrapper.apply (AsciiStringDecoderWrapper.scala:43-67): bytes 0..31 -> 32,
+ * then `new String(buf, charset)` for a single-byte charset (table from the harness), then trim */
+static void decode_charset_string(const uint8_t* b, int n, int trimming, const uint16_t* table, jvalue* v) {
+    v->type = JSTRING;
+    v->slen = 0;
+    for (int i = 0; i < n && i < MAXS; i++) v->str[v->slen++] = table[b[i] < 32 ? 32 : b[i]];
     apply_trim(v->str, &v->slen, trimming);
 }
 
@@ -195,6 +259,9 @@ static int decode_ascii_number(const uint8_t* b, int n, int is_unsigned, char* o
          * stand it in with '#' (same properties) */
         int8_t sb = (int8_t)b[i];
         char c = sb < 0 ? '#' : (char)sb;
+        /* U+0000 is an ordinary (trimmable) Java char; stand it in with U+0001 (same
+         * properties) so that it does not end the C string */
+        if (c == 0) c = 1;
         if (c == '-' || c == '+') sign = c;
         else if (c == '.' || c == ',') buf[bl++] = '.';
         else buf[bl++] = c;
@@ -455,10 +522,14 @@ static void decode_value(const ora_node* nd, const ora_options* opt, const uint8
     if (nd->tclass == ORA_ALPHA) {
         switch (nd->enc) {
         case ORA_EBCDIC: decode_ebcdic_string(b, n, opt->trimming, opt->lut, v); return;
-        case ORA_ASCII: decode_ascii_string(b, n, opt->trimming, v); return;
+        case ORA_ASCII:
+            if (opt->ascii_lut) decode_charset_string(b, n, opt->trimming, opt->ascii_lut, v);
+            else decode_ascii_string(b, n, opt->trimming, v);
+            return;
         case ORA_HEX: decode_hex(b, n, v); return;
         case ORA_RAW: v->type = JBYTES; v->blen = n < MAXS ? n : MAXS; memcpy(v->bytes, b, (size_t)v->blen); return;
-        default: /* UTF-16 (A15) is outside this restatement */ v->type = JNULL; return;
+        case ORA_UTF16: decode_utf16_string(b, n, opt->trimming, opt->utf16_big_endian, v); return;
+        default: v->type = JNULL; return;
         }
     }
     int ebc = nd->enc == ORA_EBCDIC;
@@ -593,6 +664,9 @@ static int to_precision(const jvalue* v, int P, int S, i128* out) {
     int nd = (int)strlen(v->digits);
     int sc = v->scale;
     strcpy(d, v->digits);
+    if (strcmp(d, "0") == 0) { *out = 0; return 1; }   /* zero at any scale */
+    if ((long long)S - sc > 40) return 0;              /* >= 10^41 unscaled: needs > 38 digits */
+    if ((long long)sc - S > nd + 1) { *out = 0; return 1; }  /* every digit dropped, first dropped is 0 */
     if (S >= sc) {
         for (int z = 0; z < S - sc; z++) d[nd++] = '0';
         d[nd] = 0;
@@ -635,6 +709,13 @@ static int utf16_to_utf8(const uint16_t* s, int n, uint8_t* o) {
     int k = 0;
     for (int i = 0; i < n; i++) {
         uint32_t c = s[i];
+        if (c >= 0xD800 && c <= 0xDBFF && i + 1 < n && s[i + 1] >= 0xDC00 && s[i + 1] <= 0xDFFF) {
+            c = 0x10000 + ((c - 0xD800) << 10) + (s[i + 1] - 0xDC00u);
+            i++;
+            o[k++] = (uint8_t)(0xF0 | (c >> 18)); o[k++] = (uint8_t)(0x80 | ((c >> 12) & 63));
+            o[k++] = (uint8_t)(0x80 | ((c >> 6) & 63)); o[k++] = (uint8_t)(0x80 | (c & 63));
+            continue;
+        }
         if (c < 0x80) o[k++] = (uint8_t)c;
         else if (c < 0x800) { o[k++] = (uint8_t)(0xC0 | (c >> 6)); o[k++] = (uint8_t)(0x80 | (c & 63)); }
         else { o[k++] = (uint8_t)(0xE0 | (c >> 12)); o[k++] = (uint8_t)(0x80 | ((c >> 6) & 63)); o[k++] = (uint8_t)(0x80 | (c & 63)); }

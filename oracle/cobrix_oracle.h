@@ -58,8 +58,10 @@ typedef struct {
     int32_t trimming;
     int32_t float_format;
     int32_t variable_size_occurs;
-    int32_t reserved;
+    int32_t utf16_big_endian;   /* is_utf16_big_endian (DecoderSelector.scala:86) */
     const uint16_t* lut;      /* 256-entry EBCDIC -> UTF-16 table */
+    const uint16_t* ascii_lut;/* ascii_charset other than US-ASCII: byte -> UTF-16 of that charset
+                                 (AsciiStringDecoderWrapper), else NULL */
 } ora_options;
 
 typedef struct {

@@ -7,6 +7,7 @@ golden-JSON comparison) or into per-leaf columns (for GPU parity).
 """
 from __future__ import annotations
 
+import codecs
 import ctypes
 import os
 import subprocess
@@ -40,8 +41,8 @@ class OraHandler(ctypes.Structure):
 
 class OraOptions(ctypes.Structure):
     _fields_ = [("trimming", ctypes.c_int32), ("float_format", ctypes.c_int32),
-                ("variable_size_occurs", ctypes.c_int32), ("reserved", ctypes.c_int32),
-                ("lut", ctypes.POINTER(ctypes.c_uint16))]
+                ("variable_size_occurs", ctypes.c_int32), ("utf16_big_endian", ctypes.c_int32),
+                ("lut", ctypes.POINTER(ctypes.c_uint16)), ("ascii_lut", ctypes.POINTER(ctypes.c_uint16))]
 
 
 EVENT_DTYPE = np.dtype([("rec", "<u4"), ("node", "<i4"), ("kind", "<i4"), ("isnull", "<i4"),
@@ -170,7 +171,13 @@ class OracleAst:
         self.opts = OraOptions()
         self.opts.trimming = _TRIM[cb.string_trimming]
         self.opts.float_format = _FP[cb.floating_point_format]
+        self.opts.utf16_big_endian = int(cb.is_utf16_big_endian)
         self.opts.lut = self._lut.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))
+        if cb.ascii_charset and codecs.lookup(cb.ascii_charset).name != "ascii":
+            # Java's single-byte charset tables, as Python's codec registry holds them
+            whole = bytes(range(256)).decode(cb.ascii_charset, errors="replace")
+            self._ascii_lut = np.array([ord(c) for c in whole], dtype=np.uint16)
+            self.opts.ascii_lut = self._ascii_lut.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))
 
     def node_of(self, st: cbk.Statement) -> int:
         return self.index[id(st)]

@@ -94,6 +94,24 @@ def test_fuzz_copybook_vs_oracle():
         assert not errs, (code_page, errs)
 
 
+@pytest.mark.parametrize("big_endian,charset,n", [(True, "", 3000), (False, "windows-1252", 3000),
+                                                   (True, "ISO-8859-1", 70_001)])
+def test_ascii_file_vs_oracle(big_endian, charset, n):
+    """ASCII data: DISPLAY numbers (decodeAsciiNumber, deferred to the fixup kernel), ASCII / charset
+    strings and UTF-16 PIC N through the decode kernel (A15)."""
+    from test_decode_fuzz import ASCII_COPYBOOK, _random_ascii_bytes
+    cb = cbk.parse_copybook(ASCII_COPYBOOK, data_encoding=cbk.ASCII, is_utf16_big_endian=big_endian,
+                            ascii_charset=charset)
+    rng = np.random.default_rng(11)
+    leaves = list(O._iter_leaves(cb.ast))
+    pool = [b"".join(_random_ascii_bytes(rng, p, p.data_size, big_endian) for p in leaves) for _ in range(997)]
+    recs = b"".join(pool[i % 997] if i % 5 else pool[(i * 7) % 997] for i in range(n))
+    assert len(recs) == n * cb.record_size
+    rd, batch = _fixed(ASCII_COPYBOOK, recs, is_ebcdic=False, is_utf16_big_endian=big_endian, ascii_charset=charset)
+    errs = compare_batch(batch, O.decode_fixed(rd.copybook, recs))
+    assert not errs, errs
+
+
 @pytest.mark.parametrize("start,end,rl", [(3, 2, None), (0, 0, 2000), (5, 0, 2300)])
 def test_record_offsets_and_length(start, end, rl):
     """record_start_offset / record_end_offset / record_length (FixedLenNestedReader.scala:60-94)."""
