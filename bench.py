@@ -1,15 +1,24 @@
-"""Benchmark: GPU decode of the SYN200 fixed-length numeric mix (BASELINE.json config C2).
+"""Benchmark: GPU decode of the BASELINE.json configs (default: config C2, SYN200 numeric mix).
 
-`python bench.py --gpus N --steps K --warmup W` -- one rank per GPU (torchrun for N > 1); each
-rank decodes its own shard of records already resident in HBM (weak scaling: records are
-independent, shards need no data-path collective).  A step = one full decode of the shard
-through the C ABI (`cbx_decode_fixed`): the decode kernel (numerics + tile-local strings), the
-fixup kernel for deferred values and the string scan + placement kernels, into Arrow-style columns.
-Rank 0 prints ONE JSON line.
+`python bench.py --gpus N --steps K --warmup W [--workload syn200|synstr200|rdw_narrow|wide_odo]`
+-- one rank per GPU (torchrun for N > 1); each rank decodes its own shard of records already
+resident in HBM (weak scaling: records are independent, shards need no data-path collective; for
+N > 1 one RCCL all-gather of the shard's row / string-byte counts per step gives the global
+Record_Id and string bases).  Rank 0 prints ONE JSON line.
 
-roofline: algorithmic bytes (input record bytes + every output buffer byte)
-of one decode-kernel launch / its average duration, measured with HIP events recorded by the
-library on the launch stream over the timed steps (cbx_plan_kernel_times).
+A step = one full decode of the shard through the C ABI:
+  fixed-length (C2 syn200, C3 synstr200): `cbx_decode_fixed` -- decode kernel (numerics +
+      tile-local strings), fixup kernel for deferred values, string scan + placement kernels;
+  variable-length (C4 rdw_narrow, C5 wide_odo): `cbx_frame_rdw` (GPU RDW offset discovery seeded
+      by sparse-index entries every 100 MB) + `cbx_decode_var` (segment redefines, ODO).
+
+roofline: algorithmic bytes (input record bytes + every output buffer byte) of one
+decode-kernel launch / its average duration, measured with HIP events recorded by the library on
+the launch stream over the timed steps (cbx_plan_kernel_times).
+
+end_to_end (fixed-length workloads, N = 1 view per rank): the same shard streamed from pinned host
+memory -- H2D copies of 2.5M-record chunks on a copy stream overlapped with the decode of the
+previous chunk on the decode stream (double-buffered) -- reported beside `value`, never as it.
 """
 from __future__ import annotations
 
@@ -24,12 +33,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "decoded input GB/s + records/s, fixed-len COMP-3 mix, 1-8 MI355X; % HBM peak"
 
 
-def algorithmic_bytes(plan, n_rec: int, record_bytes: int, payload_bytes: int) -> int:
+def algorithmic_bytes(plan, n_rec: int, in_bytes: int, payload_bytes: int) -> int:
     """input bytes + every output buffer byte one decode writes."""
     from cobrix_amd import native as N
-    total = n_rec * record_bytes + payload_bytes
+    total = in_bytes + payload_bytes
     for info in plan.columns:
         n = n_rec * info.n_slots
         total += (n + 7) // 8                                   # validity bits
@@ -40,11 +50,11 @@ def algorithmic_bytes(plan, n_rec: int, record_bytes: int, payload_bytes: int) -
     return total
 
 
-def measured_traffic(n_rec: int):
+def measured_traffic(tag: str):
     """HBM bytes per decode-kernel launch from the newest committed rocprofv3 FETCH_SIZE/WRITE_SIZE
-    passes of this configuration (tools/gpu_profile.sh -> profiles/<round tag>/traffic_<n_rec>.json)."""
+    passes of this configuration (tools/gpu_profile.sh -> profiles/<round tag>/traffic_<tag>.json)."""
     import glob
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_{n_rec}.json")))
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_{tag}.json")))
     if not found:
         return None, None
     with open(found[-1]) as f:
@@ -52,28 +62,224 @@ def measured_traffic(n_rec: int):
     return int(t["traffic_bytes"]), os.path.relpath(found[-1], ROOT)
 
 
-def _cpu_baseline(seconds: float = 12.0):
-    """Oracle (scalar C restatement of the reference decoders) on a bounded SYN200 sample, 1 core."""
+# ------------------------------------------------------------------------------------------------
+# workloads
+# ------------------------------------------------------------------------------------------------
+WORKLOADS = {
+    "syn200": dict(records=50_000_000, config="C2",
+                   desc="SYN200: fixed-length 200-byte EBCDIC records, numeric mix (COMP, COMP-3, zoned DISPLAY "
+                        "overpunch, IBM COMP-2, cp037 X(18)) -- BASELINE config C2",
+                   data="synthetic (cobrix_amd/synth.py SYN200, seed 20261015+rank, 0.5% malformed numerics)"),
+    "synstr200": dict(records=50_000_000, config="C3",
+                      desc="SYNSTR200: fixed-length 200-byte records, 10 x PIC X(20) cp037 -> UTF-8, trim both, "
+                           "Arrow string offsets -- BASELINE config C3",
+                      data="synthetic (cobrix_amd/synth.py SYNSTR200: lengths 0-20, 25% accented, 10% leading "
+                           "spaces, 1% control bytes)"),
+    "rdw_narrow": dict(records=150_000_000, config="C4",
+                       desc="RDW multisegment file, exp2/test5 layout (C 68 B / P 64 B records, segment redefines), "
+                            "GPU RDW offset discovery seeded every 100 MB + var-len decode -- BASELINE config C4",
+                       data="synthetic (cobrix_amd/synth.py rdw_narrow, 35% root segments)"),
+    "wide_odo": dict(records=770_000, config="C5",
+                     desc="Wide multisegment RDW file (exp3 layout + OCCURS 0 TO 2000 DEPENDING ON, 16,070 B roots, "
+                          "64 B children) -- BASELINE config C5 (per-GPU shard of the 8-GPU job)",
+                     data="synthetic (cobrix_amd/synth.py wide_odo, element counts uniform 0-2000, 0-4 children)"),
+}
+
+
+def _seeds_every(hdr, is_root, n_bytes: int, every: int):
+    """Sparse-index entry points (IndexGenerator.scala:89-113): the first root-segment header at or
+    after each `every`-byte boundary."""
+    import torch
+    roots = hdr[is_root] if is_root is not None else hdr
+    bounds = torch.arange(0, max(n_bytes, 1), every, device=hdr.device, dtype=torch.int64)
+    pos = torch.searchsorted(roots, bounds)
+    pos = pos[pos < roots.numel()]
+    return sorted(set([0] + roots[pos].tolist()))
+
+
+class _Fixed:
+    def __init__(self, name, n_rec, dev, rank, window):
+        import torch
+        from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters
+        from cobrix_amd import synth
+        if name == "syn200":
+            cb, self.stride = synth.SYN200_COPYBOOK, synth.SYN200_RECORD_SIZE
+            self.rec = synth.syn200(n_rec, seed=20261015 + rank, device=dev).view(-1)
+            params = ReaderParameters(window_bytes=window)
+        else:
+            cb, self.stride = synth.SYNSTR200_COPYBOOK, synth.SYNSTR200_RECORD_SIZE
+            self.rec = synth.synstr200(n_rec, seed=20261017 + rank, device=dev).view(-1)
+            params = ReaderParameters(window_bytes=window, ebcdic_code_page="cp037")
+        torch.cuda.synchronize()
+        self.rd = FixedLenNestedReader(cb, params)
+        self.n_rec, self.in_bytes, self.dev = n_rec, n_rec * self.stride, dev
+
+    def prepare(self, stream):
+        from cobrix_amd import native as N
+        from cobrix_amd.reader import _alloc_columns, string_capacity
+        self.L, self.h, self.stream = N.load(), self.rd.native.handle, ctypes.c_void_p(stream.cuda_stream)
+        self.cols, self.cs = _alloc_columns(self.rd.plan, self.n_rec, string_capacity(self.rd.native, self.n_rec),
+                                            self.dev)
+
+    def step(self):
+        from cobrix_amd import native as N
+        N.check(self.L.cbx_decode_fixed(self.h, self.rec.data_ptr(), self.n_rec, self.stride, 0, 0, self.cs,
+                                        self.stream))
+        return None
+
+    def end_to_end(self, chunk_rec: int = 2_500_000, passes: int = 2):
+        """H2D (pinned host) + decode, chunked and double-buffered over two streams."""
+        import torch
+        from cobrix_amd import native as N
+        from cobrix_amd.reader import _alloc_columns, string_capacity
+        host = torch.empty(self.in_bytes, dtype=torch.uint8, pin_memory=True)
+        host.copy_(self.rec)
+        chunk_rec = min(chunk_rec, self.n_rec)
+        cb = chunk_rec * self.stride
+        bufs = [torch.empty(cb, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        outs = [_alloc_columns(self.rd.plan, chunk_rec, string_capacity(self.rd.native, chunk_rec), self.dev)
+                for _ in range(2)]
+        cp, dc = torch.cuda.Stream(self.dev), torch.cuda.Stream(self.dev)
+        done = [torch.cuda.Event() for _ in range(2)]
+        copied = [torch.cuda.Event() for _ in range(2)]
+        for e in done:
+            e.record(dc)
+        dstream = ctypes.c_void_p(dc.cuda_stream)
+        n_chunks = (self.n_rec + chunk_rec - 1) // chunk_rec
+
+        def run():
+            for i in range(n_chunks):
+                b = i % 2
+                r0 = i * chunk_rec
+                m = min(chunk_rec, self.n_rec - r0)
+                cp.wait_event(done[b])
+                with torch.cuda.stream(cp):
+                    bufs[b][: m * self.stride].copy_(host[r0 * self.stride:(r0 + m) * self.stride], non_blocking=True)
+                copied[b].record(cp)
+                dc.wait_event(copied[b])
+                N.check(self.L.cbx_decode_fixed(self.h, bufs[b].data_ptr(), m, self.stride, 0, r0, outs[b][1],
+                                                dstream))
+                done[b].record(dc)
+
+        run()                          # warm-up pass
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            run()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / passes
+        N.check(self.L.cbx_plan_check(self.h, dstream))
+        del host
+        return {"value": round(self.in_bytes / dt / 1e9, 3), "unit": "GB/s", "records_per_s": round(self.n_rec / dt, 1),
+                "ms_per_pass": round(dt * 1e3, 3),
+                "how": f"{n_chunks} chunks of {chunk_rec} records: pinned-host H2D on a copy stream overlapped with "
+                       "cbx_decode_fixed of the previous chunk (double-buffered), per rank"}
+
+    def payload(self):
+        return sum(int(c["sizes"].sum().item()) for c in self.cols if "sizes" in c)
+
+
+class _VarLen:
+    def __init__(self, name, n_rec, dev, rank, window):
+        import torch
+        from cobrix_amd import synth
+        from cobrix_amd.reader import ReaderParameters, VarLenNestedReader
+        if name == "rdw_narrow":
+            self.raw, hdr = synth.rdw_narrow_large(n_rec, seed=20261016 + rank, device=dev)
+            cb, segs = synth.RDW_NARROW_COPYBOOK, synth.RDW_NARROW_SEGMENTS
+        else:
+            self.raw, hdr = synth.wide_odo(n_rec, seed=20261018 + rank, device=dev)
+            cb, segs = synth.WIDE_ODO_COPYBOOK, synth.WIDE_ODO_SEGMENTS
+        is_root = self.raw[hdr + 4] == 0xC3
+        self.in_bytes = int(self.raw.numel())
+        self.seeds = _seeds_every(hdr, is_root, self.in_bytes, 100 * 1024 * 1024)
+        self.n_expected = int(hdr.numel())
+        del hdr, is_root
+        torch.cuda.synchronize()
+        self.rd = VarLenNestedReader(cb, ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
+                                                          segment_id_redefine_map=segs, window_bytes=window))
+        self.dev = dev
+
+    def prepare(self, stream):
+        import torch
+        from cobrix_amd import native as N
+        from cobrix_amd.reader import _alloc_columns, string_capacity
+        self.L, self.h, self.stream = N.load(), self.rd.native.handle, ctypes.c_void_p(stream.cuda_stream)
+        self.cap = self.n_expected + 1
+        self.off = torch.empty(self.cap, dtype=torch.int64, device=self.dev)
+        self.ln = torch.empty(self.cap, dtype=torch.int32, device=self.dev)
+        self.sd = (ctypes.c_int64 * len(self.seeds))(*self.seeds)
+        self.prm = self.rd.rdw_params()
+        self.nfr = ctypes.c_int64(0)
+        self.n_rec = self.n_expected
+        self.cols, self.cs = _alloc_columns(self.rd.plan, self.n_rec, string_capacity(self.rd.native, self.n_rec),
+                                            self.dev)
+        self.fr0, self.fr1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        self.frame_ms = []
+
+    def step(self):
+        from cobrix_amd import native as N
+        self.fr0.record()
+        N.check(self.L.cbx_frame_rdw(self.raw.data_ptr(), self.in_bytes, self.sd, len(self.seeds),
+                                     ctypes.byref(self.prm), self.off.data_ptr(), self.ln.data_ptr(), self.cap,
+                                     ctypes.byref(self.nfr), self.stream))
+        self.fr1.record()
+        if self.nfr.value != self.n_expected:
+            raise RuntimeError(f"framing found {self.nfr.value} records, generator wrote {self.n_expected}")
+        N.check(self.L.cbx_decode_var(self.h, self.raw.data_ptr(), self.in_bytes, self.off.data_ptr(),
+                                      self.ln.data_ptr(), self.n_rec, 0, 0, self.cs, self.stream))
+        return (self.fr0, self.fr1)
+
+    def end_to_end(self):
+        return None
+
+    def payload(self):
+        return sum(int(c["sizes"].sum().item()) for c in self.cols if "sizes" in c)
+
+
+def _cpu_baseline(workload: str, seconds: float = 12.0):
+    """Oracle (scalar C restatement of the reference decoders) on a bounded sample, 1 core."""
     from cobrix_amd.copybook import parse_copybook
-    from cobrix_amd.synth import SYN200_COPYBOOK, syn200
+    from cobrix_amd import synth
     from oracle import oracle as O
-    cb = parse_copybook(SYN200_COPYBOOK)
-    ast = O.OracleAst(cb)
-    n = 2000
-    data = syn200(n, seed=99).numpy().tobytes()
-    t0 = time.perf_counter()
-    O.decode_fixed(cb, data, ast=ast)
-    dt = time.perf_counter() - t0
-    rate = n / max(dt, 1e-9)
-    n2 = int(min(max(rate * seconds, 2000), 6_000_000))
-    data = syn200(n2, seed=100).numpy().tobytes()
-    t0 = time.perf_counter()
-    O.decode_fixed(cb, data, ast=ast)
-    dt = time.perf_counter() - t0
-    return {"value": round(n2 * 200 / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
-            "records_per_s": round(n2 / dt, 1),
-            "sample": f"{n2} SYN200 records ({n2 * 200 / 1e6:.1f} MB) through oracle/cobrix_oracle.c "
-                      f"(restatement of extractRecord + decoders), 1 thread, {dt:.1f} s"}
+    if workload in ("syn200", "synstr200"):
+        text, gen, size = ((synth.SYN200_COPYBOOK, synth.syn200, 200) if workload == "syn200"
+                           else (synth.SYNSTR200_COPYBOOK, synth.synstr200, 200))
+        cb = parse_copybook(text, code_page="common" if workload == "syn200" else "cp037")
+        ast = O.OracleAst(cb)
+
+        def run(n, seed):
+            data = gen(n, seed=seed).numpy().tobytes()
+            t0 = time.perf_counter()
+            O.decode_fixed(cb, data, ast=ast)
+            return time.perf_counter() - t0, n * size
+    else:
+        text, gen = ((synth.RDW_NARROW_COPYBOOK, synth.rdw_narrow) if workload == "rdw_narrow"
+                     else (synth.WIDE_ODO_COPYBOOK, synth.wide_odo))
+        cb = parse_copybook(text, segment_redefines=["STATIC-DETAILS", "CONTACTS"])
+        ast = O.OracleAst(cb)
+
+        def run(n, seed):
+            raw_t, _ = gen(n, seed=seed)
+            raw = raw_t.numpy().tobytes()
+            t0 = time.perf_counter()
+            off, ln = O.frame_rdw(raw)
+            t1 = time.perf_counter()
+            segs = ["STATIC_DETAILS" if raw[o] == 0xC3 else "CONTACTS" for o in off]   # (untimed) segment ids
+            t2 = time.perf_counter()
+            O.decode_var(cb, raw, off, ln, active_segments=segs, ast=ast)
+            return (t1 - t0) + (time.perf_counter() - t2), len(raw)
+    n0 = 2000 if workload != "wide_odo" else 20
+    dt, nb = run(n0, 99)
+    rate = n0 / max(dt, 1e-9)
+    n = int(min(max(rate * seconds, n0), 6_000_000))
+    dt, nb = run(n, 100)
+    unit_n = {"syn200": "SYN200 records", "synstr200": "SYNSTR200 records", "rdw_narrow": "RDW records",
+              "wide_odo": "root records (+ children)"}[workload]
+    return {"value": round(nb / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{n} {unit_n} ({nb / 1e6:.1f} MB) through oracle/cobrix_oracle.c "
+                      f"(restatement of extractRecord + decoders{'' if workload.startswith('syn') else ' + RDW walk'}), "
+                      f"1 thread, {dt:.1f} s"}
 
 
 def main():
@@ -81,17 +287,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--records", type=int, default=50_000_000, help="records per GPU (200 B each)")
+    ap.add_argument("--workload", default="syn200", choices=sorted(WORKLOADS))
+    ap.add_argument("--records", type=int, default=0, help="records per GPU (root records for wide_odo); "
+                                                           "0 = the workload's default")
     ap.add_argument("--window", type=int, default=0, help="LDS window bytes (0 = plan default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-end-to-end", action="store_true")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
     from cobrix_amd import native as N
-    from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters, _alloc_columns, string_capacity
-    from cobrix_amd.synth import SYN200_COPYBOOK, SYN200_RECORD_SIZE, syn200
+    from cobrix_amd.shard import global_bases
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -101,35 +309,47 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    n_rec = args.records
-    rec = syn200(n_rec, seed=20261015 + rank, device=dev).view(-1)
-    torch.cuda.synchronize()
+    W = WORKLOADS[args.workload]
+    n_req = args.records or W["records"]
 
-    rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters(window_bytes=args.window))
-    L = N.load()
-    h = rd.native.handle
+    def progress(msg):
+        if rank == 0:
+            print(f"[bench {args.workload}] {msg}", file=sys.stderr, flush=True)
+
+    progress(f"generating {n_req} records on {dev}")
+    job = (_Fixed if args.workload in ("syn200", "synstr200") else _VarLen)(args.workload, n_req, dev, rank,
+                                                                            args.window)
     st = torch.cuda.current_stream()
-    cols, cs = _alloc_columns(rd.plan, n_rec, string_capacity(rd.native, n_rec), dev)
-    stream = ctypes.c_void_p(st.cuda_stream)
+    progress(f"{job.in_bytes / 1e9:.2f} GB generated; allocating columns")
+    job.prepare(st)
+    progress("warm-up")
+    L, h = job.L, job.h
 
     def step():
-        N.check(L.cbx_decode_fixed(h, rec.data_ptr(), n_rec, SYN200_RECORD_SIZE, 0, 0, cs, stream))
+        fr = job.step()
+        if world > 1:
+            # global Record_Id / string-byte bases of this shard (one small RCCL all-gather)
+            global_bases(job.n_rec, [c["sizes"] for c in job.cols if "sizes" in c])
+        return fr
 
     for _ in range(args.warmup):
         step()
-    N.check(L.cbx_plan_check(h, stream))
+    N.check(L.cbx_plan_check(h, job.stream))
     N.check(L.cbx_plan_set_profiling(h, 1))
+    frame_ev = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        fr = step()
+        if fr is not None:
+            frame_ev.append(fr)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    N.check(L.cbx_plan_check(h, stream))
+    N.check(L.cbx_plan_check(h, job.stream))
     dec = (ctypes.c_float * args.steps)()
     fix = (ctypes.c_float * args.steps)()
     nc = ctypes.c_int32()
@@ -140,27 +360,38 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    payload = sum(int(c["sizes"].sum().item()) for c in cols if "sizes" in c)
+    n_rec = job.n_rec
+    payload = job.payload()
     steps = args.steps
     ms_per_step = elapsed / steps * 1e3
-    in_bytes_total = n_rec * SYN200_RECORD_SIZE * world
-    gbs = in_bytes_total / (elapsed / steps) / 1e9
+    gbs = job.in_bytes * world / (elapsed / steps) / 1e9
     recs_per_s = n_rec * world / (elapsed / steps)
-    alg = algorithmic_bytes(rd.plan, n_rec, SYN200_RECORD_SIZE, payload)
+    alg = algorithmic_bytes(job.rd.plan, n_rec, job.in_bytes, payload)
     dec_avg_ms = sum(dec[: nc.value]) / max(1, nc.value)
     fix_avg_ms = sum(fix[: nc.value]) / max(1, nc.value)
     achieved = alg / (dec_avg_ms * 1e-3) / 1e9
     kind = ctypes.c_int32(0)
     N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
     kname = "cbx_jit_decode (copybook-specialised, hipRTC)" if kind.value == 1 else "cbx::decode_kernel (table-driven)"
-    traffic, traffic_src = measured_traffic(n_rec)
+    tag = str(n_rec) if args.workload == "syn200" else f"{args.workload}_{n_rec}"
+    traffic, traffic_src = measured_traffic(tag)
+    kernel_ms = {"decode_kernel": round(dec_avg_ms, 4),
+                 "post_kernels (deferred-value fixup, string scan + placement)": round(fix_avg_ms, 4)}
+    if frame_ev:
+        fms = sum(a.elapsed_time(b) for a, b in frame_ev) / len(frame_ev)
+        kernel_ms["rdw_framing (cbx_frame_rdw incl. count readback)"] = round(fms, 4)
+    e2e = None
+    if not args.no_end_to_end and world == 1:
+        progress("end-to-end (pinned host -> HBM) pass")
+        e2e = job.end_to_end()
+    progress("cpu baseline" if not args.no_cpu_baseline and world == 1 else "done")
     if rank == 0:
         out = {
-            "metric": "decoded input GB/s + records/s, fixed-len COMP-3 mix, 1-8 MI355X; % HBM peak",
+            "metric": METRIC,
             "value": round(gbs, 3),
             "unit": "GB/s",
             "records_per_s": round(recs_per_s, 1),
-            "hbm_frac_step": round(alg * world / (elapsed / steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
+            "hbm_frac_step": round(alg / (elapsed / steps) / 1e9 / HBM_PEAK_GBS, 4),
             "n_gpus": world,
             "steps": steps,
             "warmup": args.warmup,
@@ -169,22 +400,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (cobrix_amd/synth.py SYN200, seed 20261015+rank, 0.5% malformed numerics)",
-            "config": {"workload": "SYN200: fixed-length 200-byte EBCDIC records, numeric mix "
-                                   "(COMP, COMP-3, zoned DISPLAY overpunch, IBM COMP-2, cp037 X(18)) -- BASELINE config C2",
-                       "records_per_gpu": n_rec, "record_bytes": SYN200_RECORD_SIZE,
-                       "input_gb_per_gpu": round(n_rec * SYN200_RECORD_SIZE / 1e9, 3),
-                       "output_columns": rd.plan.n_columns, "parallelism": f"dp{world}",
+            "data": W["data"],
+            "config": {"workload": W["desc"], "baseline_config": W["config"],
+                       "records_per_gpu": n_rec, "input_bytes_per_gpu": job.in_bytes,
+                       "input_gb_per_gpu": round(job.in_bytes / 1e9, 3),
+                       "output_columns": job.rd.plan.n_columns, "parallelism": f"dp{world}",
                        "inputs_resident_in_hbm": True},
-            "kernel_ms": {"decode_kernel": round(dec_avg_ms, 4),
-                          "post_kernels (deferred-value fixup, string scan + placement)": round(fix_avg_ms, 4)},
+            "kernel_ms": kernel_ms,
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "algorithmic_bytes_per_launch": alg, "traffic": traffic,
                          "traffic_source": traffic_src},
         }
+        if e2e is not None:
+            out["end_to_end"] = e2e
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = _cpu_baseline()
+            out["cpu_baseline"] = _cpu_baseline(args.workload)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

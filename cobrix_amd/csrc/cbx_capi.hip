@@ -636,7 +636,14 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         const int k = contig ? 1 : 0;
         if (!P->jit_tried[k]) {
             P->jit_tried[k] = true;
-            P->jit_fn[k] = jit_get(jit_source(contig, S.win, S.nops, S.batches, S.sops), &P->jit_error);
+            // the specialised kernel is straight-line code per op: wide layouts (thousands of
+            // OCCURS slots) would take minutes in hipRTC and blow the instruction cache -- they
+            // stay on the table-driven kernel, whose op loop is the same arithmetic
+            if (S.nops.size() + S.sops.size() > (size_t)kJitMaxOps)
+                P->jit_error = "layout has " + std::to_string(S.nops.size() + S.sops.size()) +
+                               " element ops, above the specialised-kernel limit " + std::to_string(kJitMaxOps);
+            else
+                P->jit_fn[k] = jit_get(jit_source(contig, S.win, S.nops, S.batches, S.sops), &P->jit_error);
         }
         jfn = P->jit_fn[k];
     }

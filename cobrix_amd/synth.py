@@ -169,3 +169,140 @@ def rdw_narrow(n: int, seed: int = 20261016, device="cpu", big_endian: bool = Fa
     for j in range(10):
         out[hdr + 9 + j] = (0xF0 + torch.randint(0, 10, (n,), generator=g, device=device)).to(torch.uint8)
     return out, hdr
+
+
+def _cat_chunks(make, n: int, chunk: int):
+    """Concatenate generator chunks (bounded temporaries for multi-GB inputs)."""
+    parts = [make(i, min(chunk, n - s)) for i, s in enumerate(range(0, n, chunk))]
+    return torch.cat(parts) if len(parts) > 1 else parts[0]
+
+
+# --------------------------------------------------------------------------------------------
+# SYNSTR200 (config C3): 10 x PIC X(20), cp037, trim both.  Per value: length uniform 0-20,
+# 10 % shifted right behind leading spaces, each byte 25 % a Latin-1 accented letter (2-byte
+# UTF-8), 1 % a control byte (HT / LF / NEL / NUL); padding 0x40.
+# --------------------------------------------------------------------------------------------
+SYNSTR200_COPYBOOK = """
+       01  SYNSTR200-REC.
+""" + "".join(f"           05  STR-{i:02d}        PIC X(20).\n" for i in range(1, 11))
+SYNSTR200_RECORD_SIZE = 200
+# cp037 bytes of a-with-grave .. y-with-acute etc. (CodePage037: U+00C0..U+00FF)
+_CP037_ACCENTED = [0x42, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x51, 0x52, 0x53, 0x54, 0x55, 0x56, 0x57,
+                   0x58, 0x62, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x71, 0x72, 0x73, 0x74, 0x75, 0x76,
+                   0x77, 0x78, 0xCB, 0xCC, 0xCD, 0xCE, 0xCF, 0xDB, 0xDC, 0xDD, 0xDE, 0xEB, 0xEC, 0xED, 0xEE]
+_CP037_CONTROL = [0x05, 0x25, 0x15, 0x00]
+
+
+def synstr200(n: int, seed: int = 20261017, device="cpu", chunk: int = 4_000_000) -> torch.Tensor:
+    """n SYNSTR200 records -> uint8 [n, 200]."""
+    alnum = torch.tensor(_CP037_ALNUM, dtype=torch.uint8, device=device)
+    acc = torch.tensor(_CP037_ACCENTED, dtype=torch.uint8, device=device)
+    ctl = torch.tensor(_CP037_CONTROL, dtype=torch.uint8, device=device)
+
+    def make(ci: int, m: int) -> torch.Tensor:
+        g = torch.Generator(device=device)
+        g.manual_seed(seed * 1000 + ci)
+        shape = (m, 10, 20)
+        b = alnum[torch.randint(0, len(_CP037_ALNUM), shape, generator=g, device=device)]
+        u = torch.rand(shape, generator=g, device=device)
+        b = torch.where(u < 0.25, acc[torch.randint(0, len(_CP037_ACCENTED), shape, generator=g, device=device)], b)
+        b = torch.where(u > 0.99, ctl[torch.randint(0, len(_CP037_CONTROL), shape, generator=g, device=device)], b)
+        ln = torch.randint(0, 21, (m, 10, 1), generator=g, device=device)
+        shift = (torch.rand((m, 10, 1), generator=g, device=device) * (21 - ln).float()).long()
+        shift = torch.where(torch.rand((m, 10, 1), generator=g, device=device) < 0.1, shift, 0)
+        j = torch.arange(20, device=device).view(1, 1, 20)
+        keep = (j >= shift) & (j < shift + ln)
+        return torch.where(keep, b, torch.tensor(0x40, dtype=torch.uint8, device=device)).view(m, 200)
+
+    if n == 0:
+        return torch.zeros((0, 200), dtype=torch.uint8, device=device)
+    return _cat_chunks(make, n, chunk).contiguous()
+
+
+def rdw_narrow_large(n: int, seed: int = 20261016, device="cpu", chunk: int = 16_000_000):
+    """rdw_narrow in chunks (bounded temporaries): -> (bytes, header offsets)."""
+    outs, hdrs, base = [], [], 0
+    for ci, s in enumerate(range(0, n, chunk)):
+        m = min(chunk, n - s)
+        o, h = rdw_narrow(m, seed=seed * 1000 + ci, device=device)
+        outs.append(o)
+        hdrs.append(h + base)
+        base += int(o.numel())
+    return torch.cat(outs), torch.cat(hdrs)
+
+
+# --------------------------------------------------------------------------------------------
+# WIDE_ODO (config C5): the exp3_multiseg_wide layout (GEN/TestDataGen4CompaniesWide.scala:35-55)
+# with NUM-STRAT PIC 9(4) COMP in front of STRATEGY-DETAIL OCCURS 0 TO 2000 DEPENDING ON
+# NUM-STRAT; each element 9(7) COMP + 9(7) COMP-3.  C root: 4 + 16,066 bytes (records stay at the
+# maximum size, variable_size_occurs = false), P child: 4 + 60 bytes, 0-4 children per root.
+# --------------------------------------------------------------------------------------------
+WIDE_ODO_COPYBOOK = """
+        01  COMPANY-DETAILS.
+            05  SEGMENT-ID        PIC X(5).
+            05  COMPANY-ID        PIC X(10).
+            05  STATIC-DETAILS.
+               10  COMPANY-NAME      PIC X(15).
+               10  ADDRESS           PIC X(25).
+               10  TAXPAYER.
+                  15  TAXPAYER-TYPE  PIC X(1).
+                  15  TAXPAYER-STR   PIC X(8).
+                  15  TAXPAYER-NUM  REDEFINES TAXPAYER-STR
+                                     PIC 9(8) COMP.
+               10  NUM-STRAT         PIC 9(4) COMP.
+               10  STRATEGY.
+                 15  STRATEGY-DETAIL OCCURS 0 TO 2000
+                         DEPENDING ON NUM-STRAT.
+                   25  NUM1 PIC 9(7) COMP.
+                   25  NUM2 PIC 9(7) COMP-3.
+            05  CONTACTS REDEFINES STATIC-DETAILS.
+               10  PHONE-NUMBER      PIC X(17).
+               10  CONTACT-PERSON    PIC X(28).
+"""
+WIDE_ODO_SEGMENTS = RDW_NARROW_SEGMENTS
+WIDE_C_PAYLOAD, WIDE_P_PAYLOAD = 16066, 60
+
+
+def wide_odo(n_roots: int, seed: int = 20261018, device="cpu"):
+    """n_roots C records, each followed by 0-4 P records, with LE RDW headers ->
+    (bytes uint8 [total], header offsets int64 [n_records])."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    kids = torch.randint(0, 5, (n_roots,), generator=g, device=device)
+    is_c = torch.zeros(int(n_roots + kids.sum().item()), dtype=torch.bool, device=device)
+    root_pos = torch.cumsum(kids + 1, 0) - (kids + 1)
+    is_c[root_pos] = True
+    n = is_c.numel()
+    plen = torch.where(is_c, WIDE_C_PAYLOAD, WIDE_P_PAYLOAD).to(torch.int64)
+    hdr = torch.cumsum(plen + 4, 0) - (plen + 4)
+    total = int((plen + 4).sum().item())
+    out = torch.randint(0, 256, (total,), generator=g, device=device, dtype=torch.uint8)
+    lo, hi = (plen & 0xFF).to(torch.uint8), (plen >> 8).to(torch.uint8)
+    z = torch.zeros_like(lo)
+    for j, col in enumerate((z, z, lo, hi)):
+        out[hdr + j] = col
+    out[hdr + 4] = torch.where(is_c, 0xC3, 0xD7).to(torch.uint8)
+    for j in range(1, 5):
+        out[hdr + 4 + j] = 0x40
+    # C roots: NUM-STRAT (big-endian, 0..2000) at payload offset 64; elements: NUM1 binary,
+    # NUM2 packed 7 digits + F sign
+    c = hdr[is_c] + 4
+    cnt = torch.randint(0, 2001, (c.numel(),), generator=g, device=device)
+    out[c + 64] = (cnt >> 8).to(torch.uint8)
+    out[c + 65] = (cnt & 0xFF).to(torch.uint8)
+    nc = c.numel()
+    for k0 in range(0, 2000, 250):
+        k = torch.arange(k0, k0 + 250, device=device)
+        base = (c.view(-1, 1) + 66 + 8 * k.view(1, -1)).reshape(-1)
+        v = torch.randint(0, 9999999, (nc * 250,), generator=g, device=device)
+        for j in range(4):
+            out[base + j] = ((v >> (8 * (3 - j))) & 0xFF).to(torch.uint8)
+        d = v.clone()
+        digs = []
+        for _ in range(7):
+            digs.append(d % 10)
+            d = d // 10
+        digs = digs[::-1] + [torch.full_like(v, 0xF)]      # 7 digits + sign nibble
+        for j in range(4):
+            out[base + 4 + j] = ((digs[2 * j] << 4) | digs[2 * j + 1]).to(torch.uint8)
+    return out, hdr

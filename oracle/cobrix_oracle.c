@@ -1148,3 +1148,18 @@ int ora_decode_field(const ora_node* node, const ora_options* opt, const uint8_t
     out->kind = ORA_EV_VALUE;
     return to_event(node, &v, out, heap, heap_cap, heap_len) ? 0 : -2;
 }
+
+/* Batch of variable-length records (VarLenNestedIterator.fetchNext over framed payloads):
+ * record i = data[rec_off[i], rec_off[i] + rec_len[i]), active segment id act[i] (or -1). */
+int ora_extract_var(const ora_node* nodes, int32_t root, const ora_handler* handlers,
+                    const ora_options* opt, const uint8_t* data, const int64_t* rec_off,
+                    const int32_t* rec_len, const int32_t* act, int64_t n, int32_t offset_bytes,
+                    ora_event* ev, int64_t ev_cap, int64_t* n_ev,
+                    uint8_t* heap, int64_t heap_cap, int64_t* heap_len) {
+    for (int64_t i = 0; i < n; i++) {
+        int r = ora_extract_record(nodes, root, handlers, opt, data + rec_off[i], rec_len[i], offset_bytes,
+                                   act ? act[i] : -1, (uint32_t)i, ev, ev_cap, n_ev, heap, heap_cap, heap_len);
+        if (r != 0) return r;
+    }
+    return 0;
+}

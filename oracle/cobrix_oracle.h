@@ -83,6 +83,13 @@ int ora_extract_record(const ora_node* nodes, int32_t root, const ora_handler* h
                        ora_event* ev, int64_t ev_cap, int64_t* n_ev,
                        uint8_t* heap, int64_t heap_cap, int64_t* heap_len);
 
+/* Batch of variable-length records: record i = data[rec_off[i], + rec_len[i]), active segment act[i]. */
+int ora_extract_var(const ora_node* nodes, int32_t root, const ora_handler* handlers,
+                    const ora_options* opt, const uint8_t* data, const int64_t* rec_off,
+                    const int32_t* rec_len, const int32_t* act, int64_t n, int32_t offset_bytes,
+                    ora_event* ev, int64_t ev_cap, int64_t* n_ev,
+                    uint8_t* heap, int64_t heap_cap, int64_t* heap_len);
+
 /* Fixed-length batch: record i is data[i*stride, (i+1)*stride), decoded at +start_offset
  * (CobolScanners.buildScanForFixedLength + FixedLenNestedRowIterator).  Segment redefine per
  * record: if seg_field >= 0 the field's trimmed string value is looked up in seg_keys. */

@@ -73,6 +73,8 @@ def lib():
         L.ora_decode_fixed.argtypes = [P, ctypes.c_int32, P, P, P, ctypes.c_int64, ctypes.c_int32,
                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P, ctypes.c_int32,
                                        P, ctypes.c_int64, P, P, ctypes.c_int64, P]
+        L.ora_extract_var.argtypes = [P, ctypes.c_int32, P, P, P, P, P, P, ctypes.c_int64, ctypes.c_int32,
+                                      P, ctypes.c_int64, P, P, ctypes.c_int64, P]
         L.ora_extract_record.argtypes = [P, ctypes.c_int32, P, P, P, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_uint32, P, ctypes.c_int64, P, P,
                                          ctypes.c_int64, P]
@@ -265,6 +267,32 @@ def decode_records(cb: cbk.Copybook, records: Sequence[bytes], start_offset: int
                                  ctypes.byref(hl))
         if r != 0:
             raise RuntimeError(f"oracle decode failed: {r}")
+    return OracleResult(ast, ev[:n_ev.value].copy(), heap[:hl.value].tobytes(), n_rec)
+
+
+def decode_var(cb: cbk.Copybook, data: bytes, rec_off: np.ndarray, rec_len: np.ndarray,
+               active_segments: Optional[Sequence[Optional[str]]] = None, start_offset: int = 0,
+               ast: Optional[OracleAst] = None) -> OracleResult:
+    """decode_records over framed payloads of one buffer, in one C call (no per-record ctypes)."""
+    ast = ast or OracleAst(cb)
+    n_rec = len(rec_off)
+    ev_cap = max(1, n_rec * ast.max_events_per_record())
+    ev = np.zeros(ev_cap, dtype=EVENT_DTYPE)
+    heap_cap = max(64, int(np.sum(rec_len)) * 3 + 64 * n_rec + 64)
+    heap = np.zeros(heap_cap, dtype=np.uint8)
+    act = None
+    if active_segments is not None:
+        act = np.array([ast.names.get(s.upper(), -2) if s else -1 for s in active_segments], dtype=np.int32)
+    off = np.ascontiguousarray(rec_off, dtype=np.int64)
+    ln = np.ascontiguousarray(rec_len, dtype=np.int32)
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    n_ev, hl = ctypes.c_int64(0), ctypes.c_int64(0)
+    r = lib().ora_extract_var(ctypes.addressof(ast.nodes), 0, ctypes.addressof(ast.handlers),
+                              ctypes.addressof(ast.opts), _ptr(buf), _ptr(off), _ptr(ln),
+                              _ptr(act) if act is not None else None, n_rec, start_offset, _ptr(ev), ev_cap,
+                              ctypes.byref(n_ev), _ptr(heap), heap_cap, ctypes.byref(hl))
+    if r != 0:
+        raise RuntimeError(f"oracle decode failed: {r}")
     return OracleResult(ast, ev[:n_ev.value].copy(), heap[:hl.value].tobytes(), n_rec)
 
 

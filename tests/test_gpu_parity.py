@@ -234,3 +234,34 @@ def test_specialised_kernel_segments_and_offsets():
     res = O.decode_fixed(rd.copybook, recs, segment_field="SEGMENT-ID", segment_redefine_map=seg_map,
                          record_size=L, start_offset=3, end_offset=1)
     assert not compare_batch(batch, res)
+
+
+@pytest.mark.parametrize("n", [1, 4097, 50_000])
+def test_synstr200_vs_oracle(n):
+    """Config C3 (string-heavy cp037, trim both): UTF-8 payloads and Arrow offsets bit-exact."""
+    from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
+    data = synstr200(n, seed=3 + n).numpy().tobytes()
+    rd, batch = _fixed(SYNSTR200_COPYBOOK, data, ebcdic_code_page="cp037")
+    errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
+    assert not errs, errs
+
+
+def test_wide_odo_vs_oracle():
+    """Config C5 (exp3 wide layout, OCCURS 0 TO 2000 DEPENDING ON, segment redefines, RDW)."""
+    from cobrix_amd.synth import WIDE_ODO_COPYBOOK, WIDE_ODO_SEGMENTS, wide_odo
+    raw_t, hdr = wide_odo(40, seed=5)
+    raw = raw_t.numpy().tobytes()
+    params = ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
+                              segment_id_redefine_map=WIDE_ODO_SEGMENTS)
+    rd = VarLenNestedReader(WIDE_ODO_COPYBOOK, params)
+    t = raw_t.cuda()
+    off, ln = rd.frame(t, len(raw))
+    eo, el = O.frame_rdw(raw)
+    assert np.array_equal(off.cpu().numpy(), eo) and np.array_equal(ln.cpu().numpy(), el)
+    assert np.array_equal(eo - 4, hdr.numpy())
+    batch = rd.decode_device(t, len(raw), off, ln)
+    segs = [{"C": "STATIC_DETAILS", "P": "CONTACTS"}.get(G.java_trim(raw[o:o + 5].decode("cp037")))
+            for o in eo]
+    res = O.decode_records(rd.copybook, [raw[o:o + l] for o, l in zip(eo, el)], active_segments=segs)
+    errs = compare_batch(batch, res)
+    assert not errs, errs

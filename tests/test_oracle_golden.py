@@ -33,3 +33,19 @@ def test_rdw_sparse_index_known_answer():
     idx = O.sparse_index(raw, records_per_entry=10, is_root=is_root)
     assert len(idx) == 88
     assert idx[0][0] == 0 and all(a[1] == b[0] for a, b in zip(idx, idx[1:]))
+
+
+def test_oracle_batch_var_equals_per_record():
+    """ora_extract_var (one C call per batch, used by bench.py's cpu_baseline) == per-record decode."""
+    import numpy as np
+    from cobrix_amd import copybook as cbk
+    from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow
+    raw_t, _ = rdw_narrow(500, seed=3)
+    raw = raw_t.numpy().tobytes()
+    cb = cbk.parse_copybook(RDW_NARROW_COPYBOOK, segment_redefines=["STATIC-DETAILS", "CONTACTS"])
+    off, ln = O.frame_rdw(raw)
+    segs = ["STATIC_DETAILS" if raw[o] == 0xC3 else "CONTACTS" for o in off]
+    a = O.decode_var(cb, raw, off, ln, active_segments=segs)
+    b = O.decode_records(cb, [raw[o:o + n] for o, n in zip(off, ln)], active_segments=segs)
+    assert a.n_rec == b.n_rec == 500
+    assert np.array_equal(a.events, b.events) and a.heap == b.heap
