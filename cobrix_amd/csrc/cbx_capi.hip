@@ -843,42 +843,34 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     std::vector<int64_t> hs;
     if (n_seeds <= 0) hs.push_back(0);
     else hs.assign(seeds, seeds + n_seeds);
-    std::vector<int64_t> cs, ce, cr;
-    std::vector<uint8_t> ck;
+    // seed ranges (the chunk table is computed on the device from them)
+    std::vector<RdwRange> ranges(hs.size());
+    int64_t n = 0;
     for (size_t k = 0; k < hs.size(); k++) {
         const int64_t r0 = hs[k], r1 = k + 1 < hs.size() ? hs[k + 1] : n_bytes;
         if (r0 < 0 || r0 > n_bytes || r1 < r0) return fail(CBX_E_ARGUMENT, "cbx_frame_rdw: seeds must be increasing offsets");
-        for (int64_t s0 = r0; s0 < r1 || s0 == r0; s0 += chunk) {
-            cs.push_back(s0);
-            ce.push_back(std::min(s0 + chunk, r1));
-            cr.push_back(r1);
-            ck.push_back(s0 == r0);
-            if (s0 + chunk >= r1) break;
-        }
+        ranges[k] = RdwRange{r0, r1, n};
+        n += std::max<int64_t>(1, (r1 - r0 + chunk - 1) / chunk);
     }
-    const int64_t n = (int64_t)cs.size();
-    // one device block: start, end, range_end, entry, exit x2, err, base (int64) | count (u32) | known (u8)
-    const size_t bytes = sizeof(int64_t) * (8 * n + 2) + sizeof(uint32_t) * n + n + 64;
+    const int64_t nb = (n + kScanTile - 1) / kScanTile;
+    // one device block: entry, exit x2, err, base (int64 x n) | first_err, total, changed | block sums |
+    // ranges | count (u32 x n)
+    const size_t bytes = sizeof(int64_t) * (5 * n + 4 + nb) + sizeof(RdwRange) * ranges.size() + sizeof(uint32_t) * n + 64;
     uint8_t* blk = nullptr;
     HIP_CHECK(hipMallocAsync((void**)&blk, bytes, st));
     int64_t* d64 = (int64_t*)blk;
     RdwChunkArgs c{};
-    int64_t* d_start = d64;
-    int64_t* d_end = d64 + n;
-    int64_t* d_re = d64 + 2 * n;
-    c.entry = d64 + 3 * n;
-    int64_t* exits[2] = {d64 + 4 * n, d64 + 5 * n};
-    c.err = d64 + 6 * n;
-    int64_t* d_base = d64 + 7 * n;
-    unsigned long long* d_first_err = (unsigned long long*)(d64 + 8 * n);
-    c.changed = (int32_t*)(d64 + 8 * n + 1);
-    c.count = (uint32_t*)(d64 + 8 * n + 2);
-    uint8_t* d_known = (uint8_t*)(c.count + n);
-    c.start = d_start; c.end = d_end; c.range_end = d_re; c.known = d_known; c.n = n;
-    HIP_CHECK(hipMemcpyAsync(d_start, cs.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipMemcpyAsync(d_end, ce.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipMemcpyAsync(d_re, cr.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipMemcpyAsync(d_known, ck.data(), n, hipMemcpyHostToDevice, st));
+    c.entry = d64;
+    int64_t* exits[2] = {d64 + n, d64 + 2 * n};
+    c.err = d64 + 3 * n;
+    int64_t* d_base = d64 + 4 * n;
+    unsigned long long* d_first_err = (unsigned long long*)(d64 + 5 * n);   // [0] first error, [1] total
+    c.changed = (int32_t*)(d64 + 5 * n + 2);
+    int64_t* d_block_sums = d64 + 5 * n + 4;
+    RdwRange* d_ranges = (RdwRange*)(d_block_sums + nb);
+    c.count = (uint32_t*)(d_ranges + ranges.size());
+    c.ranges = d_ranges; c.n_ranges = (int32_t)ranges.size(); c.chunk = chunk; c.n = n;
+    HIP_CHECK(hipMemcpyAsync(d_ranges, ranges.data(), sizeof(RdwRange) * ranges.size(), hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemsetAsync(d_first_err, 0xFF, sizeof(unsigned long long), st));
     RdwArgs a{};
     a.data = d_data; a.n_bytes = n_bytes; a.p = *params;
@@ -900,21 +892,21 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
         HIP_CHECK(hipStreamSynchronize(st));
         if (!changed) break;
     }
-    // record counts -> bases (host scan of the chunk counts: one value per 16 KiB)
-    std::vector<uint32_t> cnt(n);
-    HIP_CHECK(hipMemcpyAsync(cnt.data(), c.count, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    std::vector<int64_t> base(n);
-    int64_t total = 0;
-    for (int64_t k = 0; k < n; k++) { base[k] = total; total += cnt[k]; }
-    HIP_CHECK(hipMemcpyAsync(d_base, base.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
+    // record counts -> bases: device exclusive scan of the chunk counts
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)c.count, n,
+                       d_block_sums);
+    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, d_block_sums, nb);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)c.count, n,
+                       (const int64_t*)d_block_sums, d_base);
     hipLaunchKernelGGL(rdw_emit_kernel, dim3(blocks), dim3(threads), 0, st, a, c, (const int64_t*)d_base, d_rec_off,
                        d_rec_len, capacity, d_first_err);
     HIP_CHECK(hipGetLastError());
-    unsigned long long first_err = 0;
-    HIP_CHECK(hipMemcpyAsync(&first_err, d_first_err, sizeof(first_err), hipMemcpyDeviceToHost, st));
+    unsigned long long res[2] = {0, 0};
+    HIP_CHECK(hipMemcpyAsync(res, d_first_err, sizeof(res), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipFreeAsync(blk, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    const unsigned long long first_err = res[0];
+    const int64_t total = (int64_t)res[1];
     if (first_err != ~0ull) {
         const long long off = (long long)(first_err >> 2);
         char msg[200];

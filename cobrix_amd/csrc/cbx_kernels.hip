@@ -365,11 +365,15 @@ __device__ __forceinline__ RdwStep rdw_step(const RdwArgs& a, int64_t pos) {
 // chunks that change, until no chunk changes: by induction from the seeds the entries are then
 // exactly the sequential walk's header positions.  A final pass writes (offset, length) of the
 // valid records at each chunk's scanned base.
+struct RdwRange {
+    int64_t r0, r1;          // seed range [r0, r1)
+    int64_t first;           // index of its first chunk
+};
+
 struct RdwChunkArgs {
-    const int64_t* start;
-    const int64_t* end;
-    const int64_t* range_end;
-    const uint8_t* known;    // entry known (a seed)
+    const RdwRange* ranges;  // chunk k of range i: [r0 + (k - first) * chunk, min(.. + chunk, r1))
+    int32_t n_ranges;
+    int64_t chunk;
     int64_t* entry;
     int64_t* exit_in;
     int64_t* exit_out;
@@ -425,16 +429,71 @@ __device__ __forceinline__ bool rdw_plausible(const RdwArgs& a, int64_t q, int64
     return true;
 }
 
+struct RdwChunk {
+    int64_t start, end, range_end;
+    bool known;              // the entry is a seed (a range's first chunk)
+};
+
+__device__ __forceinline__ RdwChunk rdw_chunk(const RdwChunkArgs& c, int64_t k) {
+    int lo = 0, hi = c.n_ranges - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (c.ranges[mid].first <= k) lo = mid; else hi = mid - 1;
+    }
+    const RdwRange r = c.ranges[lo];
+    RdwChunk ch;
+    ch.start = r.r0 + (k - r.first) * c.chunk;
+    ch.end = ch.start + c.chunk < r.r1 ? ch.start + c.chunk : r.r1;
+    ch.range_end = r.r1;
+    ch.known = k == r.first;
+    return ch;
+}
+
+// First q in [s, e) that starts a strictly plausible chain.  A strict header has two zero bytes
+// (LE: bytes 0-1, BE: bytes 2-3), so only zero-byte pairs are candidates: the chunk is scanned
+// a dword at a time with an exact zero-byte mask, and the chain test runs on candidates only.
+__device__ int64_t rdw_strict_scan(const RdwArgs& a, int64_t s, int64_t e, int64_t re) {
+    const int64_t off = a.p.big_endian ? 2 : 0;
+    const int64_t p0 = s + off, p1 = e + off;          // pair start positions [p0, p1)
+    uint32_t carry = 0;                                 // byte w-1 is zero
+    for (int64_t w = p0 & ~(int64_t)3; w < p1 && w < a.n_bytes; w += 4) {
+        uint32_t zb = 0;                                // bit j: byte w + j is zero
+        if (w + 4 <= a.n_bytes) {
+            const uint32_t x = *(const uint32_t*)(a.data + w);
+            const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+            zb = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+        } else {
+            for (int j = 0; j < 4 && w + j < a.n_bytes; j++) zb |= (a.data[w + j] == 0 ? 1u : 0u) << j;
+        }
+        // pairs starting at w-1, w, w+1, w+2 (bit i <-> position w - 1 + i)
+        uint32_t pairs = (carry & zb) | ((zb & (zb >> 1)) << 1);
+        carry = zb >> 3;
+        while (pairs) {
+            const int i = __builtin_ctz(pairs);
+            pairs &= pairs - 1;
+            const int64_t p = w - 1 + i;
+            if (p < p0 || p >= p1) continue;
+            const int64_t q = p - off;
+            if (rdw_plausible(a, q, re, true)) return q;
+        }
+    }
+    return -1;
+}
+
 __global__ void rdw_spec_kernel(RdwArgs a, RdwChunkArgs c) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c.n) return;
-    const int64_t s = c.start[k], e = c.end[k], re = c.range_end[k];
+    const RdwChunk ch = rdw_chunk(c, k);
+    const int64_t s = ch.start, e = ch.end, re = ch.range_end;
     int64_t entry = s;
-    if (!c.known[k]) {
-        bool found = false;
-        for (int strict = 1; strict >= 0 && !found; strict--)
-            for (int64_t q = s; q < e && !found; q++)
-                if (rdw_plausible(a, q, re, strict != 0)) { entry = q; found = true; }
+    if (!ch.known) {
+        const int64_t q = rdw_strict_scan(a, s, e, re);
+        if (q >= 0) {
+            entry = q;
+        } else {
+            for (int64_t p = s; p < e; p++)
+                if (rdw_plausible(a, p, re, false)) { entry = p; break; }
+        }
     }
     c.entry[k] = entry;
     const RdwWalk w = rdw_walk<false>(a, entry, e, nullptr, nullptr, 0, 0);
@@ -446,12 +505,13 @@ __global__ void rdw_spec_kernel(RdwArgs a, RdwChunkArgs c) {
 __global__ void rdw_fix_kernel(RdwArgs a, RdwChunkArgs c) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c.n) return;
-    if (c.known[k]) { c.exit_out[k] = c.exit_in[k]; return; }
+    const RdwChunk ch = rdw_chunk(c, k);
+    if (ch.known) { c.exit_out[k] = c.exit_in[k]; return; }
     const int64_t e = c.exit_in[k - 1];
     if (e == c.entry[k]) { c.exit_out[k] = c.exit_in[k]; return; }
     c.entry[k] = e;
     *c.changed = 1;
-    const RdwWalk w = rdw_walk<false>(a, e, c.end[k], nullptr, nullptr, 0, 0);
+    const RdwWalk w = rdw_walk<false>(a, e, ch.end, nullptr, nullptr, 0, 0);
     c.exit_out[k] = w.exit;
     c.count[k] = w.count;
     c.err[k] = w.err;
@@ -462,7 +522,8 @@ __global__ void rdw_emit_kernel(RdwArgs a, RdwChunkArgs c, const int64_t* base, 
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c.n) return;
     if (c.err[k] >= 0) atomicMin(first_err, (unsigned long long)c.err[k]);
-    rdw_walk<true>(a, c.entry[k], c.end[k], rec_off, rec_len, base[k], cap);
+    rdw_walk<true>(a, c.entry[k], rdw_chunk(c, k).end, rec_off, rec_len, base[k], cap);
+    if (k == c.n - 1) first_err[1] = (unsigned long long)(base[k] + c.count[k]);   // record total
 }
 
 }  // namespace cbx
