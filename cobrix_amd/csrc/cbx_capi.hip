@@ -678,7 +678,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     if (P->n_seq > 0) {
         if ((r = string_scan(P, n_tiles, st))) return r;
         if (mode == 0) {
-            const unsigned gx = (unsigned)((n_tiles + kPlaceWaves - 1) / kPlaceWaves);
+            const unsigned gx = (unsigned)((n_tiles + kPlaceWaves * kPlaceTiles - 1) / (kPlaceWaves * kPlaceTiles));
             hipLaunchKernelGGL(str_place_kernel, dim3(gx, (unsigned)std::min<int64_t>(P->n_seq, 65535)), dim3(kWave * kPlaceWaves), 0, st,
                                (const CBX_CONST SeqCall*)P->d_seqcall, (const uint32_t*)P->d_str_tot,
                                (const int64_t*)P->d_str_excl, n_tiles, c.n_rec, P->n_seq, P->d_status);

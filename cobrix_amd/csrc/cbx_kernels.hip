@@ -179,62 +179,87 @@ struct SeqCall {
     int32_t reserved;
 };
 
-// One wave per (sequence, tile): 4 tiles per workgroup, no grid-stride loop (tiles are ~1 KiB
-// each: many in flight hide the load latency).  The payload moves in 16-byte pieces: each lane
-// reads 5 dwords of the (aligned) scratch region and writes 4 realigned dwords at the
-// destination (any alignment; byte stores at the unaligned ends).
+// One wave per (sequence, kPlaceTiles consecutive tiles), 4 waves per workgroup.  The pass is
+// bound by load latency per resident wave (each tile is ~1 KiB), so every wave first issues the
+// loads of all its tiles -- scanned bases, totals, tile-local starts and the first 20 scratch
+// bytes of every lane -- and only then stores: two dependent memory round trips per wave
+// instead of two per tile.  The payload moves in 16-byte pieces: each lane reads 5 dwords of
+// the (aligned) scratch region and writes 4 realigned dwords at the destination (any
+// alignment; byte stores at the unaligned ends).
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 constexpr int kPlaceWaves = 4;
+constexpr int kPlaceTiles = 4;
 
 __global__ __launch_bounds__(kWave * kPlaceWaves) void str_place_kernel(const CBX_CONST SeqCall* seqs, const uint32_t* tot,
                                                                          const int64_t* excl, int64_t n_tiles, int64_t n_rec,
                                                                          int32_t n_seq, int32_t* status) {
     const int lane = threadIdx.x % kWave;
-    const int64_t tile = (int64_t)blockIdx.x * kPlaceWaves + threadIdx.x / kWave;
-    if (tile >= n_tiles) return;
+    const int64_t tile0 = ((int64_t)blockIdx.x * kPlaceWaves + threadIdx.x / kWave) * kPlaceTiles;
+    if (tile0 >= n_tiles) return;
     for (int seq = blockIdx.y; seq < n_seq; seq += gridDim.y) {
         const SeqCall q = ldc(seqs + seq);
-        const int64_t seq0 = excl[(int64_t)seq * n_tiles];
-        const int64_t base = excl[(int64_t)seq * n_tiles + tile] - seq0;
-        const uint32_t n = tot[(int64_t)seq * n_tiles + tile];
-        const int64_t rec = tile * kWave + lane;
-        gp(q.offsets)[rec] = q.region + base + gp(q.local)[rec];   // lanes past n_rec write padding entries
-        if (tile == n_tiles - 1 && lane == 0) {
-            gp(q.offsets)[n_rec] = q.region + base + n;
-            if (q.size) *gp(q.size) = base + n;
+        const int64_t* ex = excl + (int64_t)seq * n_tiles;
+        const uint32_t* tt = tot + (int64_t)seq * n_tiles;
+        const int64_t seq0 = ex[0];
+        const bool pre = 16 * lane + 20 <= q.tile_cap;   // this lane's first piece lies in the region
+        int64_t base[kPlaceTiles];
+        uint32_t n[kPlaceTiles], loc[kPlaceTiles], e0[kPlaceTiles];
+        u32x4a v0[kPlaceTiles];
+#pragma unroll
+        for (int u = 0; u < kPlaceTiles; u++) {
+            const int64_t tile = tile0 + u < n_tiles ? tile0 + u : n_tiles - 1;
+            base[u] = ex[tile] - seq0;
+            n[u] = tt[tile];
+            loc[u] = gp(q.local)[tile * kWave + lane];
+            const CBX_GLOBAL uint32_t* src = gp((const uint32_t*)(q.scratch + tile * (int64_t)q.tile_cap));
+            v0[u] = pre ? *(const CBX_GLOBAL u32x4a*)(src + 4 * lane) : u32x4a{0, 0, 0, 0};
+            e0[u] = pre ? src[4 * lane + 4] : 0u;
         }
-        if (base + (int64_t)n > q.capacity) {
-            if (lane == 0) atomicOr(status, 1);
-            continue;
-        }
-        const CBX_GLOBAL uint32_t* src = gp((const uint32_t*)(q.scratch + tile * (int64_t)q.tile_cap));
-        const CBX_GLOBAL uint8_t* s8 = (const CBX_GLOBAL uint8_t*)src;
-        CBX_GLOBAL uint8_t* dst = gp(q.data + base);
-        const uint32_t g0 = (uint32_t)((uint64_t)(q.data + base) & 3);
-        const uint32_t head = (4 - g0) & 3;                 // bytes before the first aligned dword
-        if (n <= head) {
-            if (lane < (int)n) dst[lane] = s8[lane];
-            continue;
-        }
-        const uint32_t ndw = (n - head) >> 2;               // whole destination dwords
-        const uint32_t tail = (n - head) & 3;
-        if (lane < (int)head) dst[lane] = s8[lane];
-        if (lane < (int)tail) dst[head + 4 * ndw + lane] = s8[head + 4 * ndw + lane];
-        CBX_GLOBAL uint32_t* d32 = (CBX_GLOBAL uint32_t*)(dst + head);
-        const uint32_t sh = head & 3;                       // source byte shift (scratch is 16-aligned)
-        const uint32_t k0 = head >> 2;                      // = 0: head < 4
-        for (uint32_t d = 4u * lane; d < ndw; d += 4u * kWave) {
-            const uint32_t k = k0 + d;
-            const u32x4a v = *(const CBX_GLOBAL u32x4a*)(src + k);
-            const uint32_t e = src[k + 4];
-            const uint32_t w0 = align_bytes(v.y, v.x, sh), w1 = align_bytes(v.z, v.y, sh);
-            const uint32_t w2 = align_bytes(v.w, v.z, sh), w3 = align_bytes(e, v.w, sh);
-            if (d + 4 <= ndw) {
-                *(CBX_GLOBAL u32x4a*)(d32 + d) = u32x4a{w0, w1, w2, w3};
-            } else {
-                d32[d] = w0;
-                if (d + 1 < ndw) d32[d + 1] = w1;
-                if (d + 2 < ndw) d32[d + 2] = w2;
+#pragma unroll
+        for (int u = 0; u < kPlaceTiles; u++) {
+            const int64_t tile = tile0 + u;
+            if (tile >= n_tiles) break;
+            const int64_t rec = tile * kWave + lane;
+            gp(q.offsets)[rec] = q.region + base[u] + loc[u];   // lanes past n_rec write padding entries
+            if (tile == n_tiles - 1 && lane == 0) {
+                gp(q.offsets)[n_rec] = q.region + base[u] + n[u];
+                if (q.size) *gp(q.size) = base[u] + n[u];
+            }
+            if (base[u] + (int64_t)n[u] > q.capacity) {
+                if (lane == 0) atomicOr(status, 1);
+                continue;
+            }
+            const CBX_GLOBAL uint32_t* src = gp((const uint32_t*)(q.scratch + tile * (int64_t)q.tile_cap));
+            const CBX_GLOBAL uint8_t* s8 = (const CBX_GLOBAL uint8_t*)src;
+            CBX_GLOBAL uint8_t* dst = gp(q.data + base[u]);
+            const uint32_t g0 = (uint32_t)((uint64_t)(q.data + base[u]) & 3);
+            const uint32_t head = (4 - g0) & 3;                 // bytes before the first aligned dword
+            if (n[u] <= head) {
+                if (lane < (int)n[u]) dst[lane] = s8[lane];
+                continue;
+            }
+            const uint32_t ndw = (n[u] - head) >> 2;            // whole destination dwords
+            const uint32_t tail = (n[u] - head) & 3;
+            if (lane < (int)head) dst[lane] = s8[lane];
+            if (lane < (int)tail) dst[head + 4 * ndw + lane] = s8[head + 4 * ndw + lane];
+            CBX_GLOBAL uint32_t* d32 = (CBX_GLOBAL uint32_t*)(dst + head);
+            const uint32_t sh = head & 3;                       // source byte shift (scratch is 16-aligned)
+            for (uint32_t d = 4u * lane; d < ndw; d += 4u * kWave) {
+                u32x4a v = v0[u];
+                uint32_t e = e0[u];
+                if (d != 4u * lane || !pre) {
+                    v = *(const CBX_GLOBAL u32x4a*)(src + d);
+                    e = src[d + 4];
+                }
+                const uint32_t w0 = align_bytes(v.y, v.x, sh), w1 = align_bytes(v.z, v.y, sh);
+                const uint32_t w2 = align_bytes(v.w, v.z, sh), w3 = align_bytes(e, v.w, sh);
+                if (d + 4 <= ndw) {
+                    *(CBX_GLOBAL u32x4a*)(d32 + d) = u32x4a{w0, w1, w2, w3};
+                } else {
+                    d32[d] = w0;
+                    if (d + 1 < ndw) d32[d + 1] = w1;
+                    if (d + 2 < ndw) d32[d + 2] = w2;
+                }
             }
         }
     }
