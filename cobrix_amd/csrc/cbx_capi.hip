@@ -54,6 +54,7 @@ struct cbx_plan {
         StrOp* d_sops = nullptr;
         GenOp* d_gops = nullptr;
         int max_str_items = 0;   // string elements in the fullest window
+        bool has_runs = false;   // some op stands for a run of OCCURS elements
     } cset, wset;
     bool contig_ok = true;       // every string element fits the single contiguous window
     int str_stage = 16;          // LDS payload staging bytes per wave
@@ -205,10 +206,40 @@ static void push_window(cbx_plan* P, cbx_plan::OpSet& S, std::vector<Elem> els, 
     w.lo = lo; w.hi = hi; w.global = global ? 1 : 0;
     w.nop_begin = (int)S.nops.size();
     w.sop_begin = (int)S.sops.size();
+    std::vector<NumOp> wn;
+    std::vector<int> wf;   // field of each numeric op
     for (const Elem& e : els) {
         const Field& d = P->dfields_h[e.field];
         if (e.str) S.sops.push_back(make_strop(d, e));
-        else S.nops.push_back(make_numop(d, e.slot, e.eo, e.odo_arr, e.odo_idx, e.n_odo));
+        else { wn.push_back(make_numop(d, e.slot, e.eo, e.odo_arr, e.odo_idx, e.n_odo)); wf.push_back(e.field); }
+    }
+    // OCCURS runs (staged windows): consecutive elements of a field along its innermost dimension
+    // become one op -- the kernel walks the run with the element stride, so wide arrays cost one
+    // op record per run instead of one per element
+    for (size_t i = 0; i < wn.size();) {
+        NumOp o = wn[i];
+        const Field& d = P->dfields_h[wf[i]];
+        size_t run = 1;
+        if (!global && d.n_dims > 0) {
+            const int stride = d.dim_stride[d.n_dims - 1];
+            const bool inner_odo = o.n_odo > 0 && o.odo_arr[o.n_odo - 1] == d.dim_array[d.n_dims - 1];
+            while (i + run < wn.size() && run < 255 && wf[i + run] == wf[i]) {
+                const NumOp& n = wn[i + run];
+                bool same = n.slot == o.slot + (int)run && n.eo == o.eo + (int)run * stride && n.n_odo == o.n_odo &&
+                            n.defer == (o.defer >= 0 ? o.defer + (int)run : -1);
+                for (int j = 0; same && j < o.n_odo; j++) {
+                    const bool last = j == o.n_odo - 1 && inner_odo;
+                    same = n.odo_arr[j] == o.odo_arr[j] && n.odo_idx[j] == o.odo_idx[j] + (last ? (int)run : 0);
+                }
+                if (!same) break;
+                run++;
+            }
+            o.run_stride = stride;
+            o.run_odo = inner_odo ? 1 : 0;
+        }
+        o.run = (uint8_t)run;
+        S.nops.push_back(o);
+        i += run;
     }
     w.nop_end = (int)S.nops.size();
     w.sop_end = (int)S.sops.size();
@@ -220,7 +251,10 @@ static void push_window(cbx_plan* P, cbx_plan::OpSet& S, std::vector<Elem> els, 
         while (j < w.nop_end && (global || S.nops[j].variant == v) && out_width(S.nops[j].out_type) == wd &&
                (S.nops[j].n_odo > 0) == odo)
             j++;
-        S.batches.push_back(Batch{v, wd, i, j, odo ? 1 : 0, 0});
+        int runs = 0;
+        for (int k = i; k < j; k++) runs |= S.nops[k].run > 1;
+        S.batches.push_back(Batch{v, wd, i, j, odo ? 1 : 0, runs});
+        S.has_runs |= runs != 0;
         i = j;
     }
     w.batch_end = (int)S.batches.size();
@@ -639,9 +673,12 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
             // the specialised kernel is straight-line code per op: wide layouts (thousands of
             // OCCURS slots) would take minutes in hipRTC and blow the instruction cache -- they
             // stay on the table-driven kernel, whose op loop is the same arithmetic
-            if (S.nops.size() + S.sops.size() > (size_t)kJitMaxOps)
-                P->jit_error = "layout has " + std::to_string(S.nops.size() + S.sops.size()) +
-                               " element ops, above the specialised-kernel limit " + std::to_string(kJitMaxOps);
+            size_t elems = S.sops.size();
+            for (const NumOp& o : S.nops) elems += o.run > 1 ? o.run : 1;
+            if (elems > (size_t)kJitMaxOps || S.win.size() > (size_t)kJitMaxWindows)
+                P->jit_error = "layout has " + std::to_string(elems) + " elements in " + std::to_string(S.win.size()) +
+                               " windows, above the specialised-kernel limits (" + std::to_string(kJitMaxOps) + ", " +
+                               std::to_string(kJitMaxWindows) + ")";
             else
                 P->jit_fn[k] = jit_get(jit_source(contig, S.win, S.nops, S.batches, S.sops), &P->jit_error);
         }

@@ -709,12 +709,16 @@ enum NumFlags : uint32_t {
 struct NumOp {
     int32_t eo;                       // element offset in the record (slot resolved, before start_off)
     uint8_t variant, size, out_type, flags;
-    uint8_t n_odo, shift, pad0, pad1; // shift: 64 - 8 * min(size, 8) (binary sign extension)
+    uint8_t n_odo, shift, run, run_odo; // shift: 64 - 8 * min(size, 8) (binary sign extension);
+                                      // run: elements r = 0..run-1 of the field's innermost OCCURS
+                                      // dimension share this record (0 / 1: a single element) at
+                                      // eo + r * run_stride, slot + r, defer + r, and -- run_odo --
+                                      // ODO index odo_idx[n_odo - 1] + r
     int32_t column;
     int32_t slot;
     int32_t defer;                    // deferral sequence of this element, -1 if never deferred
     int32_t segment;                  // segment-redefine group, -1 none
-    int32_t reserved;
+    int32_t run_stride;
     // plan-time constants of the fast paths (no table lookups or shifts by size in the kernel)
     uint64_t mask;                    // BCD8 / BIN8: low `size` bytes (after bswap); BCD16: low size-8
                                       // bytes of the leading word; ZONED16: high min(size, 8) bytes

@@ -243,6 +243,76 @@ __device__ __forceinline__ void num_batch(const KernelArgs& a, const Batch& b, c
     }
 }
 
+// Element r of an OCCURS run op (NumOp.run): offset, slot row, deferral row and innermost ODO
+// index advance with r; otherwise num_one.
+template <int V, int W, bool kOdo>
+__device__ __forceinline__ void run_elem(const KernelArgs& a, const NumOp& op, const CBX_CONST NumOp* opp, const NumCall& c,
+                                         int r, const TileCtx& t, bool ok, uint64_t r1, uint64_t r0, const int32_t* s_cnt,
+                                         int lane) {
+    if (op.segment >= 0) ok &= op.segment == t.seg;
+    if (kOdo) {
+        // ODO levels read through the op pointer (indexing the local copy would force it to scratch)
+        for (int j = 0; j < op.n_odo; j++) {
+            const int idx = opp->odo_idx[j] + (j == op.n_odo - 1 && op.run_odo ? r : 0);
+            ok &= idx < s_cnt[opp->odo_arr[j] * kWave + lane];
+        }
+    }
+    Val x = null_val();
+    bool defer = false;
+    if (V == V_GENERIC) {
+        defer = ok;
+    } else {
+        if (V == V_BCD8) x = bcd8_raw<W>(op, r1);
+        else if (V == V_BCD16) x = bcd16_raw<W>(op, r1, r0);
+        else if (V == V_BIN8) x = bin8_raw<W>(op, r1);
+        else if (V == V_ZONED16) { x = zoned16_raw<W>(op, r1, r0, defer); defer &= ok; }
+        else if (V == V_FP) x = fp_raw(op, r1);
+        x.valid &= ok;
+    }
+    const int w = W ? W : (op.out_type == CBX_O_I32 || op.out_type == CBX_O_F32 ? 4 : op.out_type == CBX_O_DEC128 ? 16 : 8);
+    store_w<W>(c.values + (int64_t)r * a.pitch * w, t.rec, x, op.out_type);
+    const uint64_t m = __ballot(x.valid);
+    gp(c.validity + (int64_t)r * a.n_tiles)[t.tile] = m;
+    if (V == V_ZONED16 || V == V_GENERIC) {
+        const uint64_t dm = __ballot(defer);
+        if (c.defer) gp(c.defer + (int64_t)r * a.n_tiles)[t.tile] = dm;
+    }
+}
+
+constexpr int kRunU = 4;   // run elements decoded per step (reads first)
+
+// A batch holding OCCURS runs: per op, its elements kRunU at a time (reads first).
+template <int V, int W, bool kOdo>
+__device__ __forceinline__ void run_batch(const KernelArgs& a, const Batch& b, const TileCtx& t, const uint8_t* src,
+                                          uint32_t rec_addr, const int32_t* s_cnt, int lane) {
+    constexpr bool kWide = V == V_BCD16 || V == V_ZONED16;
+    constexpr bool kRead = V != V_GENERIC;
+    const int lim = t.active ? t.avail - a.start_off : -1;
+    for (int i = b.begin; i < b.end; i++) {
+        const NumOp op = ldc(a.nops + i);
+        const NumCall c = ldc(a.ncall + i);
+        const int run = op.run > 1 ? op.run : 1;
+        for (int r0 = 0; r0 < run; r0 += kRunU) {
+            bool ok[kRunU];
+            uint64_t q1[kRunU], q0[kRunU];
+#pragma unroll
+            for (int u = 0; u < kRunU; u++) {
+                const int eo = op.eo + (r0 + u) * op.run_stride;
+                ok[u] = r0 + u < run && eo + op.size <= lim;
+                q1[u] = q0[u] = 0;
+                if (kRead) {
+                    const uint32_t end = rec_addr + (ok[u] ? (uint32_t)eo : 0u) + op.size;
+                    q1[u] = img_le64_ending(src, end);
+                    if (kWide) q0[u] = img_le64_ending(src, end - 8);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kRunU; u++)
+                if (r0 + u < run) run_elem<V, W, kOdo>(a, op, a.nops + i, c, r0 + u, t, ok[u], q1[u], q0[u], s_cnt, lane);
+        }
+    }
+}
+
 // A group of N <= 4 numeric ops with the op records known at compile time (the specialised
 // kernels of cbx_jit.h): the interpreter's batch step with every descriptor field folded.
 template <int V, int W, bool kOdo, int N>
@@ -344,6 +414,20 @@ __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window&
         if (kGlobal) {
             if (b.odo) num_batch<V_GENERIC, 8, true, true>(a, b, t, src, rec_addr, s_cnt, lane);
             else num_batch<V_GENERIC, 8, false, true>(a, b, t, src, rec_addr, s_cnt, lane);
+            continue;
+        }
+        if (b.runs) {  // OCCURS runs: one generic-width loop per variant
+#define CBX_RUNS(ODO)                                                                                 \
+            switch (b.variant) {                                                                      \
+            case V_BCD8: run_batch<V_BCD8, 0, ODO>(a, b, t, src, rec_addr, s_cnt, lane); break;       \
+            case V_BCD16: run_batch<V_BCD16, 0, ODO>(a, b, t, src, rec_addr, s_cnt, lane); break;     \
+            case V_BIN8: run_batch<V_BIN8, 0, ODO>(a, b, t, src, rec_addr, s_cnt, lane); break;       \
+            case V_ZONED16: run_batch<V_ZONED16, 0, ODO>(a, b, t, src, rec_addr, s_cnt, lane); break; \
+            case V_FP: run_batch<V_FP, 0, ODO>(a, b, t, src, rec_addr, s_cnt, lane); break;           \
+            default: run_batch<V_GENERIC, 0, ODO>(a, b, t, src, rec_addr, s_cnt, lane); break;        \
+            }
+            if (b.odo) { CBX_RUNS(true) } else { CBX_RUNS(false) }
+#undef CBX_RUNS
             continue;
         }
         if (b.odo) {   // elements under OCCURS DEPENDING ON: one generic-width loop per variant

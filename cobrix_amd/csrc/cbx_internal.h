@@ -42,7 +42,7 @@ struct Batch {
     int32_t variant, width;           // Variant, output bytes per value (4, 8, 16)
     int32_t begin, end;               // NumOp range
     int32_t odo;                      // ops carry OCCURS DEPENDING ON conditions
-    int32_t reserved;
+    int32_t runs;                     // some op of the batch stands for a run of OCCURS elements
 };
 
 // Per-call output addresses of one numeric op (host-resolved column + slot bases).
