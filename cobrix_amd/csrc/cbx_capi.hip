@@ -539,7 +539,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.lds_rows = (a.lds_rows + 15) & ~15;
     a.lds_counts = ((int)P->harrays.size() * kWave * 4 + 15) & ~15;
     a.str_stage = S.max_str_items > 0 ? P->str_stage : 0;
-    a.lds_wave = a.lds_rows + a.lds_counts + a.str_stage + 16;
+    a.lds_wave = a.lds_rows + a.lds_counts + a.str_stage + (a.str_stage > 0 ? 4 * kWave : 16);   // + per-lane dump slots
     a.lds_wave = (a.lds_wave + 15) & ~15;
     a.fields = (const CBX_CONST Field*)P->d_fields;
     a.arrays = (const CBX_CONST cbx_array*)P->d_arrays;

@@ -1175,9 +1175,11 @@ CBX_HD StrSpan string_span32(int trim, const uint32_t w[8], int n, int size, Lut
 
 // UTF-8 bytes of the span into out[0, utf8_len); writes of bytes outside the span (and of the
 // unused 2nd / 3rd bytes of a character) go to `dump` instead of branching per lane.
+// width: the code page's widest UTF-8 encoding (1..3) -- only that many stores per byte.  `dump`
+// should be private to the lane (a shared dump address serialises the wave's LDS stores).
 template <typename LutFn>
 CBX_HD void string_write32(const uint32_t w[8], const StrSpan& s, uint8_t* out, uint8_t* dump, int size,
-                           bool multibyte, LutFn lut) {
+                           int width, LutFn lut) {
     int k = 0;
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++) {
@@ -1185,10 +1187,10 @@ CBX_HD void string_write32(const uint32_t w[8], const StrSpan& s, uint8_t* out, 
             const bool in = j >= s.begin && j < s.end;
             const uint32_t e = lut((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
             *(in ? out + k : dump) = (uint8_t)e;
-            if (multibyte) {
+            if (width > 1) {
                 const uint32_t l = (e >> 24) & 3u;
                 *(in && l > 1 ? out + k + 1 : dump) = (uint8_t)(e >> 8);
-                *(in && l > 2 ? out + k + 2 : dump) = (uint8_t)(e >> 16);
+                if (width > 2) *(in && l > 2 ? out + k + 2 : dump) = (uint8_t)(e >> 16);
                 k += in ? (int)l : 0;
             } else {
                 k += in ? 1 : 0;

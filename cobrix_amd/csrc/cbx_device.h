@@ -363,7 +363,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
     const uint8_t* sp_src = src + rec_addr + (uint32_t)op.eo;
     uint32_t* dst32 = (uint32_t*)(c.scratch + t.tile * (int64_t)c.tile_cap);   // 16-byte aligned region
     if ((int)tot <= a.str_stage) {
-        if (fast) string_write32(wb, sp, s_str + ex, s_str + a.str_stage, op.size, op.pad > 1, lutf);
+        if (fast) string_write32(wb, sp, s_str + ex, s_str + a.str_stage + 4 * lane, op.size, op.pad, lutf);
         else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
         wave_sync_lds();
         const uint32_t* s32 = (const uint32_t*)s_str;
@@ -373,7 +373,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
         uint8_t* dst = (uint8_t*)dst32 + ex;
         if (fast) {
             uint8_t dump[4];
-            string_write32(wb, sp, dst, dump, op.size, op.pad > 1, lutf);
+            string_write32(wb, sp, dst, dump, op.size, op.pad, lutf);
         } else {
             string_write(op.kind, sp_src, sp, dst, lutf);
         }

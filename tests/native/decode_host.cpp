@@ -59,7 +59,7 @@ extern "C" int cbxh_decode(const cbx_field* cf, const uint8_t* p, int n_avail, c
         StrSpan s2 = string_span32(f.trim, w, n, f.size, lutf);
         if (s2.begin != s.begin || s2.end != s.end || s2.utf8_len != s.utf8_len) return -1;
         uint8_t out2[4 * kStrFastBytes + 8], dump[4];
-        string_write32(w, s2, out2, dump, f.size, true, lutf);
+        string_write32(w, s2, out2, dump, f.size, 3, lutf);
         for (int i = 0; i < s.utf8_len; i++) if (out2[i] != sbuf[i]) return -1;
     }
     *slen = s.utf8_len;
