@@ -1143,15 +1143,22 @@ CBX_HD uint32_t clz32(uint32_t x) { return (uint32_t)__builtin_clz(x); }
 CBX_HD uint32_t popc32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 CBX_HD uint32_t bits_below(int k) { return k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u); }
 
-// Trimmed span + UTF-8 length (StringDecoders.decodeEbcdicString / decodeAsciiString +
-// StringTools.trim*) of the first n (<= size <= 32) bytes held in w.
+// LUT entries of the size (<= 32) bytes held in w (one LDS lookup per byte, shared by the span
+// and the write).
 template <typename LutFn>
-CBX_HD StrSpan string_span32(int trim, const uint32_t w[8], int n, int size, LutFn lut) {
+CBX_HD void lut_entries32(const uint32_t w[8], int size, LutFn lut, uint32_t ev[kStrFastBytes]) {
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++) ev[j] = j < size ? lut((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) : 0u;
+}
+
+// Trimmed span + UTF-8 length (StringDecoders.decodeEbcdicString / decodeAsciiString +
+// StringTools.trim*) of the first n (<= size <= 32) bytes, from their LUT entries.
+CBX_HD StrSpan string_span32e(int trim, const uint32_t ev[kStrFastBytes], int n, int size) {
     uint32_t keep = 0, m2 = 0, m3 = 0;   // bit j: byte j not trimmable / 2-byte / 3-byte UTF-8
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++) {
         if (j < size) {
-            const uint32_t e = lut((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            const uint32_t e = ev[j];
             const uint32_t l = (e >> 24) & 3u;
             const uint32_t bit = 1u << j;
             keep |= (e >> 31) ? 0u : bit;
@@ -1173,19 +1180,25 @@ CBX_HD StrSpan string_span32(int trim, const uint32_t w[8], int n, int size, Lut
     return s;
 }
 
+template <typename LutFn>
+CBX_HD StrSpan string_span32(int trim, const uint32_t w[8], int n, int size, LutFn lut) {
+    uint32_t ev[kStrFastBytes];
+    lut_entries32(w, size, lut, ev);
+    return string_span32e(trim, ev, n, size);
+}
+
 // UTF-8 bytes of the span into out[0, utf8_len); writes of bytes outside the span (and of the
 // unused 2nd / 3rd bytes of a character) go to `dump` instead of branching per lane.
 // width: the code page's widest UTF-8 encoding (1..3) -- only that many stores per byte.  `dump`
 // should be private to the lane (a shared dump address serialises the wave's LDS stores).
-template <typename LutFn>
-CBX_HD void string_write32(const uint32_t w[8], const StrSpan& s, uint8_t* out, uint8_t* dump, int size,
-                           int width, LutFn lut) {
+CBX_HD void string_write32e(const uint32_t ev[kStrFastBytes], const StrSpan& s, uint8_t* out, uint8_t* dump, int size,
+                            int width) {
     int k = 0;
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++) {
         if (j < size) {
             const bool in = j >= s.begin && j < s.end;
-            const uint32_t e = lut((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            const uint32_t e = ev[j];
             *(in ? out + k : dump) = (uint8_t)e;
             if (width > 1) {
                 const uint32_t l = (e >> 24) & 3u;
@@ -1197,6 +1210,14 @@ CBX_HD void string_write32(const uint32_t w[8], const StrSpan& s, uint8_t* out, 
             }
         }
     }
+}
+
+template <typename LutFn>
+CBX_HD void string_write32(const uint32_t w[8], const StrSpan& s, uint8_t* out, uint8_t* dump, int size,
+                           int width, LutFn lut) {
+    uint32_t ev[kStrFastBytes];
+    lut_entries32(w, size, lut, ev);
+    string_write32e(ev, s, out, dump, size, width);
 }
 
 }  // namespace cbx

@@ -138,7 +138,8 @@ __device__ __forceinline__ uint32_t str_lut(int kind, const uint32_t* s_lut, uin
 // Elements of at most kStrFastBytes EBCDIC/ASCII bytes keep their bytes in `w` (register path).
 __device__ __forceinline__ StrSpan sop_span(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
                                             const TileCtx& t, const int32_t* s_cnt, int lane, const uint8_t* src,
-                                            uint32_t rec_addr, const uint32_t* s_lut, bool& ok, bool fast, uint32_t w[8]) {
+                                            uint32_t rec_addr, const uint32_t* s_lut, bool& ok, bool fast,
+                                            uint32_t ev[kStrFastBytes]) {
     bool el = t.active && (op.segment < 0 || op.segment == t.seg);
     if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
     const int o = a.start_off + op.eo;
@@ -146,8 +147,10 @@ __device__ __forceinline__ StrSpan sop_span(const KernelArgs& a, const StrOp& op
     const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
     auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
     if (fast) {
+        uint32_t w[8];
         img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
-        return string_span32(op.trim, w, n, op.size, lutf);
+        lut_entries32(w, op.size, lutf, ev);
+        return string_span32e(op.trim, ev, n, op.size);
     }
     StrSpan sp{0, 0, 0};
     if (ok) sp = string_span(op.kind, op.trim, src + rec_addr + (uint32_t)op.eo, n, lutf);
@@ -348,8 +351,8 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
                                             const uint32_t* s_lut, uint8_t* s_str, int lane) {
     const bool fast = sop_fast(op, global);
     bool ok;
-    uint32_t wb[8];
-    const StrSpan sp = sop_span(a, op, opp, t, s_cnt, lane, src, rec_addr, s_lut, ok, fast, wb);
+    uint32_t ev[kStrFastBytes];
+    const StrSpan sp = sop_span(a, op, opp, t, s_cnt, lane, src, rec_addr, s_lut, ok, fast, ev);
     uint32_t tot;
     const uint32_t ex = wave_excl_scan32((uint32_t)sp.utf8_len, lane, tot);
     if (a.mode == 1) {
@@ -363,7 +366,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
     const uint8_t* sp_src = src + rec_addr + (uint32_t)op.eo;
     uint32_t* dst32 = (uint32_t*)(c.scratch + t.tile * (int64_t)c.tile_cap);   // 16-byte aligned region
     if ((int)tot <= a.str_stage) {
-        if (fast) string_write32(wb, sp, s_str + ex, s_str + a.str_stage + 4 * lane, op.size, op.pad, lutf);
+        if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + 4 * lane, op.size, op.pad);
         else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
         wave_sync_lds();
         const uint32_t* s32 = (const uint32_t*)s_str;
@@ -373,7 +376,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
         uint8_t* dst = (uint8_t*)dst32 + ex;
         if (fast) {
             uint8_t dump[4];
-            string_write32(wb, sp, dst, dump, op.size, op.pad, lutf);
+            string_write32e(ev, sp, dst, dump, op.size, op.pad);
         } else {
             string_write(op.kind, sp_src, sp, dst, lutf);
         }
