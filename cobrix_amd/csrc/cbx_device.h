@@ -369,8 +369,10 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
         if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + 4 * lane, op.size, op.pad);
         else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
         wave_sync_lds();
-        const uint32_t* s32 = (const uint32_t*)s_str;
-        for (int q = lane; 4 * q < (int)tot; q += kWave) gp(dst32)[q] = s32[q];
+        // 16-byte pieces: the staging area and the scratch region are 16-byte aligned and the
+        // region (a multiple of 16 bytes >= the tile's bound) holds the rounded-up total
+        const u32x4* s128 = (const u32x4*)s_str;
+        for (int q = lane; 16 * q < (int)tot; q += kWave) gp((u32x4*)dst32)[q] = s128[q];
         wave_sync_lds();
     } else if (ok) {
         uint8_t* dst = (uint8_t*)dst32 + ex;
