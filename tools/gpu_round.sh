@@ -9,4 +9,4 @@ rc=$?; tail -3 gpurun_out/gpu_tests_$TAG.log
 timeout -k 10 300 python bench.py "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 rc=$?; cat gpurun_out/bench_$TAG.json
 [ $rc -eq 0 ] || { echo "bench failed rc=$rc"; tail -20 gpurun_out/bench_$TAG.err; exit $rc; }
-bash tools/gpu_profile.sh $TAG 5000000
+bash tools/gpu_profile.sh $TAG 50000000
