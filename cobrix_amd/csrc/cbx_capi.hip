@@ -539,8 +539,16 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.lds_rows = (a.lds_rows + 15) & ~15;
     a.lds_counts = ((int)P->harrays.size() * kWave * 4 + 15) & ~15;
     a.str_stage = S.max_str_items > 0 ? P->str_stage : 0;
-    a.lds_wave = a.lds_rows + a.lds_counts + a.str_stage + (a.str_stage > 0 ? 4 * kWave : 16);   // + per-lane dump slots
-    a.lds_wave = (a.lds_wave + 15) & ~15;
+    // per-lane dump slots for the branch-free string stores (a shared slot serialises the wave's
+    // LDS stores) -- unless the extra 4 * kWave bytes per wave cost a resident workgroup per CU
+    // (wide windowed layouts sit close to the LDS limit; C5 decode 49.7 -> 62.1 ms with them)
+    const int lds_base = a.lds_rows + a.lds_counts + a.str_stage;
+    auto lds_blocks = [](int per_wave) {
+        return (160 * 1024) / (1024 + kWavesPerBlock * ((per_wave + 15) & ~15));
+    };
+    const bool lane_dump = a.str_stage > 0 && lds_blocks(lds_base + 4 * kWave) >= lds_blocks(lds_base + 16);
+    a.dump_stride = lane_dump ? 4 : 0;
+    a.lds_wave = (lds_base + (lane_dump ? 4 * kWave : 16) + 15) & ~15;
     a.fields = (const CBX_CONST Field*)P->d_fields;
     a.arrays = (const CBX_CONST cbx_array*)P->d_arrays;
     a.n_arrays = (int)P->harrays.size();

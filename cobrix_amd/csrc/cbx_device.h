@@ -366,7 +366,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
     const uint8_t* sp_src = src + rec_addr + (uint32_t)op.eo;
     uint32_t* dst32 = (uint32_t*)(c.scratch + t.tile * (int64_t)c.tile_cap);   // 16-byte aligned region
     if ((int)tot <= a.str_stage) {
-        if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + 4 * lane, op.size, op.pad);
+        if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + a.dump_stride * lane, op.size, op.pad);
         else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
         wave_sync_lds();
         // 16-byte pieces: the staging area and the scratch region are 16-byte aligned and the

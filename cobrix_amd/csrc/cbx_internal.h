@@ -136,6 +136,7 @@ struct KernelArgs {
     int32_t lds_counts;        // OCCURS element counts
     int32_t str_stage;         // string payload staging bytes
     int32_t lds_wave;          // total per wave
+    int32_t dump_stride;       // bytes between the lanes' string dump slots (4, or 0 = one shared slot)
     uint64_t* stamps;          // diagnostic build (CBX_STAMPS) only: per-segment wave-cycle sums
 };
 
