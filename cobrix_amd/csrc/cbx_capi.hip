@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "cbx_kernels.hip"
+#include "cbx_text.h"
 
 using namespace cbx;
 
@@ -961,5 +962,105 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     }
     *n_records = total;
     if (total > capacity) return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(total));
+    return CBX_OK;
+}
+
+// Text framing (is_text): cbx_text.h.  Needs d_data readable up to n_bytes; records past n_bytes
+// (the reference's zero fill, cbx_text.h) require the caller's buffer to hold zeros up to
+// *virtual_bytes (at most n_bytes + record_size + 2).
+extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t record_size, int64_t* d_rec_off,
+                              int32_t* d_rec_len, int64_t capacity, int64_t* n_records, int64_t* virtual_bytes,
+                              void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!d_data || n_bytes < 0 || record_size < 1 || !n_records || !virtual_bytes || capacity < 0)
+        return fail(CBX_E_ARGUMENT, "cbx_frame_text: invalid arguments");
+    *n_records = 0;
+    *virtual_bytes = 0;
+    if (n_bytes == 0) return CBX_OK;   // hasNext is false on an empty stream (TextRecordExtractor.scala:33)
+    const int64_t M = (int64_t)record_size + 2;   // maxRecordSize (TextRecordExtractor.scala:28)
+    const int64_t nch = (n_bytes + kTextChunk - 1) / kTextChunk;
+    // pass 1: LF counts -> bases -> positions
+    auto scan = [&](uint32_t* cnt, int64_t n, int64_t* out, int64_t* sums) {
+        const int64_t nb = (n + kScanTile - 1) / kScanTile;
+        hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)cnt, n, sums);
+        hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, sums, nb);
+        hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)cnt, n,
+                           (const int64_t*)sums, out);
+    };
+    auto sums_len = [](int64_t n) { return (n + kScanTile - 1) / kScanTile; };
+    uint32_t* d_cnt = nullptr;
+    int64_t* d_base = nullptr;
+    int64_t* d_sums = nullptr;
+    HIP_CHECK(hipMallocAsync((void**)&d_cnt, sizeof(uint32_t) * (nch + 1), st));
+    HIP_CHECK(hipMallocAsync((void**)&d_base, sizeof(int64_t) * (nch + 1), st));
+    HIP_CHECK(hipMallocAsync((void**)&d_sums, sizeof(int64_t) * sums_len(nch + 1), st));
+    HIP_CHECK(hipMemsetAsync(d_cnt + nch, 0, sizeof(uint32_t), st));
+    const unsigned cblocks = (unsigned)((nch + 255) / 256);
+    hipLaunchKernelGGL(text_lf_kernel, dim3(cblocks), dim3(256), 0, st, d_data, n_bytes, nch, 0, d_cnt,
+                       (const int64_t*)nullptr, (int64_t*)nullptr);
+    scan(d_cnt, nch + 1, d_base, d_sums);
+    int64_t n_lf = 0;
+    HIP_CHECK(hipMemcpyAsync(&n_lf, d_base + nch, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    int64_t* d_lf = nullptr;
+    HIP_CHECK(hipMallocAsync((void**)&d_lf, sizeof(int64_t) * (n_lf + 1), st));
+    hipLaunchKernelGGL(text_lf_kernel, dim3(cblocks), dim3(256), 0, st, d_data, n_bytes, nch, 1, d_cnt,
+                       (const int64_t*)d_base, d_lf);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipFreeAsync(d_cnt, st));
+    HIP_CHECK(hipFreeAsync(d_base, st));
+    HIP_CHECK(hipFreeAsync(d_sums, st));
+    // pass 2: records per segment (n_lf line-ended segments + the tail) -> bases -> records
+    const int64_t nseg = n_lf + 1;
+    uint32_t* d_scnt = nullptr;
+    int64_t* d_sbase = nullptr;   // [nseg + 1] bases, then the tail's final start
+    HIP_CHECK(hipMallocAsync((void**)&d_scnt, sizeof(uint32_t) * (nseg + 1), st));
+    HIP_CHECK(hipMallocAsync((void**)&d_sbase, sizeof(int64_t) * (nseg + 2), st));
+    HIP_CHECK(hipMallocAsync((void**)&d_sums, sizeof(int64_t) * sums_len(nseg + 1), st));
+    HIP_CHECK(hipMemsetAsync(d_scnt + nseg, 0, sizeof(uint32_t), st));
+    const unsigned sblocks = (unsigned)((nseg + 255) / 256);
+    hipLaunchKernelGGL(text_seg_kernel, dim3(sblocks), dim3(256), 0, st, d_data, n_bytes, (const int64_t*)d_lf, n_lf,
+                       M, 0, d_scnt, (const int64_t*)nullptr, (int64_t*)nullptr, (int32_t*)nullptr, d_sbase + nseg + 1);
+    scan(d_scnt, nseg + 1, d_sbase, d_sums);
+    int64_t hv[2] = {0, 0};   // body records, tail final start
+    HIP_CHECK(hipMemcpyAsync(hv, d_sbase + nseg, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    const int64_t body = hv[0], tail_start = hv[1];
+    int rc = CBX_OK;
+    if (body > capacity) {
+        rc = fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(body));
+    } else {
+        hipLaunchKernelGGL(text_seg_kernel, dim3(sblocks), dim3(256), 0, st, d_data, n_bytes, (const int64_t*)d_lf, n_lf,
+                           M, 1, d_scnt, (const int64_t*)d_sbase, d_rec_off, d_rec_len, (int64_t*)nullptr);
+        HIP_CHECK(hipGetLastError());
+    }
+    HIP_CHECK(hipFreeAsync(d_scnt, st));
+    HIP_CHECK(hipFreeAsync(d_sbase, st));
+    HIP_CHECK(hipFreeAsync(d_sums, st));
+    HIP_CHECK(hipFreeAsync(d_lf, st));
+    if (rc) { HIP_CHECK(hipStreamSynchronize(st)); return rc; }
+    // the virtual length: the window that first reached past the data (record start s_k, the
+    // first with s_k + M >= n_bytes) was marked full (ensureBytesRead, :98-107)
+    const int64_t k = std::min<int64_t>(body, M + 1);
+    std::vector<int64_t> last(k);
+    if (k > 0) HIP_CHECK(hipMemcpyAsync(last.data(), d_rec_off + (body - k), sizeof(int64_t) * k, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    int64_t s_k = -1;
+    for (int64_t i = 0; i < k && s_k < 0; i++)
+        if (last[i] + M >= n_bytes && last[i] < n_bytes) s_k = last[i];
+    if (s_k < 0 && tail_start < n_bytes && tail_start + M >= n_bytes) s_k = tail_start;
+    const int64_t vlen = s_k >= 0 ? std::max(n_bytes, s_k + M) : n_bytes;
+    int64_t total = body;
+    if (tail_start < vlen) {   // the rest of the stream: the last record (:62-66, hasNext :33)
+        if (body + 1 > capacity) return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(body + 1));
+        const int64_t h_off = tail_start;
+        const int32_t h_len = (int32_t)(vlen - tail_start);
+        HIP_CHECK(hipMemcpyAsync(d_rec_off + body, &h_off, sizeof(int64_t), hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(d_rec_len + body, &h_len, sizeof(int32_t), hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        total++;
+    }
+    *n_records = total;
+    *virtual_bytes = vlen;
     return CBX_OK;
 }

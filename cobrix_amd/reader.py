@@ -44,6 +44,7 @@ class ReaderParameters:
     variable_size_occurs: bool = False
     record_length: Optional[int] = None
     is_record_sequence: bool = False
+    is_text: bool = False                          # LF / CRLF separated records (TextRecordExtractor)
     is_rdw_big_endian: bool = False
     is_rdw_part_rec_length: bool = False
     rdw_adjustment: int = 0
@@ -345,6 +346,23 @@ class VarLenNestedReader(_BaseReader):
         r.file_footer_bytes = p.file_end_offset
         return r
 
+    def frame_text(self, d_data, n_bytes: int, stream=None):
+        """GPU text framing (TextRecordExtractor.scala:26-108) -> (rec_off, rec_len, virtual_bytes).
+
+        Records may reach past n_bytes up to virtual_bytes (the reference's zero-filled window):
+        d_data must hold zeros there (see `decode`)."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream()
+        cap = n_bytes + 2
+        off = torch.empty(cap, dtype=torch.int64, device=d_data.device)
+        ln = torch.empty(cap, dtype=torch.int32, device=d_data.device)
+        n = ctypes.c_int64(0)
+        vb = ctypes.c_int64(0)
+        N.check(N.load().cbx_frame_text(d_data.data_ptr(), n_bytes, self.copybook.record_size, off.data_ptr(),
+                                         ln.data_ptr(), cap, ctypes.byref(n), ctypes.byref(vb),
+                                         ctypes.c_void_p(st.cuda_stream)))
+        return off[: n.value], ln[: n.value], vb.value
+
     def frame(self, d_data, n_bytes: int, seeds: Optional[Sequence[int]] = None, stream=None):
         """GPU RDW walk -> (rec_off, rec_len) device tensors of the valid records."""
         torch = _torch()
@@ -383,6 +401,13 @@ class VarLenNestedReader(_BaseReader):
 
     def decode(self, data: bytes, seeds: Optional[Sequence[int]] = None, first_record_id: int = 0) -> DecodedBatch:
         torch = _torch()
+        if self.params.is_text:
+            # zero tail for records past the data (the reference's zero-filled read window)
+            t = torch.zeros(len(data) + self.copybook.record_size + 2 + 16, dtype=torch.uint8, device="cuda")
+            if len(data):
+                t[: len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+            off, ln, vb = self.frame_text(t, len(data))
+            return self.decode_device(t, vb, off, ln, first_record_id)
         t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda") if len(data) else torch.zeros(16, dtype=torch.uint8, device="cuda")
         off, ln = self.frame(t, len(data), seeds)
         return self.decode_device(t, len(data), off, ln, first_record_id)

@@ -248,6 +248,19 @@ int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, 
                   const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len,
                   int64_t capacity, int64_t* n_records, void* stream);
 
+/* Text record framing (is_text = true) on the GPU: replaces TextRecordExtractor
+ * (cobol-parser/.../reader/extractors/raw/TextRecordExtractor.scala:26-108, chosen by
+ * VarLenNestedReader.scala:69-70).  Records end at LF or CR LF (payload without the line
+ * ending) inside a window of record_size + 2 bytes (record_size = copybook.getRecordSize); a
+ * window without one gives a forced record.  Writes payload offsets/lengths in file order.
+ * *virtual_bytes receives the stream length the reference decodes against: its read helper
+ * treats a short last read as a full window of zero bytes, so records may reach past n_bytes
+ * (by at most record_size + 2); the buffer must hold zeros there before records are decoded
+ * (pass *virtual_bytes as n_bytes to cbx_decode_var). */
+int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t record_size, int64_t* d_rec_off,
+                   int32_t* d_rec_len, int64_t capacity, int64_t* n_records, int64_t* virtual_bytes,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1163,3 +1163,59 @@ int ora_extract_var(const ora_node* nodes, int32_t root, const ora_handler* hand
     }
     return 0;
 }
+
+/* Text records (is_text): TextRecordExtractor (CP/reader/extractors/raw/TextRecordExtractor.scala:26-108)
+ * restated over a SimpleStream of n_bytes (isEndOfStream = offset >= size, SimpleStream.scala:28;
+ * next(k) returns min(k, remaining) bytes).  The window buffer is simulated literally, including
+ * ensureBytesRead (:98-107) setting bytesSize to the full window after a short read: bytes past
+ * the data then read as the buffer's zero fill.  Records are written as (offset, payload length)
+ * in stream coordinates; *virtual_bytes = the end of the last window. */
+int64_t ora_frame_text(const uint8_t* data, int64_t n_bytes, int32_t record_size, int64_t* off, int32_t* len,
+                       int64_t cap, int64_t* virtual_bytes) {
+    const int64_t M = (int64_t)record_size + 2;   /* maxRecordSize (:28) */
+    int64_t base = 0;      /* stream offset of bytes(0) */
+    int64_t size = 0;      /* bytesSize */
+    int64_t pos = 0;       /* inputStream.offset */
+    int64_t vend = 0;      /* end of the filled window */
+    int32_t last_footer = 1;   /* lastFooterSize (:31) */
+    int64_t k = 0;
+#define TB(i) ((base + (i)) < n_bytes ? data[base + (i)] : (uint8_t)0)
+    while (pos < n_bytes || size > 0) {   /* hasNext (:33) */
+        /* ensureBytesRead(maxRecordSize) (:98-107) */
+        const int64_t want = M - size;
+        if (want > 0) {
+            const int64_t got = (n_bytes - pos) < want ? (n_bytes - pos) : want;
+            if (got > 0) {
+                pos += got;
+                size = M;
+                if (base + M > vend) vend = base + M;
+            }
+        }
+        /* findEol (:46-95); buffer bytes past bytesSize are zero (fill at :89) */
+        int64_t rec_len = 0, payload = 0;
+        for (int64_t i = 0; rec_len == 0 && i < size; i++) {
+            const uint8_t b = (base + i) < vend ? TB(i) : 0;
+            if (b == 0x0D) {
+                if (i + 1 < M && ((base + i + 1) < vend && i + 1 < size ? TB(i + 1) : 0) == 0x0A) {
+                    rec_len = i + 2;
+                    payload = i;
+                }
+            } else if (b == 0x0A) {
+                rec_len = i + 1;
+                payload = i;
+            }
+        }
+        if (rec_len == 0) {
+            if (pos >= n_bytes) { rec_len = size; payload = size; }                       /* last record */
+            else { rec_len = size - last_footer; payload = size - last_footer; }         /* no line break */
+        }
+        if (k < cap) { off[k] = base; len[k] = (int32_t)payload; }
+        k++;
+        base += rec_len;
+        size -= rec_len;
+        last_footer = (int32_t)(rec_len - payload);
+    }
+#undef TB
+    *virtual_bytes = vend > n_bytes ? vend : n_bytes;
+    return k;
+}

@@ -103,6 +103,8 @@ int ora_decode_fixed(const ora_node* nodes, int32_t root, const ora_handler* han
 /* RDW framing (RecordHeaderParserRDW.getRecordMetadata + VRLRecordReader.fetchRecordUsingRdwHeaders).
  * Emits payload (offset, length) per valid record. Returns number of records, <0 on error:
  * -1 capacity, -2 zero-length RDW, -3 RDW too big. err_offset receives the failing header offset. */
+int64_t ora_frame_text(const uint8_t* data, int64_t n_bytes, int32_t record_size, int64_t* off, int32_t* len,
+                       int64_t cap, int64_t* virtual_bytes);
 int64_t ora_frame_rdw(const uint8_t* data, int64_t n_bytes, int32_t big_endian, int32_t adjustment,
                       int32_t file_header_bytes, int32_t file_footer_bytes,
                       int64_t* rec_off, int32_t* rec_len, int64_t cap, int64_t* err_offset);

@@ -81,6 +81,8 @@ def lib():
         L.ora_frame_rdw.argtypes = [P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.c_int32, P, P, ctypes.c_int64, P]
         L.ora_frame_rdw.restype = ctypes.c_int64
+        L.ora_frame_text.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, P, ctypes.c_int64, P]
+        L.ora_frame_text.restype = ctypes.c_int64
         L.ora_sparse_index.argtypes = [P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, P, P, P, P,
                                        ctypes.c_int64]
@@ -308,6 +310,19 @@ def frame_rdw(data: bytes, big_endian: bool = False, adjustment: int = 0, file_h
     if n < 0:
         raise RuntimeError(f"RDW framing error {n} at offset {eo.value}")
     return off[:n].copy(), ln[:n].copy()
+
+
+def frame_text(data: bytes, record_size: int) -> Tuple[np.ndarray, np.ndarray, int]:
+    """TextRecordExtractor restated (cobrix_oracle.c ora_frame_text): (offsets, payload lengths,
+    virtual stream length -- records may reach past len(data) into the reference's zero fill)."""
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    cap = len(data) + 2
+    off = np.zeros(cap, np.int64)
+    ln = np.zeros(cap, np.int32)
+    vb = ctypes.c_int64(0)
+    n = lib().ora_frame_text(_ptr(buf), len(data), record_size, _ptr(off), _ptr(ln), cap, ctypes.byref(vb))
+    assert n <= cap
+    return off[:n].copy(), ln[:n].copy(), vb.value
 
 
 def sparse_index(data: bytes, big_endian: bool = False, adjustment: int = 0,
