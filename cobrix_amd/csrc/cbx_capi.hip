@@ -995,7 +995,7 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     HIP_CHECK(hipMallocAsync((void**)&d_base, sizeof(int64_t) * (nch + 1), st));
     HIP_CHECK(hipMallocAsync((void**)&d_sums, sizeof(int64_t) * sums_len(nch + 1), st));
     HIP_CHECK(hipMemsetAsync(d_cnt + nch, 0, sizeof(uint32_t), st));
-    const unsigned cblocks = (unsigned)((nch + 255) / 256);
+    const unsigned cblocks = (unsigned)((nch + 3) / 4);   // 4 waves per block, one chunk each
     hipLaunchKernelGGL(text_lf_kernel, dim3(cblocks), dim3(256), 0, st, d_data, n_bytes, nch, 0, d_cnt,
                        (const int64_t*)nullptr, (int64_t*)nullptr);
     scan(d_cnt, nch + 1, d_base, d_sums);

@@ -14,53 +14,70 @@
 // (closed form below).  A CR counts as part of the line ending only when it lies inside the
 // record that ends at the LF, so the line-ending length depends on where the previous segment's
 // last record started: a segment walks back over the run of long segments before it (none in
-// ordinary text).  Passes: LF count per 256-byte chunk -> scan -> LF positions -> per-segment
+// ordinary text).  Passes: LF count per 16 KiB chunk (one wave each) -> scan -> LF positions -> per-segment
 // record counts -> scan -> records; the final record after the last LF (its length depends on
 // the virtual length) is settled by the host.
 #pragma once
 
 namespace cbx {
 
-constexpr int kTextChunk = 256;   // bytes per thread in the LF passes
+constexpr int kTextChunk = 16384;   // bytes per wave in the LF passes (64 lanes x 16 B x 16 steps)
 
-__device__ __forceinline__ int lf_in_word(uint32_t w) {
-    const uint32_t x = w ^ 0x0A0A0A0Au;   // LF bytes -> 0
-    int c = 0;
+__device__ __forceinline__ uint32_t lf_mask16(const uint8_t* p, int64_t i, int64_t n, bool vec) {
+    // bit b set when byte i + b is an LF (bytes at or past n never are)
+    uint32_t m = 0;
+    if (vec && i + 16 <= n) {
+        const uint4 v = *(const uint4*)(p + i);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int b = 0; b < 4; b++) c += ((x >> (8 * b)) & 0xFFu) == 0u;
-    return c;
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) m |= (((w[k] >> (8 * b)) & 0xFFu) == 0x0Au ? 1u : 0u) << (4 * k + b);
+    } else {
+        for (int b = 0; b < 16 && i + b < n; b++) m |= (p[i + b] == 0x0A ? 1u : 0u) << b;
+    }
+    return m;
 }
 
-// mode 0: LF count of the thread's chunk into count[t]; mode 1: LF positions at lf[base[t]...]
+// One wave per kTextChunk-byte chunk, lanes on consecutive 16-byte groups (coalesced).
+// mode 0: LF count of the chunk into count[chunk]; mode 1: LF positions in file order at
+// lf[base[chunk]...] (wave prefix sums of the lanes' counts per step).
 __global__ __launch_bounds__(256) void text_lf_kernel(const uint8_t* __restrict__ data, int64_t n, int64_t n_chunks,
                                                       int mode, uint32_t* __restrict__ count,
                                                       const int64_t* __restrict__ base, int64_t* __restrict__ lf) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_chunks) return;
-    const int64_t b0 = t * kTextChunk, b1 = b0 + kTextChunk < n ? b0 + kTextChunk : n;
-    const bool words = ((uintptr_t)data & 3u) == 0;
+    const int lane = threadIdx.x & 63;
+    const int64_t chunk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (chunk >= n_chunks) return;
+    const bool vec = ((uintptr_t)data & 15u) == 0;
+    const int64_t c0 = chunk * kTextChunk;
     uint32_t c = 0;
-    int64_t out = mode ? base[t] : 0;
-    int64_t i = b0;
-    if (words) {
-        for (; i + 4 <= b1; i += 4) {
-            const uint32_t w = *(const uint32_t*)(data + i);
-            if (mode == 0) {
-                c += (uint32_t)lf_in_word(w);
-            } else if (lf_in_word(w)) {
+    int64_t out = mode ? base[chunk] : 0;
+    for (int step = 0; step < kTextChunk / (64 * 16); step++) {
+        const int64_t i = c0 + (int64_t)step * 1024 + lane * 16;
+        if (c0 + (int64_t)step * 1024 >= n) break;   // wave-uniform
+        uint32_t m = i < n ? lf_mask16(data, i, n, vec) : 0u;
+        const uint32_t k = (uint32_t)__popc(m);
+        if (mode == 0) { c += k; continue; }
+        uint32_t pre = k;   // inclusive wave scan
 #pragma unroll
-                for (int b = 0; b < 4; b++)
-                    if (((w >> (8 * b)) & 0xFFu) == 0x0Au) lf[out++] = i + b;
-            }
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(pre, d, 64);
+            if (lane >= d) pre += y;
         }
-    }
-    for (; i < b1; i++) {
-        if (data[i] == 0x0A) {
-            if (mode == 0) c++;
-            else lf[out++] = i;
+        const uint32_t tot = __shfl(pre, 63, 64);
+        int64_t o = out + (pre - k);
+        while (m) {
+            const int b = __ffs(m) - 1;
+            lf[o++] = i + b;
+            m &= m - 1;
         }
+        out += tot;
     }
-    if (mode == 0) count[t] = c;
+    if (mode == 0) {
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+        if (lane == 0) count[chunk] = c;
+    }
 }
 
 __device__ __forceinline__ int64_t text_ceil_div(int64_t a, int64_t b) { return a <= 0 ? 0 : (a + b - 1) / b; }
