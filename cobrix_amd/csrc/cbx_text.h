@@ -13,8 +13,7 @@
 // a longer one starts with forced records whose lengths follow from the previous line ending
 // (closed form below).  A CR counts as part of the line ending only when it lies inside the
 // record that ends at the LF, so the line-ending length depends on where the previous segment's
-// last record started: a segment walks back over the run of long segments before it (none in
-// ordinary text).  Passes: LF count per 16 KiB chunk (one wave each) -> scan -> LF positions -> per-segment
+// last record started: a segment walks back only while that dependence is real (rare).  Passes: LF count per 16 KiB chunk (one wave each) -> scan -> LF positions -> per-segment
 // record counts -> scan -> records; the final record after the last LF (its length depends on
 // the virtual length) is settled by the host.
 #pragma once
@@ -96,16 +95,25 @@ __device__ __forceinline__ int text_eol_len(const uint8_t* data, int64_t p, int6
     return (p - 1 >= start && data[p - 1] == 0x0D) ? 2 : 1;
 }
 
-// Line-ending length of the EOL before segment j (1 before the first record, :31).
+// Line-ending length of the EOL that ends segment i, given the line-ending length f before it.
+__device__ __forceinline__ int text_seg_out(const uint8_t* data, const int64_t* lf, int64_t i, int64_t M, int f) {
+    const int64_t s0 = i > 0 ? lf[i - 1] + 1 : 0;
+    if (lf[i] - s0 < M) return text_eol_len(data, lf[i], s0);
+    int64_t c;
+    return text_eol_len(data, lf[i], text_final_start(s0, lf[i], M, f, &c));
+}
+
+// Line-ending length of the EOL before segment j (1 before the first record, :31).  Walks back
+// only while a segment's result depends on its input (a long segment whose last record starts
+// right at a CR): short segments and almost all long ones map both inputs to the same length.
 __device__ int text_footer_before(const uint8_t* data, const int64_t* lf, int64_t j, int64_t M) {
     int64_t k = j - 1;
-    while (k >= 0 && lf[k] - (k > 0 ? lf[k - 1] + 1 : 0) >= M) k--;
-    int f = k < 0 ? 1 : text_eol_len(data, lf[k], k > 0 ? lf[k - 1] + 1 : 0);
-    for (int64_t i = k + 1; i < j; i++) {
-        int64_t c;
-        const int64_t fs = text_final_start(i > 0 ? lf[i - 1] + 1 : 0, lf[i], M, f, &c);
-        f = text_eol_len(data, lf[i], fs);
+    int f = 1;
+    for (; k >= 0; k--) {
+        const int a = text_seg_out(data, lf, k, M, 1), b = text_seg_out(data, lf, k, M, 2);
+        if (a == b) { f = a; break; }
     }
+    for (int64_t i = k + 1; i < j; i++) f = text_seg_out(data, lf, i, M, f);
     return f;
 }
 
@@ -121,13 +129,7 @@ __global__ __launch_bounds__(256) void text_seg_kernel(const uint8_t* __restrict
     if (j > n_lf) return;
     const int64_t s0 = j > 0 ? lf[j - 1] + 1 : 0;
     const bool tail = j == n_lf;
-    // fast path: a short segment after a short segment needs no walk back
-    int f;
-    if (j == 0) f = 1;
-    else {
-        const int64_t sp = j > 1 ? lf[j - 2] + 1 : 0;
-        f = lf[j - 1] - sp < M ? text_eol_len(data, lf[j - 1], sp) : text_footer_before(data, lf, j, M);
-    }
+    const int f = text_footer_before(data, lf, j, M);
     int64_t c, fs;
     if (!tail) {
         fs = text_final_start(s0, lf[j], M, f, &c);

@@ -120,6 +120,20 @@ class TestGpuText:
         np.testing.assert_array_equal(go, oo)
         np.testing.assert_array_equal(gl, ol)
 
+    @pytest.mark.parametrize("sep", [b"\n", b"\r\n"])
+    def test_all_lines_longer_than_window(self, sep):
+        """Every line needs forced records, so every segment's line ending depends on the previous
+        one's (bounded walk back; a quadratic walk would time out here)."""
+        rng = np.random.default_rng(12)
+        lines = [bytes(rng.integers(65, 90, size=int(rng.integers(23, 90)), dtype=np.uint8)) for _ in range(60_000)]
+        lines[::97] = [b"\r" * 23] * len(lines[::97])
+        data = sep.join(lines)
+        go, gl, gv = self._frame(data, 20)
+        oo, ol, ov = O.frame_text(data, 20)
+        assert gv == ov
+        np.testing.assert_array_equal(go, oo)
+        np.testing.assert_array_equal(gl, ol)
+
     def test_reference_ascii_text_file_rows(self):
         from cobrix_amd.reader import ReaderParameters, VarLenNestedReader
         rd = VarLenNestedReader(T01_COPYBOOK, ReaderParameters(is_ebcdic=False, is_text=True,
