@@ -1016,28 +1016,42 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     int64_t* d_sbase = nullptr;   // [nseg + 1] bases, then the tail's final start
     HIP_CHECK(hipMallocAsync((void**)&d_scnt, sizeof(uint32_t) * (nseg + 1), st));
     HIP_CHECK(hipMallocAsync((void**)&d_sbase, sizeof(int64_t) * (nseg + 2), st));
+    unsigned long long* d_big = nullptr;   // [0] count of segments with many forced records, [1..] their indices
+    HIP_CHECK(hipMallocAsync((void**)&d_big, sizeof(unsigned long long) * (1 + kBigSegCap), st));
+    HIP_CHECK(hipMemsetAsync(d_big, 0, sizeof(unsigned long long), st));
     HIP_CHECK(hipMallocAsync((void**)&d_sums, sizeof(int64_t) * sums_len(nseg + 1), st));
     HIP_CHECK(hipMemsetAsync(d_scnt + nseg, 0, sizeof(uint32_t), st));
     const unsigned sblocks = (unsigned)((nseg + 255) / 256);
     hipLaunchKernelGGL(text_seg_kernel, dim3(sblocks), dim3(256), 0, st, d_data, n_bytes, (const int64_t*)d_lf, n_lf,
-                       M, 0, d_scnt, (const int64_t*)nullptr, (int64_t*)nullptr, (int32_t*)nullptr, d_sbase + nseg + 1);
+                       M, 0, d_scnt, (const int64_t*)nullptr, (int64_t*)nullptr, (int32_t*)nullptr, d_sbase + nseg + 1,
+                       d_big, 0);
     scan(d_scnt, nseg + 1, d_sbase, d_sums);
     int64_t hv[2] = {0, 0};   // body records, tail final start
+    unsigned long long n_big = 0;
     HIP_CHECK(hipMemcpyAsync(hv, d_sbase + nseg, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&n_big, d_big, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    const int32_t big_ok = n_big > 0 && n_big <= kBigSegCap;
     const int64_t body = hv[0], tail_start = hv[1];
     int rc = CBX_OK;
     if (body > capacity) {
         rc = fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(body));
     } else {
         hipLaunchKernelGGL(text_seg_kernel, dim3(sblocks), dim3(256), 0, st, d_data, n_bytes, (const int64_t*)d_lf, n_lf,
-                           M, 1, d_scnt, (const int64_t*)d_sbase, d_rec_off, d_rec_len, (int64_t*)nullptr);
+                           M, 1, d_scnt, (const int64_t*)d_sbase, d_rec_off, d_rec_len, (int64_t*)nullptr, d_big, big_ok);
         HIP_CHECK(hipGetLastError());
+        if (big_ok) {
+            hipLaunchKernelGGL(text_forced_kernel, dim3((unsigned)n_big, 64), dim3(256), 0, st, d_data, n_bytes,
+                               (const int64_t*)d_lf, n_lf, M, (const unsigned long long*)d_big, (const int64_t*)d_sbase,
+                               d_rec_off, d_rec_len);
+            HIP_CHECK(hipGetLastError());
+        }
     }
     HIP_CHECK(hipFreeAsync(d_scnt, st));
     HIP_CHECK(hipFreeAsync(d_sbase, st));
     HIP_CHECK(hipFreeAsync(d_sums, st));
     HIP_CHECK(hipFreeAsync(d_lf, st));
+    HIP_CHECK(hipFreeAsync(d_big, st));
     if (rc) { HIP_CHECK(hipStreamSynchronize(st)); return rc; }
     // the virtual length: the window that first reached past the data (record start s_k, the
     // first with s_k + M >= n_bytes) was marked full (ensureBytesRead, :98-107)

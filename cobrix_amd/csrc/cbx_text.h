@@ -20,6 +20,8 @@
 
 namespace cbx {
 
+constexpr int kForcedInline = 64;   // forced records a segment's own thread writes; more -> text_forced_kernel
+constexpr int kBigSegCap = 1024;    // segments listed for text_forced_kernel (beyond: written inline)
 constexpr int kTextChunk = 16384;   // bytes per wave in the LF passes (64 lanes x 16 B x 16 steps)
 
 __device__ __forceinline__ uint32_t lf_mask16(const uint8_t* p, int64_t i, int64_t n, bool vec) {
@@ -124,7 +126,8 @@ __global__ __launch_bounds__(256) void text_seg_kernel(const uint8_t* __restrict
                                                        const int64_t* __restrict__ lf, int64_t n_lf, int64_t M,
                                                        int mode, uint32_t* __restrict__ cnt,
                                                        const int64_t* __restrict__ base, int64_t* __restrict__ rec_off,
-                                                       int32_t* __restrict__ rec_len, int64_t* __restrict__ tail_start) {
+                                                       int32_t* __restrict__ rec_len, int64_t* __restrict__ tail_start,
+                                                       unsigned long long* __restrict__ big, int32_t big_ok) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j > n_lf) return;
     const int64_t s0 = j > 0 ? lf[j - 1] + 1 : 0;
@@ -143,6 +146,10 @@ __global__ __launch_bounds__(256) void text_seg_kernel(const uint8_t* __restrict
     if (mode == 0) {
         cnt[j] = (uint32_t)(c + (tail ? 0 : 1));
         if (tail) *tail_start = fs;
+        if (c > kForcedInline) {   // big[0]: count, big[1..]: segment indices
+            const unsigned long long k = atomicAdd(big, 1ull);
+            if (k < (unsigned long long)kBigSegCap) big[1 + k] = (unsigned long long)j;
+        }
         return;
     }
     int64_t o = base[j];
@@ -151,15 +158,43 @@ __global__ __launch_bounds__(256) void text_seg_kernel(const uint8_t* __restrict
         rec_len[o] = (int32_t)(M - f);
         o++;
         const int64_t s1 = s0 + M - f;
-        for (int64_t i = 1; i < c; i++, o++) {
-            rec_off[o] = s1 + (i - 1) * M;
-            rec_len[o] = (int32_t)M;
+        if (c > kForcedInline && big_ok) {
+            o += c - 1;   // text_forced_kernel
+        } else {
+            for (int64_t i = 1; i < c; i++, o++) {
+                rec_off[o] = s1 + (i - 1) * M;
+                rec_len[o] = (int32_t)M;
+            }
         }
     }
     if (!tail) {
         const int64_t p = lf[j];
         rec_off[o] = fs;
         rec_len[o] = (int32_t)(p - fs - (text_eol_len(data, p, fs) - 1));
+    }
+}
+
+// The forced records 1..c-1 of the listed long segments, spread over gridDim.y blocks each.
+__global__ __launch_bounds__(256) void text_forced_kernel(const uint8_t* __restrict__ data, int64_t n,
+                                                          const int64_t* __restrict__ lf, int64_t n_lf, int64_t M,
+                                                          const unsigned long long* __restrict__ big,
+                                                          const int64_t* __restrict__ base, int64_t* __restrict__ rec_off,
+                                                          int32_t* __restrict__ rec_len) {
+    const int64_t j = (int64_t)big[1 + blockIdx.x];
+    const int64_t s0 = j > 0 ? lf[j - 1] + 1 : 0;
+    const int f = text_footer_before(data, lf, j, M);
+    int64_t c;
+    if (j < n_lf) {
+        text_final_start(s0, lf[j], M, f, &c);
+    } else {
+        const int64_t s1 = s0 + M - f;
+        c = s0 + M >= n ? 0 : 1 + text_ceil_div(n - M - s1, M);
+    }
+    const int64_t s1 = s0 + M - f;
+    const int64_t o = base[j];
+    for (int64_t i = 1 + (int64_t)blockIdx.y * blockDim.x + threadIdx.x; i < c; i += (int64_t)gridDim.y * blockDim.x) {
+        rec_off[o + i] = s1 + (i - 1) * M;
+        rec_len[o + i] = (int32_t)M;
     }
 }
 

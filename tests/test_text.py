@@ -110,9 +110,12 @@ class TestGpuText:
 
     @pytest.mark.parametrize("data,rs", [(b"", 3), (b"\n", 3), (b"\r\n", 3), (b"\n" * 1000, 2),
                                          (b"X" * 100_003, 7), (b"AB\nCD\n", 3), (b"ABCD\r\nEF", 3),
-                                         (b"\r" * 999 + b"\n", 4), ((b"Y" * 21 + b"\r\n") * 3000, 20)],
+                                         (b"\r" * 999 + b"\n", 4), ((b"Y" * 21 + b"\r\n") * 3000, 20),
+                                         (b"Q" * 50_000 + b"\r\n" + b"R" * 10 + b"\n" + b"S" * 30_001, 5),
+                                         ((b"Z" * 700 + b"\n") * 1500, 5), (b"W" * 2_000_001, 3)],
                              ids=["empty", "lf", "crlf", "lf_only", "no_eol", "trailing_lf", "cr_at_window_end",
-                                  "cr_run", "crlf_at_window_edge"])
+                                  "cr_run", "crlf_at_window_edge", "few_long_lines", "many_long_lines",
+                                  "no_eol_2M"])
     def test_frame_edge_cases(self, data, rs):
         go, gl, gv = self._frame(data, rs)
         oo, ol, ov = O.frame_text(data, rs)
