@@ -13,8 +13,13 @@ import numpy as np
 from .codepages_data import CODE_PAGES
 
 
-def lut_for(name: str) -> List[int]:
-    """Code-page table by name (CodePage.getCodePageByName)."""
+def lut_for(name) -> List[int]:
+    """Code-page table by name (CodePage.getCodePageByName), or a custom CodePage's own
+    256-entry table (ebcdic_code_page_class, CodePage.getCodePageByClass)."""
+    if isinstance(name, (list, tuple)):
+        if len(name) != 256:
+            raise ValueError("a code page table has 256 entries")
+        return [int(c) for c in name]
     if name not in CODE_PAGES:
         raise ValueError(f"The code page '{name}' is not one of the builtin EBCDIC code pages.")
     return CODE_PAGES[name]

@@ -38,6 +38,7 @@ class ReaderParameters:
     """Subset of ReaderParameters (ReaderParameters.scala:65-103) that shapes the decode path."""
     is_ebcdic: bool = True
     ebcdic_code_page: str = "common"
+    ebcdic_code_page_table: Optional[List[int]] = None   # ebcdic_code_page_class: a custom CodePage's table
     floating_point_format: str = "IBM"
     is_utf16_big_endian: bool = True
     ascii_charset: str = ""
@@ -48,8 +49,10 @@ class ReaderParameters:
     is_rdw_big_endian: bool = False
     is_rdw_part_rec_length: bool = False
     rdw_adjustment: int = 0
+    enable_indexes: bool = True
     input_split_records: Optional[int] = None
     input_split_size_mb: Optional[int] = None
+    hdfs_default_block_size_mb: Optional[int] = None   # getSplitSizeMB fallback (VarLenNestedReader.scala:237-243)
     start_offset: int = 0
     end_offset: int = 0
     file_start_offset: int = 0
@@ -60,10 +63,13 @@ class ReaderParameters:
     segment_field: Optional[str] = None
     segment_id_redefine_map: Dict[str, str] = field(default_factory=dict)
     segment_id_filter: Optional[List[str]] = None
+    segment_id_levels: List[str] = field(default_factory=list)   # segment_id_level0.. / segment_id_root
+    segment_id_prefix: str = ""
     drop_group_fillers: bool = False
     drop_value_fillers: bool = True
     non_terminals: Sequence[str] = ()
     occurs_mappings: Dict[str, Dict[str, int]] = field(default_factory=dict)
+    debug_fields_policy: str = "none"             # DebugFieldsPolicy: none / hex / raw
     window_bytes: int = 0
     # fixed-length batches of at least this many records run a copybook-specialised kernel
     # (hipRTC, compiled once per layout): 0 = library default, < 0 = never
@@ -244,17 +250,34 @@ def string_capacity(native_plan, n_rec: int, exact: Optional[Sequence[int]] = No
     return list(out)
 
 
+def parse_copybook_for(copybook_contents: str, params: ReaderParameters) -> cbk.Copybook:
+    """The reader's loadCopyBook (CP/reader/FixedLenNestedReader.scala:100-143,
+    CP/reader/VarLenNestedReader.scala:182-226): parse options taken from ReaderParameters."""
+    segment_redefines = sorted(set(params.segment_id_redefine_map.values()))
+    return cbk.parse_copybook(
+        copybook_contents, data_encoding=cbk.EBCDIC if params.is_ebcdic else cbk.ASCII,
+        drop_group_fillers=params.drop_group_fillers, drop_value_fillers=params.drop_value_fillers,
+        segment_redefines=segment_redefines, string_trimming=params.string_trimming_policy,
+        code_page=params.ebcdic_code_page_table or params.ebcdic_code_page,
+        floating_point_format=params.floating_point_format,
+        is_utf16_big_endian=params.is_utf16_big_endian, ascii_charset=params.ascii_charset,
+        non_terminals=params.non_terminals, occurs_handlers=params.occurs_mappings,
+        debug_fields_policy=params.debug_fields_policy)
+
+
+def reader_schema(cb: cbk.Copybook, params: ReaderParameters, variable_length: bool):
+    """The reader's CobolSchema -> createSparkSchema (SC/schema/CobolSchema.scala:77-113): the
+    variable-length reader adds File_Id / Record_Id and one Seg_IdN column per segment level
+    (CP/reader/VarLenNestedReader.scala:223-225); the fixed-length reader neither."""
+    levels = len(params.segment_id_levels) if (variable_length and params.segment_field) else 0
+    return spark_schema(cb, params.schema_policy == "collapse_root",
+                        params.generate_record_id and variable_length, seg_id_levels=levels)
+
+
 class _BaseReader:
     def __init__(self, copybook_contents: str, params: ReaderParameters):
         self.params = params
-        segment_redefines = sorted(set(params.segment_id_redefine_map.values()))
-        self.copybook = cbk.parse_copybook(
-            copybook_contents, data_encoding=cbk.EBCDIC if params.is_ebcdic else cbk.ASCII,
-            drop_group_fillers=params.drop_group_fillers, drop_value_fillers=params.drop_value_fillers,
-            segment_redefines=segment_redefines, string_trimming=params.string_trimming_policy,
-            code_page=params.ebcdic_code_page, floating_point_format=params.floating_point_format,
-            is_utf16_big_endian=params.is_utf16_big_endian, ascii_charset=params.ascii_charset,
-            non_terminals=params.non_terminals, occurs_handlers=params.occurs_mappings)
+        self.copybook = parse_copybook_for(copybook_contents, params)
         if params.variable_size_occurs:
             raise N.CbxError(N.CBX_E_UNSUPPORTED, "variable_size_occurs=true is not on the GPU path yet")
         self.plan = build_plan(self.copybook, segment_field=params.segment_field,

@@ -79,3 +79,26 @@ def spark_schema(cb: Copybook, collapse_root: bool, generate_record_id: bool = F
     gen += [SparkField(f"Seg_Id{i}", "generated", None, stype=(ST_STRING, 0, 0))
             for i in range(seg_id_levels)]
     return gen + fields
+
+
+def _type_json(f: SparkField):
+    if f.kind == "struct":
+        t = {"type": "struct", "fields": [field_json(c) for c in (f.children or [])]}
+    else:
+        tag, p, s = f.stype
+        t = f"decimal({p},{s})" if tag == ST_DECIMAL else ST_NAMES[tag]
+    if f.is_array:
+        return {"type": "array", "elementType": t, "containsNull": True}
+    return t
+
+
+def field_json(f: SparkField) -> dict:
+    """StructField.jsonValue: generated File_Id / Record_Id are non-nullable
+    (SC/schema/CobolSchema.scala:104-107), every other field nullable."""
+    nullable = not (f.kind == "generated" and f.name in ("File_Id", "Record_Id"))
+    return {"name": f.name, "type": _type_json(f), "nullable": nullable, "metadata": {}}
+
+
+def schema_json(fields: List[SparkField]) -> dict:
+    """`df.schema.json` of the reference's DataFrame, as a parsed JSON value."""
+    return {"type": "struct", "fields": [field_json(f) for f in fields]}

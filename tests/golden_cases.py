@@ -1,0 +1,274 @@
+"""The reference's own integration specs, as data: copybook + data file + Spark options + the
+golden outputs they assert (SCT = spark-cobol/src/test/scala/za/co/absa/cobrix/spark/cobol/).
+
+Each case runs through a `spark.read.format("cobol").options(...)`-equivalent read (cobrix_amd.options
+-> reader) and is compared with the reference's golden rows (`df.toJSON` / pretty JSON), its
+schema JSON (`df.schema.json`) and, where the spec has one, its layout
+(`Copybook.generateRecordLayoutPositions`).  The CPU suite runs every case through the oracle; the
+GPU suite runs the same cases through libcobrix_hip.so and compares with both.
+"""
+from __future__ import annotations
+
+import json
+from decimal import Decimal
+from typing import Any, Dict, List, Optional
+
+import goldens as G
+
+# SCT/source/utils/CustomCodePage.scala: the test code page the reference loads by class name
+# (ebcdic_code_page_class) -- a fixture table: byte -> Unicode code point
+_SPC = 0x20
+
+
+def _custom_code_page() -> List[int]:
+    t = [_SPC] * 256
+    t[64] = t[65] = 0x20
+
+    def put(start: int, chars: str):
+        for i, ch in enumerate(chars):
+            if ch != "\0":
+                t[start + i] = ord(ch)
+
+    put(75, ".<(+|")
+    put(80, "&")
+    put(90, "!$*);")
+    put(96, "-/")
+    put(106, "|,%_>?")
+    put(121, "`:#@\0=")
+    t[125] = _SPC
+    put(129, "ABCDEFGHI")
+    put(145, "JKLMNOPQR")
+    put(161, "~STUVWXYZ")
+    t[176] = ord("^")
+    put(186, "[]")
+    put(192, "{abcdefghi-")
+    put(208, "}jklmnopqr")
+    put(226, "stuvwxyz")
+    put(240, "0123456789")
+    return t
+
+
+CUSTOM_CODE_PAGE = _custom_code_page()
+CUSTOM_CODE_PAGE_CLASS = "za.co.absa.cobrix.spark.cobol.source.utils.CustomCodePage"
+
+T5_SEG = {"segment_field": "SEGMENT_ID", "generate_record_id": "true", "schema_retention_policy": "collapse_root"}
+
+CASES: Dict[str, Dict[str, Any]] = {
+    "test1": dict(spec="SCT/source/integration/Test1FixedLengthRecordsSpec.scala:38-66",
+                  copybook="test1_copybook.cob", data="test1_data/example.bin",
+                  options={"schema_retention_policy": "collapse_root"},
+                  expected="test1_expected/test1.txt", schema="test1_expected/test1_schema.json", take=60),
+    "test3": dict(spec="SCT/source/integration/Test3SegmentFieldSpec.scala:79-84",
+                  copybook="test3_copybook.cob", data="test3_data/TRAN2.AUG31.DATA.dat",
+                  options={"schema_retention_policy": "collapse_root", "segment_field": "SIGNATURE",
+                           "segment_filter": "S9276511"},
+                  expected="test3_expected/test3.txt", schema="test3_expected/test3_schema.json", take=60),
+    **{f"test3_trim_{t}": dict(spec="SCT/source/integration/Test3SegmentFieldSpec.scala:86-116",
+                               copybook="test3_copybook.cob", data="test3_data/TRAN2.AUG31.DATA.dat",
+                               options={"schema_retention_policy": "collapse_root", "segment_field": "SIGNATURE",
+                                        "segment_filter": "S9276511", "string_trimming_policy": t},
+                               expected=f"test3_expected/test3_trim_{t}.txt", take=60)
+       for t in ("none", "left", "right", "both")},
+    "test5": dict(spec="SCT/source/integration/Test5MultisegmentSpec.scala:44-93",
+                  copybook="test5_copybook.cob", data="test5_data/COMP.DETAILS.SEP30.DATA.dat",
+                  options={"is_record_sequence": "true", "segment_id_level0": "C", "segment_id_level1": "P",
+                           "segment_id_prefix": "A", **T5_SEG},
+                  expected="test5_expected/test5.txt", schema="test5_expected/test5_schema.json",
+                  sort=("File_Id", "Record_Id"), take=60),
+    "test5a": dict(spec="SCT/source/integration/Test5MultisegmentSpec.scala:95-148",
+                   copybook="test5_copybook.cob", data="test5_data/COMP.DETAILS.SEP30.DATA.dat",
+                   options={"is_record_sequence": "true", "input_split_records": "100", "segment_id_root": "C",
+                            "segment_id_prefix": "B", **T5_SEG},
+                   expected="test5_expected/test5a.txt", schema="test5_expected/test5a_schema.json",
+                   sort=("File_Id", "Record_Id"), take=60),
+    "test5c": dict(spec="SCT/source/integration/Test5MultisegmentSpec.scala:150-203",
+                   copybook="test5_copybook.cob", data="test5_data/COMP.DETAILS.SEP30.DATA.dat",
+                   options={"is_record_sequence": "true", "input_split_records": "100", "segment_id_root": "C",
+                            "segment_id_prefix": "B", "redefine_segment_id_map:0": "STATIC-DETAILS => C,D",
+                            "redefine-segment-id-map:1": "CONTACTS => P", **T5_SEG},
+                   expected="test5_expected/test5c.txt", schema="test5_expected/test5c_schema.json",
+                   sort=("File_Id", "Record_Id"), take=60),
+    "test5b": dict(spec="SCT/source/integration/Test5MultisegmentSpec.scala:220-271",
+                   copybook="test5_copybook.cob", data="test5b_data/COMP.DETAILS.FEB02.DATA.RDW.BE.dat",
+                   options={"is_record_sequence": "true", "is_rdw_big_endian": "true", "segment_id_level0": "C",
+                            "segment_id_level1": "P", "segment_id_prefix": "A", **T5_SEG},
+                   expected="test5_expected/test5b.txt", schema="test5_expected/test5b_schema.json",
+                   sort=("File_Id", "Record_Id"), take=60),
+    "test6": dict(spec="SCT/source/integration/Test6TypeVarietySpec.scala:37-100",
+                  copybook="test6_copybook.cob", data="test6_data/INTEGR.TYPES.NOV28.DATA.dat",
+                  options={"schema_retention_policy": "collapse_root", "floating_point_format": "IEEE754"},
+                  expected="test6_expected/test6.txt", schema="test6_expected/test6_schema.json",
+                  sort=("ID",), take=100, na_fill=True),
+    **{name: dict(spec="SCT/source/integration/Test7FillersSpec.scala:37-108",
+                  copybook="test7_fillers.cob", data="test7_data/TEST.FILLERS.DEC07.DATA.dat",
+                  options={"schema_retention_policy": "collapse_root", "drop_group_fillers": dg,
+                           "drop_value_fillers": dv},
+                  expected=f"test7_expected/{name}.txt", schema=f"test7_expected/{name}_schema.json",
+                  sort=("AMOUNT",), take=100)
+       for name, dv, dg in (("test7", "true", "true"), ("test7a", "true", "false"),
+                            ("test7b", "false", "true"), ("test7c", "false", "false"))},
+    "test8_printable": dict(spec="SCT/source/integration/Test8NonPrintables.scala:72-75",
+                            copybook="test8_copybook.cob", data="test8_data/TRAN2.MAR14.DATA.dat",
+                            options={"schema_retention_policy": "collapse_root", "ebcdic_code_page": "common"},
+                            expected="test8_expected/test8_printable.txt", schema="test8_expected/test8_schema.json",
+                            take=60),
+    "test8_non_printable": dict(spec="SCT/source/integration/Test8NonPrintables.scala:77-81",
+                                copybook="test8_copybook.cob", data="test8_data/TRAN2.MAR14.DATA.dat",
+                                options={"schema_retention_policy": "collapse_root",
+                                         "ebcdic_code_page": "common_extended", "string_trimming_policy": "none"},
+                                expected="test8_expected/test8_non_printable.txt", take=60),
+    "test9_cp037": dict(spec="SCT/source/integration/Test9CodePages.scala:69-72",
+                        copybook="test9_copybook.cob", data="test9_data/TRAN.APR14.NPT.DATA.dat",
+                        options={"schema_retention_policy": "collapse_root", "ebcdic_code_page": "cp037"},
+                        expected="test9_expected/test9_cp037.txt", schema="test9_expected/test9_schema.json", take=60),
+    "test9_cp037_ext": dict(spec="SCT/source/integration/Test9CodePages.scala:74-78",
+                            copybook="test9_copybook.cob", data="test9_data/TRAN.APR14.NPT.DATA.dat",
+                            options={"schema_retention_policy": "collapse_root", "ebcdic_code_page": "cp037_extended",
+                                     "string_trimming_policy": "none"},
+                            expected="test9_expected/test9_cp037_ext.txt", take=60),
+    "test9_cp_custom": dict(spec="SCT/source/integration/Test9CodePages.scala:80-84",
+                            copybook="test9_copybook.cob", data="test9_data/TRAN.APR14.NPT.DATA.dat",
+                            options={"schema_retention_policy": "collapse_root",
+                                     "ebcdic_code_page_class": CUSTOM_CODE_PAGE_CLASS,
+                                     "string_trimming_policy": "none"},
+                            expected="test9_expected/test9_cp_custom.txt", take=60),
+    "test13a": dict(spec="SCT/source/integration/Test13aFixedLenFileHeadersSpec.scala:74-103",
+                    copybook="test13a_file_header_footer.cob", data="test13a_data/TRAN2.JUN24.DATA.dat",
+                    options={"schema_retention_policy": "collapse_root", "file_start_offset": "10",
+                             "file_end_offset": "12"},
+                    expected="test13_expected/test13a.txt", schema="test13_expected/test13a_schema.json",
+                    sort=("COMPANY_ID", "AMOUNT"), take=60),
+    "test13a_index": dict(spec="SCT/source/integration/Test13aFixedLenFileHeadersSpec.scala:105-135",
+                          copybook="test13a_file_header_footer.cob", data="test13a_data/TRAN2.JUN24.DATA.dat",
+                          options={"schema_retention_policy": "collapse_root", "input_split_records": "10",
+                                   "file_start_offset": "10", "file_end_offset": "12"},
+                          expected="test13_expected/test13a.txt", sort=("COMPANY_ID", "AMOUNT"), take=60),
+    "test13b": dict(spec="SCT/source/integration/Test13bVarLenFileHeadersSpec.scala:57-95",
+                    copybook="test13b_vrl_file_headers.cob", data="test13b_data/COMP.DETAILS.JUN02.DATA.RDW.BE.dat",
+                    options={"schema_retention_policy": "collapse_root", "is_record_sequence": "true",
+                             "is_rdw_big_endian": "true", "segment_field": "SEGMENT_ID", "segment_id_level0": "C",
+                             "segment_id_level1": "P", "generate_record_id": "true", "segment_id_prefix": "A",
+                             "file_start_offset": "100", "file_end_offset": "120"},
+                    expected="test13_expected/test13b.txt", schema="test13_expected/test13b_schema.json", take=60),
+    "test14": dict(spec="SCT/source/integration/Test14RdwAdjustmentsSpec.scala:39-80",
+                   copybook="test14_copybook.cob", data="test14_data/COMP.DETAILS.JUL02.DATA.dat",
+                   options={"is_record_sequence": "true", "segment_id_level0": "C", "segment_id_level1": "P",
+                            "segment_id_prefix": "A", "redefine_segment_id_map:0": "STATIC-DETAILS => C,D",
+                            "redefine-segment-id-map:1": "CONTACTS => P", "is_rdw_part_of_record_length": "true",
+                            **T5_SEG},
+                   expected="test14_expected/test14.txt", schema="test14_expected/test14_schema.json",
+                   sort=("File_Id", "Record_Id"), take=60),
+    "test14_adjustment": dict(spec="SCT/source/integration/Test14RdwAdjustmentsSpec.scala:82-123",
+                              copybook="test14_copybook.cob", data="test14_data/COMP.DETAILS.JUL02.DATA.dat",
+                              options={"is_record_sequence": "true", "segment_id_level0": "C",
+                                       "segment_id_level1": "P", "segment_id_prefix": "A",
+                                       "redefine_segment_id_map:0": "STATIC-DETAILS => C,D",
+                                       "redefine-segment-id-map:1": "CONTACTS => P", "rdw_adjustment": "-4",
+                                       **T5_SEG},
+                              expected="test14_expected/test14.txt", sort=("File_Id", "Record_Id"), take=60),
+    "test16": dict(spec="SCT/source/integration/Test16FixedLenSegmentRedefinesSpec.scala:78-109",
+                   copybook="test16_fix_len_segments.cob", data="test16_data/ENTITY.DB.AUG12.DATA.FIX.LEN.dat",
+                   options={"schema_retention_policy": "collapse_root", "segment_field": "SEGMENT_ID",
+                            "redefine_segment_id_map:0": "COMPANY => C", "redefine-segment-id-map:1": "PERSON => P",
+                            "redefine-segment-id-map:2": "PO-BOX => B"},
+                   expected="test16_expected/test16.txt", schema="test16_expected/test16_schema.json", take=50),
+    "test17a": dict(spec="SCT/source/integration/Test17HierarchicalSpec.scala:34-75",
+                    copybook="test17_hierarchical.cob", data="test17/HIERARCHICAL.DATA.RDW.dat",
+                    options={"pedantic": "true", "is_record_sequence": "true", "generate_record_id": "true",
+                             "schema_retention_policy": "collapse_root", "segment_field": "SEGMENT_ID",
+                             "redefine_segment_id_map:1": "COMPANY => 1", "redefine-segment-id-map:2": "DEPT => 2",
+                             "redefine-segment-id-map:3": "EMPLOYEE => 3", "redefine-segment-id-map:4": "OFFICE => 4",
+                             "redefine-segment-id-map:5": "CUSTOMER => 5", "redefine-segment-id-map:6": "CONTACT => 6",
+                             "redefine-segment-id-map:7": "CONTRACT => 7"},
+                    expected="test17_expected/test17a.txt", schema="test17_expected/test17a_schema.json",
+                    sort=("File_Id", "Record_Id"), take=300),
+    "test17b": dict(spec="SCT/source/integration/Test17HierarchicalSpec.scala:77-115",
+                    copybook="test17_hierarchical.cob", data="test17/HIERARCHICAL.DATA.RDW.dat",
+                    options={"pedantic": "true", "is_record_sequence": "true", "generate_record_id": "true",
+                             "schema_retention_policy": "collapse_root", "segment_field": "SEGMENT_ID",
+                             "segment_id_level0": "1", "segment_id_level1": "2,5", "segment_id_level2": "3,4,6,7",
+                             "segment_id_prefix": "A",
+                             "redefine_segment_id_map:1": "COMPANY => 1", "redefine-segment-id-map:2": "DEPT => 2",
+                             "redefine-segment-id-map:3": "EMPLOYEE => 3", "redefine-segment-id-map:4": "OFFICE => 4",
+                             "redefine-segment-id-map:5": "CUSTOMER => 5", "redefine-segment-id-map:6": "CONTACT => 6",
+                             "redefine-segment-id-map:7": "CONTRACT => 7"},
+                    expected="test17_expected/test17b.txt", schema="test17_expected/test17b_schema.json",
+                    sort=("File_Id", "Record_Id"), take=300),
+    "test19": dict(spec="SCT/source/integration/Test19DisplayNumParsingSpec.scala:32-75",
+                   copybook="test19_display_num.cob", data="test19_display_num/data.dat",
+                   options={"pedantic": "true", "generate_record_id": "true", "schema_retention_policy": "collapse_root"},
+                   expected="test19_display_num_expected/test19.txt",
+                   schema="test19_display_num_expected/test19_schema.json", sort=("File_Id", "Record_Id"), take=300),
+}
+
+# layout goldens: (copybook, parse options, expected) -- Copybook.generateRecordLayoutPositions
+LAYOUTS = {
+    "test6": ("test6_copybook.cob", {}, "test6_expected/test6_layout.txt"),
+    "test7": ("test7_fillers.cob", dict(drop_group_fillers=True, drop_value_fillers=True), "test7_expected/test7_layout.txt"),
+    "test7a": ("test7_fillers.cob", dict(drop_group_fillers=False, drop_value_fillers=True), "test7_expected/test7a_layout.txt"),
+    "test7b": ("test7_fillers.cob", dict(drop_group_fillers=True, drop_value_fillers=False), "test7_expected/test7b_layout.txt"),
+    "test7c": ("test7_fillers.cob", dict(drop_group_fillers=False, drop_value_fillers=False), "test7_expected/test7c_layout.txt"),
+    "test13a": ("test13a_file_header_footer.cob", {}, "test13_expected/test13a_layout.txt"),
+    "test13b": ("test13b_vrl_file_headers.cob", {}, "test13_expected/test13b_layout.txt"),
+    "test16": ("test16_fix_len_segments.cob", {}, "test16_expected/test16_layout.txt"),
+    "test17a": ("test17_hierarchical.cob", {}, "test17_expected/test17a_layout.txt"),
+    "test19": ("test19_display_num.cob", {}, "test19_display_num_expected/test19_layout.txt"),
+}
+
+
+def register_custom_code_pages() -> None:
+    from cobrix_amd.options import register_code_page_class
+    register_code_page_class(CUSTOM_CODE_PAGE_CLASS, CUSTOM_CODE_PAGE)
+
+
+def load_json_values(path: str) -> List[Any]:
+    """Golden rows: one JSON value per line (df.toJSON), concatenated pretty objects (prettyJSON per
+    row) or one pretty JSON array (convertDataFrameToPrettyJSON)."""
+    text = G.read(*path.split("/")).decode("utf-8")
+    dec = json.JSONDecoder(parse_float=Decimal)
+    out: List[Any] = []
+    i = 0
+    while True:
+        while i < len(text) and text[i].isspace():
+            i += 1
+        if i >= len(text):
+            break
+        v, i = dec.raw_decode(text, i)
+        out.extend(v if isinstance(v, list) else [v])
+    return out
+
+
+def _sort_key(row: dict, cols) -> tuple:
+    """Spark orderBy ascending: nulls first."""
+    key = []
+    for c in cols:
+        v = row.get(c)
+        key.append((0, 0) if v is None else (1, v))
+    return tuple(key)
+
+
+def spark_order(rows: List[dict], cols) -> List[dict]:
+    return sorted(rows, key=lambda r: _sort_key(r, cols)) if cols else list(rows)
+
+
+def params(case: Dict[str, Any]):
+    from cobrix_amd.options import parse_options
+    register_custom_code_pages()
+    return parse_options(case["options"])
+
+
+def copybook_text(case) -> str:
+    return G.read(case["copybook"]).decode("latin-1")
+
+
+def data_bytes(case) -> bytes:
+    return G.read(*case["data"].split("/"))
+
+
+def expected_rows(case) -> List[Any]:
+    return load_json_values(case["expected"])
+
+
+def compare(case, rows: List[dict]) -> List[str]:
+    rows = spark_order(rows, case.get("sort"))[: case.get("take", len(rows))]
+    return G.compare_rows(rows, expected_rows(case), na_fill=case.get("na_fill", False))
