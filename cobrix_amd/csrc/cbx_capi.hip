@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "cbx_kernels.hip"
+#include "cbx_select.h"
 #include "cbx_text.h"
 
 using namespace cbx;
@@ -68,6 +69,7 @@ struct cbx_plan {
     std::vector<int32_t> col_is_string;   // per column: 1 if string/binary
     std::vector<int32_t> col_slots;       // per column: slots
     std::vector<int32_t> col_max_bytes;   // per column: max payload bytes per value
+    std::vector<int32_t> segid_cols;      // segment levels with a Seg_Id column
     // device copies
     Field* d_fields = nullptr;
     DeferSeq* d_defer = nullptr;
@@ -414,9 +416,25 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
         if (d.variant == V_STRING) P->str_stage = std::max(P->str_stage, kWave * d.size * d.max_utf8);
     P->str_stage = std::min(P->str_stage, kStrStageBytes);
 
-    // ---- segment map: keys to UTF-8
+    // ---- segment map: keys to UTF-8, Seg_IdN string columns
     cbx_segment_map sm = opts->segments;
     if (opts->has_segments) {
+        if (sm.n_keys < 0 || sm.n_keys > CBX_MAX_SEG_KEYS || sm.n_levels < 0 || sm.n_levels > CBX_MAX_SEG_LEVELS ||
+            sm.prefix_len < 0 || sm.prefix_len > CBX_MAX_SEG_PREFIX || (sm.field_is_int && (sm.field < 0 || sm.field >= n_fields))) {
+            delete P; return fail(CBX_E_ARGUMENT, "cbx_plan_create: bad segment map");
+        }
+        if (sm.field_is_int && !(fields[sm.field].flags & CBX_F_INTEGRAL)) {
+            delete P; return fail(CBX_E_UNSUPPORTED, "segment field must be a string or an integral field");
+        }
+        for (int l = 0; l < sm.n_levels; l++) {
+            const int c = sm.level_column[l];
+            if (c < 0) continue;
+            if (c >= P->n_columns) { delete P; return fail(CBX_E_ARGUMENT, "cbx_plan_create: bad Seg_Id column"); }
+            P->col_is_string[c] = 1;
+            P->col_slots[c] = 1;
+            P->col_max_bytes[c] = sm.prefix_len + 64;   // prefix _ fileId _ rootId _L<l> _ counter
+            P->segid_cols.push_back(l);
+        }
         for (int k = 0; k < sm.n_keys; k++) {
             std::string u8;
             for (int j = 0; j < opts->segments.key_len[k]; j++) {
@@ -494,6 +512,9 @@ static int string_scan(cbx_plan* P, int64_t n_tiles, hipStream_t st) {
 struct CallShape {
     const uint8_t* data; int64_t data_len; const int64_t* rec_off; const int32_t* rec_len;
     int64_t n_rec; int32_t stride; int32_t start_off; int64_t first_record_id;
+    const int64_t* rec_id = nullptr;    // selected records: per-record Record_Id
+    const int32_t* rec_seg = nullptr;   // selected records: per-record active segment
+    int32_t file_id = -1;               // File_Id of the batch (-1: the plan's)
 };
 
 static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, int mode, hipStream_t st) {
@@ -511,7 +532,9 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.stride = c.stride;
     a.start_off = c.start_off;
     a.first_record_id = c.first_record_id;
-    a.file_id = P->opts.file_id;
+    a.rec_id = c.rec_id;
+    a.rec_seg = c.rec_seg;
+    a.file_id = c.file_id >= 0 ? c.file_id : P->opts.file_id;
     a.mode = mode;
     // staging mode
     const int sdw = c.stride / 4;
@@ -978,6 +1001,8 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     *virtual_bytes = 0;
     if (n_bytes == 0) return CBX_OK;   // hasNext is false on an empty stream (TextRecordExtractor.scala:33)
     const int64_t M = (int64_t)record_size + 2;   // maxRecordSize (TextRecordExtractor.scala:28)
+    if (record_size > INT32_MAX - 2 || n_bytes / M >= (int64_t)UINT32_MAX - 2)   // per-segment counts are 32-bit
+        return fail(CBX_E_ARGUMENT, "cbx_frame_text: record_size too large or too many records per line for one call");
     const int64_t nch = (n_bytes + kTextChunk - 1) / kTextChunk;
     // pass 1: LF counts -> bases -> positions
     auto scan = [&](uint32_t* cnt, int64_t n, int64_t* out, int64_t* sums) {
@@ -1010,6 +1035,17 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     HIP_CHECK(hipFreeAsync(d_cnt, st));
     HIP_CHECK(hipFreeAsync(d_base, st));
     HIP_CHECK(hipFreeAsync(d_sums, st));
+    // line-ending length before every segment (scan of per-segment maps, cbx_text.h)
+    const int64_t n_eol_tiles = (n_lf + 1 + kEolTile - 1) / kEolTile;
+    uint8_t* d_eol = nullptr;   // [n_eol_tiles] tile maps | [n_lf + 1] f before each segment
+    HIP_CHECK(hipMallocAsync((void**)&d_eol, n_eol_tiles + n_lf + 1 + 16, st));
+    uint8_t* d_fb = d_eol + n_eol_tiles;
+    hipLaunchKernelGGL(text_eol_kernel, dim3((unsigned)n_eol_tiles), dim3(kEolThreads), 0, st, d_data, (const int64_t*)d_lf,
+                       n_lf, M, 0, d_eol, (const uint8_t*)nullptr, (uint8_t*)nullptr);
+    hipLaunchKernelGGL(text_eol_scan_kernel, dim3(1), dim3(1), 0, st, d_eol, n_eol_tiles);
+    hipLaunchKernelGGL(text_eol_kernel, dim3((unsigned)n_eol_tiles), dim3(kEolThreads), 0, st, d_data, (const int64_t*)d_lf,
+                       n_lf, M, 2, (uint8_t*)nullptr, (const uint8_t*)d_eol, d_fb);
+    HIP_CHECK(hipGetLastError());
     // pass 2: records per segment (n_lf line-ended segments + the tail) -> bases -> records
     const int64_t nseg = n_lf + 1;
     uint32_t* d_scnt = nullptr;
@@ -1024,7 +1060,7 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     const unsigned sblocks = (unsigned)((nseg + 255) / 256);
     hipLaunchKernelGGL(text_seg_kernel, dim3(sblocks), dim3(256), 0, st, d_data, n_bytes, (const int64_t*)d_lf, n_lf,
                        M, 0, d_scnt, (const int64_t*)nullptr, (int64_t*)nullptr, (int32_t*)nullptr, d_sbase + nseg + 1,
-                       d_big, 0);
+                       d_big, 0, (const uint8_t*)d_fb);
     scan(d_scnt, nseg + 1, d_sbase, d_sums);
     int64_t hv[2] = {0, 0};   // body records, tail final start
     unsigned long long n_big = 0;
@@ -1035,15 +1071,17 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     const int64_t body = hv[0], tail_start = hv[1];
     int rc = CBX_OK;
     if (body > capacity) {
+        *n_records = body;   // required size (at least; the tail record may add one)
         rc = fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(body));
     } else {
         hipLaunchKernelGGL(text_seg_kernel, dim3(sblocks), dim3(256), 0, st, d_data, n_bytes, (const int64_t*)d_lf, n_lf,
-                           M, 1, d_scnt, (const int64_t*)d_sbase, d_rec_off, d_rec_len, (int64_t*)nullptr, d_big, big_ok);
+                           M, 1, d_scnt, (const int64_t*)d_sbase, d_rec_off, d_rec_len, (int64_t*)nullptr, d_big, big_ok,
+                           (const uint8_t*)d_fb);
         HIP_CHECK(hipGetLastError());
         if (big_ok) {
             hipLaunchKernelGGL(text_forced_kernel, dim3((unsigned)n_big, 64), dim3(256), 0, st, d_data, n_bytes,
                                (const int64_t*)d_lf, n_lf, M, (const unsigned long long*)d_big, (const int64_t*)d_sbase,
-                               d_rec_off, d_rec_len);
+                               d_rec_off, d_rec_len, (const uint8_t*)d_fb);
             HIP_CHECK(hipGetLastError());
         }
     }
@@ -1052,6 +1090,7 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     HIP_CHECK(hipFreeAsync(d_sums, st));
     HIP_CHECK(hipFreeAsync(d_lf, st));
     HIP_CHECK(hipFreeAsync(d_big, st));
+    HIP_CHECK(hipFreeAsync(d_eol, st));
     if (rc) { HIP_CHECK(hipStreamSynchronize(st)); return rc; }
     // the virtual length: the window that first reached past the data (record start s_k, the
     // first with s_k + M >= n_bytes) was marked full (ensureBytesRead, :98-107)
@@ -1066,7 +1105,10 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     const int64_t vlen = s_k >= 0 ? std::max(n_bytes, s_k + M) : n_bytes;
     int64_t total = body;
     if (tail_start < vlen) {   // the rest of the stream: the last record (:62-66, hasNext :33)
-        if (body + 1 > capacity) return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(body + 1));
+        if (body + 1 > capacity) {
+            *n_records = body + 1;
+            return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(body + 1));
+        }
         const int64_t h_off = tail_start;
         const int32_t h_len = (int32_t)(vlen - tail_start);
         HIP_CHECK(hipMemcpyAsync(d_rec_off + body, &h_off, sizeof(int64_t), hipMemcpyHostToDevice, st));
@@ -1076,5 +1118,298 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     }
     *n_records = total;
     *virtual_bytes = vlen;
+    return CBX_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Variable-length record streams: record selection, selected decode (+ Seg_IdN columns), sparse
+// index (cbx_select.h).  Temporaries are stream-ordered allocations released on every exit path.
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct AsyncBlock {   // one hipMallocAsync block, freed (stream-ordered) when the scope ends
+    void* p = nullptr;
+    hipStream_t st;
+    explicit AsyncBlock(hipStream_t s) : st(s) {}
+    ~AsyncBlock() { if (p) (void)hipFreeAsync(p, st); }
+};
+
+// exclusive scan of n uint32 values into int64 out (cbx_kernels.hip scan passes); sums: nb int64
+void device_scan(const uint32_t* in, int64_t n, int64_t* out, int64_t* sums, hipStream_t st) {
+    const int64_t nb = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, sums);
+    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, sums, nb);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, (const int64_t*)sums, out);
+}
+
+int64_t scan_sums_len(int64_t n) { return (n + kScanTile - 1) / kScanTile; }
+
+unsigned blocks_for(int64_t n, int threads) { return (unsigned)std::max<int64_t>(1, (n + threads - 1) / threads); }
+}  // namespace
+
+extern "C" int cbx_select_records(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                                  const int32_t* d_rec_len, int64_t n_rec, int32_t start_offset,
+                                  const cbx_index_entry* entries, int32_t n_entries, cbx_selection* out,
+                                  int64_t* n_selected, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!P || !out || !n_selected || n_rec < 0 || start_offset < 0 || (n_rec > 0 && (!d_data || !d_rec_off || !d_rec_len)) ||
+        (n_entries > 0 && !entries) || n_entries < 0)
+        return fail(CBX_E_ARGUMENT, "cbx_select_records: invalid arguments");
+    *n_selected = 0;
+    const int L = P->opts.has_segments ? P->opts.segments.n_levels : 0;
+    if (n_rec > 0 && (!out->rec_off || !out->rec_len || !out->record_id || !out->segment || (L > 0 && !out->seg_state)))
+        return fail(CBX_E_ARGUMENT, "cbx_select_records: output arrays required");
+    if (n_rec == 0) return CBX_OK;
+    std::vector<int64_t> h_from, h_rid, h_end;
+    if (n_entries == 0) { h_from.push_back(0); h_rid.push_back(0); h_end.push_back(-1); }
+    for (int e = 0; e < n_entries; e++) {
+        if (e > 0 && entries[e].offset_from < entries[e - 1].offset_from)
+            return fail(CBX_E_ARGUMENT, "cbx_select_records: entries must be in file order");
+        h_from.push_back(entries[e].offset_from);
+        h_rid.push_back(entries[e].record_index);
+        h_end.push_back(entries[e].offset_to);
+    }
+    const int n_ent = (int)h_from.size();
+    const int64_t n_runs = (n_rec + kSelRun - 1) / kSelRun;
+    const int64_t nb = scan_sums_len(n_runs + 1);
+    // block: ent_from | ent_rid | ent_end | ent_first | base (n_runs + 1) | sums (nb) | SegSum (n_runs) | counts | key (n_rec)
+    const size_t off_sum = sizeof(int64_t) * (4 * (size_t)n_ent + (n_runs + 1) + nb);
+    const size_t off_cnt = off_sum + sizeof(SegSum) * n_runs;
+    const size_t off_key = off_cnt + sizeof(uint32_t) * (n_runs + 1);
+    AsyncBlock blk(st);
+    HIP_CHECK(hipMallocAsync(&blk.p, off_key + n_rec + 64, st));
+    int64_t* d64 = (int64_t*)blk.p;
+    int64_t* ent_from = d64;
+    int64_t* ent_rid = d64 + n_ent;
+    int64_t* ent_end = d64 + 2 * n_ent;
+    int64_t* ent_first = d64 + 3 * n_ent;
+    int64_t* base = d64 + 4 * n_ent;
+    int64_t* sums = base + n_runs + 1;
+    SegSum* runs = (SegSum*)((uint8_t*)blk.p + off_sum);
+    uint32_t* counts = (uint32_t*)((uint8_t*)blk.p + off_cnt);
+    int8_t* key = (int8_t*)((uint8_t*)blk.p + off_key);
+    HIP_CHECK(hipMemcpyAsync(ent_from, h_from.data(), sizeof(int64_t) * n_ent, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(ent_rid, h_rid.data(), sizeof(int64_t) * n_ent, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(ent_end, h_end.data(), sizeof(int64_t) * n_ent, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemsetAsync(counts + n_runs, 0, sizeof(uint32_t), st));
+    SelArgs a{};
+    a.data = d_data; a.n_bytes = n_bytes; a.rec_off = d_rec_off; a.rec_len = d_rec_len; a.n = n_rec;
+    a.start_off = start_offset; a.L = L;
+    a.m = P->opts.has_segments ? (const CBX_CONST cbx_segment_map*)P->d_segmap : nullptr;
+    a.lut = P->d_lut;
+    a.fields = (const CBX_CONST Field*)P->d_fields;
+    a.ent_first = ent_first; a.ent_rid = ent_rid; a.ent_end = ent_end; a.n_ent = n_ent; a.key = key;
+    a.footer = out->footer_bytes;
+    hipLaunchKernelGGL(sel_entry_first_kernel, dim3(blocks_for(n_ent, 64)), dim3(64), 0, st, d_rec_off, n_rec,
+                       (const int64_t*)ent_from, n_ent, ent_first);
+    hipLaunchKernelGGL(sel_key_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(sel_sum_kernel, dim3(blocks_for(n_runs, 256)), dim3(256), 0, st, a, runs, n_runs);
+    hipLaunchKernelGGL(sel_scan_kernel, dim3(1), dim3(kSelScanThreads), 0, st, runs, n_runs, L);
+    hipLaunchKernelGGL(sel_emit_kernel, dim3(blocks_for(n_runs, 256)), dim3(256), 0, st, a, (const SegSum*)runs, n_runs, 0,
+                       counts, (const int64_t*)nullptr, *out);
+    device_scan(counts, n_runs + 1, base, sums, st);
+    hipLaunchKernelGGL(sel_emit_kernel, dim3(blocks_for(n_runs, 256)), dim3(256), 0, st, a, (const SegSum*)runs, n_runs, 1,
+                       counts, (const int64_t*)base, *out);
+    HIP_CHECK(hipGetLastError());
+    int64_t total = 0;
+    HIP_CHECK(hipMemcpyAsync(&total, base + n_runs, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    *n_selected = total;
+    return CBX_OK;
+}
+
+extern "C" int cbx_decode_selected(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, const cbx_selection* sel,
+                                   int64_t n_rec, int32_t start_offset, cbx_column* columns, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!P || !sel || (n_rec > 0 && (!sel->rec_off || !sel->rec_len || !sel->record_id || !sel->segment)) || n_bytes < 0)
+        return fail(CBX_E_ARGUMENT, "cbx_decode_selected: invalid arguments");
+    const int L = P->opts.has_segments ? P->opts.segments.n_levels : 0;
+    if (n_rec > 0 && !P->segid_cols.empty() && !sel->seg_state)
+        return fail(CBX_E_ARGUMENT, "cbx_decode_selected: seg_state required for Seg_Id columns");
+    CallShape c{d_data, n_bytes, sel->rec_off, sel->rec_len, n_rec, 0, start_offset, 0};
+    c.rec_id = sel->record_id;
+    c.rec_seg = sel->segment;
+    c.file_id = sel->file_id;
+    int r = decode_common(P, c, columns, nullptr, st);
+    if (r) return r;
+    // Seg_IdN columns (slot 0 of each string column): lengths -> scanned offsets -> bytes
+    for (int l : P->segid_cols) {
+        const cbx_column& col = columns[P->opts.segments.level_column[l]];
+        if (n_rec == 0) {
+            HIP_CHECK(hipMemsetAsync(col.offsets, 0, sizeof(int64_t), st));
+            if (col.data_sizes) HIP_CHECK(hipMemsetAsync(col.data_sizes, 0, sizeof(int64_t), st));
+            continue;
+        }
+        AsyncBlock blk(st);
+        const int64_t nb = scan_sums_len(n_rec + 1);
+        HIP_CHECK(hipMallocAsync(&blk.p, sizeof(uint32_t) * (n_rec + 1) + sizeof(int64_t) * nb + 16, st));
+        int64_t* sums = (int64_t*)blk.p;
+        uint32_t* len = (uint32_t*)(sums + nb);
+        SegIdArgs g{};
+        g.state = sel->seg_state; g.n = n_rec; g.L = L; g.level = l; g.file_id = sel->file_id;
+        g.prefix_len = P->opts.segments.prefix_len;
+        g.m = (const CBX_CONST cbx_segment_map*)P->d_segmap;
+        hipLaunchKernelGGL(segid_len_kernel, dim3(blocks_for(n_rec + 1, 256)), dim3(256), 0, st, g, len);
+        device_scan(len, n_rec + 1, col.offsets, sums, st);
+        hipLaunchKernelGGL(segid_write_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, g, (int64_t*)col.offsets,
+                           col.data, col.data_capacity, col.validity, P->d_status);
+        if (col.data_sizes)
+            HIP_CHECK(hipMemcpyAsync(col.data_sizes, col.offsets + n_rec, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        HIP_CHECK(hipGetLastError());
+    }
+    return CBX_OK;
+}
+
+namespace cbx {
+__global__ void idx_gather_kernel(const int64_t* idx, int64_t k, const int64_t* rec_off, int32_t header_bytes,
+                                  int32_t has_header, int64_t* from, int64_t* recno) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    from[j] = rec_off[idx[j]] - header_bytes;
+    recno[j] = idx[j] + has_header;
+}
+__global__ void idx_rank_kernel(const int64_t* ranks, int64_t k, const int64_t* cand, int64_t* idx) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < k) idx[j] = cand[ranks[j]];
+}
+}  // namespace cbx
+
+extern "C" int cbx_sparse_index(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                                const int32_t* d_rec_len, int64_t n_rec, const cbx_index_params* prm,
+                                cbx_index_entry* entries, int64_t capacity, int64_t* n_entries, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!P || !prm || !n_entries || capacity < 0 || (capacity > 0 && !entries) || n_rec < 0 ||
+        (n_rec > 0 && (!d_rec_off || !d_rec_len || !d_data)) || (prm->header_bytes != 0 && prm->header_bytes != 4) ||
+        prm->records_per_entry < 0 || (prm->records_per_entry == 0 && prm->bytes_per_entry <= 0))
+        return fail(CBX_E_ARGUMENT, "cbx_sparse_index: invalid arguments");
+    *n_entries = 0;
+    const bool hier = prm->hierarchical && P->opts.has_segments && P->opts.segments.n_levels > 0;
+    if (prm->hierarchical && !hier) return fail(CBX_E_ARGUMENT, "cbx_sparse_index: hierarchical cuts need segment levels in the plan");
+    const int64_t hh = prm->has_file_header ? 1 : 0;
+    std::vector<int64_t> from{0}, recno{0};   // the first mandatory entry
+    if (n_rec > 0) {
+        const int64_t nb = scan_sums_len(n_rec + 1);
+        AsyncBlock blk(st);
+        // flags (n + 1 u32) | excl (n + 1) | cand (n) | sums (nb) | key (n i8)
+        const size_t off_excl = ((sizeof(uint32_t) * (n_rec + 1)) + 15) & ~(size_t)15;
+        const size_t off_cand = off_excl + sizeof(int64_t) * (n_rec + 1);
+        const size_t off_sums = off_cand + sizeof(int64_t) * n_rec;
+        const size_t off_key = off_sums + sizeof(int64_t) * nb;
+        HIP_CHECK(hipMallocAsync(&blk.p, off_key + n_rec + 64, st));
+        uint8_t* b = (uint8_t*)blk.p;
+        uint32_t* flag = (uint32_t*)b;
+        int64_t* excl = (int64_t*)(b + off_excl);
+        int64_t* cand = (int64_t*)(b + off_cand);
+        int64_t* sums = (int64_t*)(b + off_sums);
+        int8_t* key = (int8_t*)(b + off_key);
+        IdxArgs ia{};
+        ia.rec_off = d_rec_off; ia.rec_len = d_rec_len; ia.n = n_rec; ia.n_bytes = n_bytes;
+        ia.header_bytes = prm->header_bytes; ia.has_header = (int32_t)hh;
+        ia.m = (const CBX_CONST cbx_segment_map*)P->d_segmap;
+        if (hier) {
+            // IndexGenerator.getSegmentId reads the field without the record start offset (:153-156)
+            SelArgs sa{};
+            sa.data = d_data; sa.n_bytes = n_bytes; sa.rec_off = d_rec_off; sa.rec_len = d_rec_len; sa.n = n_rec;
+            sa.start_off = 0; sa.m = ia.m; sa.lut = P->d_lut; sa.fields = (const CBX_CONST Field*)P->d_fields; sa.key = key;
+            hipLaunchKernelGGL(sel_key_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, sa);
+            ia.key = key;
+        }
+        hipLaunchKernelGGL(idx_flag_kernel, dim3(blocks_for(n_rec + 1, 256)), dim3(256), 0, st, ia, flag);
+        device_scan(flag, n_rec + 1, excl, sums, st);
+        hipLaunchKernelGGL(idx_compact_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, ia, (const uint32_t*)flag,
+                           (const int64_t*)excl, cand);
+        HIP_CHECK(hipGetLastError());
+        int64_t n_cand = 0;
+        HIP_CHECK(hipMemcpyAsync(&n_cand, excl + n_rec, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        std::vector<int64_t> split_idx;         // framed index of every split (host list) ...
+        int64_t* d_split = nullptr;              // ... or device list of n_split
+        int64_t n_split = 0;
+        AsyncBlock blk2(st);
+        if (n_cand > 0) {
+            const int64_t N = prm->records_per_entry, S = prm->bytes_per_entry;
+            if (N > 0 && !hier) {
+                // every valid record but the stream's last is a candidate: splits at numbers k N
+                for (int64_t k = 1;; k++) {
+                    const int64_t i = k * N - hh;
+                    if (i >= n_cand) break;
+                    split_idx.push_back(i);
+                }
+            } else if (N == 0 && prm->subtract_size) {
+                int64_t last = 0;
+                HIP_CHECK(hipMemcpyAsync(&last, cand + n_cand - 1, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+                int64_t last_off = 0, first_cand = 0;
+                HIP_CHECK(hipStreamSynchronize(st));
+                HIP_CHECK(hipMemcpyAsync(&last_off, d_rec_off + last, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipMemcpyAsync(&first_cand, cand, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                const int64_t K = (last_off - prm->header_bytes) / S + 1;
+                HIP_CHECK(hipMallocAsync(&blk2.p, sizeof(int64_t) * (2 * K + 2), st));
+                int64_t* rj = (int64_t*)blk2.p;
+                hipLaunchKernelGGL(idx_size_kernel, dim3(blocks_for(K, 256)), dim3(256), 0, st, ia, (const int64_t*)cand, n_cand,
+                                   S, K, rj);
+                HIP_CHECK(hipGetLastError());
+                std::vector<int64_t> h(K);
+                HIP_CHECK(hipMemcpyAsync(h.data(), rj, sizeof(int64_t) * K, hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                // rank_k = k + max(rank_0, max_{j<=k}(r_j - j)), rank_0 = 0 iff candidate 0 is record number 0
+                int64_t mx = (hh == 0 && first_cand == 0) ? 0 : -1;
+                std::vector<int64_t> ranks;
+                for (int64_t k = 1; k <= K; k++) {
+                    mx = std::max(mx, h[k - 1]);
+                    const int64_t rk = k + mx;
+                    if (rk >= n_cand) break;
+                    ranks.push_back(rk);
+                }
+                n_split = (int64_t)ranks.size();
+                if (n_split > 0) {
+                    int64_t* d_ranks = rj;                 // reuse: K >= n_split
+                    d_split = rj + K + 1;                  // needs n_split <= K + 1 entries
+                    HIP_CHECK(hipMemcpyAsync(d_ranks, ranks.data(), sizeof(int64_t) * n_split, hipMemcpyHostToDevice, st));
+                    hipLaunchKernelGGL(idx_rank_kernel, dim3(blocks_for(n_split, 256)), dim3(256), 0, st, (const int64_t*)d_ranks,
+                                       n_split, (const int64_t*)cand, d_split);
+                    HIP_CHECK(hipGetLastError());
+                }
+            } else {
+                // chain walk by one wave: records (hierarchical) or size with the split reset
+                HIP_CHECK(hipMallocAsync(&blk2.p, sizeof(int64_t) * (n_cand + 2), st));
+                d_split = (int64_t*)blk2.p + 1;
+                hipLaunchKernelGGL(idx_walk_kernel, dim3(1), dim3(64), 0, st, ia, (const int64_t*)cand, n_cand, N > 0 ? 0 : 2, N,
+                                   S, d_split, n_cand, (int64_t*)blk2.p);
+                HIP_CHECK(hipGetLastError());
+                HIP_CHECK(hipMemcpyAsync(&n_split, blk2.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+            }
+        }
+        if (!split_idx.empty()) {
+            n_split = (int64_t)split_idx.size();
+            HIP_CHECK(hipMallocAsync(&blk2.p, sizeof(int64_t) * n_split, st));
+            d_split = (int64_t*)blk2.p;
+            HIP_CHECK(hipMemcpyAsync(d_split, split_idx.data(), sizeof(int64_t) * n_split, hipMemcpyHostToDevice, st));
+        }
+        if (n_split > 0) {
+            AsyncBlock blk3(st);
+            HIP_CHECK(hipMallocAsync(&blk3.p, sizeof(int64_t) * 2 * n_split, st));
+            int64_t* d_from = (int64_t*)blk3.p;
+            int64_t* d_recno = d_from + n_split;
+            hipLaunchKernelGGL(idx_gather_kernel, dim3(blocks_for(n_split, 256)), dim3(256), 0, st, (const int64_t*)d_split,
+                               n_split, d_rec_off, prm->header_bytes, (int32_t)hh, d_from, d_recno);
+            HIP_CHECK(hipGetLastError());
+            from.resize(1 + n_split);
+            recno.resize(1 + n_split);
+            HIP_CHECK(hipMemcpyAsync(from.data() + 1, d_from, sizeof(int64_t) * n_split, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(recno.data() + 1, d_recno, sizeof(int64_t) * n_split, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+        }
+    }
+    const int64_t n = (int64_t)from.size();
+    *n_entries = n;
+    if (n > capacity) return fail(CBX_E_CAPACITY, "index capacity " + std::to_string(capacity) + " < " + std::to_string(n));
+    for (int64_t k = 0; k < n; k++) {
+        entries[k].offset_from = from[k];
+        entries[k].offset_to = k + 1 < n ? from[k + 1] : -1;
+        entries[k].record_index = recno[k];
+        entries[k].file_id = prm->file_id;
+        entries[k].reserved = 0;
+    }
     return CBX_OK;
 }

@@ -69,11 +69,23 @@ __device__ __forceinline__ uint4 load16_guarded(const uint8_t* data, int64_t ga,
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// FixedLenNestedRowIterator.getSegmentId / VRLRecordReader.getSegmentId:
-// extractPrimitiveField(field).toString.trim, looked up in the segment-redefine map.
-__device__ int segment_of(const KernelArgs& a, const uint32_t* lut, const uint8_t* rec, int avail) {
-    const CBX_CONST cbx_segment_map* m = a.segmap;
-    int o = a.start_off + m->field_offset;
+// FixedLenNestedRowIterator.getSegmentId / VRLRecordReader.getSegmentId (VRLRecordReader.scala:188-198):
+// extractPrimitiveField(field, record, start_off).toString.trim, looked up in the segment map's
+// keys.  Returns the key index, -1 when no key matches.  A string field is compared as trimmed
+// UTF-8 text; an integral field by value (its decimal text equals a key exactly when the key is
+// that integer written canonically); a null value is the empty id "".
+__device__ int segment_key(const CBX_CONST cbx_segment_map* m, const uint32_t* lut, const CBX_CONST Field* fields,
+                           const uint8_t* rec, int avail, int start_off) {
+    int o = start_off + m->field_offset;
+    if (m->field_is_int) {
+        const Field f = ldc(fields + m->field);
+        Val v = null_val();
+        if (o + f.size <= avail) v = decode_count_int(f, rec + o);
+        for (int k = 0; k < m->n_keys; k++) {
+            if (v.valid ? (m->key_is_int[k] && m->key_int[k] == (int64_t)v.lo) : m->key_len[k] == 0) return k;
+        }
+        return -1;
+    }
     int n = m->field_size;
     if (o > avail) o = avail;
     if (o + n > avail) n = avail - o;
@@ -96,9 +108,14 @@ __device__ int segment_of(const KernelArgs& a, const uint32_t* lut, const uint8_
                 pos++;
             }
         }
-        if (eq && pos == kl) return m->key_segment[k];
+        if (eq && pos == kl) return k;
     }
     return -1;
+}
+
+__device__ __forceinline__ int segment_of(const KernelArgs& a, const uint32_t* lut, const uint8_t* rec, int avail) {
+    const int k = segment_key(a.segmap, lut, a.fields, rec, avail, a.start_off);
+    return k >= 0 ? a.segmap->key_segment[k] : -1;
 }
 
 __device__ __forceinline__ void store_value(const DevColumn& c, int out_type, int64_t v, const Val& x) {
@@ -391,7 +408,9 @@ __device__ __forceinline__ void decode_generated(const KernelArgs& a, const Wind
     for (int i = w.gen_begin; i < w.gen_end; i++) {
         const GenOp g = ldc(a.gops + i);
         const DevColumn col = ldc(a.cols + g.column);
-        Val x{g.kind == CBX_K_RECORD_ID ? (uint64_t)(a.first_record_id + t.rec) : (uint64_t)(int64_t)a.file_id, 0, true};
+        // Record_Id: the selection's per-record ids (cbx_decode_selected), else first_record_id + r
+        const int64_t rid = a.rec_id ? (t.active ? a.rec_id[t.rec] : 0) : a.first_record_id + t.rec;
+        Val x{g.kind == CBX_K_RECORD_ID ? (uint64_t)rid : (uint64_t)(int64_t)a.file_id, 0, true};
         if (t.active) store_value(col, g.out_type, t.rec, x);
         const uint64_t m = __ballot(t.active);
         if (lane == 0) gp(col.validity)[t.tile] = m;
@@ -627,7 +646,8 @@ __device__ __forceinline__ TileCtx tile_ctx(const KernelArgs& a, int64_t tile, i
 __device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, const uint8_t* rp, int lane,
                                               const uint32_t* s_lut, int32_t* s_cnt) {
     // ---- segment redefine selection
-    if (a.segmap && t.active) t.seg = segment_of(a, s_lut, rp, t.avail);
+    if (a.rec_seg) t.seg = t.active ? a.rec_seg[t.rec] : -1;   // selected records: segment known
+    else if (a.segmap && t.active) t.seg = segment_of(a, s_lut, rp, t.avail);
     if (a.mode == 0 && a.seg_col >= 0) {
         const DevColumn c = ldc(a.cols + a.seg_col);
         if (t.active) gp((int32_t*)c.values)[t.rec] = t.seg;

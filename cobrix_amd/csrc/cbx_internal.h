@@ -102,6 +102,8 @@ struct KernelArgs {
     int32_t stride;            // fixed: record stride (avail length)
     int32_t start_off;         // record_start_offset
     int64_t first_record_id;
+    const int64_t* rec_id;     // per-record Record_Id (selected records), nullptr: first_record_id + r
+    const int32_t* rec_seg;    // per-record active segment (selected records), nullptr: from segmap
     int32_t file_id;
     int32_t mode;              // 0 decode, 1 string sizes only
     // fixed-length contiguous staging: the tile's byte span is loaded with 16-byte loads and

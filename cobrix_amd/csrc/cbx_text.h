@@ -13,7 +13,8 @@
 // a longer one starts with forced records whose lengths follow from the previous line ending
 // (closed form below).  A CR counts as part of the line ending only when it lies inside the
 // record that ends at the LF, so the line-ending length depends on where the previous segment's
-// last record started: a segment walks back only while that dependence is real (rare).  Passes: LF count per 16 KiB chunk (one wave each) -> scan -> LF positions -> per-segment
+// last record started: a scan of per-segment maps over {1, 2} resolves it.  Passes: LF count per
+// 16 KiB chunk (one wave each) -> scan -> LF positions -> line-ending map scan -> per-segment
 // record counts -> scan -> records; the final record after the last LF (its length depends on
 // the virtual length) is settled by the host.
 #pragma once
@@ -105,18 +106,69 @@ __device__ __forceinline__ int text_seg_out(const uint8_t* data, const int64_t* 
     return text_eol_len(data, lf[i], text_final_start(s0, lf[i], M, f, &c));
 }
 
-// Line-ending length of the EOL before segment j (1 before the first record, :31).  Walks back
-// only while a segment's result depends on its input (a long segment whose last record starts
-// right at a CR): short segments and almost all long ones map both inputs to the same length.
-__device__ int text_footer_before(const uint8_t* data, const int64_t* lf, int64_t j, int64_t M) {
-    int64_t k = j - 1;
-    int f = 1;
-    for (; k >= 0; k--) {
-        const int a = text_seg_out(data, lf, k, M, 1), b = text_seg_out(data, lf, k, M, 2);
-        if (a == b) { f = a; break; }
+// Line-ending length of the EOL before every segment (1 before the first record, :31).  Segment i
+// maps the length before it, f in {1, 2}, to the length of its own line ending: a 2-bit map
+// (bit 0: f = 1 -> 2, bit 1: f = 2 -> 2).  The lengths are an exclusive scan of those maps under
+// composition, applied to f = 1 -- three passes (block compositions, their scan, apply), linear
+// in the segment count whatever the data (long lines ending right after a CR chain every
+// segment's result to its predecessor's).
+constexpr int kEolThreads = 256;
+constexpr int kEolItems = 8;
+constexpr int kEolTile = kEolThreads * kEolItems;
+
+__device__ __forceinline__ uint32_t eol_map(const uint8_t* data, const int64_t* lf, int64_t i, int64_t M) {
+    return (text_seg_out(data, lf, i, M, 1) == 2 ? 1u : 0u) | (text_seg_out(data, lf, i, M, 2) == 2 ? 2u : 0u);
+}
+__device__ __forceinline__ uint32_t eol_apply(uint32_t m, uint32_t f) { return ((m >> (f - 1)) & 1u) ? 2u : 1u; }
+// a then b
+__device__ __forceinline__ uint32_t eol_compose(uint32_t a, uint32_t b) {
+    return (eol_apply(b, eol_apply(a, 1)) == 2 ? 1u : 0u) | (eol_apply(b, eol_apply(a, 2)) == 2 ? 2u : 0u);
+}
+constexpr uint32_t kEolIdentity = 2u;   // 1 -> 1, 2 -> 2
+
+// pass 0: composition of each tile's maps -> tot[tile]; pass 2: f before every segment j <= n_lf,
+// starting from the tile's incoming map pre[tile]
+__global__ __launch_bounds__(kEolThreads) void text_eol_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ lf,
+                                                               int64_t n_lf, int64_t M, int pass, uint8_t* __restrict__ tot,
+                                                               const uint8_t* __restrict__ pre, uint8_t* __restrict__ f_before) {
+    __shared__ uint8_t s_m[kEolThreads];
+    const int64_t i0 = (int64_t)blockIdx.x * kEolTile + (int64_t)threadIdx.x * kEolItems;
+    uint32_t maps[kEolItems];
+    uint32_t acc = kEolIdentity;
+#pragma unroll
+    for (int k = 0; k < kEolItems; k++) {
+        maps[k] = i0 + k < n_lf ? eol_map(data, lf, i0 + k, M) : kEolIdentity;
+        acc = eol_compose(acc, maps[k]);
     }
-    for (int64_t i = k + 1; i < j; i++) f = text_seg_out(data, lf, i, M, f);
-    return f;
+    s_m[threadIdx.x] = (uint8_t)acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {   // exclusive scan of the threads' compositions (in place)
+        uint32_t run = kEolIdentity;
+        for (int t = 0; t < kEolThreads; t++) {
+            const uint32_t x = s_m[t];
+            s_m[t] = (uint8_t)run;
+            run = eol_compose(run, x);
+        }
+        if (pass == 0) tot[blockIdx.x] = (uint8_t)run;
+    }
+    __syncthreads();
+    if (pass == 0) return;
+    uint32_t f = eol_apply(eol_compose(pre[blockIdx.x], s_m[threadIdx.x]), 1);
+#pragma unroll
+    for (int k = 0; k < kEolItems; k++) {
+        if (i0 + k <= n_lf) f_before[i0 + k] = (uint8_t)f;
+        f = eol_apply(maps[k], f);
+    }
+}
+
+// pass 1: exclusive scan of the tile compositions (one thread: a tile covers 2048 segments)
+__global__ void text_eol_scan_kernel(uint8_t* tot, int64_t n_tiles) {
+    uint32_t run = kEolIdentity;
+    for (int64_t t = 0; t < n_tiles; t++) {
+        const uint32_t x = tot[t];
+        tot[t] = (uint8_t)run;
+        run = eol_compose(run, x);
+    }
 }
 
 // One thread per segment j in [0, n_lf]: segment n_lf is the tail after the last LF (forced
@@ -127,12 +179,13 @@ __global__ __launch_bounds__(256) void text_seg_kernel(const uint8_t* __restrict
                                                        int mode, uint32_t* __restrict__ cnt,
                                                        const int64_t* __restrict__ base, int64_t* __restrict__ rec_off,
                                                        int32_t* __restrict__ rec_len, int64_t* __restrict__ tail_start,
-                                                       unsigned long long* __restrict__ big, int32_t big_ok) {
+                                                       unsigned long long* __restrict__ big, int32_t big_ok,
+                                                       const uint8_t* __restrict__ f_before) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j > n_lf) return;
     const int64_t s0 = j > 0 ? lf[j - 1] + 1 : 0;
     const bool tail = j == n_lf;
-    const int f = text_footer_before(data, lf, j, M);
+    const int f = f_before[j];
     int64_t c, fs;
     if (!tail) {
         fs = text_final_start(s0, lf[j], M, f, &c);
@@ -179,10 +232,10 @@ __global__ __launch_bounds__(256) void text_forced_kernel(const uint8_t* __restr
                                                           const int64_t* __restrict__ lf, int64_t n_lf, int64_t M,
                                                           const unsigned long long* __restrict__ big,
                                                           const int64_t* __restrict__ base, int64_t* __restrict__ rec_off,
-                                                          int32_t* __restrict__ rec_len) {
+                                                          int32_t* __restrict__ rec_len, const uint8_t* __restrict__ f_before) {
     const int64_t j = (int64_t)big[1 + blockIdx.x];
     const int64_t s0 = j > 0 ? lf[j - 1] + 1 : 0;
-    const int f = text_footer_before(data, lf, j, M);
+    const int f = f_before[j];
     int64_t c;
     if (j < n_lf) {
         text_final_start(s0, lf[j], M, f, &c);

@@ -17,6 +17,8 @@ LIB_PATH = os.path.join(_HERE, "libcobrix_hip_%s.so" % os.environ["CBX_LIB_VARIA
 CBX_MAX_DIMS = 4
 CBX_MAX_SEG_KEYS = 32
 CBX_MAX_SEG_KEY_LEN = 32
+CBX_MAX_SEG_LEVELS = 8
+CBX_MAX_SEG_PREFIX = 64
 
 # kinds / out types / flags (keep in sync with include/cobrix_hip.h)
 K_STRING, K_STRING_ASCII, K_HEX, K_RAW, K_BCD, K_BINARY, K_ZONED = 1, 2, 3, 4, 5, 6, 7
@@ -35,8 +37,9 @@ OUT_WIDTH = {O_I32: 4, O_I64: 8, O_DEC64: 8, O_DEC128: 16, O_F32: 4, O_F64: 8}
 EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx_plan_destroy",
                     "cbx_string_bound", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
                     "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
-                    "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text")
-ABI_VERSION = 4
+                    "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text",
+                    "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected")
+ABI_VERSION = 5
 
 
 class NativeLibraryError(RuntimeError):
@@ -71,7 +74,14 @@ class CbxSegmentMap(ctypes.Structure):
     _fields_ = [("field_offset", ctypes.c_int32), ("field_size", ctypes.c_int32), ("n_keys", ctypes.c_int32),
                 ("key_len", ctypes.c_int32 * CBX_MAX_SEG_KEYS),
                 ("key", (ctypes.c_uint16 * CBX_MAX_SEG_KEY_LEN) * CBX_MAX_SEG_KEYS),
-                ("key_segment", ctypes.c_int32 * CBX_MAX_SEG_KEYS)]
+                ("key_segment", ctypes.c_int32 * CBX_MAX_SEG_KEYS),
+                ("key_level", ctypes.c_int32 * CBX_MAX_SEG_KEYS),
+                ("key_in_filter", ctypes.c_int32 * CBX_MAX_SEG_KEYS),
+                ("key_is_int", ctypes.c_int32 * CBX_MAX_SEG_KEYS),
+                ("key_int", ctypes.c_int64 * CBX_MAX_SEG_KEYS),
+                ("field", ctypes.c_int32), ("field_is_int", ctypes.c_int32), ("n_levels", ctypes.c_int32),
+                ("has_filter", ctypes.c_int32), ("level_column", ctypes.c_int32 * CBX_MAX_SEG_LEVELS),
+                ("prefix_len", ctypes.c_int32), ("prefix", ctypes.c_uint8 * CBX_MAX_SEG_PREFIX)]
 
 
 class CbxPlanOptions(ctypes.Structure):
@@ -90,6 +100,24 @@ class CbxColumn(ctypes.Structure):
 class CbxRdwParams(ctypes.Structure):
     _fields_ = [("big_endian", ctypes.c_int32), ("adjustment", ctypes.c_int32),
                 ("file_header_bytes", ctypes.c_int32), ("file_footer_bytes", ctypes.c_int32)]
+
+
+class CbxIndexEntry(ctypes.Structure):
+    _fields_ = [("offset_from", ctypes.c_int64), ("offset_to", ctypes.c_int64), ("record_index", ctypes.c_int64),
+                ("file_id", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class CbxIndexParams(ctypes.Structure):
+    _fields_ = [("records_per_entry", ctypes.c_int64), ("bytes_per_entry", ctypes.c_int64),
+                ("subtract_size", ctypes.c_int32), ("header_bytes", ctypes.c_int32),
+                ("has_file_header", ctypes.c_int32), ("hierarchical", ctypes.c_int32),
+                ("file_id", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class CbxSelection(ctypes.Structure):
+    _fields_ = [("rec_off", ctypes.c_void_p), ("rec_len", ctypes.c_void_p), ("record_id", ctypes.c_void_p),
+                ("segment", ctypes.c_void_p), ("seg_state", ctypes.c_void_p), ("file_id", ctypes.c_int32),
+                ("footer_bytes", ctypes.c_int32)]
 
 
 _lib = None
@@ -128,6 +156,9 @@ def load():
     L.cbx_plan_kernel_times.argtypes = [P, P, P, i32, P]
     L.cbx_plan_kernel_kind.argtypes = [P, P]
     L.cbx_plan_specialize.argtypes = [P, P, i64, P, i32]
+    L.cbx_sparse_index.argtypes = [P, P, i64, P, P, i64, P, P, i64, P, P]
+    L.cbx_select_records.argtypes = [P, P, i64, P, P, i64, i32, P, i32, P, P, P]
+    L.cbx_decode_selected.argtypes = [P, P, i64, P, i64, i32, P, P]
     if L.cbx_abi_version() != ABI_VERSION:
         raise NativeLibraryError(f"{LIB_PATH}: ABI {L.cbx_abi_version()} != {ABI_VERSION}; rebuild it")
     _lib = L

@@ -12,8 +12,9 @@ int32 "active segment" column, plus generated File_Id / Record_Id.
 from __future__ import annotations
 
 import ctypes
+import re
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import copybook as cbk
 from . import native as N
@@ -50,6 +51,7 @@ class DecodePlan:
     segment_column: int = -1
     record_id_column: int = -1
     file_id_column: int = -1
+    seg_id_columns: List[int] = field(default_factory=list)   # Seg_Id0.. string columns
 
     @property
     def n_columns(self) -> int:
@@ -124,9 +126,27 @@ def _kind_and_flags(p: cbk.Primitive, cb: cbk.Copybook) -> Tuple[int, int]:
     raise UnsupportedLayout(f"{p.name}: usage {d.compact}")
 
 
+_CANONICAL_INT = re.compile(r"^-?(0|[1-9][0-9]*)$")
+
+
+def segment_keys(redefine_map: Dict[str, str], levels: List[str], seg_filter: Optional[List[str]]) -> List[str]:
+    """Distinct segment ids named by the options, in a fixed order: levels, redefine map, filter."""
+    keys: List[str] = []
+    for lv in levels:
+        for k in lv.split(","):
+            if k not in keys:
+                keys.append(k)
+    for k in list(redefine_map) + list(seg_filter or []):
+        if k not in keys:
+            keys.append(k)
+    return keys
+
+
 def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
                segment_redefine_map: Optional[Dict[str, str]] = None, generate_record_id: bool = False,
-               file_id: int = 0, window_bytes: int = 0, jit_min_records: int = 0) -> DecodePlan:
+               file_id: int = 0, window_bytes: int = 0, jit_min_records: int = 0,
+               segment_levels: Sequence[str] = (), segment_filter: Optional[List[str]] = None,
+               segment_prefix: str = "") -> DecodePlan:
     fields: List[N.CbxField] = []
     arrays: List[N.CbxArray] = []
     columns: List[ColumnInfo] = []
@@ -220,26 +240,61 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
 
     opts = N.CbxPlanOptions()
     seg_col = -1
-    if segment_field is not None and segment_redefine_map:
+    levels = list(segment_levels) if segment_field is not None else []
+    seg_filter = segment_filter if segment_field is not None else None
+    red = dict(segment_redefine_map or {}) if segment_field is not None else {}
+    seg_id_cols: List[int] = []
+    if segment_field is not None and (red or levels or seg_filter is not None):
+        # the segment map (cobrix_hip.h cbx_segment_map): every key the options name, with what
+        # each option says about it (redefine group, Seg_Id level, filter membership)
         sf = cb.get_field_by_name(segment_field)
-        if not isinstance(sf, cbk.Primitive) or not isinstance(sf.dtype, cbk.AlphaNumeric) or sf.dtype.enc != cbk.EBCDIC:
-            raise UnsupportedLayout("segment field must be an EBCDIC alphanumeric field")
-        if len(segment_redefine_map) > N.CBX_MAX_SEG_KEYS:
+        if not isinstance(sf, cbk.Primitive):
+            raise UnsupportedLayout("segment field must be a primitive field")
+        field_is_int = isinstance(sf.dtype, cbk.Integral) and sf.dtype.precision <= 18
+        if not field_is_int and not (isinstance(sf.dtype, cbk.AlphaNumeric) and
+                                     (sf.dtype.enc == cbk.EBCDIC or (sf.dtype.enc == cbk.ASCII and _charset_strings(cb)))):
+            raise UnsupportedLayout("segment field must be an EBCDIC (or charset ASCII) string or an integral field")
+        if sf.is_array:
+            raise UnsupportedLayout("segment field must not be an OCCURS array")
+        keys = segment_keys(red, levels, seg_filter)
+        if len(keys) > N.CBX_MAX_SEG_KEYS:
             raise UnsupportedLayout("too many segment ids")
+        if len(levels) > N.CBX_MAX_SEG_LEVELS:
+            raise UnsupportedLayout("too many segment id levels")
+        pre = segment_prefix.encode("utf-8")
+        if len(pre) > N.CBX_MAX_SEG_PREFIX:
+            raise UnsupportedLayout("segment_id_prefix too long")
+        level_sets = [lv.split(",") for lv in levels]
         opts.has_segments = 1
         sm = opts.segments
-        sm.field_offset, sm.field_size, sm.n_keys = sf.offset, sf.actual_size, len(segment_redefine_map)
-        for k, (key, grp) in enumerate(segment_redefine_map.items()):
+        sm.field_offset, sm.field_size, sm.n_keys = sf.offset, sf.actual_size, len(keys)
+        sm.field = field_of_node.get(id(sf), -1)
+        sm.field_is_int = int(field_is_int)
+        if field_is_int and sm.field < 0:
+            raise UnsupportedLayout("integral segment field is not decoded (FILLER)")
+        for k, key in enumerate(keys):
             u = [ord(c) for c in key]
             if len(u) > N.CBX_MAX_SEG_KEY_LEN:
                 raise UnsupportedLayout("segment id too long")
             for j, x in enumerate(u):
                 sm.key[k][j] = x
             sm.key_len[k] = len(u)
-            gname = cbk._transform_identifier(grp).upper()
-            matches = [i for i, g in enumerate(seg_groups) if g.name.upper() == gname]
-            sm.key_segment[k] = matches[0] if matches else -1
-        seg_col = add_column(kind="segment", out_type=N.O_I32)
+            sm.key_segment[k] = -1
+            if key in red:
+                gname = cbk._transform_identifier(red[key]).upper()
+                matches = [i for i, g in enumerate(seg_groups) if g.name.upper() == gname]
+                sm.key_segment[k] = matches[0] if matches else -1
+            sm.key_level[k] = next((i for i, ids in enumerate(level_sets) if key in ids), -1)
+            sm.key_in_filter[k] = int(seg_filter is not None and key in seg_filter)
+            if field_is_int and _CANONICAL_INT.match(key) and -(1 << 63) <= int(key) < (1 << 63):
+                sm.key_is_int[k], sm.key_int[k] = 1, int(key)
+        sm.n_levels = len(levels)
+        sm.has_filter = int(seg_filter is not None)
+        sm.prefix_len = len(pre)
+        for j, b in enumerate(pre):
+            sm.prefix[j] = b
+        if red:
+            seg_col = add_column(kind="segment", out_type=N.O_I32)
     rid_col = fid_col = -1
     if generate_record_id:
         fid_col = add_column(kind="file_id", out_type=N.O_I32)
@@ -250,6 +305,12 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
         f = N.CbxField()
         f.kind, f.out_type, f.segment, f.column = N.K_RECORD_ID, N.O_I64, -1, rid_col
         fields.append(f)
+    for lv in range(len(levels) if opts.has_segments else 0):
+        c = add_column(kind="seg_id", out_type=N.O_STRING)
+        opts.segments.level_column[lv] = c
+        seg_id_cols.append(c)
+    for lv in range(len(levels) if opts.has_segments else 0, N.CBX_MAX_SEG_LEVELS):
+        opts.segments.level_column[lv] = -1
     opts.n_columns = len(columns)
     opts.file_id = file_id
     opts.window_bytes = window_bytes
@@ -259,7 +320,7 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
     for i in range(256):
         opts.lut[i] = int(lut[i])
     return DecodePlan(cb, fields, arrays, columns, opts, field_of_node, array_of_node, seg_groups,
-                      seg_col, rid_col, fid_col)
+                      seg_col, rid_col, fid_col, seg_id_cols)
 
 
 def _iter_prims(g: cbk.Group):

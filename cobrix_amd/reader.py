@@ -201,6 +201,8 @@ class DecodedBatch:
             if self.generate_record_id:
                 row["File_Id"] = value(plan.file_id_column, 0, r)
                 row["Record_Id"] = value(plan.record_id_column, 0, r)
+            for lv, ci in enumerate(plan.seg_id_columns):
+                row[f"Seg_Id{lv}"] = value(ci, 0, r)
             if self.collapse_root:
                 for _, v in recs:
                     row.update(v)
@@ -275,15 +277,23 @@ def reader_schema(cb: cbk.Copybook, params: ReaderParameters, variable_length: b
 
 
 class _BaseReader:
+    VARIABLE_LENGTH = False
+
     def __init__(self, copybook_contents: str, params: ReaderParameters):
         self.params = params
         self.copybook = parse_copybook_for(copybook_contents, params)
         if params.variable_size_occurs:
             raise N.CbxError(N.CBX_E_UNSUPPORTED, "variable_size_occurs=true is not on the GPU path yet")
+        var = self.VARIABLE_LENGTH
+        # the fixed-length reader only uses the redefine map (FixedLenNestedRowIterator.scala:50-70);
+        # segment levels, filter and record ids belong to the variable-length iterator
         self.plan = build_plan(self.copybook, segment_field=params.segment_field,
                                segment_redefine_map=params.segment_id_redefine_map or None,
-                               generate_record_id=params.generate_record_id, window_bytes=params.window_bytes,
-                               jit_min_records=params.jit_min_records)
+                               generate_record_id=params.generate_record_id and var, window_bytes=params.window_bytes,
+                               jit_min_records=params.jit_min_records,
+                               segment_levels=params.segment_id_levels if var else (),
+                               segment_filter=params.segment_id_filter if var else None,
+                               segment_prefix=params.segment_id_prefix)
         self.native = NativePlan(self.plan)
 
     @property
@@ -291,7 +301,7 @@ class _BaseReader:
         return self.params.schema_policy == "collapse_root"
 
     def spark_schema(self):
-        return spark_schema(self.copybook, self.collapse_root, self.params.generate_record_id)
+        return reader_schema(self.copybook, self.params, self.VARIABLE_LENGTH)
 
     def close(self):
         self.native.close()
@@ -345,7 +355,7 @@ class FixedLenNestedReader(_BaseReader):
         N.check(L.cbx_decode_fixed(self.native.handle, d_data.data_ptr(), n_rec, stride, self.params.start_offset,
                                    first_record_id, cs, ctypes.c_void_p(st.cuda_stream)))
         N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
-        return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, self.params.generate_record_id)
+        return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, False)
 
     def decode(self, data: bytes, first_record_id: int = 0) -> DecodedBatch:
         torch = _torch()
@@ -358,7 +368,13 @@ class FixedLenNestedReader(_BaseReader):
 
 
 class VarLenNestedReader(_BaseReader):
-    """GPU drop-in for VarLenNestedReader (CP/reader/VarLenNestedReader.scala:46-310), RDW framing."""
+    """GPU drop-in for VarLenNestedReader (CP/reader/VarLenNestedReader.scala:46-310).
+
+    Pipeline per file (what CobolScanners.buildScanForVarLenIndex runs as one Spark task per index
+    entry, SC/source/scanners/CobolScanners.scala:38-55): frame (RDW walk / text lines / fixed-length
+    records) -> sparse index (IndexGenerator) -> record selection (VarLenNestedIterator: Record_Id,
+    Seg_IdN, segment_filter, root-reached) -> decode.  Every stage runs on the GPU."""
+    VARIABLE_LENGTH = True
 
     def rdw_params(self) -> N.CbxRdwParams:
         p = self.params
@@ -369,11 +385,12 @@ class VarLenNestedReader(_BaseReader):
         r.file_footer_bytes = p.file_end_offset
         return r
 
+    # ---- framing
     def frame_text(self, d_data, n_bytes: int, stream=None):
         """GPU text framing (TextRecordExtractor.scala:26-108) -> (rec_off, rec_len, virtual_bytes).
 
         Records may reach past n_bytes up to virtual_bytes (the reference's zero-filled window):
-        d_data must hold zeros there (see `decode`)."""
+        d_data must hold zeros there (see `read`)."""
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream()
         cap = n_bytes + 2
@@ -402,8 +419,128 @@ class VarLenNestedReader(_BaseReader):
                                         ctypes.c_void_p(st.cuda_stream)))
         return off[: n.value], ln[: n.value]
 
+    def frame_fixed(self, d_data, n_bytes: int):
+        """RecordHeaderParserFixedLen (CP/parser/headerparsers/RecordHeaderParserFixedLen.scala:40-50)
+        through VRLRecordReader: a file header record, then records of the copybook's size while
+        a whole record remains and the rest is not the footer."""
+        torch = _torch()
+        p = self.params
+        rs = self.copybook.record_size
+        first = p.file_start_offset
+        n = 0
+        if n_bytes - first >= rs:
+            # record k valid iff n_bytes - off_k >= rs and (no footer or n_bytes - off_k > footer)
+            lim = n_bytes - rs
+            if p.file_end_offset > 0:
+                lim = min(lim, n_bytes - p.file_end_offset - 1)
+            n = max(0, (lim - first) // rs + 1) if lim >= first else 0
+        off = first + rs * torch.arange(n, dtype=torch.int64, device=d_data.device)
+        ln = torch.full((n,), rs, dtype=torch.int32, device=d_data.device)
+        return off, ln
+
+    def header_bytes(self) -> int:
+        return 4 if self.params.is_record_sequence else 0
+
+    def has_file_header(self) -> bool:
+        p = self.params
+        return p.file_start_offset > (4 if p.is_record_sequence else 0)
+
+    # ---- sparse index
+    def index_params(self, file_id: int = 0) -> N.CbxIndexParams:
+        """VarLenNestedReader.generateIndex split parameters (:125-180, getSplitSizeMB :237-243)."""
+        p = self.params
+        prm = N.CbxIndexParams()
+        split_mb = p.input_split_size_mb if p.input_split_size_mb is not None else p.hdfs_default_block_size_mb
+        if p.input_split_records is not None:
+            if not 1 <= p.input_split_records <= 1000000000:
+                raise ValueError(f"Invalid input split size. The requested number of records is {p.input_split_records}.")
+            prm.records_per_entry = p.input_split_records
+        elif split_mb is not None:
+            if not 1 <= split_mb <= 2000:
+                raise ValueError(f"Invalid input split size of {split_mb} MB.")
+            prm.bytes_per_entry, prm.subtract_size = split_mb * 1024 * 1024, 1
+        else:
+            prm.bytes_per_entry, prm.subtract_size = 100 * 1024 * 1024, 0   # Constants.defaultIndexEntrySizeMB
+        prm.header_bytes = self.header_bytes()
+        prm.has_file_header = int(self.has_file_header())
+        prm.hierarchical = int(bool(p.segment_field) and bool(p.segment_id_levels))
+        prm.file_id = file_id
+        return prm
+
+    def generate_index(self, d_data, n_bytes: int, rec_off, rec_len, file_id: int = 0,
+                       stream=None) -> List[SparseIndexEntry]:
+        """GPU sparse index over the framed file (IndexGenerator.sparseIndexGenerator)."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream()
+        prm = self.index_params(file_id)
+        L = N.load()
+        n = ctypes.c_int64(0)
+        cap = 1024
+        while True:
+            ents = (N.CbxIndexEntry * cap)()
+            rc = L.cbx_sparse_index(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(),
+                                    rec_len.data_ptr(), int(rec_off.numel()), ctypes.byref(prm), ents, cap,
+                                    ctypes.byref(n), ctypes.c_void_p(st.cuda_stream))
+            if rc == N.CBX_E_CAPACITY and n.value > cap:
+                cap = n.value
+                continue
+            N.check(rc)
+            break
+        return [SparseIndexEntry(e.offset_from, e.offset_to, e.file_id, e.record_index) for e in ents[: n.value]]
+
+    def index_generation_needed(self) -> bool:
+        """VarLenNestedReader.isIndexGenerationNeeded (:85): no record length field on this path."""
+        return self.params.enable_indexes
+
+    # ---- selection + decode
+    def select(self, d_data, n_bytes: int, rec_off, rec_len, entries: Optional[Sequence[SparseIndexEntry]] = None,
+               file_id: int = 0, stream=None) -> Dict[str, Any]:
+        """VarLenNestedIterator over every entry: Record_Id, Seg_IdN state, filters (GPU)."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream()
+        n = int(rec_off.numel())
+        dev = d_data.device
+        nl = self.plan.options.segments.n_levels if self.plan.options.has_segments else 0
+        sel = {"rec_off": torch.empty(max(1, n), dtype=torch.int64, device=dev),
+               "rec_len": torch.empty(max(1, n), dtype=torch.int32, device=dev),
+               "record_id": torch.empty(max(1, n), dtype=torch.int64, device=dev),
+               "segment": torch.empty(max(1, n), dtype=torch.int32, device=dev),
+               "seg_state": torch.empty(max(1, n * (1 + nl)), dtype=torch.int64, device=dev)}
+        cs = N.CbxSelection()
+        for k in ("rec_off", "rec_len", "record_id", "segment", "seg_state"):
+            setattr(cs, k, sel[k].data_ptr())
+        cs.file_id = file_id
+        cs.footer_bytes = self.params.file_end_offset
+        ents = None
+        if entries:
+            ents = (N.CbxIndexEntry * len(entries))()
+            for i, e in enumerate(entries):
+                ents[i].offset_from, ents[i].offset_to = e.offset_from, e.offset_to
+                ents[i].record_index, ents[i].file_id = e.record_index, e.file_id
+        ns = ctypes.c_int64(0)
+        N.check(N.load().cbx_select_records(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(),
+                                            rec_len.data_ptr(), n, self.params.start_offset, ents,
+                                            len(entries) if entries else 0, ctypes.byref(cs), ctypes.byref(ns),
+                                            ctypes.c_void_p(st.cuda_stream)))
+        sel["n"] = ns.value
+        sel["struct"] = cs
+        return sel
+
+    def decode_selected(self, d_data, n_bytes: int, sel: Dict[str, Any], stream=None) -> DecodedBatch:
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream()
+        n_rec = sel["n"]
+        cols, cs = _alloc_columns(self.plan, n_rec, string_capacity(self.native, n_rec), d_data.device)
+        L = N.load()
+        N.check(L.cbx_decode_selected(self.native.handle, d_data.data_ptr(), n_bytes, ctypes.byref(sel["struct"]),
+                                      n_rec, self.params.start_offset, cs, ctypes.c_void_p(st.cuda_stream)))
+        N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
+        return DecodedBatch(self.plan, n_rec, cols, 0, self.collapse_root, self.params.generate_record_id)
+
     def decode_device(self, d_data, n_bytes: int, rec_off, rec_len, first_record_id: int = 0,
                       stream=None, exact_strings: bool = False) -> DecodedBatch:
+        """Decode framed records as one index entry starting at first_record_id, without the
+        selection stage (cbx_decode_var: Record_Id = first_record_id + r)."""
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream()
         n_rec = int(rec_off.numel())
@@ -422,18 +559,43 @@ class VarLenNestedReader(_BaseReader):
         N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
         return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, self.params.generate_record_id)
 
-    def decode(self, data: bytes, seeds: Optional[Sequence[int]] = None, first_record_id: int = 0) -> DecodedBatch:
+    def _device_file(self, data: bytes):
         torch = _torch()
+        extra = self.copybook.record_size + 2 + 16 if self.params.is_text else 0
+        t = torch.zeros(max(16, len(data) + extra), dtype=torch.uint8, device="cuda")
+        if len(data):
+            t[: len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+        return t
+
+    def frame_file(self, t, n_bytes: int):
+        """(rec_off, rec_len, bytes the records are decoded against) of a whole file."""
         if self.params.is_text:
-            # zero tail for records past the data (the reference's zero-filled read window)
-            t = torch.zeros(len(data) + self.copybook.record_size + 2 + 16, dtype=torch.uint8, device="cuda")
-            if len(data):
-                t[: len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+            return self.frame_text(t, n_bytes)
+        if self.params.is_record_sequence:
+            off, ln = self.frame(t, n_bytes)
+            return off, ln, n_bytes
+        off, ln = self.frame_fixed(t, n_bytes)
+        return off, ln, n_bytes
+
+    def read(self, data: bytes, file_id: int = 0) -> DecodedBatch:
+        """A whole file, as the reference reads it: sparse-index entries (when index generation
+        applies) each read by its own VarLenNestedIterator, concatenated in file order."""
+        t = self._device_file(data)
+        off, ln, vb = self.frame_file(t, len(data))
+        entries = None
+        if self.index_generation_needed() and not self.params.is_text:
+            entries = self.generate_index(t, len(data), off, ln, file_id)
+        sel = self.select(t, vb, off, ln, entries, file_id)
+        return self.decode_selected(t, vb, sel)
+
+    def decode(self, data: bytes, seeds: Optional[Sequence[int]] = None, first_record_id: int = 0) -> DecodedBatch:
+        """Frame + decode as one entry (no selection stage)."""
+        t = self._device_file(data)
+        if self.params.is_text:
             off, ln, vb = self.frame_text(t, len(data))
             return self.decode_device(t, vb, off, ln, first_record_id)
-        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda") if len(data) else torch.zeros(16, dtype=torch.uint8, device="cuda")
-        off, ln = self.frame(t, len(data), seeds)
+        off, ln = self.frame(t, len(data), seeds) if self.params.is_record_sequence else self.frame_fixed(t, len(data))
         return self.decode_device(t, len(data), off, ln, first_record_id)
 
     def get_row_iterator(self, data: bytes) -> Iterator[dict]:
-        return iter(self.decode(data).to_rows())
+        return iter(self.read(data).to_rows())

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 4
+#define CBX_ABI_VERSION 5
 
 /* status codes */
 #define CBX_OK 0
@@ -126,17 +126,37 @@ typedef struct {
     int32_t reserved;
 } cbx_array;
 
-/* Segment-redefine selection (FixedLenNestedRowIterator.getSegmentId + redefine map):
- * the trimmed value of the segment-id field (an EBCDIC string field) is compared with each
- * key; a match activates segment `segment`; no match leaves every segment group null. */
+/* Segment ids (the `segment_field` of a multisegment file) and everything keyed by them:
+ *   - segment-redefine selection (FixedLenNestedRowIterator.getSegmentId + redefine map,
+ *     CP/reader/iterator/FixedLenNestedRowIterator.scala:64-99, VarLenNestedIterator.scala:91-93),
+ *   - Seg_IdN generation (segment_id_level0.., SegmentIdAccumulator.scala:19-86),
+ *   - segment_filter and root-reached filtering (VarLenNestedIterator.scala:138-147),
+ *   - root-segment index cuts (IndexGenerator.scala:89-113).
+ * A record's segment id is extractPrimitiveField(field).toString.trim (VRLRecordReader.scala:188-198):
+ * for a string field the trimmed decoded text (compared with the UTF-8 key bytes), for an integral
+ * field the decimal text of its value (keys that are canonical integers are compared by value:
+ * key_is_int / key_int).  Each distinct key carries everything the options say about it. */
 #define CBX_MAX_SEG_KEYS 32
 #define CBX_MAX_SEG_KEY_LEN 32
+#define CBX_MAX_SEG_LEVELS 8
+#define CBX_MAX_SEG_PREFIX 64
 typedef struct {
     int32_t field_offset, field_size;   /* segment-id field (relative to decode base) */
     int32_t n_keys;
     int32_t key_len[CBX_MAX_SEG_KEYS];
     uint16_t key[CBX_MAX_SEG_KEYS][CBX_MAX_SEG_KEY_LEN];  /* UTF-16 code units */
-    int32_t key_segment[CBX_MAX_SEG_KEYS];
+    int32_t key_segment[CBX_MAX_SEG_KEYS];   /* redefine segment the key activates, -1 none */
+    int32_t key_level[CBX_MAX_SEG_KEYS];     /* first segment_id_level listing the key, -1 none */
+    int32_t key_in_filter[CBX_MAX_SEG_KEYS]; /* 1: listed in segment_filter */
+    int32_t key_is_int[CBX_MAX_SEG_KEYS];    /* integral segment field: key is a canonical integer */
+    int64_t key_int[CBX_MAX_SEG_KEYS];
+    int32_t field;           /* index of the segment-id field in the field table */
+    int32_t field_is_int;    /* the segment-id field is integral (compared by value) */
+    int32_t n_levels;        /* segment_id_level count = Seg_IdN columns */
+    int32_t has_filter;      /* segment_filter given */
+    int32_t level_column[CBX_MAX_SEG_LEVELS];   /* output string column of Seg_Id<l>, -1 none */
+    int32_t prefix_len;
+    uint8_t prefix[CBX_MAX_SEG_PREFIX];       /* segment_id_prefix, UTF-8 */
 } cbx_segment_map;
 
 typedef struct {
@@ -247,6 +267,69 @@ typedef struct {
 int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,
                   const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len,
                   int64_t capacity, int64_t* n_records, void* stream);
+
+/* ---- variable-length record streams: sparse index, record selection, selected decode ----
+ *
+ * Sparse index (IndexGenerator.sparseIndexGenerator, CP/reader/index/IndexGenerator.scala:33-157,
+ * called by VarLenNestedReader.generateIndex, CP/reader/VarLenNestedReader.scala:125-180) over a
+ * file already framed on the GPU (cbx_frame_rdw over the whole file, or fixed-length records).
+ * Entries are cut every records_per_entry records, or by size: bytes_per_entry with
+ * subtract_size != 0 (input_split_size_mb / HDFS block size: the split size is subtracted, not
+ * reset), or the 100 MB default (reset); with `hierarchical` only at records whose segment id is
+ * a level-0 key of the plan's segment map.  The first entry is (0, -1, file_id, 0); the last
+ * entry's offset_to is -1.  record_index counts every header read (the file header record too). */
+typedef struct {
+    int64_t offset_from, offset_to;
+    int64_t record_index;
+    int32_t file_id;
+    int32_t reserved;
+} cbx_index_entry;
+
+typedef struct {
+    int64_t records_per_entry;  /* input_split_records; 0 = split by size */
+    int64_t bytes_per_entry;    /* split size in bytes when records_per_entry == 0 */
+    int32_t subtract_size;      /* isSplitBySize: an explicit MB size (subtracted) vs the default (reset) */
+    int32_t header_bytes;       /* record header length: 4 (RDW) or 0 (fixed-length record parser) */
+    int32_t has_file_header;    /* a file-header record precedes the first framed record */
+    int32_t hierarchical;       /* cut only at level-0 segment records (segment levels given) */
+    int32_t file_id;
+    int32_t reserved;
+} cbx_index_params;
+
+int cbx_sparse_index(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                     const int32_t* d_rec_len, int64_t n_rec, const cbx_index_params* params,
+                     cbx_index_entry* entries, int64_t capacity, int64_t* n_entries, void* stream);
+
+/* Record selection over framed records (VarLenNestedIterator.fetchNext + VRLRecordReader record
+ * numbering, CP/reader/iterator/VarLenNestedIterator.scala:80-147, VRLRecordReader.scala:55-74):
+ * records are numbered per index entry (Record_Id = entry.record_index + ordinal inside the entry;
+ * entries = NULL: one entry (0, -1, file_id, 0)), Seg_IdN state is accumulated per entry,
+ * records before the first root of an entry (when segment levels are given) and records outside
+ * segment_filter are dropped.  Output arrays (device, capacity n_rec each) receive the selected
+ * records in file order; seg_state holds (1 + n_levels) int64 per record: the root record id
+ * (-1: no root seen in the entry) then per level -2 (null) or the level counter. */
+typedef struct {
+    int64_t* rec_off;          /* payload offsets */
+    int32_t* rec_len;          /* payload lengths */
+    int64_t* record_id;        /* Record_Id */
+    int32_t* segment;          /* active segment redefine index, -1 none */
+    int64_t* seg_state;        /* [n][1 + n_levels], may be NULL when the plan has no levels */
+    int32_t file_id;           /* File_Id of the batch (written by cbx_decode_selected) */
+    int32_t footer_bytes;      /* in: file_end_offset -- the reference bounds each entry's stream to
+                                  offset_to and its header parser then reads records within
+                                  file_end_offset of that bound as the footer: they are dropped */
+} cbx_selection;
+
+int cbx_select_records(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                       const int32_t* d_rec_len, int64_t n_rec, int32_t start_offset,
+                       const cbx_index_entry* entries, int32_t n_entries, cbx_selection* out,
+                       int64_t* n_selected, void* stream);
+
+/* Decode selected records: as cbx_decode_var, with Record_Id and the active segment taken from
+ * the selection and the Seg_IdN string columns written from its seg_state
+ * (SegmentIdAccumulator.getSegmentLevelId: prefix_fileId_rootRecordId[_L<level>_<counter>]). */
+int cbx_decode_selected(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const cbx_selection* sel,
+                        int64_t n_rec, int32_t start_offset, cbx_column* columns, void* stream);
 
 /* Text record framing (is_text = true) on the GPU: replaces TextRecordExtractor
  * (cobol-parser/.../reader/extractors/raw/TextRecordExtractor.scala:26-108, chosen by

@@ -166,8 +166,11 @@ class Entry:
     record_index: int
 
 
-def sparse_index(cb: cbk.Copybook, data: bytes, p, file_id: int = 0) -> List[Entry]:
-    """VarLenNestedReader.generateIndex (:125-180) -> IndexGenerator.sparseIndexGenerator (:33-157)."""
+def sparse_index(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
+                 default_entry_bytes: Optional[int] = None) -> List[Entry]:
+    """VarLenNestedReader.generateIndex (:125-180) -> IndexGenerator.sparseIndexGenerator (:33-157).
+    default_entry_bytes replaces Constants.defaultIndexEntrySizeMB (tests of the reset rule on
+    small files)."""
     rp = header_parser(cb, p)
     split_records = p.input_split_records
     split_mb = p.input_split_size_mb if p.input_split_size_mb is not None else p.hdfs_default_block_size_mb
@@ -181,7 +184,7 @@ def sparse_index(cb: cbk.Copybook, data: bytes, p, file_id: int = 0) -> List[Ent
     root_ids = root_id.split(",")
     really_hier = seg_reader is not None and is_hier
     split_by_size = split_records is None and split_mb is not None
-    bytes_per = (split_mb if split_mb is not None else DEFAULT_ENTRY_MB) * MEGABYTE
+    bytes_per = split_mb * MEGABYTE if split_mb is not None else (default_entry_bytes or DEFAULT_ENTRY_MB * MEGABYTE)
 
     def need_split(records: int, size: int) -> bool:
         return records >= split_records if split_records is not None else size >= bytes_per

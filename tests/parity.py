@@ -89,3 +89,66 @@ def compare_batch(batch, res: "O.OracleResult", max_report: int = 10) -> List[st
         if len(errs) >= max_report:
             break
     return errs
+
+
+def compare_sample(batch, idx: np.ndarray, res: "O.OracleResult", max_report: int = 10) -> List[str]:
+    """Like compare_batch for a sample of a (large) device batch: res holds the oracle's decode of
+    the records idx (in that order); every value of those records is gathered on the device and
+    compared bit for bit (validity, fixed-width values, string bytes)."""
+    import torch
+    plan = batch.plan
+    ocols = O.columns(res)
+    errs: List[str] = []
+    n = batch.n_rec
+    pitch = 64 * ((n + 63) // 64)
+    words = pitch // 64
+    dev_idx = torch.as_tensor(idx, dtype=torch.int64, device=batch.cols[0]["validity"].device)
+    for ci, info in enumerate(plan.columns):
+        if info.kind != "value" or info.hidden:
+            continue
+        c = batch.cols[ci]
+        o = ocols.get(res.ast.node_of(info.node))
+        exp_valid = np.zeros((info.n_slots, len(idx)), dtype=bool)
+        if o is not None:
+            exp_valid[o["slot"], o["rec"]] = o["valid"]
+        vw = c["validity"].view(info.n_slots, words)
+        for s in range(info.n_slots):
+            w = vw[s, dev_idx // 64]
+            got_valid = ((w >> (dev_idx % 64)) & 1).cpu().numpy().astype(bool)
+            if not np.array_equal(got_valid, exp_valid[s]):
+                k = int(np.nonzero(got_valid != exp_valid[s])[0][0])
+                errs.append(f"{info.node.name}[{s}]: validity differs at record {idx[k]}")
+        if o is None:
+            continue
+        m = o["valid"]
+        rec, slot = o["rec"][m], o["slot"][m]
+        ot = info.out_type
+        if ot in (N.O_STRING, N.O_BINARY):
+            offs = c["offsets"].view(info.n_slots, pitch + 1)
+            for k in range(len(rec)):
+                r, s = int(idx[rec[k]]), int(slot[k])
+                a0, a1 = int(offs[s, r]), int(offs[s, r + 1])
+                got = bytes(c["data"][a0:a1].cpu().numpy())
+                want = res.heap[int(o["lo"][m][k]):int(o["lo"][m][k]) + int(o["hi"][m][k])]
+                if got != want:
+                    errs.append(f"{info.node.name}: string differs at record {r}: {got!r} vs {want!r}")
+                    break
+            continue
+        w = N.OUT_WIDTH[ot]
+        vals = c["values"]
+        pos = torch.as_tensor(slot * pitch + idx[rec], dtype=torch.int64, device=vals.device)
+        lo = o["lo"][m].astype(np.int64)
+        if ot == N.O_DEC128:
+            v2 = vals.view(-1, 2)[pos].cpu().numpy()
+            bad = (v2[:, 0] != lo) | (v2[:, 1] != o["hi"][m].astype(np.int64))
+        elif w == 4:
+            got = vals.view(-1)[pos].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+            bad = got != (lo & 0xFFFFFFFF)
+        else:
+            bad = vals.view(-1)[pos].cpu().numpy().astype(np.int64) != lo
+        if bad.any():
+            k = int(np.nonzero(bad)[0][0])
+            errs.append(f"{info.node.name}: {int(bad.sum())} values differ, first record {idx[rec[k]]}")
+        if len(errs) >= max_report:
+            break
+    return errs

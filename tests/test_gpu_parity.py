@@ -236,12 +236,16 @@ def test_specialised_kernel_segments_and_offsets():
     assert not compare_batch(batch, res)
 
 
-@pytest.mark.parametrize("n", [1, 4097, 50_000])
-def test_synstr200_vs_oracle(n):
-    """Config C3 (string-heavy cp037, trim both): UTF-8 payloads and Arrow offsets bit-exact."""
+@pytest.mark.parametrize("n,jit", [(1, 0), (4097, 0), (50_000, 0), (50_000, 1), (300_001, 0)])
+def test_synstr200_vs_oracle(n, jit):
+    """Config C3 (string-heavy cp037, trim both): UTF-8 payloads and Arrow offsets bit-exact, on
+    both kernels (jit=1 forces the copybook-specialised kernel the bench runs; 300,001 records pass
+    the default specialisation threshold)."""
     from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
     data = synstr200(n, seed=3 + n).numpy().tobytes()
-    rd, batch = _fixed(SYNSTR200_COPYBOOK, data, ebcdic_code_page="cp037")
+    rd, batch = _fixed(SYNSTR200_COPYBOOK, data, ebcdic_code_page="cp037", jit_min_records=jit)
+    if n >= 262_144 or jit == 1:
+        assert _kernel_kind(rd) == 1
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
     assert not errs, errs
 
@@ -265,3 +269,26 @@ def test_wide_odo_vs_oracle():
     res = O.decode_records(rd.copybook, [raw[o:o + l] for o, l in zip(eo, el)], active_segments=segs)
     errs = compare_batch(batch, res)
     assert not errs, errs
+
+
+def test_syn200_full_size_sampled_parity():
+    """The bench's own configuration (C2: 50 M SYN200 records = 10 GB resident in HBM, the
+    copybook-specialised kernel): 6,000 records sampled across the whole batch (random, plus the
+    first and last tiles) are bit-exact against the oracle, and every string offset row is monotone."""
+    from parity import compare_sample
+    n = 50_000_000
+    rec = syn200(n, seed=20261015, device="cuda")
+    rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters())
+    batch = rd.decode_device(rec.view(-1), n * 200)
+    assert _kernel_kind(rd) == 1
+    rng = np.random.default_rng(2)
+    idx = np.unique(np.concatenate([np.arange(128), n - 128 + np.arange(128), rng.integers(0, n, 5744)]))
+    sample = rec[torch.as_tensor(idx, device="cuda")].cpu().numpy().tobytes()
+    errs = compare_sample(batch, idx, O.decode_fixed(rd.copybook, sample))
+    assert not errs, errs
+    for ci, info in enumerate(rd.plan.columns):
+        if info.out_type == 7:   # O_STRING: offsets non-decreasing over all 50 M records
+            offs = batch.cols[ci]["offsets"][: n + 1]
+            assert bool((offs[1:] >= offs[:-1]).all())
+    del batch, rec
+    torch.cuda.empty_cache()

@@ -137,17 +137,49 @@ class TestGpuText:
         np.testing.assert_array_equal(go, oo)
         np.testing.assert_array_equal(gl, ol)
 
+    @pytest.mark.parametrize("rs,n", [(20, 200_000), (7, 400_000)])
+    def test_chained_line_endings(self, rs, n):
+        """Lines of 2 * rs + 2 bytes ending in CR LF: every segment's line-ending length depends on
+        its predecessor's (a forced record ends right at the CR), so any walk back over segments is
+        quadratic here; the map scan is linear."""
+        data = (b"Y" * (2 * rs + 2) + b"\r\n") * n
+        go, gl, gv = self._frame(data, rs)
+        oo, ol, ov = O.frame_text(data, rs)
+        assert gv == ov
+        np.testing.assert_array_equal(go, oo)
+        np.testing.assert_array_equal(gl, ol)
+
+    def test_capacity_reports_required_size(self):
+        import ctypes
+        from cobrix_amd import native as N
+        torch = self.torch
+        data = b"AB\nCD\nEF"
+        t = torch.zeros(64, dtype=torch.uint8, device="cuda")
+        t[: len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+        off = torch.empty(8, dtype=torch.int64, device="cuda")
+        ln = torch.empty(8, dtype=torch.int32, device="cuda")
+        n, vb = ctypes.c_int64(0), ctypes.c_int64(0)
+        rc = N.load().cbx_frame_text(t.data_ptr(), len(data), 3, off.data_ptr(), ln.data_ptr(), 1, ctypes.byref(n),
+                                     ctypes.byref(vb), None)
+        assert rc == N.CBX_E_CAPACITY and n.value >= 2
+        rc = N.load().cbx_frame_text(t.data_ptr(), len(data), 3, off.data_ptr(), ln.data_ptr(), 2, ctypes.byref(n),
+                                     ctypes.byref(vb), None)
+        assert rc == N.CBX_E_CAPACITY and n.value == 3
+
     def test_reference_ascii_text_file_rows(self):
         from cobrix_amd.reader import ReaderParameters, VarLenNestedReader
         rd = VarLenNestedReader(T01_COPYBOOK, ReaderParameters(is_ebcdic=False, is_text=True,
                                                                schema_policy="collapse_root"))
         assert rd.decode(T01_TEXT).to_rows() == T01_EXPECTED
 
-    def test_text_decode_vs_oracle(self):
+    @pytest.mark.parametrize("jit", [0, 1])
+    def test_text_decode_vs_oracle(self, jit):
+        """Text records through the default kernel choice and forced onto the copybook-specialised
+        (windowed) kernel the large var-len batches run."""
         from cobrix_amd.reader import ReaderParameters, VarLenNestedReader
         from parity import compare_batch
         data = _adversarial(np.random.default_rng(9), 300_000)
-        rd = VarLenNestedReader(T01_COPYBOOK, ReaderParameters(is_ebcdic=False, is_text=True))
+        rd = VarLenNestedReader(T01_COPYBOOK, ReaderParameters(is_ebcdic=False, is_text=True, jit_min_records=jit))
         batch = rd.decode(data)
         off, ln, vb = O.frame_text(data, rd.copybook.record_size)
         padded = data + b"\0" * (vb - len(data))
