@@ -2,15 +2,17 @@
 
 `python bench.py --gpus N --steps K --warmup W [--workload syn200|synstr200|rdw_narrow|wide_odo]`
 -- one rank per GPU (torchrun for N > 1); each rank decodes its own shard of records already
-resident in HBM (weak scaling: records are independent, shards need no data-path collective; for
-N > 1 one RCCL all-gather of the shard's row / string-byte counts per step gives the global
-Record_Id and string bases).  Rank 0 prints ONE JSON line.
+resident in HBM (weak scaling: records are independent, shards need no data-path collective;
+fixed-length shards know their Record_Id base statically, variable-length shards get it from one
+RCCL all-gather of their framed record counts per step).  Rank 0 prints ONE JSON line.
 
 A step = one full decode of the shard through the C ABI:
   fixed-length (C2 syn200, C3 synstr200): `cbx_decode_fixed` -- decode kernel (numerics +
       tile-local strings), fixup kernel for deferred values, string scan + placement kernels;
   variable-length (C4 rdw_narrow, C5 wide_odo): `cbx_frame_rdw` (GPU RDW offset discovery seeded
-      by sparse-index entries every 100 MB) + `cbx_decode_var` (segment redefines, ODO).
+      by the sparse-index entries cbx_sparse_index cut at setup, 100 MB at root segments) +
+      `cbx_decode_var` (segment redefines, ODO); for N > 1 one all-gather of the shard's record count
+      between framing and decode gives its Record_Id base.
 
 roofline: algorithmic bytes (input record bytes + every output buffer byte) of one
 decode-kernel launch / its average duration, measured with HIP events recorded by the library on
@@ -86,17 +88,6 @@ WORKLOADS = {
 }
 
 
-def _seeds_every(hdr, is_root, n_bytes: int, every: int):
-    """Sparse-index entry points (IndexGenerator.scala:89-113): the first root-segment header at or
-    after each `every`-byte boundary."""
-    import torch
-    roots = hdr[is_root] if is_root is not None else hdr
-    bounds = torch.arange(0, max(n_bytes, 1), every, device=hdr.device, dtype=torch.int64)
-    pos = torch.searchsorted(roots, bounds)
-    pos = pos[pos < roots.numel()]
-    return sorted(set([0] + roots[pos].tolist()))
-
-
 class _Fixed:
     def __init__(self, name, n_rec, dev, rank, window):
         import torch
@@ -113,6 +104,7 @@ class _Fixed:
         torch.cuda.synchronize()
         self.rd = FixedLenNestedReader(cb, params)
         self.n_rec, self.in_bytes, self.dev = n_rec, n_rec * self.stride, dev
+        self.record_base = rank * n_rec
 
     def prepare(self, stream):
         from cobrix_amd import native as N
@@ -121,10 +113,11 @@ class _Fixed:
         self.cols, self.cs = _alloc_columns(self.rd.plan, self.n_rec, string_capacity(self.rd.native, self.n_rec),
                                             self.dev)
 
-    def step(self):
+    def step(self, world=1):
         from cobrix_amd import native as N
-        N.check(self.L.cbx_decode_fixed(self.h, self.rec.data_ptr(), self.n_rec, self.stride, 0, 0, self.cs,
-                                        self.stream))
+        # fixed-length shards: rank r holds records [r n, (r + 1) n) -- the Record_Id base is static
+        N.check(self.L.cbx_decode_fixed(self.h, self.rec.data_ptr(), self.n_rec, self.stride, 0, self.record_base,
+                                        self.cs, self.stream))
         return None
 
     def end_to_end(self, chunk_rec: int = 2_500_000, passes: int = 2):
@@ -180,6 +173,14 @@ class _Fixed:
 
 
 class _VarLen:
+    """C4 / C5: one file (per rank: its shard, a contiguous run of the global file's index entries).
+
+    Setup (untimed, as the reference's index pass is a separate Spark job): the shard is framed
+    once on the GPU from its start and cut into sparse-index entries by cbx_sparse_index (100 MB
+    entries at root segments); the entries' offsets seed every step's framing.  A step = RDW framing
+    seeded by the entries + (N > 1) one all-gather of the shard's record count, whose exclusive
+    prefix is the shard's Record_Id base (cobrix_amd/shard.py record_bases) + decode."""
+
     def __init__(self, name, n_rec, dev, rank, window):
         import torch
         from cobrix_amd import synth
@@ -190,14 +191,22 @@ class _VarLen:
         else:
             self.raw, hdr = synth.wide_odo(n_rec, seed=20261018 + rank, device=dev)
             cb, segs = synth.WIDE_ODO_COPYBOOK, synth.WIDE_ODO_SEGMENTS
-        is_root = self.raw[hdr + 4] == 0xC3
         self.in_bytes = int(self.raw.numel())
-        self.seeds = _seeds_every(hdr, is_root, self.in_bytes, 100 * 1024 * 1024)
         self.n_expected = int(hdr.numel())
-        del hdr, is_root
+        del hdr
         torch.cuda.synchronize()
+        # segment_id_root only shapes the index (cuts at roots); the decode plan is the C4/C5 one
         self.rd = VarLenNestedReader(cb, ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
                                                           segment_id_redefine_map=segs, window_bytes=window))
+        idx_rd = VarLenNestedReader(cb, ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
+                                                         segment_id_levels=["C"], input_split_size_mb=100))
+        t0 = time.perf_counter()
+        off, ln = idx_rd.frame(self.raw, self.in_bytes)
+        self.entries = idx_rd.generate_index(self.raw, self.in_bytes, off, ln)
+        torch.cuda.synchronize()
+        self.index_ms = (time.perf_counter() - t0) * 1e3
+        self.seeds = [e.offset_from for e in self.entries]
+        del off, ln, idx_rd
         self.dev = dev
 
     def prepare(self, stream):
@@ -215,10 +224,11 @@ class _VarLen:
         self.cols, self.cs = _alloc_columns(self.rd.plan, self.n_rec, string_capacity(self.rd.native, self.n_rec),
                                             self.dev)
         self.fr0, self.fr1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        self.frame_ms = []
+        self.record_base = 0
 
-    def step(self):
+    def step(self, world=1):
         from cobrix_amd import native as N
+        from cobrix_amd.shard import record_bases
         self.fr0.record()
         N.check(self.L.cbx_frame_rdw(self.raw.data_ptr(), self.in_bytes, self.sd, len(self.seeds),
                                      ctypes.byref(self.prm), self.off.data_ptr(), self.ln.data_ptr(), self.cap,
@@ -226,8 +236,10 @@ class _VarLen:
         self.fr1.record()
         if self.nfr.value != self.n_expected:
             raise RuntimeError(f"framing found {self.nfr.value} records, generator wrote {self.n_expected}")
+        if world > 1:
+            self.record_base, _ = record_bases(self.nfr.value)     # Record_Id base of this shard
         N.check(self.L.cbx_decode_var(self.h, self.raw.data_ptr(), self.in_bytes, self.off.data_ptr(),
-                                      self.ln.data_ptr(), self.n_rec, 0, 0, self.cs, self.stream))
+                                      self.ln.data_ptr(), self.n_rec, 0, self.record_base, self.cs, self.stream))
         return (self.fr0, self.fr1)
 
     def end_to_end(self):
@@ -237,49 +249,105 @@ class _VarLen:
         return sum(int(c["sizes"].sum().item()) for c in self.cols if "sizes" in c)
 
 
-def _cpu_baseline(workload: str, seconds: float = 12.0):
-    """Oracle (scalar C restatement of the reference decoders) on a bounded sample, 1 core."""
+def _probe_reference_jvm():
+    """the reference CPU path runs only where a JVM + Spark + a Cobrix jar exist."""
+    import shutil
+    found = {t: shutil.which(t) for t in ("java", "spark-submit")}
+    if all(found.values()):
+        return "java and spark-submit present (reference run not wired into this bench)"
+    return "probed on this host: " + ", ".join(f"{t} {'found' if v else 'absent'}" for t, v in found.items()) + \
+        " -- the reference Cobrix/Spark CPU path cannot run here; the oracle restatement is timed instead"
+
+
+def _cpu_threads() -> int:
+    """Host cores of this GPU's share: a 1-GPU box exposes the whole machine in nproc but allots 16
+    CPUs per GPU (CBX_CPU_THREADS overrides)."""
+    return int(os.environ.get("CBX_CPU_THREADS", str(min(16, os.cpu_count() or 1))))
+
+
+def _cpu_baseline(workload: str, seconds: float = 10.0):
+    """The oracle (scalar C restatement of the reference decoders) on a bounded sample of the same
+    workload, at 1 thread and at the GPU's host-core share (threads over record chunks: ctypes
+    releases the GIL inside the C calls).  For RDW workloads the header walk stays sequential, as
+    the reference's index pass is per file (IndexGenerator.scala:61-120); decode is split."""
+    import threading
+    import numpy as np
     from cobrix_amd.copybook import parse_copybook
     from cobrix_amd import synth
     from oracle import oracle as O
-    if workload in ("syn200", "synstr200"):
+    fixed = workload in ("syn200", "synstr200")
+    if fixed:
         text, gen, size = ((synth.SYN200_COPYBOOK, synth.syn200, 200) if workload == "syn200"
                            else (synth.SYNSTR200_COPYBOOK, synth.synstr200, 200))
         cb = parse_copybook(text, code_page="common" if workload == "syn200" else "cp037")
-        ast = O.OracleAst(cb)
-
-        def run(n, seed):
-            data = gen(n, seed=seed).numpy().tobytes()
-            t0 = time.perf_counter()
-            O.decode_fixed(cb, data, ast=ast)
-            return time.perf_counter() - t0, n * size
     else:
         text, gen = ((synth.RDW_NARROW_COPYBOOK, synth.rdw_narrow) if workload == "rdw_narrow"
                      else (synth.WIDE_ODO_COPYBOOK, synth.wide_odo))
         cb = parse_copybook(text, segment_redefines=["STATIC-DETAILS", "CONTACTS"])
-        ast = O.OracleAst(cb)
+    ast = O.OracleAst(cb)
+    lib = O.lib()
+    chunk = 20_000 if workload != "wide_odo" else 50
 
-        def run(n, seed):
-            raw_t, _ = gen(n, seed=seed)
-            raw = raw_t.numpy().tobytes()
-            t0 = time.perf_counter()
-            off, ln = O.frame_rdw(raw)
-            t1 = time.perf_counter()
-            segs = ["STATIC_DETAILS" if raw[o] == 0xC3 else "CONTACTS" for o in off]   # (untimed) segment ids
-            t2 = time.perf_counter()
-            O.decode_var(cb, raw, off, ln, active_segments=segs, ast=ast)
-            return (t1 - t0) + (time.perf_counter() - t2), len(raw)
-    n0 = 2000 if workload != "wide_odo" else 20
-    dt, nb = run(n0, 99)
-    rate = n0 / max(dt, 1e-9)
-    n = int(min(max(rate * seconds, n0), 6_000_000))
-    dt, nb = run(n, 100)
+    def make(n, seed):
+        if fixed:
+            data = gen(n, seed=seed).numpy().tobytes()
+            return data, None, None, None
+        raw = gen(n, seed=seed)[0].numpy().tobytes()
+        t0 = time.perf_counter()
+        off, ln = O.frame_rdw(raw)                          # sequential header walk (timed below)
+        t_frame = time.perf_counter() - t0
+        act = np.array([ast.names.get("STATIC_DETAILS" if raw[o] == 0xC3 else "CONTACTS") for o in off], np.int32)
+        return raw, (off, ln, act), t_frame, None
+
+    def decode_range(data, fr, r0, r1):
+        ev = np.zeros(chunk * ast.max_events_per_record(), dtype=O.EVENT_DTYPE)
+        heap = np.zeros(chunk * ast.max_heap_per_record() + 64, dtype=np.uint8)
+        n_ev, hl = ctypes.c_int64(0), ctypes.c_int64(0)
+        buf = np.frombuffer(data, dtype=np.uint8)
+        for c0 in range(r0, r1, chunk):
+            c1 = min(r1, c0 + chunk)
+            n_ev.value = hl.value = 0
+            if fixed:
+                r = lib.ora_decode_fixed(ctypes.addressof(ast.nodes), 0, ctypes.addressof(ast.handlers),
+                                         ctypes.addressof(ast.opts), buf[c0 * size:].ctypes.data, c1 - c0, size, 0, -1, 0,
+                                         None, 0, ev.ctypes.data, len(ev), ctypes.byref(n_ev), heap.ctypes.data,
+                                         len(heap), ctypes.byref(hl))
+            else:
+                off, ln, act = fr
+                r = lib.ora_extract_var(ctypes.addressof(ast.nodes), 0, ctypes.addressof(ast.handlers),
+                                        ctypes.addressof(ast.opts), buf.ctypes.data, off[c0:].ctypes.data,
+                                        ln[c0:].ctypes.data, act[c0:].ctypes.data, c1 - c0, 0, ev.ctypes.data, len(ev),
+                                        ctypes.byref(n_ev), heap.ctypes.data, len(heap), ctypes.byref(hl))
+            if r != 0:
+                raise RuntimeError(f"oracle decode failed {r}")
+
+    def timed(data, fr, t_frame, threads):
+        n = (len(data) // size) if fixed else len(fr[0])
+        bounds = [n * t // threads for t in range(threads + 1)]
+        ths = [threading.Thread(target=decode_range, args=(data, fr, bounds[t], bounds[t + 1])) for t in range(threads)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        return time.perf_counter() - t0 + (t_frame or 0.0), n
+
+    n0 = 4000 if workload != "wide_odo" else 40
+    d0, f0, tf0, _ = make(n0, 99)
+    dt, _ = timed(d0, f0, tf0, 1)
+    n = int(min(max(n0 / max(dt, 1e-9) * seconds, n0), 6_000_000 if workload != "wide_odo" else 60_000))
+    data, fr, t_frame, _ = make(n, 100)
+    dt1, nrec = timed(data, fr, t_frame, 1)
+    T = _cpu_threads()
+    dtT, _ = timed(data, fr, t_frame, T)
     unit_n = {"syn200": "SYN200 records", "synstr200": "SYNSTR200 records", "rdw_narrow": "RDW records",
               "wide_odo": "root records (+ children)"}[workload]
-    return {"value": round(nb / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{n} {unit_n} ({nb / 1e6:.1f} MB) through oracle/cobrix_oracle.c "
-                      f"(restatement of extractRecord + decoders{'' if workload.startswith('syn') else ' + RDW walk'}), "
-                      f"1 thread, {dt:.1f} s"}
+    return {"value": round(len(data) / dtT / 1e9, 6), "unit": "GB/s", "cores": T, "kind": "port",
+            "value_1_core": round(len(data) / dt1 / 1e9, 6),
+            "sample": f"{n} {unit_n} ({len(data) / 1e6:.1f} MB, {nrec} records) through oracle/cobrix_oracle.c "
+                      f"(restatement of extractRecord + decoders{'' if fixed else '; RDW header walk sequential'}): "
+                      f"{dt1:.1f} s at 1 thread, {dtT:.2f} s at {T} threads",
+            "reference_jvm": _probe_reference_jvm()}
 
 
 def main():
@@ -299,7 +367,6 @@ def main():
     import torch.distributed as dist
 
     from cobrix_amd import native as N
-    from cobrix_amd.shard import global_bases
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -326,11 +393,7 @@ def main():
     L, h = job.L, job.h
 
     def step():
-        fr = job.step()
-        if world > 1:
-            # global Record_Id / string-byte bases of this shard (one small RCCL all-gather)
-            global_bases(job.n_rec, [c["sizes"] for c in job.cols if "sizes" in c])
-        return fr
+        return job.step(world)
 
     for _ in range(args.warmup):
         step()
@@ -380,6 +443,8 @@ def main():
     if frame_ev:
         fms = sum(a.elapsed_time(b) for a, b in frame_ev) / len(frame_ev)
         kernel_ms["rdw_framing (cbx_frame_rdw incl. count readback)"] = round(fms, 4)
+    if hasattr(job, "entries"):
+        kernel_ms["sparse_index_setup (untimed: frame + cbx_sparse_index, once)"] = round(job.index_ms, 3)
     e2e = None
     if not args.no_end_to_end and world == 1:
         progress("end-to-end (pinned host -> HBM) pass")
@@ -407,6 +472,8 @@ def main():
                        "output_columns": job.rd.plan.n_columns, "parallelism": f"dp{world}",
                        "inputs_resident_in_hbm": True},
             "kernel_ms": kernel_ms,
+            **({"seeds": f"{len(job.entries)} sparse-index entries from cbx_sparse_index (100 MB, root segments)"}
+               if hasattr(job, "entries") else {}),
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "algorithmic_bytes_per_launch": alg, "traffic": traffic,

@@ -62,6 +62,32 @@ def global_bases(local_rows, local_string_bytes: Sequence = (), group=None):
     return excl[rank, 0], excl[rank, 1:], allv.sum(0)
 
 
+def record_bases(local_records, group=None) -> Tuple[int, int]:
+    """Record_Id base of this rank's shard of one variable-length file and the file's record total.
+
+    Each rank frames a contiguous run of the file's index entries and knows only its own record
+    count; the reference numbers records from the entry's recordIndex on (IndexGenerator counts every
+    record before it, VRLRecordReader.scala:55, 71).  The exclusive prefix of the ranks' counts is
+    that number for the shard's first record: one all-gather, no sequential index pass."""
+    rb, _, tot = global_bases(local_records, (), group)
+    return int(rb), int(tot[0])
+
+
+def entry_shards(entries, n_bytes: int, world: int) -> List[Tuple[int, int]]:
+    """Contiguous runs of sparse-index entries per rank, balanced by bytes: [first, end) entry index
+    ranges.  An entry goes to the rank whose byte share holds its first byte (offset_from), so the
+    runs are contiguous and in file order; a rank may get none when entries are large."""
+    if world <= 0 or n_bytes < 0:
+        raise ValueError("bad shard arguments")
+    owner = [min(world - 1, e.offset_from * world // max(n_bytes, 1)) for e in entries]
+    out = []
+    for r in range(world):
+        ks = [k for k, o in enumerate(owner) if o == r]
+        first = ks[0] if ks else (out[-1][1] if out else 0)
+        out.append((first, ks[-1] + 1 if ks else first))
+    return out
+
+
 def init_from_env(backend: Optional[str] = None):
     """torch.distributed init from torchrun's environment (RANK / WORLD_SIZE / MASTER_*);
     no-op for a single process.  Returns (world, rank, local_rank)."""

@@ -62,3 +62,64 @@ def test_global_bases_gloo(world):
         assert rb == sum(rows[:rank])
         assert sb == [sum(s0[:rank]), sum(s1[:rank])]
         assert tot == [sum(rows), sum(s0), sum(s1)]
+
+
+def _varlen_worker(rank, world, port, q):
+    """One rank of a 2-way split of ONE variable-length file (test5, Test5MultisegmentSpec.scala:95-148
+    options): the rank frames only its run of index entries, learns its Record_Id base from the
+    count all-gather (shard.record_bases) and numbers its entries from it."""
+    import torch.distributed as dist
+    import goldens as G
+    import numpy as np
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import parse_copybook_for
+    from cobrix_amd.shard import entry_shards, record_bases
+    from oracle import oracle as O
+    from oracle import reader_oracle as RO
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    raw = G.read("test5_data", "COMP.DETAILS.SEP30.DATA.dat")
+    p, _ = parse_options({"is_record_sequence": "true", "input_split_records": "100", "segment_field": "SEGMENT_ID",
+                          "segment_id_root": "C", "segment_id_prefix": "B", "generate_record_id": "true"})
+    cb = parse_copybook_for(G.read("test5_copybook.cob").decode("latin-1"), p)
+    entries = RO.sparse_index(cb, raw, p)          # entry byte offsets (the split plan)
+    k0, k1 = entry_shards(entries, len(raw), world)[rank]
+    mine = entries[k0:k1]
+    lo = mine[0].offset_from if mine else len(raw)
+    hi = (mine[-1].offset_to if mine[-1].offset_to > 0 else len(raw)) if mine else len(raw)
+    off, _ = O.frame_rdw(raw[lo:hi])               # this rank's records only
+    base, total = record_bases(len(off))
+    local = [RO.Entry(e.offset_from, e.offset_to, e.file_id,
+                      base + int(np.searchsorted(off + lo, e.offset_from))) for e in mine]
+    recs = RO.var_len_records(cb, raw, p, entries=local) if local else []
+    q.put((rank, total, [(r.record_id, r.seg_ids) for r in recs]))
+    dist.destroy_process_group()
+
+
+def test_varlen_shards_record_ids_gloo():
+    """Record_Id and Seg_Id of a file split over 2 ranks (each framing only its entries) equal the
+    single-rank read of the whole file."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_varlen_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import goldens as G
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import parse_copybook_for
+    from oracle import reader_oracle as RO
+    raw = G.read("test5_data", "COMP.DETAILS.SEP30.DATA.dat")
+    p, _ = parse_options({"is_record_sequence": "true", "input_split_records": "100", "segment_field": "SEGMENT_ID",
+                          "segment_id_root": "C", "segment_id_prefix": "B", "generate_record_id": "true"})
+    cb = parse_copybook_for(G.read("test5_copybook.cob").decode("latin-1"), p)
+    whole = [(r.record_id, r.seg_ids) for r in RO.var_len_records(cb, raw, p)]
+    split = res[0][2] + res[1][2]
+    assert res[0][1] == res[1][1] == 1000
+    assert len(res[0][2]) > 100 and len(res[1][2]) > 100
+    assert split == whole
