@@ -100,8 +100,9 @@ struct cbx_plan {
     uint64_t* d_stamps = nullptr;   // diagnostic build only
     // copybook-specialised kernel (cbx_jit.h), built on the first large contiguous decode
     int64_t jit_min = 262144;
-    bool jit_tried[2] = {false, false};      // [windowed, contiguous] op set
-    hipFunction_t jit_fn[2] = {nullptr, nullptr};
+    // specialised kernels: [0] windowed op set, [kp] contiguous op set with kp chunks per lane
+    bool jit_tried[kPre + 1] = {};
+    hipFunction_t jit_fn[kPre + 1] = {};
     std::string jit_error;
     int last_kind = 0;
     int32_t* d_status = nullptr;
@@ -539,7 +540,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // staging mode
     const int sdw = c.stride / 4;
     const bool contig = !c.rec_off && P->contig_ok && c.stride > 0 && c.stride % 4 == 0 && a.base_shift % 4 == 0 &&
-                        (3 + kWave * sdw + 3) / 4 <= 16 * kWave;
+                        contig_kp(sdw) <= kPre;
     a.contig = contig ? 1 : 0;
     const cbx_plan::OpSet& S = contig ? P->cset : P->wset;
     if (contig) {
@@ -699,7 +700,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // copybook-specialised kernel for large contiguous batches (cbx_jit.h)
     hipFunction_t jfn = nullptr;
     if (mode == 0 && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
-        const int k = contig ? 1 : 0;
+        const int k = contig ? contig_kp(sdw) : 0;
         if (!P->jit_tried[k]) {
             P->jit_tried[k] = true;
             // the specialised kernel is straight-line code per op: wide layouts (thousands of
@@ -712,7 +713,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                                " windows, above the specialised-kernel limits (" + std::to_string(kJitMaxOps) + ", " +
                                std::to_string(kJitMaxWindows) + ")";
             else
-                P->jit_fn[k] = jit_get(jit_source(contig, S.win, S.nops, S.batches, S.sops), &P->jit_error);
+                P->jit_fn[k] = jit_get(jit_source(contig, k, S.win, S.nops, S.batches, S.sops), &P->jit_error);
         }
         jfn = P->jit_fn[k];
     }
@@ -826,7 +827,7 @@ extern "C" int cbx_debug_stamps(cbx_plan* P, uint64_t* out) {
 extern "C" int cbx_plan_specialize(cbx_plan* P, char* source, int64_t source_cap, int64_t* source_len, int32_t compile) {
     if (!P) return fail(CBX_E_ARGUMENT, "cbx_plan_specialize: invalid arguments");
     const cbx_plan::OpSet& S = P->contig_ok ? P->cset : P->wset;
-    const std::string src = jit_source(P->contig_ok, S.win, S.nops, S.batches, S.sops);
+    const std::string src = jit_source(P->contig_ok, P->contig_ok ? kPre : 0, S.win, S.nops, S.batches, S.sops);
     if (source_len) *source_len = (int64_t)src.size();
     if (source && source_cap > 0) {
         const size_t n = std::min<size_t>(src.size(), (size_t)source_cap - 1);

@@ -74,17 +74,20 @@ __device__ __forceinline__ uint4 load16_guarded(const uint8_t* data, int64_t ga,
 // keys.  Returns the key index, -1 when no key matches.  A string field is compared as trimmed
 // UTF-8 text; an integral field by value (its decimal text equals a key exactly when the key is
 // that integer written canonically); a null value is the empty id "".
+// Every read of the map is indexed by wave-uniform values (scalar loads): a per-lane index would
+// make it a vector load, and its wait inside the decode loop would also cover the prefetched tile.
 __device__ int segment_key(const CBX_CONST cbx_segment_map* m, const uint32_t* lut, const CBX_CONST Field* fields,
                            const uint8_t* rec, int avail, int start_off) {
     int o = start_off + m->field_offset;
+    int found = -1;
     if (m->field_is_int) {
         const Field f = ldc(fields + m->field);
         Val v = null_val();
         if (o + f.size <= avail) v = decode_count_int(f, rec + o);
-        for (int k = 0; k < m->n_keys; k++) {
-            if (v.valid ? (m->key_is_int[k] && m->key_int[k] == (int64_t)v.lo) : m->key_len[k] == 0) return k;
+        for (int k = m->n_keys - 1; k >= 0; k--) {   // the first matching key wins
+            if (v.valid ? (m->key_is_int[k] && m->key_int[k] == (int64_t)v.lo) : m->key_len[k] == 0) found = k;
         }
-        return -1;
+        return found;
     }
     int n = m->field_size;
     if (o > avail) o = avail;
@@ -94,28 +97,38 @@ __device__ int segment_key(const CBX_CONST cbx_segment_map* m, const uint32_t* l
     int b = 0, e = n;
     while (b < e && (lut[p[b]] >> 31)) b++;
     while (e > b && (lut[p[e - 1]] >> 31)) e--;
-    // keys are stored as UTF-8 (key[k][] holds bytes, key_len[k] their count)
+    // keys are stored as UTF-8 (key[k][] holds bytes, key_len[k] their count); each lane walks its
+    // trimmed field's UTF-8 bytes in step with the key position
     for (int k = 0; k < m->n_keys; k++) {
-        const CBX_CONST uint16_t* key = m->key[k];
-        int kl = m->key_len[k];
-        int pos = 0;
-        bool eq = true;
-        for (int i = b; i < e && eq; i++) {
-            uint32_t en = lut[p[i]];
-            int l = (en >> 24) & 3;
-            for (int j = 0; j < l; j++) {
-                if (pos >= kl || key[pos] != ((en >> (8 * j)) & 0xFF)) { eq = false; break; }
-                pos++;
+        const int kl = m->key_len[k];
+        int i = b, j = 0;
+        bool eq = found < 0;
+        for (int pos = 0; pos < kl; pos++) {
+            // dword reads (there is no 16-bit scalar load): key rows are dword aligned
+            const uint32_t kw = ((const CBX_CONST uint32_t*)m->key[k])[pos >> 1];
+            const uint32_t kb = (pos & 1) ? kw >> 16 : kw & 0xFFFF;
+            uint32_t en = 0;
+            while (eq && i < e && ((en = lut[p[i]]) >> 24 & 3) == 0) i++;   // characters with no output bytes
+            if (eq) {
+                if (i >= e || ((en >> (8 * j)) & 0xFF) != kb) eq = false;
+                else if (++j >= (int)((en >> 24) & 3)) { j = 0; i++; }
             }
         }
-        if (eq && pos == kl) return k;
+        while (eq && i < e && ((lut[p[i]] >> 24) & 3) == 0) i++;
+        if (eq && i == e) found = k;
     }
-    return -1;
+    return found;
 }
 
 __device__ __forceinline__ int segment_of(const KernelArgs& a, const uint32_t* lut, const uint8_t* rec, int avail) {
     const int k = segment_key(a.segmap, lut, a.fields, rec, avail, a.start_off);
-    return k >= 0 ? a.segmap->key_segment[k] : -1;
+    int seg = -1;
+    for (int j = 0; j < a.segmap->n_keys; j++) {
+        int ks = a.segmap->key_segment[j];
+        asm volatile("" : "+s"(ks));   // a scalar load: keeps the compiler from folding the select into a lane-indexed load
+        seg = k == j ? ks : seg;
+    }
+    return seg;
 }
 
 __device__ __forceinline__ void store_value(const DevColumn& c, int out_type, int64_t v, const Val& x) {
@@ -402,14 +415,17 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
     }
 }
 
-// Generated columns of a window (File_Id / Record_Id).
+// Generated columns of a window (File_Id / Record_Id).  kSel: the call may carry per-record
+// Record_Ids (selected variable-length records); the contiguous fixed-length loop never does, and
+// must not issue that load (a load behind the prefetched tile makes its wait cover the prefetch).
+template <bool kSel = true>
 __device__ __forceinline__ void decode_generated(const KernelArgs& a, const Window& w, const TileCtx& t, int lane) {
     if (a.mode == 1) return;
     for (int i = w.gen_begin; i < w.gen_end; i++) {
         const GenOp g = ldc(a.gops + i);
         const DevColumn col = ldc(a.cols + g.column);
         // Record_Id: the selection's per-record ids (cbx_decode_selected), else first_record_id + r
-        const int64_t rid = a.rec_id ? (t.active ? a.rec_id[t.rec] : 0) : a.first_record_id + t.rec;
+        const int64_t rid = (kSel && a.rec_id) ? (t.active ? a.rec_id[t.rec] : 0) : a.first_record_id + t.rec;
         Val x{g.kind == CBX_K_RECORD_ID ? (uint64_t)rid : (uint64_t)(int64_t)a.file_id, 0, true};
         if (t.active) store_value(col, g.out_type, t.rec, x);
         const uint64_t m = __ballot(t.active);
@@ -487,10 +503,21 @@ __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window&
 // Contiguous staging of a fixed-length tile: the tile's byte span [t0b, t0b + n * stride) is
 // fetched with 16-byte loads (consecutive lanes on consecutive chunks, 1 KiB per
 // wave-instruction) and written to LDS rows of cpitch bytes (odd dword count when padding pays).
-// A tile span inside the input is loaded in one go into kPre registers per lane, issued one tile
-// ahead (the decode of tile t overlaps the loads of tile t + stride); the last tile (span
-// reaching past the input) is staged synchronously with guarded loads.
+// The loads of tile t + stride are issued before tile t is decoded, KP per lane, ALL of them
+// unconditionally through a range-checked buffer descriptor over [a0, end of input): chunks past
+// the span get an out-of-range offset (no memory access, zero data), and a span reaching past the
+// input is never faulted on -- its tile is restaged synchronously with guarded loads.  Loads
+// that are always issued and always overwrite the same registers leave the compiler no reason to
+// copy the buffer (a copy would wait for the loads, the whole prefetch) anywhere in the loop.
+// KP: chunks per lane -- exact for the specialised kernel (ceil(chunks per span / 64)), the plan
+// limit (kPre) for the table-driven one.
 constexpr int kPre = 16;   // 16-byte chunks per lane: a 16 KiB tile span (plan limit for contig)
+
+// Chunks per lane that cover any tile span of records of stride_dw dwords (up to 3 dwords of
+// misalignment in front of the first record).
+__host__ __device__ constexpr int contig_kp(int stride_dw) {
+    return ((3 + kWave * stride_dw + 3) / 4 + kWave - 1) / kWave;
+}
 
 struct ContigSpan {
     int64_t a0;      // 16-byte aligned start of the span
@@ -513,14 +540,25 @@ __device__ __forceinline__ ContigSpan contig_span(const KernelArgs& a, int64_t t
     return sp;
 }
 
-// Issue the loads of an in-bounds span (no wait): unconditional loads at clamped chunk indices.
-__device__ __forceinline__ void contig_issue(const KernelArgs& a, const ContigSpan& sp, int lane, uint4 (&buf)[kPre]) {
+// Issue the KP loads of a span (no wait).  The descriptor is built from wave-uniform values made
+// provably uniform (readfirstlane), so no waterfall loop wraps the loads.
+template <int KP>
+__device__ __forceinline__ void contig_issue(const KernelArgs& a, const ContigSpan& sp, int lane, uint4 (&buf)[KP]) {
+    int64_t left = a.data_len - sp.a0;
+    left = left < 0 ? 0 : (left > (1 << 20) ? (1 << 20) : left);
+    const uint64_t base = (uint64_t)(a.data + sp.a0);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane((int)left);
+    const int nch = __builtin_amdgcn_readfirstlane(sp.nch);
+    void* bp = (void*)(((uint64_t)hi << 32) | lo);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bp, (short)0, nbytes, 0x00020000);
 #pragma unroll
-    for (int u = 0; u < kPre; u++) {
-        if (u * kWave < sp.nch) {   // wave-uniform
-            const int c = u * kWave + lane;
-            buf[u] = *(const uint4*)(a.data + sp.a0 + 16 * (int64_t)(c < sp.nch ? c : sp.nch - 1));
-        }
+    for (int u = 0; u < KP; u++) {
+        const int c = u * kWave + lane;
+        const int off = c < nch ? 16 * c : 0x7ffffff0;   // past the descriptor's range: no access
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        buf[u] = make_uint4(v[0], v[1], v[2], v[3]);
     }
 }
 
@@ -542,13 +580,14 @@ __device__ __forceinline__ void contig_put(const KernelArgs& a, const ContigSpan
     }
 }
 
-__device__ __forceinline__ void contig_store(const KernelArgs& a, const ContigSpan& sp, int lane, const uint4 (&buf)[kPre],
+template <int KP>
+__device__ __forceinline__ void contig_store(const KernelArgs& a, const ContigSpan& sp, int lane, const uint4 (&buf)[KP],
                                              uint8_t* s_img) {
     // opaque lane index: keeps the compiler from computing the LDS addresses when the loads
     // are issued (a tile earlier) and holding them in registers across the decode
     asm volatile("" : "+v"(lane));
 #pragma unroll
-    for (int u = 0; u < kPre; u++) {
+    for (int u = 0; u < KP; u++) {
         const int c = u * kWave + lane;
         if (u * kWave < sp.nch && c < sp.nch) contig_put(a, sp, c, buf[u], s_img);
     }
@@ -622,7 +661,10 @@ __device__ __forceinline__ uint32_t stage_window(const KernelArgs& a, const Wind
     return (uint32_t)(lane * pitch + my_mis - w.lo);
 }
 
-// Per-lane tile context: record index, base offset and available bytes.
+// Per-lane tile context: record index, base offset and available bytes.  kFramed: the call may
+// carry framed records (rec_off / rec_len); the contiguous loop never does, and must not issue
+// those loads (their wait would cover the prefetched tile).
+template <bool kFramed = true>
 __device__ __forceinline__ TileCtx tile_ctx(const KernelArgs& a, int64_t tile, int lane) {
     TileCtx t;
     t.tile = tile;
@@ -631,7 +673,7 @@ __device__ __forceinline__ TileCtx tile_ctx(const KernelArgs& a, int64_t tile, i
     t.base = a.base_shift;
     t.avail = 0;
     t.seg = -1;
-    if (a.rec_off) {
+    if (kFramed && a.rec_off) {
         if (t.active) { t.base += a.rec_off[t.rec]; t.avail = a.rec_len[t.rec]; }
     } else if (t.active) {
         t.base += t.rec * (int64_t)a.stride;
@@ -643,10 +685,11 @@ __device__ __forceinline__ TileCtx tile_ctx(const KernelArgs& a, int64_t tile, i
 // Per-record prologue: segment-redefine selection and OCCURS DEPENDING ON element counts
 // (their count columns written here), reading the record at rp (the LDS image in contiguous
 // mode -- no HBM loads in that loop besides the staging loads -- or HBM).
+template <bool kSel = true>
 __device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, const uint8_t* rp, int lane,
                                               const uint32_t* s_lut, int32_t* s_cnt) {
     // ---- segment redefine selection
-    if (a.rec_seg) t.seg = t.active ? a.rec_seg[t.rec] : -1;   // selected records: segment known
+    if (kSel && a.rec_seg) t.seg = t.active ? a.rec_seg[t.rec] : -1;   // selected records: segment known
     else if (a.segmap && t.active) t.seg = segment_of(a, s_lut, rp, t.avail);
     if (a.mode == 0 && a.seg_col >= 0) {
         const DevColumn c = ldc(a.cols + a.seg_col);
@@ -736,20 +779,21 @@ __device__ __forceinline__ WaveLds wave_lds(const KernelArgs& a, uint8_t* smem, 
 // ahead.  Nothing else in this loop loads from HBM (prologue and decode read the LDS image), so
 // no wait on the staging loads or on earlier stores sits in the decode.  `body` decodes one
 // staged tile: body(a, t, img, rec_addr, lds, lane, stamps).
-template <typename Body>
+template <int KP, typename Body>
 __device__ __forceinline__ void contig_loop(const KernelArgs& a, const WaveLds& l, int64_t tile, int64_t tstep,
                                             int lane, const Body& body) {
-    uint4 buf[kPre];
+    uint4 buf[KP];
     bool have = false;
     if (tile < a.n_tiles) {
         const ContigSpan sp = contig_span(a, tile);
-        if (sp.inb) { contig_issue(a, sp, lane, buf); have = true; }
+        contig_issue<KP>(a, sp, lane, buf);
+        have = sp.inb;
     }
     Stamps st;
     st.init();
     while (tile < a.n_tiles) {
         const ContigSpan sp = contig_span(a, tile);
-        if (have) contig_store(a, sp, lane, buf, l.img);
+        if (have) contig_store<KP>(a, sp, lane, buf, l.img);
         else contig_stage_guarded(a, sp, lane, l.img);
         wave_sync_lds();
         st.mark(0);   // staging: wait for the prefetched loads + LDS writes
@@ -757,12 +801,13 @@ __device__ __forceinline__ void contig_loop(const KernelArgs& a, const WaveLds& 
         have = false;
         if (next < a.n_tiles) {
             const ContigSpan sn = contig_span(a, next);
-            if (sn.inb) { contig_issue(a, sn, lane, buf); have = true; }
+            contig_issue<KP>(a, sn, lane, buf);
+            have = sn.inb;
         }
         st.mark(1);   // prefetch issue
-        TileCtx t = tile_ctx(a, tile, lane);
+        TileCtx t = tile_ctx<false>(a, tile, lane);
         const uint32_t rec0 = (uint32_t)(lane * a.cpitch + 4 * sp.mis_dw);   // record start in the image
-        tile_prologue(a, t, l.img + rec0, lane, l.lut, l.cnt);
+        tile_prologue<false>(a, t, l.img + rec0, lane, l.lut, l.cnt);
         st.mark(2);   // prologue
         body(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
         wave_sync_lds();

@@ -35,7 +35,7 @@ struct InterpBody {
             const Window w = ldc(a.windows + wi);
             if (a.mode == 1 && w.sop_begin == w.sop_end) continue;
             if (w.global) {
-                decode_generated(a, w, t, lane);   // contig plans: generated columns only
+                decode_generated<false>(a, w, t, lane);   // contig plans: generated columns only
                 continue;
             }
 #ifdef CBX_STAMPS
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void decode_kernel(KernelAr
     const int64_t tstep = (int64_t)gridDim.x * kWavesPerBlock;
 
     if (a.contig) {
-        contig_loop(a, l, tile, tstep, lane, InterpBody{});
+        contig_loop<kPre>(a, l, tile, tstep, lane, InterpBody{});
         return;
     }
 
