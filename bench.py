@@ -7,16 +7,20 @@ fixed-length shards know their Record_Id base statically, variable-length shards
 RCCL all-gather of their framed record counts per step).  Rank 0 prints ONE JSON line.
 
 A step = one full decode of the shard through the C ABI:
-  fixed-length (C2 syn200, C3 synstr200): `cbx_decode_fixed` -- decode kernel (numerics +
-      tile-local strings), fixup kernel for deferred values, string scan + placement kernels;
+  fixed-length (C2 syn200, C3 synstr200): `cbx_decode_fixed` -- decode kernel (numerics and
+      strings; with the default --strings views every string value is written once, into an Arrow
+      string view + its tile's data region) + fixup kernel for deferred values (--strings offsets:
+      Arrow large-string offsets, + string scan and placement kernels);
   variable-length (C4 rdw_narrow, C5 wide_odo): `cbx_frame_rdw` (GPU RDW offset discovery seeded
       by the sparse-index entries cbx_sparse_index cut at setup, 100 MB at root segments) +
       `cbx_decode_var` (segment redefines, ODO); for N > 1 one all-gather of the shard's record count
       between framing and decode gives its Record_Id base.
 
-roofline: algorithmic bytes (input record bytes + every output buffer byte) of one
-decode-kernel launch / its average duration, measured with HIP events recorded by the library on
-the launch stream over the timed steps (cbx_plan_kernel_times).
+roofline: algorithmic bytes (input record bytes + every output buffer byte of the
+layout produced -- validity bits, values, 16-byte string views + the payload of views longer than
+12 bytes, or int64 offsets + payload) of one decode-kernel launch / its average duration, measured
+with HIP events recorded by the library on the launch stream over the timed steps
+(cbx_plan_kernel_times).
 
 end_to_end (fixed-length workloads, N = 1 view per rank): the same shard streamed from pinned host
 memory -- H2D copies of 2.5M-record chunks on a copy stream overlapped with the decode of the
@@ -39,24 +43,34 @@ METRIC = "decoded input GB/s + records/s, fixed-len COMP-3 mix, 1-8 MI355X; % HB
 
 
 def algorithmic_bytes(plan, n_rec: int, in_bytes: int, payload_bytes: int) -> int:
-    """input bytes + every output buffer byte one decode writes."""
+    """input bytes + every output buffer byte one decode writes (payload_bytes: the
+    string payload written to data buffers -- all of it in the offsets layout, the values longer
+    than 12 bytes in the view layout)."""
     from cobrix_amd import native as N
     total = in_bytes + payload_bytes
+    views = bool(plan.options.string_views)
     for info in plan.columns:
         n = n_rec * info.n_slots
         total += (n + 7) // 8                                   # validity bits
         if info.out_type in (N.O_STRING, N.O_BINARY):
-            total += 8 * (n + info.n_slots)                     # int64 offsets (n_rec + 1 per slot)
+            total += 16 * n if views else 8 * (n + info.n_slots)   # views / int64 offsets (n_rec + 1 per slot)
         else:
             total += n * N.OUT_WIDTH[info.out_type]
     return total
+
+
+def _round_key(path: str):
+    """Natural order of profiles/<round>_<variant> directories (r02_b after r02_a, r01_v10 after r01_v9)."""
+    import re
+    d = os.path.basename(os.path.dirname(path))
+    return [int(x) if x.isdigit() else x for x in re.split(r"(\d+)", d)]
 
 
 def measured_traffic(tag: str):
     """HBM bytes per decode-kernel launch from the newest committed rocprofv3 FETCH_SIZE/WRITE_SIZE
     passes of this configuration (tools/gpu_profile.sh -> profiles/<round tag>/traffic_<tag>.json)."""
     import glob
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_{tag}.json")))
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_{tag}.json")), key=_round_key)
     if not found:
         return None, None
     with open(found[-1]) as f:
@@ -89,18 +103,18 @@ WORKLOADS = {
 
 
 class _Fixed:
-    def __init__(self, name, n_rec, dev, rank, window):
+    def __init__(self, name, n_rec, dev, rank, window, views):
         import torch
         from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters
         from cobrix_amd import synth
         if name == "syn200":
             cb, self.stride = synth.SYN200_COPYBOOK, synth.SYN200_RECORD_SIZE
             self.rec = synth.syn200(n_rec, seed=20261015 + rank, device=dev).view(-1)
-            params = ReaderParameters(window_bytes=window)
+            params = ReaderParameters(window_bytes=window, string_views=views)
         else:
             cb, self.stride = synth.SYNSTR200_COPYBOOK, synth.SYNSTR200_RECORD_SIZE
             self.rec = synth.synstr200(n_rec, seed=20261017 + rank, device=dev).view(-1)
-            params = ReaderParameters(window_bytes=window, ebcdic_code_page="cp037")
+            params = ReaderParameters(window_bytes=window, ebcdic_code_page="cp037", string_views=views)
         torch.cuda.synchronize()
         self.rd = FixedLenNestedReader(cb, params)
         self.n_rec, self.in_bytes, self.dev = n_rec, n_rec * self.stride, dev
@@ -169,7 +183,22 @@ class _Fixed:
                        "cbx_decode_fixed of the previous chunk (double-buffered), per rank"}
 
     def payload(self):
-        return sum(int(c["sizes"].sum().item()) for c in self.cols if "sizes" in c)
+        return _payload(self.cols, self.n_rec)
+
+
+def _payload(cols, n_rec: int) -> int:
+    """String payload bytes the last decode wrote to data buffers: per-slot sizes (offsets layout)
+    or the lengths of views longer than 12 bytes (view layout)."""
+    import torch
+    tot = 0
+    for c in cols:
+        if "sizes" in c:
+            tot += int(c["sizes"].sum().item())
+        elif "views" in c:
+            pitch = 64 * ((n_rec + 63) // 64)
+            ln = c["views"].view(-1, pitch, 16)[:, :n_rec].reshape(-1, 16)[:, :4].contiguous().view(torch.int32).view(-1)
+            tot += int(torch.where(ln > 12, ln, 0).to(torch.int64).sum().item())
+    return tot
 
 
 class _VarLen:
@@ -181,7 +210,7 @@ class _VarLen:
     seeded by the entries + (N > 1) one all-gather of the shard's record count, whose exclusive
     prefix is the shard's Record_Id base (cobrix_amd/shard.py record_bases) + decode."""
 
-    def __init__(self, name, n_rec, dev, rank, window):
+    def __init__(self, name, n_rec, dev, rank, window, views):
         import torch
         from cobrix_amd import synth
         from cobrix_amd.reader import ReaderParameters, VarLenNestedReader
@@ -197,7 +226,8 @@ class _VarLen:
         torch.cuda.synchronize()
         # segment_id_root only shapes the index (cuts at roots); the decode plan is the C4/C5 one
         self.rd = VarLenNestedReader(cb, ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
-                                                          segment_id_redefine_map=segs, window_bytes=window))
+                                                          segment_id_redefine_map=segs, window_bytes=window,
+                                                          string_views=views))
         idx_rd = VarLenNestedReader(cb, ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
                                                          segment_id_levels=["C"], input_split_size_mb=100))
         t0 = time.perf_counter()
@@ -246,7 +276,7 @@ class _VarLen:
         return None
 
     def payload(self):
-        return sum(int(c["sizes"].sum().item()) for c in self.cols if "sizes" in c)
+        return _payload(self.cols, self.n_rec)
 
 
 def _probe_reference_jvm():
@@ -359,6 +389,8 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="records per GPU (root records for wide_odo); "
                                                            "0 = the workload's default")
     ap.add_argument("--window", type=int, default=0, help="LDS window bytes (0 = plan default)")
+    ap.add_argument("--strings", default="views", choices=["views", "offsets"],
+                    help="string column layout: Arrow string views (one pass) or Arrow large-string offsets")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true")
     args = ap.parse_args()
@@ -384,8 +416,9 @@ def main():
             print(f"[bench {args.workload}] {msg}", file=sys.stderr, flush=True)
 
     progress(f"generating {n_req} records on {dev}")
+    views = args.strings == "views"
     job = (_Fixed if args.workload in ("syn200", "synstr200") else _VarLen)(args.workload, n_req, dev, rank,
-                                                                            args.window)
+                                                                            args.window, views)
     st = torch.cuda.current_stream()
     progress(f"{job.in_bytes / 1e9:.2f} GB generated; allocating columns")
     job.prepare(st)
@@ -436,10 +469,11 @@ def main():
     kind = ctypes.c_int32(0)
     N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
     kname = "cbx_jit_decode (copybook-specialised, hipRTC)" if kind.value == 1 else "cbx::decode_kernel (table-driven)"
-    tag = str(n_rec) if args.workload == "syn200" else f"{args.workload}_{n_rec}"
+    tag = f"{args.workload}_{args.strings}_{n_rec}"
     traffic, traffic_src = measured_traffic(tag)
     kernel_ms = {"decode_kernel": round(dec_avg_ms, 4),
-                 "post_kernels (deferred-value fixup, string scan + placement)": round(fix_avg_ms, 4)}
+                 ("post_kernels (deferred-value fixup)" if views else
+                  "post_kernels (deferred-value fixup, string scan + placement)"): round(fix_avg_ms, 4)}
     if frame_ev:
         fms = sum(a.elapsed_time(b) for a, b in frame_ev) / len(frame_ev)
         kernel_ms["rdw_framing (cbx_frame_rdw incl. count readback)"] = round(fms, 4)
@@ -470,6 +504,8 @@ def main():
                        "records_per_gpu": n_rec, "input_bytes_per_gpu": job.in_bytes,
                        "input_gb_per_gpu": round(job.in_bytes / 1e9, 3),
                        "output_columns": job.rd.plan.n_columns, "parallelism": f"dp{world}",
+                       "string_layout": "Arrow string views (16 B views + long payloads, one pass)" if views
+                       else "Arrow large-string (int64 offsets + payload, scan + placement)",
                        "inputs_resident_in_hbm": True},
             "kernel_ms": kernel_ms,
             **({"seeds": f"{len(job.entries)} sparse-index entries from cbx_sparse_index (100 MB, root segments)"}

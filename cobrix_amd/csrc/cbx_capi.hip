@@ -69,6 +69,7 @@ struct cbx_plan {
     std::vector<int32_t> col_is_string;   // per column: 1 if string/binary
     std::vector<int32_t> col_slots;       // per column: slots
     std::vector<int32_t> col_max_bytes;   // per column: max payload bytes per value
+    bool view = false;                    // string columns in the string-view layout
     std::vector<int32_t> segid_cols;      // segment levels with a Seg_Id column
     // device copies
     Field* d_fields = nullptr;
@@ -346,6 +347,7 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     if (const char* e = getenv("CBX_JIT"))
         if (e[0] == '0') P->jit_min = -1;   // operator switch: table-driven kernel only
     P->n_columns = opts->n_columns;
+    P->view = opts->string_views != 0;
     if (P->n_columns <= 0) { delete P; return fail(CBX_E_ARGUMENT, "cbx_plan_create: n_columns must be positive"); }
     P->hfields.assign(fields, fields + n_fields);
     if (n_arrays) P->harrays.assign(arrays, arrays + n_arrays);
@@ -416,6 +418,10 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     for (const Field& d : P->dfields_h)
         if (d.variant == V_STRING) P->str_stage = std::max(P->str_stage, kWave * d.size * d.max_utf8);
     P->str_stage = std::min(P->str_stage, kStrStageBytes);
+    if (P->view)   // the register path (fields of <= kStrFastBytes) always stages its tile's long payloads
+        for (const Field& d : P->dfields_h)
+            if (d.variant == V_STRING && d.size <= kStrFastBytes && (d.kind == CBX_K_STRING || d.kind == CBX_K_STRING_ASCII))
+                P->str_stage = std::max(P->str_stage, kWave * d.size * d.max_utf8);
 
     // ---- segment map: keys to UTF-8, Seg_IdN string columns
     cbx_segment_map sm = opts->segments;
@@ -488,9 +494,26 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
     delete P;
 }
 
+// String-view layout: bytes of a slot region owned by one tile (the tile's payload bound, 16-aligned)
+// and tiles per Arrow data buffer (buffers of at most 1 GiB, a whole number of tiles each).
+static int64_t view_tile_bytes(const cbx_plan* P, int c) { return ((int64_t)kWave * P->col_max_bytes[c] + 15) & ~(int64_t)15; }
+static int64_t view_tiles_per_buf(int64_t tile_bytes) { return std::max<int64_t>(1, (int64_t(1) << 30) / std::max<int64_t>(16, tile_bytes)); }
+
 extern "C" int cbx_string_bound(const cbx_plan* P, int64_t n_rec, int64_t* out_bytes) {
     if (!P || n_rec < 0 || !out_bytes) return fail(CBX_E_ARGUMENT, "cbx_string_bound: invalid arguments");
-    for (int c = 0; c < P->n_columns; c++) out_bytes[c] = P->col_is_string[c] ? n_rec * (int64_t)P->col_max_bytes[c] : 0;
+    const int64_t n_tiles = (n_rec + kWave - 1) / kWave;
+    for (int c = 0; c < P->n_columns; c++)
+        out_bytes[c] = !P->col_is_string[c] ? 0 : P->view ? n_tiles * view_tile_bytes(P, c) : n_rec * (int64_t)P->col_max_bytes[c];
+    return CBX_OK;
+}
+
+extern "C" int cbx_string_view_geometry(const cbx_plan* P, int64_t* tile_bytes, int64_t* buffer_bytes) {
+    if (!P || !tile_bytes || !buffer_bytes) return fail(CBX_E_ARGUMENT, "cbx_string_view_geometry: invalid arguments");
+    for (int c = 0; c < P->n_columns; c++) {
+        const int64_t tb = P->col_is_string[c] ? view_tile_bytes(P, c) : 0;
+        tile_bytes[c] = tb;
+        buffer_bytes[c] = tb ? view_tiles_per_buf(tb) * tb : 0;
+    }
     return CBX_OK;
 }
 
@@ -518,6 +541,9 @@ struct CallShape {
     int32_t file_id = -1;               // File_Id of the batch (-1: the plan's)
 };
 
+// Prologue parts the plan needs (contig_loop's kPro): segment map 1, OCCURS DEPENDING ON arrays 2.
+static int jit_pro(const cbx_plan* P) { return (P->opts.has_segments ? 1 : 0) | (P->harrays.empty() ? 0 : 2); }
+
 static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, int mode, hipStream_t st) {
     const int64_t n_tiles = (c.n_rec + kWave - 1) / kWave;
     KernelArgs a{};
@@ -537,6 +563,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.rec_seg = c.rec_seg;
     a.file_id = c.file_id >= 0 ? c.file_id : P->opts.file_id;
     a.mode = mode;
+    a.str_view = P->view ? 1 : 0;
     // staging mode
     const int sdw = c.stride / 4;
     const bool contig = !c.rec_off && P->contig_ok && c.stride > 0 && c.stride % 4 == 0 && a.base_shift % 4 == 0 &&
@@ -563,7 +590,8 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.gops = (const CBX_CONST GenOp*)S.d_gops;
     a.lds_rows = (a.lds_rows + 15) & ~15;
     a.lds_counts = ((int)P->harrays.size() * kWave * 4 + 15) & ~15;
-    a.str_stage = S.max_str_items > 0 ? P->str_stage : 0;
+    // string-view layout: a 16-byte inline slot per lane in front of the packed long payloads
+    a.str_stage = S.max_str_items > 0 ? P->str_stage + (P->view && mode == 0 ? 16 * kWave : 0) : 0;
     // per-lane dump slots for the branch-free string stores (a shared slot serialises the wave's
     // LDS stores) -- unless the extra 4 * kWave bytes per wave cost a resident workgroup per CU
     // (wide windowed layouts sit close to the LDS limit; C5 decode 49.7 -> 62.1 ms with them)
@@ -595,7 +623,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // column table + per-op address tables: stream-ordered uploads from pageable host memory
     // (staged by the runtime, so the host vectors are free again when the call returns)
     const int n_defer_seq = (int)P->hdefer.size();
-    if (mode == 0 && P->n_seq > 0) {
+    if (mode == 0 && P->n_seq > 0 && !P->view) {
         int rr;
         P->h_seq_scratch.resize(P->n_seq);
         int64_t scratch = 0;
@@ -643,13 +671,20 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
             const cbx_column& col = columns[op.column];
             StrCall sc{};
             sc.validity = col.validity + (int64_t)op.slot * n_tiles;
-            sc.local = P->d_local + (int64_t)op.seq * a.pitch;
-            sc.scratch = P->d_scratch + P->h_seq_scratch[op.seq];
-            sc.tile_cap = P->seq_tile_cap[op.seq];
+            if (P->view) {   // the caller's buffers: views + the slot's region, tile_bytes per tile
+                sc.tile_cap = view_tile_bytes(P, op.column);
+                sc.scratch = col.data + (int64_t)op.slot * col.data_capacity;
+                sc.views = (uint8_t*)col.values + (int64_t)op.slot * a.pitch * 16;
+                sc.tiles_per_buf = view_tiles_per_buf(sc.tile_cap);
+            } else {
+                sc.local = P->d_local + (int64_t)op.seq * a.pitch;
+                sc.scratch = P->d_scratch + P->h_seq_scratch[op.seq];
+                sc.tile_cap = P->seq_tile_cap[op.seq];
+            }
             P->h_scall[i] = sc;
         }
-        P->h_seqcall.resize(P->n_seq);
-        for (int q = 0; q < P->n_seq; q++) {
+        P->h_seqcall.resize(P->view ? 0 : P->n_seq);   // placement pass only in the offsets layout
+        for (int q = 0; q < (int)P->h_seqcall.size(); q++) {
             const Field& d = P->dfields_h[P->seq_field[q]];
             const cbx_column& col = columns[d.column];
             const int sl = P->seq_slot[q];
@@ -664,7 +699,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
             sq.tile_cap = (int32_t)P->seq_tile_cap[q];
             P->h_seqcall[q] = sq;
         }
-        if (P->n_seq > 0)
+        if (P->n_seq > 0 && !P->view)
             HIP_CHECK(hipMemcpyAsync(P->d_seqcall, P->h_seqcall.data(), sizeof(SeqCall) * P->n_seq, hipMemcpyHostToDevice, st));
         if (P->h_ncall.size() > P->ncall_cap) {
             HIP_CHECK(hipStreamSynchronize(st));
@@ -713,7 +748,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                                " windows, above the specialised-kernel limits (" + std::to_string(kJitMaxOps) + ", " +
                                std::to_string(kJitMaxWindows) + ")";
             else
-                P->jit_fn[k] = jit_get(jit_source(contig, k, S.win, S.nops, S.batches, S.sops), &P->jit_error);
+                P->jit_fn[k] = jit_get(jit_source(contig, k, jit_pro(P), P->view, S.win, S.nops, S.batches, S.sops), &P->jit_error);
         }
         jfn = P->jit_fn[k];
     }
@@ -745,7 +780,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                            (const CBX_CONST DeferSeq*)P->d_defer, n_defer);
         HIP_CHECK(hipGetLastError());
     }
-    if (P->n_seq > 0) {
+    if (P->n_seq > 0 && !(P->view && mode == 0)) {
         if ((r = string_scan(P, n_tiles, st))) return r;
         if (mode == 0) {
             const unsigned gx = (unsigned)((n_tiles + kPlaceWaves * kPlaceTiles - 1) / (kPlaceWaves * kPlaceTiles));
@@ -768,6 +803,7 @@ static int decode_common(cbx_plan* P, const CallShape& c, cbx_column* columns, i
     if (sizes_only) {
         for (int i = 0; i < P->n_columns; i++) sizes_only[i] = 0;
         if (P->n_seq == 0 || c.n_rec == 0) return CBX_OK;
+        if (P->view) return cbx_string_bound(P, c.n_rec, sizes_only);   // the layout's capacity is per tile
         int r = launch(P, c, nullptr, 1, st);
         if (r) return r;
         // sequence total = excl[last tile] + tot[last tile] - excl[first tile]
@@ -786,9 +822,20 @@ static int decode_common(cbx_plan* P, const CallShape& c, cbx_column* columns, i
         }
         return CBX_OK;
     }
-    for (int i = 0; i < P->n_columns; i++)
-        if (P->col_is_string[i] && c.n_rec > 0 && (!columns[i].offsets || (!columns[i].data && columns[i].data_capacity > 0)))
+    for (int i = 0; i < P->n_columns; i++) {
+        if (!P->col_is_string[i] || c.n_rec == 0) continue;
+        if (P->view) {
+            const int64_t need = (c.n_rec + kWave - 1) / kWave * view_tile_bytes(P, i);
+            if (!columns[i].values || !columns[i].data)
+                return fail(CBX_E_ARGUMENT, "column " + std::to_string(i) + ": string-view buffers (values, data) required");
+            if (columns[i].data_capacity < need)
+                return fail(CBX_E_CAPACITY, "column " + std::to_string(i) + ": string-view data_capacity " +
+                                                std::to_string(columns[i].data_capacity) + " < " + std::to_string(need) +
+                                                " (cbx_string_bound)");
+        } else if (!columns[i].offsets || (!columns[i].data && columns[i].data_capacity > 0)) {
             return fail(CBX_E_ARGUMENT, "column " + std::to_string(i) + ": string buffers required");
+        }
+    }
     return launch(P, c, columns, 0, st);
 }
 
@@ -827,7 +874,7 @@ extern "C" int cbx_debug_stamps(cbx_plan* P, uint64_t* out) {
 extern "C" int cbx_plan_specialize(cbx_plan* P, char* source, int64_t source_cap, int64_t* source_len, int32_t compile) {
     if (!P) return fail(CBX_E_ARGUMENT, "cbx_plan_specialize: invalid arguments");
     const cbx_plan::OpSet& S = P->contig_ok ? P->cset : P->wset;
-    const std::string src = jit_source(P->contig_ok, P->contig_ok ? kPre : 0, S.win, S.nops, S.batches, S.sops);
+    const std::string src = jit_source(P->contig_ok, P->contig_ok ? kPre : 0, jit_pro(P), P->view, S.win, S.nops, S.batches, S.sops);
     if (source_len) *source_len = (int64_t)src.size();
     if (source && source_cap > 0) {
         const size_t n = std::min<size_t>(src.size(), (size_t)source_cap - 1);
@@ -1234,7 +1281,21 @@ extern "C" int cbx_decode_selected(cbx_plan* P, const uint8_t* d_data, int64_t n
     if (r) return r;
     // Seg_IdN columns (slot 0 of each string column): lengths -> scanned offsets -> bytes
     for (int l : P->segid_cols) {
-        const cbx_column& col = columns[P->opts.segments.level_column[l]];
+        const int ci = P->opts.segments.level_column[l];
+        const cbx_column& col = columns[ci];
+        if (P->view) {   // views written where the values are made: no scan
+            if (n_rec == 0) continue;
+            SegIdArgs g{};
+            g.state = sel->seg_state; g.n = n_rec; g.L = L; g.level = l; g.file_id = sel->file_id;
+            g.prefix_len = P->opts.segments.prefix_len;
+            g.m = (const CBX_CONST cbx_segment_map*)P->d_segmap;
+            const int64_t tb = view_tile_bytes(P, ci);
+            const int64_t pitch = (n_rec + kWave - 1) / kWave * kWave;
+            hipLaunchKernelGGL(segid_view_kernel, dim3(blocks_for(pitch, 256)), dim3(256), 0, st, g, (u32x4*)col.values,
+                               col.data, tb, view_tiles_per_buf(tb), col.validity, pitch);
+            HIP_CHECK(hipGetLastError());
+            continue;
+        }
         if (n_rec == 0) {
             HIP_CHECK(hipMemsetAsync(col.offsets, 0, sizeof(int64_t), st));
             if (col.data_sizes) HIP_CHECK(hipMemsetAsync(col.data_sizes, 0, sizeof(int64_t), st));

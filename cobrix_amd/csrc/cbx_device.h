@@ -370,11 +370,70 @@ __device__ __forceinline__ void num_group(const KernelArgs& a, const NumOp (&op)
     for (int u = 0; u < N; u++) num_one<V, W, kOdo, false>(a, op[u], i0 + u, t, ok[u], r1[u], r0[u], s_cnt, lane);
 }
 
+// String-view layout (cbx_plan_options.string_views): the element's Arrow view -- length, then the
+// UTF-8 bytes inline (<= 12, zero padded) or their first 4 bytes + data buffer index + offset.
+// Payloads longer than 12 bytes are packed (wave scan) into the tile's region of the slot's data
+// buffer: staged in LDS and copied out in 16-byte pieces when the tile's long payload fits the
+// staging area, else written straight from the lanes.  Short payloads go to a 16-byte LDS slot
+// per lane and into the view.  One pass, no scan across tiles, no placement kernel.
+__device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrOp& op, const StrCall& c, const TileCtx& t,
+                                                 const StrSpan& sp, bool ok, bool fast, const uint32_t (&ev)[kStrFastBytes],
+                                                 const uint8_t* sp_src, const uint32_t* s_lut, uint8_t* s_str, int lane) {
+    const int len = ok ? sp.utf8_len : 0;
+    const bool lng = len > 12;
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32(lng ? (uint32_t)len : 0u, lane, tot);
+    gp(c.validity)[t.tile] = __ballot(ok);
+    auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
+    uint8_t* s_short = s_str + 16 * lane;          // this lane's inline bytes
+    uint8_t* s_long = s_str + 16 * kWave;          // the tile's long payloads, packed
+    // wave-uniform; always true for the register path (the plan sizes the staging area for it in
+    // this layout), so its unrolled byte writes never target global memory
+    const bool staged = fast || (int)tot <= a.str_stage - 16 * kWave;
+    uint8_t* region = c.scratch + t.tile * c.tile_cap;           // 16-byte aligned
+    uint8_t* dump = s_str + a.str_stage + a.dump_stride * lane;
+    *(u32x4*)s_short = u32x4{0u, 0u, 0u, 0u};
+    if (lng && !staged) {
+        if (fast) string_write32e(ev, sp, region + ex, dump, op.size, op.pad);
+        else string_write(op.kind, sp_src, sp, region + ex, lutf);
+    } else {
+        uint8_t* dst = lng ? s_long + ex : s_short;
+        if (fast) string_write32e(ev, sp, dst, dump, op.size, op.pad);
+        else if (ok) string_write(op.kind, sp_src, sp, dst, lutf);
+    }
+    wave_sync_lds();
+    if (staged) {
+        const u32x4* s128 = (const u32x4*)s_long;
+        for (int q = lane; 16 * q < (int)tot; q += kWave) gp((u32x4*)region)[q] = s128[q];
+    }
+    u32x4 v;
+    if (!lng) {
+        const u32x4 w = *(const u32x4*)s_short;
+        v = u32x4{(uint32_t)len, w.x, w.y, w.z};
+    } else {
+        uint32_t pre;
+        if (staged) {
+            const uint32_t* q = (const uint32_t*)(s_long + (ex & ~3u));
+            pre = align_bytes(q[1], q[0], ex & 3u);
+        } else {
+            // the lane's own bytes, written above through the vector memory path
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const CBX_GLOBAL uint8_t* g = gp(region + ex);
+            pre = (uint32_t)g[0] | (uint32_t)g[1] << 8 | (uint32_t)g[2] << 16 | (uint32_t)g[3] << 24;
+        }
+        const int64_t tb = t.tile / c.tiles_per_buf;
+        v = u32x4{(uint32_t)len, pre, (uint32_t)tb, (uint32_t)((t.tile - tb * c.tiles_per_buf) * c.tile_cap + ex)};
+    }
+    gp((u32x4*)c.views)[t.rec] = v;
+    wave_sync_lds();   // the staging area is reused by the next element
+}
+
 // One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):
 // span + tile-local scan; the tile's payload is staged contiguously in LDS and copied with
 // dword stores to the tile's scratch region; the tile-local start of every value and the
 // tile's byte total are recorded for the compaction kernel, which places tiles after a
 // device-wide scan of the totals (two-pass string offsets, no cross-tile waiting).
+template <bool kView>
 __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
                                             const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
                                             const uint8_t* src, uint32_t rec_addr, bool global,
@@ -383,6 +442,10 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
     bool ok;
     uint32_t ev[kStrFastBytes];
     const StrSpan sp = sop_span(a, op, opp, t, s_cnt, lane, src, rec_addr, s_lut, ok, fast, ev);
+    if (kView && a.mode == 0) {
+        str_view_element(a, op, c, t, sp, ok, fast, ev, src + rec_addr + (uint32_t)op.eo, s_lut, s_str, lane);
+        return;
+    }
     uint32_t tot;
     const uint32_t ex = wave_excl_scan32((uint32_t)sp.utf8_len, lane, tot);
     if (a.mode == 1) {
@@ -444,7 +507,8 @@ __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window&
     for (int i = w.sop_begin; i < w.sop_end; i++) {
         const StrOp op = ldc(a.sops + i);
         const StrCall c = sizes ? StrCall{} : ldc(a.scall + i);
-        str_element(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
+        if (a.str_view) str_element<true>(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
+        else str_element<false>(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
     }
     if (sizes) return;
     decode_generated(a, w, t, lane);
@@ -505,8 +569,11 @@ __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window&
 // wave-instruction) and written to LDS rows of cpitch bytes (odd dword count when padding pays).
 // The loads of tile t + stride are issued before tile t is decoded, KP per lane, ALL of them
 // unconditionally through a range-checked buffer descriptor over [a0, end of input): chunks past
-// the span get an out-of-range offset (no memory access, zero data), and a span reaching past the
-// input is never faulted on -- its tile is restaged synchronously with guarded loads.  Loads
+// the span get an out-of-range offset (no memory access, zero data), and nothing past the input
+// is read.  The range check is per dword (a chunk straddling the end of the input returns its
+// in-range dwords), and the records end on a dword boundary (stride and base are multiples of 4),
+// so every byte of the last tile arrives -- tests/test_gpu_parity.py decodes batches whose input
+// ends 8 bytes into a chunk.  Loads
 // that are always issued and always overwrite the same registers leave the compiler no reason to
 // copy the buffer (a copy would wait for the loads, the whole prefetch) anywhere in the loop.
 // KP: chunks per lane -- exact for the specialised kernel (ceil(chunks per span / 64)), the plan
@@ -524,23 +591,21 @@ struct ContigSpan {
     int mis_dw;      // dwords between a0 and the first record
     int span_dw;     // dwords of the tile's records
     int nch;         // 16-byte chunks to load
-    bool inb;        // whole span inside the input
 };
 
 __device__ __forceinline__ ContigSpan contig_span(const KernelArgs& a, int64_t tile) {
     ContigSpan sp;
     const int64_t t0b = a.base_shift + tile * kWave * (int64_t)a.stride;
     const int64_t left = a.n_rec - tile * kWave;
-    const int nrec_tile = left < kWave ? (int)left : kWave;
+    const int nrec_tile = left < kWave ? (left > 0 ? (int)left : 0) : kWave;   // 0 past the last tile
     sp.a0 = t0b & ~(int64_t)15;
     sp.mis_dw = (int)((t0b - sp.a0) >> 2);
     sp.span_dw = nrec_tile * a.stride_dw;
     sp.nch = (sp.mis_dw + sp.span_dw + 3) >> 2;
-    sp.inb = sp.a0 + 16 * (int64_t)sp.nch <= a.data_len;
     return sp;
 }
 
-// Issue the KP loads of a span (no wait).  The descriptor is built from wave-uniform values made
+// Issue the KP loads of a span (no wait); chunks outside the input read as zeros.  The descriptor is built from wave-uniform values made
 // provably uniform (readfirstlane), so no waterfall loop wraps the loads.
 template <int KP>
 __device__ __forceinline__ void contig_issue(const KernelArgs& a, const ContigSpan& sp, int lane, uint4 (&buf)[KP]) {
@@ -590,24 +655,6 @@ __device__ __forceinline__ void contig_store(const KernelArgs& a, const ContigSp
     for (int u = 0; u < KP; u++) {
         const int c = u * kWave + lane;
         if (u * kWave < sp.nch && c < sp.nch) contig_put(a, sp, c, buf[u], s_img);
-    }
-}
-
-// Synchronous guarded staging (the span reaches past the end of the input).
-__device__ __forceinline__ void contig_stage_guarded(const KernelArgs& a, const ContigSpan& sp, int lane, uint8_t* s_img) {
-    constexpr int kRound = 8;
-    for (int c0 = 0; c0 < sp.nch; c0 += kRound * kWave) {
-        uint4 buf[kRound];
-#pragma unroll
-        for (int u = 0; u < kRound; u++) {
-            const int c = c0 + u * kWave + lane;
-            buf[u] = c < sp.nch ? load16_guarded(a.data, sp.a0 + 16 * (int64_t)c, a.data_len) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < kRound; u++) {
-            const int c = c0 + u * kWave + lane;
-            if (c < sp.nch) contig_put(a, sp, c, buf[u], s_img);
-        }
     }
 }
 
@@ -685,13 +732,15 @@ __device__ __forceinline__ TileCtx tile_ctx(const KernelArgs& a, int64_t tile, i
 // Per-record prologue: segment-redefine selection and OCCURS DEPENDING ON element counts
 // (their count columns written here), reading the record at rp (the LDS image in contiguous
 // mode -- no HBM loads in that loop besides the staging loads -- or HBM).
-template <bool kSel = true>
+// kSeg / kArr: the plan may have a segment map / OCCURS DEPENDING ON arrays (the specialised
+// kernel compiles only the parts its plan has).
+template <bool kSel = true, bool kSeg = true, bool kArr = true>
 __device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, const uint8_t* rp, int lane,
                                               const uint32_t* s_lut, int32_t* s_cnt) {
     // ---- segment redefine selection
     if (kSel && a.rec_seg) t.seg = t.active ? a.rec_seg[t.rec] : -1;   // selected records: segment known
-    else if (a.segmap && t.active) t.seg = segment_of(a, s_lut, rp, t.avail);
-    if (a.mode == 0 && a.seg_col >= 0) {
+    else if (kSeg && a.segmap && t.active) t.seg = segment_of(a, s_lut, rp, t.avail);
+    if (kSeg && a.mode == 0 && a.seg_col >= 0) {
         const DevColumn c = ldc(a.cols + a.seg_col);
         if (t.active) gp((int32_t*)c.values)[t.rec] = t.seg;
         const uint64_t m = __ballot(t.active);
@@ -699,7 +748,7 @@ __device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, c
     }
 
     // ---- OCCURS DEPENDING ON element counts (extractArray, RecordExtractors.scala:66-114)
-    for (int ai = 0; ai < a.n_arrays; ai++) {
+    for (int ai = 0; kArr && ai < a.n_arrays; ai++) {
         const cbx_array ar = ldc(a.arrays + ai);
         int cnt = ar.max_count;
         if (ar.dependee >= 0 && t.active) {
@@ -778,38 +827,34 @@ __device__ __forceinline__ WaveLds wave_lds(const KernelArgs& a, uint8_t* smem, 
 // Fixed-length records, the whole tile span staged once per tile, its loads issued one tile
 // ahead.  Nothing else in this loop loads from HBM (prologue and decode read the LDS image), so
 // no wait on the staging loads or on earlier stores sits in the decode.  `body` decodes one
-// staged tile: body(a, t, img, rec_addr, lds, lane, stamps).
-template <int KP, typename Body>
+// staged tile in two parts, body.pre and body.post (img, rec_addr, lds, lane, stamps).  kLate:
+// the next tile's loads are issued between the two parts instead of before both -- the
+// specialised kernel puts a layout's string elements in `pre` when it also has numerics, so the
+// string phase's register peak does not stack on the prefetch registers.
+template <int KP, int kPro, bool kLate, typename Body>
 __device__ __forceinline__ void contig_loop(const KernelArgs& a, const WaveLds& l, int64_t tile, int64_t tstep,
                                             int lane, const Body& body) {
     uint4 buf[KP];
-    bool have = false;
-    if (tile < a.n_tiles) {
-        const ContigSpan sp = contig_span(a, tile);
-        contig_issue<KP>(a, sp, lane, buf);
-        have = sp.inb;
-    }
+    if (tile < a.n_tiles) contig_issue<KP>(a, contig_span(a, tile), lane, buf);
     Stamps st;
     st.init();
     while (tile < a.n_tiles) {
         const ContigSpan sp = contig_span(a, tile);
-        if (have) contig_store<KP>(a, sp, lane, buf, l.img);
-        else contig_stage_guarded(a, sp, lane, l.img);
+        contig_store<KP>(a, sp, lane, buf, l.img);
         wave_sync_lds();
         st.mark(0);   // staging: wait for the prefetched loads + LDS writes
         const int64_t next = tile + tstep;
-        have = false;
-        if (next < a.n_tiles) {
-            const ContigSpan sn = contig_span(a, next);
-            contig_issue<KP>(a, sn, lane, buf);
-            have = sn.inb;
-        }
+        // issued even past the last tile (a span of no chunks: every offset out of range, no
+        // access), so the buffer is always redefined here and never live across the decode
+        if (!kLate) contig_issue<KP>(a, contig_span(a, next), lane, buf);
         st.mark(1);   // prefetch issue
         TileCtx t = tile_ctx<false>(a, tile, lane);
         const uint32_t rec0 = (uint32_t)(lane * a.cpitch + 4 * sp.mis_dw);   // record start in the image
-        tile_prologue<false>(a, t, l.img + rec0, lane, l.lut, l.cnt);
+        tile_prologue<false, (kPro & 1) != 0, (kPro & 2) != 0>(a, t, l.img + rec0, lane, l.lut, l.cnt);
         st.mark(2);   // prologue
-        body(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
+        body.pre(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
+        if (kLate) contig_issue<KP>(a, contig_span(a, next), lane, buf);
+        body.post(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
         wave_sync_lds();
         st.mark(5);   // end of tile
         tile = next;

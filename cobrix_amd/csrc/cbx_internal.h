@@ -58,7 +58,10 @@ struct StrCall {
     uint64_t* validity;       // validity words of (column, slot)
     uint32_t* local;          // tile-local start of every value of the slot (pitch entries)
     uint8_t* scratch;         // tile regions of the slot: tile t at scratch + t * tile_cap
+                              // (string-view layout: the slot's region of the caller's data buffer)
     int64_t tile_cap;         // bytes per tile region (64 * size * widest UTF-8 expansion, 16-aligned)
+    uint8_t* views;           // string-view layout: the slot's 16-byte views (pitch entries)
+    int64_t tiles_per_buf;    // string-view layout: tiles per Arrow data buffer
 };
 
 // Generated column (File_Id / Record_Id).
@@ -106,6 +109,7 @@ struct KernelArgs {
     const int32_t* rec_seg;    // per-record active segment (selected records), nullptr: from segmap
     int32_t file_id;
     int32_t mode;              // 0 decode, 1 string sizes only
+    int32_t str_view;          // string columns in the Arrow string-view layout
     // fixed-length contiguous staging: the tile's byte span is loaded with 16-byte loads and
     // scattered dword-wise into rows of `cpitch` bytes (odd dword count: conflict-free lanes)
     int32_t contig;

@@ -29,8 +29,10 @@ namespace cbx {
 
 // Interpreter body of the contiguous loop: the plan's windows, read from the tables at run time.
 struct InterpBody {
-    __device__ __forceinline__ void operator()(const KernelArgs& a, const TileCtx& t, const uint8_t* img,
-                                               uint32_t rec_addr, const WaveLds& l, int lane, Stamps& st) const {
+    __device__ __forceinline__ void post(const KernelArgs&, const TileCtx&, const uint8_t*, uint32_t, const WaveLds&, int,
+                                         Stamps&) const {}
+    __device__ __forceinline__ void pre(const KernelArgs& a, const TileCtx& t, const uint8_t* img,
+                                        uint32_t rec_addr, const WaveLds& l, int lane, Stamps& st) const {
         for (int wi = 0; wi < a.n_windows; wi++) {
             const Window w = ldc(a.windows + wi);
             if (a.mode == 1 && w.sop_begin == w.sop_end) continue;
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void decode_kernel(KernelAr
     const int64_t tstep = (int64_t)gridDim.x * kWavesPerBlock;
 
     if (a.contig) {
-        contig_loop<kPre>(a, l, tile, tstep, lane, InterpBody{});
+        contig_loop<kPre, 3, false>(a, l, tile, tstep, lane, InterpBody{});
         return;
     }
 

@@ -253,18 +253,8 @@ __global__ void segid_len_kernel(SegIdArgs a, uint32_t* len) {
     len[r] = r < a.n ? segid_len(a, r, valid) : 0u;
 }
 
-__global__ void segid_write_kernel(SegIdArgs a, int64_t* offsets, uint8_t* data, int64_t capacity, uint64_t* validity,
-                                   int32_t* status) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool act = r < a.n;
-    bool valid = false;
-    uint32_t n = act ? segid_len(a, r, valid) : 0u;
-    const uint64_t m = __ballot(act && valid);
-    if ((threadIdx.x & 63) == 0 && r < a.n + 63) validity[r / 64] = m;
-    if (!act || !valid) return;
-    const int64_t o = offsets[r];
-    if (o + n > capacity) { atomicOr(status, 1); return; }
-    uint8_t* p = data + o;
+// The Seg_Id text of record r at p (segid_len bytes).
+__device__ __forceinline__ void segid_emit(const SegIdArgs& a, int64_t r, uint8_t* p) {
     const int64_t* st = a.state + r * (int64_t)(1 + a.L);
     if (st[0] >= 0) {
         for (int i = 0; i < a.prefix_len; i++) *p++ = a.m->prefix[i];
@@ -279,6 +269,53 @@ __global__ void segid_write_kernel(SegIdArgs a, int64_t* offsets, uint8_t* data,
         *p++ = '_';
         p += put_dec(p, st[1 + a.level]);
     }
+}
+
+__global__ void segid_write_kernel(SegIdArgs a, int64_t* offsets, uint8_t* data, int64_t capacity, uint64_t* validity,
+                                   int32_t* status) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = r < a.n;
+    bool valid = false;
+    uint32_t n = act ? segid_len(a, r, valid) : 0u;
+    const uint64_t m = __ballot(act && valid);
+    if ((threadIdx.x & 63) == 0 && r < a.n + 63) validity[r / 64] = m;
+    if (!act || !valid) return;
+    const int64_t o = offsets[r];
+    if (o + n > capacity) { atomicOr(status, 1); return; }
+    segid_emit(a, r, data + o);
+}
+
+// String-view layout of a Seg_Id column (one thread per record, 256-thread blocks: a wave is a
+// tile): every value is written into its tile's region of the data buffer (wave scan) and its
+// view built from the bytes just written (inline when at most 12 bytes).
+__global__ __launch_bounds__(256) void segid_view_kernel(SegIdArgs a, u32x4* views, uint8_t* data, int64_t tile_bytes,
+                                                         int64_t tiles_per_buf, uint64_t* validity, int64_t pitch) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool act = r < a.n;
+    bool valid = false;
+    const uint32_t n = act ? segid_len(a, r, valid) : 0u;
+    const uint64_t m = __ballot(act && valid);
+    if (lane == 0 && r < pitch) validity[r / 64] = m;
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32(n, lane, tot);
+    if (r >= pitch) return;
+    const int64_t tile = r / 64;
+    uint8_t* p = data + tile * tile_bytes + ex;
+    if (act && valid) segid_emit(a, r, p);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read back this lane's own bytes
+    uint32_t w[3] = {0u, 0u, 0u};
+    const uint32_t k = n > 12 ? 4u : n;
+#pragma unroll
+    for (uint32_t j = 0; j < 12; j++)
+        if (j < k) w[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
+    u32x4 v{n, w[0], w[1], w[2]};
+    if (n > 12) {
+        const int64_t tb = tile / tiles_per_buf;
+        v.z = (uint32_t)tb;
+        v.w = (uint32_t)((tile - tb * tiles_per_buf) * tile_bytes + ex);
+    }
+    views[r] = v;
 }
 
 // ------------------------------------------------------------------------------------------

@@ -35,11 +35,11 @@ OUT_WIDTH = {O_I32: 4, O_I64: 8, O_DEC64: 8, O_DEC128: 16, O_F32: 4, O_F64: 8}
 
 # every symbol include/cobrix_hip.h declares
 EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx_plan_destroy",
-                    "cbx_string_bound", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
+                    "cbx_string_bound", "cbx_string_view_geometry", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
                     "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
                     "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text",
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class NativeLibraryError(RuntimeError):
@@ -87,7 +87,7 @@ class CbxSegmentMap(ctypes.Structure):
 class CbxPlanOptions(ctypes.Structure):
     _fields_ = [("n_columns", ctypes.c_int32), ("file_id", ctypes.c_int32), ("has_segments", ctypes.c_int32),
                 ("window_bytes", ctypes.c_int32), ("segment_column", ctypes.c_int32),
-                ("jit_min_records", ctypes.c_int32), ("reserved", ctypes.c_int32 * 2),
+                ("jit_min_records", ctypes.c_int32), ("string_views", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("lut", ctypes.c_uint32 * 256),
                 ("segments", CbxSegmentMap)]
 
@@ -145,6 +145,7 @@ def load():
     L.cbx_plan_destroy.argtypes = [P]
     L.cbx_plan_destroy.restype = None
     L.cbx_string_bound.argtypes = [P, i64, P]
+    L.cbx_string_view_geometry.argtypes = [P, P, P]
     L.cbx_string_sizes_fixed.argtypes = [P, P, i64, i32, i32, P, P]
     L.cbx_plan_check.argtypes = [P, P]
     L.cbx_decode_fixed.argtypes = [P, P, i64, i32, i32, i64, P, P]

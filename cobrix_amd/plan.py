@@ -146,7 +146,7 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
                segment_redefine_map: Optional[Dict[str, str]] = None, generate_record_id: bool = False,
                file_id: int = 0, window_bytes: int = 0, jit_min_records: int = 0,
                segment_levels: Sequence[str] = (), segment_filter: Optional[List[str]] = None,
-               segment_prefix: str = "") -> DecodePlan:
+               segment_prefix: str = "", string_views: bool = False) -> DecodePlan:
     fields: List[N.CbxField] = []
     arrays: List[N.CbxArray] = []
     columns: List[ColumnInfo] = []
@@ -316,6 +316,7 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
     opts.window_bytes = window_bytes
     opts.segment_column = seg_col
     opts.jit_min_records = jit_min_records
+    opts.string_views = 1 if string_views else 0
     lut = utf8_lut(ascii_charset_table(cb.ascii_charset) if _charset_strings(cb) else lut_for(cb.code_page))
     for i in range(256):
         opts.lut[i] = int(lut[i])

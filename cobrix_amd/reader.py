@@ -74,6 +74,9 @@ class ReaderParameters:
     # fixed-length batches of at least this many records run a copybook-specialised kernel
     # (hipRTC, compiled once per layout): 0 = library default, < 0 = never
     jit_min_records: int = 0
+    # output layout of string columns: Arrow large-string (offsets, two-pass placement) or Arrow
+    # string views (one pass: every value written once by the decode kernel; cobrix_hip.h)
+    string_views: bool = False
 
 
 @dataclass
@@ -104,7 +107,11 @@ class DecodedBatch:
         vb = c["validity"].cpu().numpy().view(np.uint64)
         bits = np.unpackbits(vb.view(np.uint8), bitorder="little").reshape(info.n_slots, pitch * 64)
         out["validity"] = bits[:, :self.n_rec].astype(bool)
-        if c.get("offsets") is not None:
+        if c.get("views") is not None:
+            vw = c["views"].cpu().numpy().reshape(info.n_slots, 64 * pitch, 16)[:, : self.n_rec]
+            data = c["data"].cpu().numpy().tobytes()
+            out["strings"] = [decode_views(vw[s], data, c["buffer_bytes"], s * c["capacity"]) for s in range(info.n_slots)]
+        elif c.get("offsets") is not None:
             # slot s: offsets[s * (pitch + 1) .. + n_rec], absolute into data (slot regions)
             out["offsets"] = c["offsets"].cpu().numpy().reshape(info.n_slots, 64 * pitch + 1)[:, : self.n_rec + 1]
             out["data"] = c["data"].cpu().numpy().tobytes()
@@ -134,6 +141,9 @@ class DecodedBatch:
                 return None
             v = slot * self.n_rec + r
             ot = info.out_type
+            if ot in (N.O_STRING, N.O_BINARY) and "strings" in c:
+                b = c["strings"][slot][r]
+                return b.decode("utf-8") if ot == N.O_STRING else b
             if ot in (N.O_STRING, N.O_BINARY):
                 off = c["offsets"][slot]
                 b = c["data"][int(off[r]):int(off[r + 1])]
@@ -223,7 +233,17 @@ def _alloc_columns(plan: DecodePlan, n_rec: int, slot_capacity: Sequence[int], d
     for ci, info in enumerate(plan.columns):
         n = pitch * info.n_slots
         c: Dict[str, Any] = {"validity": torch.zeros(max(1, info.n_slots * pitch_words), dtype=torch.int64, device=device)}
-        if info.out_type in (N.O_STRING, N.O_BINARY):
+        if info.out_type in (N.O_STRING, N.O_BINARY) and plan.options.string_views:
+            # string views: 16 bytes per value + per-slot regions of whole tiles (cobrix_hip.h)
+            cap = int(slot_capacity[ci])
+            c["views"] = torch.zeros(max(1, n * 16), dtype=torch.uint8, device=device)
+            c["data"] = torch.empty(max(1, cap * info.n_slots), dtype=torch.uint8, device=device)
+            c["capacity"] = cap
+            c["tile_bytes"], c["buffer_bytes"] = view_geometry(cap, pitch_words)
+            cstructs[ci].values = c["views"].data_ptr()
+            cstructs[ci].data = c["data"].data_ptr()
+            cstructs[ci].data_capacity = cap
+        elif info.out_type in (N.O_STRING, N.O_BINARY):
             cap = int(slot_capacity[ci])
             c["offsets"] = torch.zeros(info.n_slots * (pitch + 1), dtype=torch.int64, device=device)
             c["data"] = torch.empty(max(1, cap * info.n_slots), dtype=torch.uint8, device=device)
@@ -241,6 +261,35 @@ def _alloc_columns(plan: DecodePlan, n_rec: int, slot_capacity: Sequence[int], d
         cstructs[ci].validity = c["validity"].data_ptr()
         cols.append(c)
     return cols, cstructs
+
+
+def view_geometry(capacity: int, n_tiles: int) -> Tuple[int, int]:
+    """String-view layout: (tile_bytes, buffer_bytes) of a slot region of `capacity` bytes for
+    n_tiles tiles (cbx_string_bound's capacity; buffers of whole tiles, at most 1 GiB each --
+    cbx_string_view_geometry)."""
+    if n_tiles <= 0 or capacity <= 0:
+        return 0, 0
+    tb = capacity // n_tiles
+    return tb, max(1, (1 << 30) // max(16, tb)) * tb
+
+
+def decode_views(views: np.ndarray, data: bytes, buffer_bytes: int, region: int) -> List[bytes]:
+    """Payload bytes of Arrow string views (16 bytes each: length, inline bytes or prefix +
+    buffer index + offset) whose data buffers are cut from `data` at `region` in pieces of
+    buffer_bytes."""
+    v = views.reshape(-1, 16)
+    ln = v[:, 0:4].copy().view(np.int32).reshape(-1)
+    bi = v[:, 8:12].copy().view(np.int32).reshape(-1)
+    of = v[:, 12:16].copy().view(np.int32).reshape(-1)
+    out = []
+    for i in range(v.shape[0]):
+        n = int(ln[i])
+        if n <= 12:
+            out.append(bytes(v[i, 4:4 + n]))
+        else:
+            s = region + int(bi[i]) * buffer_bytes + int(of[i])
+            out.append(data[s:s + n])
+    return out
 
 
 def string_capacity(native_plan, n_rec: int, exact: Optional[Sequence[int]] = None) -> List[int]:
@@ -293,7 +342,7 @@ class _BaseReader:
                                jit_min_records=params.jit_min_records,
                                segment_levels=params.segment_id_levels if var else (),
                                segment_filter=params.segment_id_filter if var else None,
-                               segment_prefix=params.segment_id_prefix)
+                               segment_prefix=params.segment_id_prefix, string_views=params.string_views)
         self.native = NativePlan(self.plan)
 
     @property

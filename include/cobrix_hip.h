@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 5
+#define CBX_ABI_VERSION 6
 
 /* status codes */
 #define CBX_OK 0
@@ -168,7 +168,8 @@ typedef struct {
     int32_t jit_min_records;/* batches of at least this many records run a kernel
                                specialised for the copybook (compiled once with hipRTC);
                                0 = default (262144), < 0 = never */
-    int32_t reserved[2];
+    int32_t string_views;   /* string/binary columns in the Arrow string-view layout (below) */
+    int32_t reserved;
     uint32_t lut[256];      /* code page: UTF-8 bytes (0-23), length (24-25), trimmable (31) */
     cbx_segment_map segments;
 } cbx_plan_options;
@@ -183,7 +184,19 @@ typedef struct {
  * offsets[s * (pitch + 1) + r], r = 0 .. n_rec (absolute byte positions in `data`; entries past
  * n_rec are padding).  data_capacity = cbx_string_bound(...) always suffices; a smaller
  * capacity (e.g. from cbx_string_sizes_*) is honoured: payload never overflows its region, an
- * overflow is reported by cbx_plan_check. */
+ * overflow is reported by cbx_plan_check.
+ *
+ * String-view layout (cbx_plan_options.string_views != 0; Arrow Utf8View / BinaryView): `values`
+ * holds n_slots * pitch views of 16 bytes (value (s, r) at view s * pitch + r): int32 length, then
+ * the UTF-8 bytes inline when length <= 12 (zero padded), else their first 4 bytes, an int32
+ * data-buffer index and an int32 offset into that buffer.  `data` holds n_slots regions of
+ * data_capacity bytes; a region is cut into data buffers of buffer_bytes (the last one shorter):
+ * buffer k of slot s starts at data + s * data_capacity + k * buffer_bytes
+ * (cbx_string_view_geometry).  Every tile of 64 records owns tile_bytes of its slot's region,
+ * so a value is written once, where the decode kernel produces it -- no scan over the batch and
+ * no placement pass.  data_capacity must be at least ceil(n_rec / 64) * tile_bytes
+ * (cbx_string_bound returns that in this layout; a smaller one fails the call with
+ * CBX_E_CAPACITY).  `offsets` and `data_sizes` are unused. */
 typedef struct {
     void* values;          /* fixed-width values (NULL for strings) */
     uint64_t* validity;
@@ -204,8 +217,14 @@ int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const cbx_array* 
 void cbx_plan_destroy(cbx_plan* plan);
 
 /* Upper bound of a string column's payload per slot for n_rec records (n_rec * field size *
- * widest UTF-8 expansion of the code page); out_bytes[n_columns] (0 for non-string columns). */
+ * widest UTF-8 expansion of the code page; string-view layout: ceil(n_rec / 64) * tile_bytes);
+ * out_bytes[n_columns] (0 for non-string columns). */
 int cbx_string_bound(const cbx_plan* plan, int64_t n_rec, int64_t* out_bytes);
+
+/* String-view layout geometry per column (0 for non-string columns): tile_bytes[n_columns] =
+ * bytes of a slot region owned by one tile of 64 records, buffer_bytes[n_columns] = bytes per
+ * Arrow data buffer of a slot (a whole number of tiles, at most 1 GiB). */
+int cbx_string_view_geometry(const cbx_plan* plan, int64_t* tile_bytes, int64_t* buffer_bytes);
 
 /* Exact payload sizes (optional pre-pass, synchronous): out_sizes[n_columns] receives, per
  * string column, the largest slot payload of the batch (0 for non-string columns). */

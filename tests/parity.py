@@ -52,14 +52,15 @@ def compare_batch(batch, res: "O.OracleResult", max_report: int = 10) -> List[st
         v = slot * n_rec + rec
         ot = info.out_type
         if ot in (N.O_STRING, N.O_BINARY):
-            off = g["offsets"]
-            data = g["data"]
             heap = res.heap
             lo, hi = o["lo"][m], o["hi"][m]
             nbad = 0
             for k in range(len(v)):
-                so = off[slot[k]]   # per-slot Arrow offsets (absolute into data)
-                a = data[int(so[rec[k]]):int(so[rec[k] + 1])]
+                if "strings" in g:   # string-view layout, decoded by host_column
+                    a = g["strings"][slot[k]][rec[k]]
+                else:
+                    so = g["offsets"][slot[k]]   # per-slot Arrow offsets (absolute into data)
+                    a = g["data"][int(so[rec[k]]):int(so[rec[k] + 1])]
                 b = heap[int(lo[k]):int(lo[k]) + int(hi[k])]
                 if a != b:
                     nbad += 1
@@ -124,11 +125,24 @@ def compare_sample(batch, idx: np.ndarray, res: "O.OracleResult", max_report: in
         rec, slot = o["rec"][m], o["slot"][m]
         ot = info.out_type
         if ot in (N.O_STRING, N.O_BINARY):
-            offs = c["offsets"].view(info.n_slots, pitch + 1)
+            views = c["views"].view(info.n_slots, pitch, 16) if "views" in c else None
+            offs = c["offsets"].view(info.n_slots, pitch + 1) if views is None else None
             for k in range(len(rec)):
                 r, s = int(idx[rec[k]]), int(slot[k])
-                a0, a1 = int(offs[s, r]), int(offs[s, r + 1])
-                got = bytes(c["data"][a0:a1].cpu().numpy())
+                if views is not None:
+                    vb = views[s, r].cpu().numpy()
+                    ln, bi, of = (int(x) for x in vb.view(np.int32)[[0, 2, 3]])
+                    if ln <= 12:
+                        got = bytes(vb[4:4 + ln])
+                    else:
+                        a0 = s * c["capacity"] + bi * c["buffer_bytes"] + of
+                        got = bytes(c["data"][a0:a0 + ln].cpu().numpy())
+                        if got[:4] != bytes(vb[4:8]):
+                            errs.append(f"{info.node.name}: view prefix differs at record {r}")
+                            break
+                else:
+                    a0, a1 = int(offs[s, r]), int(offs[s, r + 1])
+                    got = bytes(c["data"][a0:a1].cpu().numpy())
                 want = res.heap[int(o["lo"][m][k]):int(o["lo"][m][k]) + int(o["hi"][m][k])]
                 if got != want:
                     errs.append(f"{info.node.name}: string differs at record {r}: {got!r} vs {want!r}")

@@ -22,6 +22,11 @@ def _gpu():
         pytest.skip("no GPU")
 
 
+def _replace(p, **kw):
+    import dataclasses
+    return dataclasses.replace(p, **kw)
+
+
 def gpu_rows(case, **extra):
     from cobrix_amd.reader import FixedLenNestedReader, VarLenNestedReader
     p, var_len = GC.params(case)
@@ -36,12 +41,13 @@ def gpu_rows(case, **extra):
 
 
 @pytest.mark.parametrize("name", sorted(GC.CASES))
-@pytest.mark.parametrize("jit", [-1, 1])
-def test_gpu_golden_rows(name, jit):
-    """Both decode kernels (table-driven: jit=-1; copybook-specialised: jit=1) reproduce the
-    reference's golden rows and the oracle's full row set."""
+@pytest.mark.parametrize("jit,views", [(-1, False), (1, False), (-1, True), (1, True)])
+def test_gpu_golden_rows(name, jit, views):
+    """Both decode kernels (table-driven: jit=-1; copybook-specialised: jit=1), in both string
+    layouts (Arrow offsets / Arrow string views), reproduce the reference's golden rows and the
+    oracle's full row set."""
     case = GC.CASES[name]
-    rd, rows = gpu_rows(case, jit_min_records=jit)
+    rd, rows = gpu_rows(case, jit_min_records=jit, string_views=views)
     errs = GC.compare(case, rows)
     assert not errs, errs[:10]
     p, var_len = GC.params(case)
@@ -121,6 +127,7 @@ def test_gpu_sparse_index_modes(extra, override, n):
     assert got == exp
 
 
+@pytest.mark.parametrize("views", [False, True])
 @pytest.mark.parametrize("extra", [
     {"segment_id_level0": "C", "segment_id_level1": "P", "segment_id_prefix": "XYZ", "input_split_records": "1000",
      "generate_record_id": "true"},
@@ -130,9 +137,9 @@ def test_gpu_sparse_index_modes(extra, override, n):
     {"segment_id_level0": "P", "segment_id_level1": "C", "segment_filter": "C,P", "input_split_size_mb": "1",
      "file_start_offset": "100", "file_end_offset": "120", "generate_record_id": "true"},
 ])
-def test_gpu_selection_vs_oracle(extra):
+def test_gpu_selection_vs_oracle(extra, views):
     """Record_Id per entry, Seg_IdN, segment_filter and root-reached filtering on 20 k records
-    (both decode kernels)."""
+    (both decode kernels, both string layouts)."""
     from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow
     raw = rdw_narrow(20_000, seed=11)[0].numpy().tobytes()
     if "file_start_offset" in extra:
@@ -140,6 +147,8 @@ def test_gpu_selection_vs_oracle(extra):
     for jit in (-1, 1):
         rd, p = _var_reader(RDW_NARROW_COPYBOOK, {**_SYN_OPTS, **extra})
         rd.params.jit_min_records = jit
+        if views:
+            rd = type(rd)(RDW_NARROW_COPYBOOK, _replace(rd.params, string_views=True))
         rows = rd.read(raw, file_id=2).to_rows()
         exp = RO.var_len_rows(rd.copybook, raw, p, file_id=2)
         assert len(rows) == len(exp)

@@ -206,16 +206,18 @@ def _jit_cases():
     return {"test1": t1, "test6": t6, "syn200": syn, "fuzz_cp037": fz}
 
 
+@pytest.mark.parametrize("views", [False, True])
 @pytest.mark.parametrize("case", ["test1", "test6", "syn200", "fuzz_cp037"])
-def test_specialised_kernel_vs_oracle(case):
-    """The copybook-specialised kernel (hipRTC, cbx_jit.h) gives the oracle's results bit for bit."""
+def test_specialised_kernel_vs_oracle(case, views):
+    """The copybook-specialised kernel (hipRTC, cbx_jit.h) gives the oracle's results bit for bit,
+    in both string layouts (Arrow offsets / Arrow string views)."""
     cb_text, data, kw, okw = _jit_cases()[case]
-    rd, batch = _fixed(cb_text, data, jit_min_records=1, **kw)
+    rd, batch = _fixed(cb_text, data, jit_min_records=1, string_views=views, **kw)
     assert _kernel_kind(rd) == 1, "specialised kernel did not run"
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data, **okw))
     assert not errs, errs
     # the table-driven kernel on the same plan layout agrees as well
-    rd2, batch2 = _fixed(cb_text, data, jit_min_records=-1, **kw)
+    rd2, batch2 = _fixed(cb_text, data, jit_min_records=-1, string_views=views, **kw)
     assert _kernel_kind(rd2) == 0
     assert not compare_batch(batch2, O.decode_fixed(rd2.copybook, data, **okw))
 
@@ -236,14 +238,15 @@ def test_specialised_kernel_segments_and_offsets():
     assert not compare_batch(batch, res)
 
 
+@pytest.mark.parametrize("views", [False, True])
 @pytest.mark.parametrize("n,jit", [(1, 0), (4097, 0), (50_000, 0), (50_000, 1), (300_001, 0)])
-def test_synstr200_vs_oracle(n, jit):
-    """Config C3 (string-heavy cp037, trim both): UTF-8 payloads and Arrow offsets bit-exact, on
-    both kernels (jit=1 forces the copybook-specialised kernel the bench runs; 300,001 records pass
-    the default specialisation threshold)."""
+def test_synstr200_vs_oracle(n, jit, views):
+    """Config C3 (string-heavy cp037, trim both): UTF-8 payloads bit-exact in both string layouts
+    (Arrow offsets, Arrow string views), on both kernels (jit=1 forces the copybook-specialised
+    kernel the bench runs; 300,001 records pass the default specialisation threshold)."""
     from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
     data = synstr200(n, seed=3 + n).numpy().tobytes()
-    rd, batch = _fixed(SYNSTR200_COPYBOOK, data, ebcdic_code_page="cp037", jit_min_records=jit)
+    rd, batch = _fixed(SYNSTR200_COPYBOOK, data, ebcdic_code_page="cp037", jit_min_records=jit, string_views=views)
     if n >= 262_144 or jit == 1:
         assert _kernel_kind(rd) == 1
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
@@ -271,14 +274,15 @@ def test_wide_odo_vs_oracle():
     assert not errs, errs
 
 
-def test_syn200_full_size_sampled_parity():
+@pytest.mark.parametrize("views", [False, True])
+def test_syn200_full_size_sampled_parity(views):
     """The bench's own configuration (C2: 50 M SYN200 records = 10 GB resident in HBM, the
     copybook-specialised kernel): 6,000 records sampled across the whole batch (random, plus the
     first and last tiles) are bit-exact against the oracle, and every string offset row is monotone."""
     from parity import compare_sample
     n = 50_000_000
     rec = syn200(n, seed=20261015, device="cuda")
-    rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters())
+    rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters(string_views=views))
     batch = rd.decode_device(rec.view(-1), n * 200)
     assert _kernel_kind(rd) == 1
     rng = np.random.default_rng(2)
@@ -287,8 +291,43 @@ def test_syn200_full_size_sampled_parity():
     errs = compare_sample(batch, idx, O.decode_fixed(rd.copybook, sample))
     assert not errs, errs
     for ci, info in enumerate(rd.plan.columns):
-        if info.out_type == 7:   # O_STRING: offsets non-decreasing over all 50 M records
+        if info.out_type == 7 and not views:   # O_STRING: offsets non-decreasing over all 50 M records
             offs = batch.cols[ci]["offsets"][: n + 1]
             assert bool((offs[1:] >= offs[:-1]).all())
+    del batch, rec
+    torch.cuda.empty_cache()
+
+
+def test_synstr200_full_size_sampled_views():
+    """Config C3 at the bench's size (50 M SYNSTR200 records, string views, the specialised
+    kernel): a sample across the batch is bit-exact; every view is well-formed (inline bytes past
+    the length are zero, long views point inside their tile's region)."""
+    from parity import compare_sample
+    from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
+    n = 50_000_000
+    rec = synstr200(n, seed=20261017, device="cuda")
+    rd = FixedLenNestedReader(SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_views=True))
+    batch = rd.decode_device(rec.view(-1), n * 200)
+    assert _kernel_kind(rd) == 1
+    rng = np.random.default_rng(5)
+    idx = np.unique(np.concatenate([np.arange(128), n - 128 + np.arange(128), rng.integers(0, n, 3744)]))
+    sample = rec[torch.as_tensor(idx, device="cuda")].cpu().numpy().tobytes()
+    errs = compare_sample(batch, idx, O.decode_fixed(rd.copybook, sample))
+    assert not errs, errs
+    c = batch.cols[0]
+    v = c["views"].view(-1, 16)[:n].view(torch.int32)
+    ln = v[:, 0]
+    assert int(ln.min()) >= 0 and int(ln.max()) <= 40
+    short = ln <= 12
+    # inline padding is zero: the bytes of word k of a short view past its length
+    for k in (1, 2, 3):
+        w = v[:, k].to(torch.int64) & 0xFFFFFFFF
+        keep = (ln - 4 * (k - 1)).clamp(0, 4)
+        mask = torch.where(keep >= 4, torch.full_like(w, 0xFFFFFFFF), (1 << (8 * keep.to(torch.int64))) - 1)
+        assert bool(((w & ~mask)[short] == 0).all())
+    tiles = torch.arange(n, device="cuda") // 64
+    pos = v[:, 2].to(torch.int64) * c["buffer_bytes"] + v[:, 3].to(torch.int64)
+    lo = tiles * c["tile_bytes"]
+    assert bool(((pos >= lo) & (pos + ln.to(torch.int64) <= lo + c["tile_bytes"]))[~short].all())
     del batch, rec
     torch.cuda.empty_cache()
