@@ -191,13 +191,14 @@ __device__ __forceinline__ bool sop_fast(const StrOp& op, bool global) {
     return !global && op.size <= kStrFastBytes && (op.kind == CBX_K_STRING || op.kind == CBX_K_STRING_ASCII);
 }
 
+// Value of record (tile * 64 + lane) of a slot row: the tile's row base is wave-uniform (scalar
+// registers) and the lane offset a 32-bit vector offset, so the store takes the saddr form.
 template <int W>
-__device__ __forceinline__ void store_w(void* values, int64_t v, const Val& x, int out_type) {
-    // v: element index within the slot row
+__device__ __forceinline__ void store_w(void* values, int64_t tile, int lane, const Val& x, int out_type) {
     const int w = W ? W : (out_type == CBX_O_I32 || out_type == CBX_O_F32 ? 4 : out_type == CBX_O_DEC128 ? 16 : 8);
-    if (w == 4) gp((uint32_t*)values)[v] = (uint32_t)x.lo;
-    else if (w == 8) gp((uint64_t*)values)[v] = x.lo;
-    else gp((u32x4*)values)[v] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
+    if (w == 4) (gp((uint32_t*)values) + tile * kWave)[lane] = (uint32_t)x.lo;
+    else if (w == 8) (gp((uint64_t*)values) + tile * kWave)[lane] = x.lo;
+    else (gp((u32x4*)values) + tile * kWave)[lane] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
 }
 
 // One batch of numeric ops (same decoder variant V, output width W).  Decoding is branch-free
@@ -223,7 +224,7 @@ __device__ __forceinline__ void num_one(const KernelArgs& a, const NumOp& op, in
     }
     const NumCall c = ldc(a.ncall + i);
     // every lane stores (slot rows are padded to 64 * n_tiles values): no exec-mask branches
-    store_w<W>(c.values, t.rec, x, op.out_type);
+    store_w<W>(c.values, t.tile, lane, x, op.out_type);
     const uint64_t m = __ballot(x.valid);
     gp(c.validity)[t.tile] = m;
     if (V == V_ZONED16 || V == V_GENERIC || kGlobal) {
@@ -303,7 +304,7 @@ __device__ __forceinline__ void run_elem(const KernelArgs& a, const NumOp& op, c
         x.valid &= ok;
     }
     const int w = W ? W : (op.out_type == CBX_O_I32 || op.out_type == CBX_O_F32 ? 4 : op.out_type == CBX_O_DEC128 ? 16 : 8);
-    store_w<W>(c.values + (int64_t)r * a.pitch * w, t.rec, x, op.out_type);
+    store_w<W>(c.values + (int64_t)r * a.pitch * w, t.tile, lane, x, op.out_type);
     const uint64_t m = __ballot(x.valid);
     gp(c.validity + (int64_t)r * a.n_tiles)[t.tile] = m;
     if (V == V_ZONED16 || V == V_GENERIC) {
@@ -424,7 +425,7 @@ __device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrO
         const int64_t tb = t.tile / c.tiles_per_buf;
         v = u32x4{(uint32_t)len, pre, (uint32_t)tb, (uint32_t)((t.tile - tb * c.tiles_per_buf) * c.tile_cap + ex)};
     }
-    gp((u32x4*)c.views)[t.rec] = v;
+    (gp((u32x4*)c.views) + t.tile * kWave)[lane] = v;
     wave_sync_lds();   // the staging area is reused by the next element
 }
 
@@ -442,7 +443,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
     bool ok;
     uint32_t ev[kStrFastBytes];
     const StrSpan sp = sop_span(a, op, opp, t, s_cnt, lane, src, rec_addr, s_lut, ok, fast, ev);
-    if (kView && a.mode == 0) {
+    if (kView) {   // decode mode only: the view layout has no sizes pre-pass (cbx_string_bound)
         str_view_element(a, op, c, t, sp, ok, fast, ev, src + rec_addr + (uint32_t)op.eo, s_lut, s_str, lane);
         return;
     }
@@ -453,7 +454,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
         return;
     }
     gp(c.validity)[t.tile] = __ballot(ok);
-    gp(c.local)[t.rec] = ex;
+    (gp(c.local) + t.tile * kWave)[lane] = ex;
     if (lane == 0) gp(a.str_tot)[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
     auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
     const uint8_t* sp_src = src + rec_addr + (uint32_t)op.eo;

@@ -57,7 +57,7 @@ struct InterpBody {
 
 __global__ __launch_bounds__(kWave * kWavesPerBlock) void decode_kernel(KernelArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int wid = threadIdx.x / kWave;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform to the compiler
     const int lane = threadIdx.x % kWave;
     const WaveLds l = wave_lds(a, smem, wid);
     for (int i = threadIdx.x; i < 256; i += blockDim.x) l.lut[i] = a.lut[i];

@@ -1,0 +1,37 @@
+"""Build the library from another git revision as cobrix_amd/libcobrix_hip_<name>.so (A/B timing
+within one GPU call: CBX_LIB_VARIANT=<name> python bench.py ...).  Diagnostic; never shipped.
+
+Usage: python tools/build_variant.py <git rev> <name>
+"""
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    rev, name = sys.argv[1], sys.argv[2]
+    import __graft_entry__ as G
+    with tempfile.TemporaryDirectory() as d:
+        arch = subprocess.run(["git", "archive", rev, "cobrix_amd/csrc", "include"], cwd=ROOT, check=True,
+                              capture_output=True).stdout
+        subprocess.run(["tar", "-x", "-C", d], input=arch, check=True)
+        csrc = os.path.join(d, "cobrix_amd", "csrc")
+        inc = os.path.join(d, "include")
+        G.JIT_HEADERS = (("cobrix_hip.h", os.path.join(inc, "cobrix_hip.h")),
+                         ("cbx_decode.h", os.path.join(csrc, "cbx_decode.h")),
+                         ("cbx_internal.h", os.path.join(csrc, "cbx_internal.h")),
+                         ("cbx_device.h", os.path.join(csrc, "cbx_device.h")))
+        G.CSRC = csrc
+        G._write_jit_bundle()
+        out = os.path.join(ROOT, "cobrix_amd", f"libcobrix_hip_{name}.so")
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                        "-I" + inc, "-I" + csrc, "-o", out, os.path.join(csrc, "cbx_capi.hip"), "-lhiprtc"], check=True)
+        print(out)
+
+
+if __name__ == "__main__":
+    main()

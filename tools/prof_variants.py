@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--records", type=int, default=10_000_000)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--only", default=None, help="run one variant (for rocprofv3 passes)")
+    ap.add_argument("--views", action="store_true", help="string columns in the string-view layout")
     a = ap.parse_args()
     import torch
     from cobrix_amd import native as N
@@ -49,7 +50,7 @@ def main():
     for name, keep in VARIANTS.items():
         if a.only and name != a.only:
             continue
-        rd = FixedLenNestedReader(variant(SYN200_COPYBOOK, keep), ReaderParameters())
+        rd = FixedLenNestedReader(variant(SYN200_COPYBOOK, keep), ReaderParameters(string_views=a.views))
         cols, cs = _alloc_columns(rd.plan, a.records, string_capacity(rd.native, a.records), rec.device)
         h = rd.native.handle
         N.check(L.cbx_decode_fixed(h, rec.data_ptr(), a.records, 200, 0, 0, cs, st))

@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=10_000_000)
     ap.add_argument("--variant", default="full")
+    ap.add_argument("--views", action="store_true")
     a = ap.parse_args()
     import torch
     from cobrix_amd import native as N
@@ -30,7 +31,7 @@ def main():
     L = N.load()
     L.cbx_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    rd = FixedLenNestedReader(variant(SYN200_COPYBOOK, VARIANTS[a.variant]), ReaderParameters())
+    rd = FixedLenNestedReader(variant(SYN200_COPYBOOK, VARIANTS[a.variant]), ReaderParameters(string_views=a.views))
     cols, cs = _alloc_columns(rd.plan, a.records, string_capacity(rd.native, a.records), rec.device)
     h = rd.native.handle
     out = (ctypes.c_uint64 * 8)()
