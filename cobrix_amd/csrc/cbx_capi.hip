@@ -590,8 +590,9 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.gops = (const CBX_CONST GenOp*)S.d_gops;
     a.lds_rows = (a.lds_rows + 15) & ~15;
     a.lds_counts = ((int)P->harrays.size() * kWave * 4 + 15) & ~15;
-    // string-view layout: a 16-byte inline slot per lane in front of the packed long payloads
-    a.str_stage = S.max_str_items > 0 ? P->str_stage + (P->view && mode == 0 ? 16 * kWave : 0) : 0;
+    // string-view layout: the inline slots (16 bytes per short value) share the area with the long
+    // payloads, which it holds for any tile as long as it is at least 16 bytes per lane
+    a.str_stage = S.max_str_items > 0 ? (P->view && mode == 0 ? std::max(P->str_stage, 16 * kWave) : P->str_stage) : 0;
     // per-lane dump slots for the branch-free string stores (a shared slot serialises the wave's
     // LDS stores) -- unless the extra 4 * kWave bytes per wave cost a resident workgroup per CU
     // (wide windowed layouts sit close to the LDS limit; C5 decode 49.7 -> 62.1 ms with them)
@@ -758,6 +759,11 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     const hipError_t oe = jfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, jfn, kWave * kWavesPerBlock, lds)
                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, decode_kernel, kWave * kWavesPerBlock, lds);
     if (oe == hipSuccess && occ > 0) blocks_per_cu = std::min(blocks_per_cu, occ);
+    // string-dominated contiguous layouts run best at 4 workgroups (8 waves) per CU: SYNSTR200 (10 x
+    // X(20)) decodes in 8.7 ms at 4, 13.4 ms at 5 and 11.6 ms at 3, while SYN200 (1 string, 27
+    // numerics) and the windowed C4/C5 layouts gain from every extra resident workgroup
+    if (contig && S.sops.size() >= S.nops.size() && S.sops.size() > 0) blocks_per_cu = std::min(blocks_per_cu, 4);
+    if (const char* e = getenv("CBX_MAX_BLOCKS_PER_CU")) blocks_per_cu = std::max(1, std::min(blocks_per_cu, atoi(e)));   // tuning
     const int64_t blocks_needed = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t grid = std::min<int64_t>(blocks_needed, (int64_t)P->num_cus * blocks_per_cu);
     const bool prof = P->profiling && mode == 0;
@@ -954,8 +960,10 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     if (!d_data || n_bytes < 0 || !params || !n_records || (n_seeds > 0 && !seeds))
         return fail(CBX_E_ARGUMENT, "cbx_frame_rdw: invalid arguments");
     *n_records = 0;
-    // seed ranges cut into chunks (rdw_spec_kernel / rdw_fix_kernel / rdw_emit_kernel)
-    int64_t chunk = 16 * 1024;
+    // seed ranges cut into chunks (rdw_spec_kernel / rdw_fix_kernel / rdw_place_kernel)
+    // 64 KiB chunks: C4's 65-byte records ~1,000 per chunk; C5's 16 KB records still leave every
+    // chunk a few headers (framing 13.9 ms at 16 KiB -> 3.4 ms; C4 4.6 -> 4.5 ms)
+    int64_t chunk = 64 * 1024;
     if (const char* e = getenv("CBX_RDW_CHUNK_BYTES")) chunk = std::max<int64_t>(8, atoll(e));   // tests: many chunks
     std::vector<int64_t> hs;
     if (n_seeds <= 0) hs.push_back(0);
@@ -972,9 +980,18 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     const int64_t nb = (n + kScanTile - 1) / kScanTile;
     // one device block: entry, exit x2, err, base (int64 x n) | first_err, total, changed | block sums |
     // ranges | count (u32 x n)
+    // staging: chunk bytes / 40 records per chunk (C4's ~65-byte records use ~60 % of it; chunks of
+    // shorter records are walked again by the placement pass)
+    const int64_t stage_cap = (std::max<int64_t>(16, chunk / 40) + 7) & ~(int64_t)7;
     const size_t bytes = sizeof(int64_t) * (5 * n + 4 + nb) + sizeof(RdwRange) * ranges.size() + sizeof(uint32_t) * n + 64;
+    const size_t stage_bytes = (size_t)n * stage_cap * (sizeof(int64_t) + sizeof(int32_t));
     uint8_t* blk = nullptr;
+    uint8_t* stage = nullptr;
     HIP_CHECK(hipMallocAsync((void**)&blk, bytes, st));
+    if (hipMallocAsync((void**)&stage, stage_bytes, st) != hipSuccess) {
+        (void)hipFreeAsync(blk, st);
+        return fail(CBX_E_HIP, "cbx_frame_rdw: staging allocation of " + std::to_string(stage_bytes) + " bytes failed");
+    }
     int64_t* d64 = (int64_t*)blk;
     RdwChunkArgs c{};
     c.entry = d64;
@@ -987,6 +1004,9 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     RdwRange* d_ranges = (RdwRange*)(d_block_sums + nb);
     c.count = (uint32_t*)(d_ranges + ranges.size());
     c.ranges = d_ranges; c.n_ranges = (int32_t)ranges.size(); c.chunk = chunk; c.n = n;
+    c.stage_off = (int64_t*)stage;
+    c.stage_len = (int32_t*)(stage + (size_t)n * stage_cap * sizeof(int64_t));
+    c.stage_cap = stage_cap;
     HIP_CHECK(hipMemcpyAsync(d_ranges, ranges.data(), sizeof(RdwRange) * ranges.size(), hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemsetAsync(d_first_err, 0xFF, sizeof(unsigned long long), st));
     RdwArgs a{};
@@ -1015,11 +1035,12 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(kScanBlock), 0, st, d_block_sums, nb);
     hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)c.count, n,
                        (const int64_t*)d_block_sums, d_base);
-    hipLaunchKernelGGL(rdw_emit_kernel, dim3(blocks), dim3(threads), 0, st, a, c, (const int64_t*)d_base, d_rec_off,
-                       d_rec_len, capacity, d_first_err);
+    hipLaunchKernelGGL(rdw_place_kernel, dim3((unsigned)((n + kRdwPlaceWaves - 1) / kRdwPlaceWaves)), dim3(kWave * kRdwPlaceWaves),
+                       0, st, a, c, (const int64_t*)d_base, d_rec_off, d_rec_len, capacity, d_first_err);
     HIP_CHECK(hipGetLastError());
     unsigned long long res[2] = {0, 0};
     HIP_CHECK(hipMemcpyAsync(res, d_first_err, sizeof(res), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipFreeAsync(stage, st));
     HIP_CHECK(hipFreeAsync(blk, st));
     HIP_CHECK(hipStreamSynchronize(st));
     const unsigned long long first_err = res[0];

@@ -375,25 +375,29 @@ __device__ __forceinline__ void num_group(const KernelArgs& a, const NumOp (&op)
 // UTF-8 bytes inline (<= 12, zero padded) or their first 4 bytes + data buffer index + offset.
 // Payloads longer than 12 bytes are packed (wave scan) into the tile's region of the slot's data
 // buffer: staged in LDS and copied out in 16-byte pieces when the tile's long payload fits the
-// staging area, else written straight from the lanes.  Short payloads go to a 16-byte LDS slot
-// per lane and into the view.  One pass, no scan across tiles, no placement kernel.
+// staging area, else written straight from the lanes.  Short payloads go to 16-byte LDS slots in
+// front of the long ones (one scan places both: every lane takes 16 bytes or its length, so the
+// area a plan sizes for 64 values of the field -- at least 1 KiB -- holds the tile) and into the
+// view.  One pass, no scan across tiles, no placement kernel.
 __device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrOp& op, const StrCall& c, const TileCtx& t,
                                                  const StrSpan& sp, bool ok, bool fast, const uint32_t (&ev)[kStrFastBytes],
                                                  const uint8_t* sp_src, const uint32_t* s_lut, uint8_t* s_str, int lane) {
     const int len = ok ? sp.utf8_len : 0;
     const bool lng = len > 12;
-    uint32_t tot;
-    const uint32_t ex = wave_excl_scan32(lng ? (uint32_t)len : 0u, lane, tot);
+    // one scan: short slots counted above bit 20, long payload bytes below (<= 64 * 96 bytes)
+    uint32_t both;
+    const uint32_t exb = wave_excl_scan32(lng ? (uint32_t)len : (1u << 20), lane, both);
+    const uint32_t ex = exb & 0xFFFFFu, tot = both & 0xFFFFFu, n_short = both >> 20;
     gp(c.validity)[t.tile] = __ballot(ok);
     auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
-    uint8_t* s_short = s_str + 16 * lane;          // this lane's inline bytes
-    uint8_t* s_long = s_str + 16 * kWave;          // the tile's long payloads, packed
+    uint8_t* s_short = s_str + 16 * (exb >> 20);   // this lane's inline bytes
+    uint8_t* s_long = s_str + 16 * n_short;        // the tile's long payloads, packed (16-aligned)
     // wave-uniform; always true for the register path (the plan sizes the staging area for it in
     // this layout), so its unrolled byte writes never target global memory
-    const bool staged = fast || (int)tot <= a.str_stage - 16 * kWave;
+    const bool staged = fast || (int)(16 * n_short + tot) <= a.str_stage;
     uint8_t* region = c.scratch + t.tile * c.tile_cap;           // 16-byte aligned
     uint8_t* dump = s_str + a.str_stage + a.dump_stride * lane;
-    *(u32x4*)s_short = u32x4{0u, 0u, 0u, 0u};
+    if (!lng) *(u32x4*)s_short = u32x4{0u, 0u, 0u, 0u};   // inline bytes are zero padded
     if (lng && !staged) {
         if (fast) string_write32e(ev, sp, region + ex, dump, op.size, op.pad);
         else string_write(op.kind, sp_src, sp, region + ex, lutf);

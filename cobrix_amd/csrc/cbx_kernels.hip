@@ -324,7 +324,8 @@ __global__ __launch_bounds__(256) void fixup_kernel(KernelArgs a, const CBX_CONS
 
 // ------------------------------------------------------------------------------------------
 // RDW framing (RecordHeaderParserRDW.getRecordMetadata + VRLRecordReader.fetchRecordUsingRdwHeaders)
-// One lane per seed segment [seeds[k], seeds[k+1]); pass 0 counts, pass 1 writes.
+// One lane per chunk of a seed range walks its header chain; the walk stages the records it finds
+// in a per-chunk region, and one placement pass moves them to their final positions.
 // ------------------------------------------------------------------------------------------
 struct RdwArgs {
     const uint8_t* data;
@@ -390,8 +391,13 @@ __device__ __forceinline__ RdwStep rdw_step(const RdwArgs& a, int64_t pos) {
 // start; the seed itself for a range's first chunk) to its exit (first header position >= end);
 // then rounds of the fix kernel replace each entry with the predecessor's exit and re-walk the
 // chunks that change, until no chunk changes: by induction from the seeds the entries are then
-// exactly the sequential walk's header positions.  A final pass writes (offset, length) of the
-// valid records at each chunk's scanned base.
+// exactly the sequential walk's header positions.  Every walk stages (offset, length) of the
+// valid records it finds in its chunk's region of a staging area (up to `stage_cap` records, in
+// 64-byte pieces: a lane buffers 8 records in registers, so its stores are whole segments instead
+// of 8-byte scatters); after a device scan of the counts, the placement kernel copies each
+// chunk's records to its base with coalesced wave loads / stores (a chunk with more records than
+// its region holds is walked again and written directly).  The data is walked once per
+// speculation round; in the common case (every speculated entry right) exactly once.
 struct RdwRange {
     int64_t r0, r1;          // seed range [r0, r1)
     int64_t first;           // index of its first chunk
@@ -408,6 +414,9 @@ struct RdwChunkArgs {
     int64_t* err;            // per chunk: (error position << 2 | code) or -1
     int32_t* changed;
     int64_t n;
+    int64_t* stage_off;      // chunk k's records: [k * stage_cap, k * stage_cap + min(count, stage_cap))
+    int32_t* stage_len;
+    int64_t stage_cap;       // a multiple of 8
 };
 
 struct RdwWalk {
@@ -416,11 +425,15 @@ struct RdwWalk {
     int64_t err;
 };
 
-template <bool kEmit>
+// kMode 0: count; 1: stage the records at rec_off/rec_len[0, cap) (cap a multiple of 8; records
+// past cap are counted, not kept); 2: write them at rec_off/rec_len[out ..) below cap.
+template <int kMode>
 __device__ RdwWalk rdw_walk(const RdwArgs& a, int64_t pos, int64_t end, int64_t* rec_off, int32_t* rec_len,
                             int64_t out, int64_t cap) {
     RdwWalk w{pos, 0, -1};
     if (pos < 0) { w.exit = pos; return w; }
+    int64_t bo[8];
+    int32_t bl[8];
     while (pos < end) {
         const RdwStep s = rdw_step(a, pos);
         if (s.err) {
@@ -430,11 +443,31 @@ __device__ RdwWalk rdw_walk(const RdwArgs& a, int64_t pos, int64_t end, int64_t*
         }
         if (s.stop) { pos = s.next; break; }
         if (s.valid) {
-            if (kEmit && out < cap) { rec_off[out] = s.off; rec_len[out] = s.len; }
+            if (kMode == 2 && out < cap) { rec_off[out] = s.off; rec_len[out] = s.len; }
+            if (kMode == 1) {
+                const uint32_t slot = w.count & 7u;
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if ((uint32_t)j == slot) { bo[j] = s.off; bl[j] = s.len; }
+                if (slot == 7u && (int64_t)w.count < cap) {   // 8 records: 64 + 32 contiguous bytes
+                    int64_t* d = rec_off + (w.count - 7);
+                    int32_t* e = rec_len + (w.count - 7);
+#pragma unroll
+                    for (int j = 0; j < 8; j += 2) *(int4*)(d + j) = make_int4((int)bo[j], (int)(bo[j] >> 32), (int)bo[j + 1], (int)(bo[j + 1] >> 32));
+                    *(int4*)e = make_int4(bl[0], bl[1], bl[2], bl[3]);
+                    *(int4*)(e + 4) = make_int4(bl[4], bl[5], bl[6], bl[7]);
+                }
+            }
             out++;
             w.count++;
         }
         pos = s.next;
+    }
+    if (kMode == 1) {   // the last partial group
+        const uint32_t done = w.count & ~7u;
+#pragma unroll
+        for (int j = 0; j < 7; j++)
+            if ((uint32_t)j < (w.count & 7u) && (int64_t)(done + j) < cap) { rec_off[done + j] = bo[j]; rec_len[done + j] = bl[j]; }
     }
     w.exit = pos;
     return w;
@@ -523,7 +556,7 @@ __global__ void rdw_spec_kernel(RdwArgs a, RdwChunkArgs c) {
         }
     }
     c.entry[k] = entry;
-    const RdwWalk w = rdw_walk<false>(a, entry, e, nullptr, nullptr, 0, 0);
+    const RdwWalk w = rdw_walk<1>(a, entry, e, c.stage_off + k * c.stage_cap, c.stage_len + k * c.stage_cap, 0, c.stage_cap);
     c.exit_out[k] = w.exit;
     c.count[k] = w.count;
     c.err[k] = w.err;
@@ -538,19 +571,39 @@ __global__ void rdw_fix_kernel(RdwArgs a, RdwChunkArgs c) {
     if (e == c.entry[k]) { c.exit_out[k] = c.exit_in[k]; return; }
     c.entry[k] = e;
     *c.changed = 1;
-    const RdwWalk w = rdw_walk<false>(a, e, ch.end, nullptr, nullptr, 0, 0);
+    const RdwWalk w = rdw_walk<1>(a, e, ch.end, c.stage_off + k * c.stage_cap, c.stage_len + k * c.stage_cap, 0, c.stage_cap);
     c.exit_out[k] = w.exit;
     c.count[k] = w.count;
     c.err[k] = w.err;
 }
 
-__global__ void rdw_emit_kernel(RdwArgs a, RdwChunkArgs c, const int64_t* base, int64_t* rec_off, int32_t* rec_len,
-                                int64_t cap, unsigned long long* first_err) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per chunk: its staged records -> rec_off / rec_len[base, base + count) (coalesced);
+// a chunk whose count passed the staging capacity is walked again by one lane, writing directly.
+constexpr int kRdwPlaceWaves = 4;
+
+__global__ __launch_bounds__(kWave * kRdwPlaceWaves) void rdw_place_kernel(RdwArgs a, RdwChunkArgs c, const int64_t* base,
+                                                                          int64_t* rec_off, int32_t* rec_len, int64_t cap,
+                                                                          unsigned long long* first_err) {
+    const int lane = threadIdx.x % kWave;
+    const int64_t k = (int64_t)blockIdx.x * kRdwPlaceWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     if (k >= c.n) return;
-    if (c.err[k] >= 0) atomicMin(first_err, (unsigned long long)c.err[k]);
-    rdw_walk<true>(a, c.entry[k], rdw_chunk(c, k).end, rec_off, rec_len, base[k], cap);
-    if (k == c.n - 1) first_err[1] = (unsigned long long)(base[k] + c.count[k]);   // record total
+    const int64_t b = base[k];
+    const int64_t n = c.count[k];
+    if (lane == 0) {
+        if (c.err[k] >= 0) atomicMin(first_err, (unsigned long long)c.err[k]);
+        if (k == c.n - 1) first_err[1] = (unsigned long long)(b + n);   // record total
+    }
+    if (c.err[k] >= 0) return;
+    if (n > c.stage_cap) {
+        if (lane == 0) rdw_walk<2>(a, c.entry[k], rdw_chunk(c, k).end, rec_off, rec_len, b, cap);
+        return;
+    }
+    const int64_t* so = c.stage_off + k * c.stage_cap;
+    const int32_t* sl = c.stage_len + k * c.stage_cap;
+    for (int64_t j = lane; j < n && b + j < cap; j += kWave) {
+        rec_off[b + j] = so[j];
+        rec_len[b + j] = sl[j];
+    }
 }
 
 }  // namespace cbx
