@@ -101,9 +101,11 @@ struct cbx_plan {
     uint64_t* d_stamps = nullptr;   // diagnostic build only
     // copybook-specialised kernel (cbx_jit.h), built on the first large contiguous decode
     int64_t jit_min = 262144;
-    // specialised kernels: [0] windowed op set, [kp] contiguous op set with kp chunks per lane
-    bool jit_tried[kPre + 1] = {};
-    hipFunction_t jit_fn[kPre + 1] = {};
+    // specialised kernels: [0] windowed op set, [kp] contiguous op set with kp chunks per lane,
+    // [kPre + 1 + kp] the contiguous op set over variable-length spans (span_loop)
+    bool jit_tried[2 * kPre + 2] = {};
+    hipFunction_t jit_fn[2 * kPre + 2] = {};
+    int rec_extent = 0;          // bytes past the decode base that any field (any OCCURS element) reaches
     std::string jit_error;
     int last_kind = 0;
     int32_t* d_status = nullptr;
@@ -418,6 +420,12 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     for (const Field& d : P->dfields_h)
         if (d.variant == V_STRING) P->str_stage = std::max(P->str_stage, kWave * d.size * d.max_utf8);
     P->str_stage = std::min(P->str_stage, kStrStageBytes);
+    for (const cbx_field& f : P->hfields) {
+        int64_t e = (int64_t)f.offset + f.size;
+        for (int k = 0; k < f.n_dims; k++) e += (int64_t)(f.dim_count[k] - 1) * f.dim_stride[k];
+        if (f.kind != CBX_K_RECORD_ID && f.kind != CBX_K_FILE_ID)
+            P->rec_extent = std::max(P->rec_extent, (int)std::min<int64_t>(e, 1 << 30));
+    }
     if (P->view)   // the register path (fields of <= kStrFastBytes) always stages its tile's long payloads
         for (const Field& d : P->dfields_h)
             if (d.variant == V_STRING && d.size <= kStrFastBytes && (d.kind == CBX_K_STRING || d.kind == CBX_K_STRING_ASCII))
@@ -569,8 +577,30 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     const bool contig = !c.rec_off && P->contig_ok && c.stride > 0 && c.stride % 4 == 0 && a.base_shift % 4 == 0 &&
                         contig_kp(sdw) <= kPre;
     a.contig = contig ? 1 : 0;
-    const cbx_plan::OpSet& S = contig ? P->cset : P->wset;
-    if (contig) {
+    // variable-length records through the specialised span kernel (span_loop): decode calls over
+    // framed records (not a selection, whose per-record ids / segments stay on the windowed
+    // kernel), a layout whose single window spans at most 1/64 of the span staging
+    const int span_ext = c.start_off + P->rec_extent;
+    const int span_kp = (int)std::min<int64_t>(kPre, ((int64_t)kWave * (span_ext + 8) + 32 + 1023) / 1024);
+    hipFunction_t span_fn = nullptr;
+    if (c.rec_off && !c.rec_id && !c.rec_seg && P->contig_ok && mode == 0 && P->jit_min >= 0 && c.n_rec >= P->jit_min &&
+        (int64_t)kWave * span_ext <= 16 * 1024 && !getenv("CBX_NO_SPAN")) {
+        const int k = kPre + 1 + span_kp;
+        if (!P->jit_tried[k]) {
+            P->jit_tried[k] = true;
+            P->jit_fn[k] = jit_get(jit_source(true, span_kp, jit_pro(P), P->view, P->cset.win, P->cset.nops, P->cset.batches,
+                                              P->cset.sops, true), &P->jit_error);
+        }
+        span_fn = P->jit_fn[k];
+    }
+    const bool span = span_fn != nullptr;
+    const cbx_plan::OpSet& S = (contig || span) ? P->cset : P->wset;
+    if (span) {
+        a.span_ext = span_ext;
+        const int nch = (P->rec_extent + 15 + 15) >> 4;
+        a.span_pitch = 16 * nch + 4;   // as a staged window's rows (push_window)
+        a.lds_rows = kGuard + std::max(span_kp * 1024 + 64, kWave * a.span_pitch) + kGuard;
+    } else if (contig) {
         a.stride_dw = sdw;
         // pad rows to an odd dword count only when the plain stride would give >= 4-way bank
         // conflicts on the per-lane dword reads (gcd(stride_dw, 32) >= 4); 2-way is cheaper
@@ -734,8 +764,8 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // resident blocks per CU: the LDS bound and the runtime's occupancy (registers); the grid
     // never exceeds what can be co-resident, so the static tile order of the look-back holds
     // copybook-specialised kernel for large contiguous batches (cbx_jit.h)
-    hipFunction_t jfn = nullptr;
-    if (mode == 0 && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
+    hipFunction_t jfn = span_fn;
+    if (!span && mode == 0 && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
         const int k = contig ? contig_kp(sdw) : 0;
         if (!P->jit_tried[k]) {
             P->jit_tried[k] = true;
@@ -749,7 +779,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                                " windows, above the specialised-kernel limits (" + std::to_string(kJitMaxOps) + ", " +
                                std::to_string(kJitMaxWindows) + ")";
             else
-                P->jit_fn[k] = jit_get(jit_source(contig, k, jit_pro(P), P->view, S.win, S.nops, S.batches, S.sops), &P->jit_error);
+                P->jit_fn[k] = jit_get(jit_source(contig, k, jit_pro(P), P->view, S.win, S.nops, S.batches, S.sops, false), &P->jit_error);
         }
         jfn = P->jit_fn[k];
     }
@@ -880,7 +910,7 @@ extern "C" int cbx_debug_stamps(cbx_plan* P, uint64_t* out) {
 extern "C" int cbx_plan_specialize(cbx_plan* P, char* source, int64_t source_cap, int64_t* source_len, int32_t compile) {
     if (!P) return fail(CBX_E_ARGUMENT, "cbx_plan_specialize: invalid arguments");
     const cbx_plan::OpSet& S = P->contig_ok ? P->cset : P->wset;
-    const std::string src = jit_source(P->contig_ok, P->contig_ok ? kPre : 0, jit_pro(P), P->view, S.win, S.nops, S.batches, S.sops);
+    const std::string src = jit_source(P->contig_ok, P->contig_ok ? kPre : 0, jit_pro(P), P->view, S.win, S.nops, S.batches, S.sops, false);
     if (source_len) *source_len = (int64_t)src.size();
     if (source && source_cap > 0) {
         const size_t n = std::min<size_t>(src.size(), (size_t)source_cap - 1);

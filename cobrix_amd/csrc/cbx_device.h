@@ -867,4 +867,119 @@ __device__ __forceinline__ void contig_loop(const KernelArgs& a, const WaveLds& 
     st.flush(a, lane);
 }
 
+// ---- variable-length records staged by byte span ----
+// cbx_decode_var over records that lie close together in the input (RDW / text framing): a tile's
+// byte span [min payload offset, max(offset + max(length, span_ext))) that fits KP 16-byte chunks
+// per lane is staged like a fixed-length tile -- buffer loads issued one tile ahead, nothing else
+// loaded from HBM in the decode -- and lane r decodes its record at (offset - span start) in the
+// image.  The record offsets / lengths themselves are loaded two tiles ahead.  A tile whose span
+// does not fit (long records, records far apart) is staged record by record over [0, span_ext)
+// (stage_window), like the windowed kernel.  Lanes past n_rec reuse the last record, length 0.
+__device__ __forceinline__ void span_recs(const KernelArgs& a, int64_t tile, int lane, int64_t& off, int32_t& len) {
+    const int64_t r = tile * kWave + lane;
+    const int64_t rc = r < a.n_rec ? r : a.n_rec - 1;   // loads always issued (registers always defined)
+    const int64_t o = a.rec_off[rc];
+    const int32_t l = a.rec_len[rc];
+    off = a.base_shift + o;
+    len = r < a.n_rec ? l : 0;
+}
+
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+#pragma unroll
+    for (int m = 1; m < kWave; m <<= 1) {
+        const int64_t o = __shfl_xor(v, m, kWave);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int64_t wave_max64(int64_t v) {
+#pragma unroll
+    for (int m = 1; m < kWave; m <<= 1) {
+        const int64_t o = __shfl_xor(v, m, kWave);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// The span of a tile (nch = 0: past the last tile, or too wide for KP chunks per lane).
+template <int KP>
+__device__ __forceinline__ ContigSpan span_of(const KernelArgs& a, int64_t tile, int64_t off, int32_t len) {
+    const int64_t lo = wave_min64(off);
+    const int64_t hi = wave_max64(off + (len > a.span_ext ? len : a.span_ext));
+    ContigSpan sp;
+    sp.a0 = lo & ~(int64_t)15;
+    const int64_t nch = (hi - sp.a0 + 15) >> 4;
+    sp.nch = (tile < a.n_tiles && nch <= (int64_t)KP * kWave) ? (int)nch : 0;
+    sp.mis_dw = 0;
+    sp.span_dw = 0;
+    return sp;
+}
+
+template <int KP>
+__device__ __forceinline__ void span_store(const ContigSpan& sp, int lane, const uint4 (&buf)[KP], uint8_t* s_img) {
+    asm volatile("" : "+v"(lane));
+#pragma unroll
+    for (int u = 0; u < KP; u++) {
+        const int c = u * kWave + lane;
+        if (u * kWave < sp.nch && c < sp.nch) *(uint4*)(s_img + 16 * c) = buf[u];
+    }
+}
+
+template <int KP, int kPro, bool kLate, typename Body>
+__device__ __forceinline__ void span_loop(const KernelArgs& a, const WaveLds& l, int64_t tile, int64_t tstep,
+                                          int lane, const Body& body) {
+    if (tile >= a.n_tiles) return;
+    uint4 buf[KP];
+    int64_t off_c, off_n;
+    int32_t len_c, len_n;
+    span_recs(a, tile, lane, off_c, len_c);
+    span_recs(a, tile + tstep, lane, off_n, len_n);
+    ContigSpan sp_c = span_of<KP>(a, tile, off_c, len_c);
+    contig_issue<KP>(a, sp_c, lane, buf);
+    Stamps st;
+    st.init();
+    while (tile < a.n_tiles) {
+        const int64_t next = tile + tstep;
+        const ContigSpan sp = sp_c;
+        const int64_t off = off_c;
+        const int32_t len = len_c;
+        if (sp.nch > 0) span_store<KP>(sp, lane, buf, l.img);
+        // the next tile's span (its offsets were loaded a tile ago) and the offsets of the one after
+        sp_c = span_of<KP>(a, next, off_n, len_n);
+        off_c = off_n;
+        len_c = len_n;
+        span_recs(a, next + tstep, lane, off_n, len_n);
+        TileCtx t;
+        t.tile = tile;
+        t.rec = tile * kWave + lane;
+        t.active = t.rec < a.n_rec;
+        t.base = off;
+        t.avail = t.active ? len : 0;
+        t.seg = -1;
+        uint32_t rec_addr;
+        if (sp.nch > 0) {
+            rec_addr = (uint32_t)(off - sp.a0) + (uint32_t)a.start_off;
+        } else {   // record by record: [0, span_ext) of every record's decode base
+            Window w{};
+            w.lo = 0;
+            w.hi = a.span_ext - a.start_off;
+            w.pitch = a.span_pitch;
+            rec_addr = stage_window(a, w, t, l.img, lane);
+        }
+        wave_sync_lds();
+        st.mark(0);
+        if (!kLate) contig_issue<KP>(a, sp_c, lane, buf);
+        st.mark(1);
+        tile_prologue<false, (kPro & 1) != 0, (kPro & 2) != 0>(a, t, l.img + rec_addr - a.start_off, lane, l.lut, l.cnt);
+        st.mark(2);
+        body.pre(a, t, (const uint8_t*)l.img, rec_addr, l, lane, st);
+        if (kLate) contig_issue<KP>(a, sp_c, lane, buf);
+        body.post(a, t, (const uint8_t*)l.img, rec_addr, l, lane, st);
+        wave_sync_lds();
+        st.mark(5);
+        tile = next;
+    }
+    st.flush(a, lane);
+}
+
 }  // namespace cbx

@@ -113,6 +113,10 @@ struct KernelArgs {
     // fixed-length contiguous staging: the tile's byte span is loaded with 16-byte loads and
     // scattered dword-wise into rows of `cpitch` bytes (odd dword count: conflict-free lanes)
     int32_t contig;
+    // variable-length span staging (span_loop): bytes a record's fields reach past its decode base
+    // plus start_off, and the row pitch of the record-by-record fallback
+    int32_t span_ext;
+    int32_t span_pitch;
     int32_t cpitch;
     int32_t stride_dw;         // stride / 4
     float inv_stride_dw;       // 1 / stride_dw

@@ -331,3 +331,40 @@ def test_synstr200_full_size_sampled_views():
     assert bool(((pos >= lo) & (pos + ln.to(torch.int64) <= lo + c["tile_bytes"]))[~short].all())
     del batch, rec
     torch.cuda.empty_cache()
+
+
+def _var_decode_vs_oracle(raw: bytes, views: bool, **kw):
+    from cobrix_amd.synth import RDW_NARROW_COPYBOOK, RDW_NARROW_SEGMENTS
+    params = ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
+                              segment_id_redefine_map=RDW_NARROW_SEGMENTS, string_views=views, **kw)
+    rd = VarLenNestedReader(RDW_NARROW_COPYBOOK, params)
+    t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+    off, ln = rd.frame(t, len(raw))
+    eo, el = O.frame_rdw(raw)
+    assert np.array_equal(off.cpu().numpy(), eo) and np.array_equal(ln.cpu().numpy(), el)
+    batch = rd.decode_device(t, len(raw), off, ln)
+    segs = [{"C": "STATIC_DETAILS", "P": "CONTACTS"}.get(G.java_trim(raw[o:o + min(5, l)].decode("cp037")))
+            for o, l in zip(eo, el)]
+    res = O.decode_records(rd.copybook, [raw[o:o + l] for o, l in zip(eo, el)], active_segments=segs)
+    return rd, compare_batch(batch, res)
+
+
+@pytest.mark.parametrize("views", [False, True])
+def test_var_span_kernel_vs_oracle(views):
+    """The specialised span kernel (variable-length tiles staged by byte span, span_loop) on the C4
+    layout, and on records of 1-3,000 bytes where many tiles overflow the span staging and fall
+    back to record-by-record windows (short records: trailing fields null / truncated)."""
+    from cobrix_amd.synth import rdw_narrow
+    raw = rdw_narrow(20_000, seed=21)[0].numpy().tobytes()
+    rd, errs = _var_decode_vs_oracle(raw, views, jit_min_records=1)
+    assert _kernel_kind(rd) == 1 and not errs, errs
+    rng = np.random.default_rng(4)
+    body = bytearray()
+    for i in range(5000):
+        ln = int(rng.integers(1, 3000)) if rng.random() < 0.2 else int(rng.integers(1, 90))
+        payload = bytearray(rng.integers(0x40, 0xFA, ln, dtype=np.uint8).tobytes())
+        payload[:5] = (b"\xC3" if i % 3 else b"\xD7") + b"\x40" * 4   # segment id C / P (cp037)
+        payload = payload[:ln]
+        body += bytes([0, 0, ln & 0xFF, ln >> 8]) + bytes(payload)
+    rd, errs = _var_decode_vs_oracle(bytes(body), views, jit_min_records=1)
+    assert _kernel_kind(rd) == 1 and not errs, errs
