@@ -42,15 +42,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 METRIC = "decoded input GB/s + records/s, fixed-len COMP-3 mix, 1-8 MI355X; % HBM peak"
 
 
-def algorithmic_bytes(plan, n_rec: int, in_bytes: int, payload_bytes: int) -> int:
+def algorithmic_bytes(plan, n_rec: int, in_bytes: int, payload_bytes: int, present=None) -> int:
     """input bytes + every output buffer byte one decode writes (payload_bytes: the
     string payload written to data buffers -- all of it in the offsets layout, the values longer
-    than 12 bytes in the view layout)."""
+    than 12 bytes in the view layout).  present[column]: elements that exist (OCCURS DEPENDING ON:
+    the records' element counts) -- absent elements are not algorithmic output, whatever the
+    slot-major layout writes for them."""
     from cobrix_amd import native as N
     total = in_bytes + payload_bytes
     views = bool(plan.options.string_views)
+    present = present or {}
     for info in plan.columns:
-        n = n_rec * info.n_slots
+        n = present.get(info.index, n_rec * info.n_slots)
         total += (n + 7) // 8                                   # validity bits
         if info.out_type in (N.O_STRING, N.O_BINARY):
             total += 16 * n if views else 8 * (n + info.n_slots)   # views / int64 offsets (n_rec + 1 per slot)
@@ -184,6 +187,25 @@ class _Fixed:
 
     def payload(self):
         return _payload(self.cols, self.n_rec)
+
+
+def present_elements(plan, cols, n_rec: int):
+    """Per value column under one OCCURS DEPENDING ON level: the elements the records hold (the sum
+    of the array's count column); columns under fixed OCCURS or deeper nesting keep every slot."""
+    import torch
+    out = {}
+    for f in plan.fields:
+        if f.n_dims != 1:
+            continue
+        ar = plan.arrays[f.dim_array[0]]
+        if ar.dependee < 0 or ar.count_column < 0:
+            continue
+        cnt = cols[ar.count_column]["values"][:n_rec].to(dtype=torch.int64)
+        if ar.segment >= 0 and plan.segment_column >= 0:   # arrays of an inactive segment redefine are absent
+            seg = cols[plan.segment_column]["values"][:n_rec]
+            cnt = cnt * (seg == ar.segment)
+        out[f.column] = int(cnt.sum().item())
+    return out
 
 
 def _payload(cols, n_rec: int) -> int:
@@ -462,7 +484,7 @@ def main():
     ms_per_step = elapsed / steps * 1e3
     gbs = job.in_bytes * world / (elapsed / steps) / 1e9
     recs_per_s = n_rec * world / (elapsed / steps)
-    alg = algorithmic_bytes(job.rd.plan, n_rec, job.in_bytes, payload)
+    alg = algorithmic_bytes(job.rd.plan, n_rec, job.in_bytes, payload, present_elements(job.rd.plan, job.cols, n_rec))
     dec_avg_ms = sum(dec[: nc.value]) / max(1, nc.value)
     fix_avg_ms = sum(fix[: nc.value]) / max(1, nc.value)
     achieved = alg / (dec_avg_ms * 1e-3) / 1e9

@@ -85,3 +85,28 @@ def test_alloc_columns_view_layout(monkeypatch):
         assert c["tile_bytes"] == 64 * 20
     # accounting: input + validity + 16-byte views + long payload
     assert algorithmic_bytes(plan, n, 200 * n, 777) == 200 * n + 777 + 10 * ((n + 7) // 8 + 16 * n)
+
+
+def test_present_elements_counts_only_live_odo_elements():
+    """bench.algorithmic_bytes counts the elements records hold: the ODO counts of records whose
+    segment redefine holds the array (C5 accounting)."""
+    torch = pytest.importorskip("torch")
+    from bench import algorithmic_bytes, present_elements
+    from cobrix_amd.copybook import parse_copybook
+    from cobrix_amd.plan import build_plan
+    from cobrix_amd.synth import WIDE_ODO_COPYBOOK, WIDE_ODO_SEGMENTS
+    cb = parse_copybook(WIDE_ODO_COPYBOOK, segment_redefines=sorted(set(WIDE_ODO_SEGMENTS.values())))
+    plan = build_plan(cb, segment_field="SEGMENT-ID", segment_redefine_map=WIDE_ODO_SEGMENTS)
+    n = 5
+    cols = [{"values": torch.zeros(64 * c.n_slots, dtype=torch.int32)} for c in plan.columns]
+    arr = [a for a in plan.arrays if a.dependee >= 0][0]
+    cols[arr.count_column]["values"][:n] = torch.tensor([10, 2000, 7, 0, 3], dtype=torch.int32)
+    seg = torch.tensor([arr.segment, -1, arr.segment, arr.segment, 1 - arr.segment], dtype=torch.int32)
+    cols[plan.segment_column]["values"][:n] = seg
+    pres = present_elements(plan, cols, n)
+    odo_cols = {f.column for f in plan.fields if f.n_dims == 1}
+    assert set(pres) == odo_cols and all(v == 10 + 7 + 0 for v in pres.values())
+    full = algorithmic_bytes(plan, n, 0, 0)
+    live = algorithmic_bytes(plan, n, 0, 0, pres)
+    per = sum(4 * (n * plan.columns[c].n_slots - pres[c]) for c in odo_cols)
+    assert full - live >= per
