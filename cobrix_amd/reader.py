@@ -124,6 +124,140 @@ class DecodedBatch:
             out["values"] = v
         return out
 
+    # ---- Arrow (the columnar bridge) ----
+    def _slot_arrays(self, ci: int):
+        """Per slot row of column ci: a pyarrow array of the n_rec records (values + validity bitmap,
+        straight from the decode's buffers: string views / large-string offsets, unscaled decimals
+        as decimal128, float bit patterns)."""
+        import pyarrow as pa
+        c = self.cols[ci]
+        info = self.plan.columns[ci]
+        n, pw = self.n_rec, (self.n_rec + 63) // 64
+        pitch = 64 * pw
+        vbits = c["validity"].cpu().numpy().view(np.uint64).reshape(info.n_slots, pw)
+        ot = info.out_type
+        out = []
+        if "views" in c:
+            views = c["views"].cpu().numpy().reshape(info.n_slots, pitch, 16)
+            data = c["data"].cpu().numpy()
+            cap, bb = c["capacity"], max(1, c["buffer_bytes"])
+        elif "offsets" in c:
+            offs = c["offsets"].cpu().numpy().reshape(info.n_slots, pitch + 1)
+            data = c["data"].cpu().numpy()
+        else:
+            vals = c["values"].cpu().numpy()
+        for s in range(info.n_slots):
+            valid = pa.py_buffer(vbits[s].tobytes())
+            if "views" in c:
+                region = data[s * cap:(s + 1) * cap]
+                bufs = [pa.py_buffer(region[k:k + bb].tobytes()) for k in range(0, max(len(region), 1), bb)]
+                typ = pa.string_view() if ot == N.O_STRING else pa.binary_view()
+                arr = pa.Array.from_buffers(typ, n, [valid, pa.py_buffer(views[s, :n].tobytes())] + bufs)
+            elif "offsets" in c:
+                typ = pa.large_string() if ot == N.O_STRING else pa.large_binary()
+                arr = pa.Array.from_buffers(typ, n, [valid, pa.py_buffer(offs[s, :n + 1].tobytes()), pa.py_buffer(data.tobytes())])
+            elif ot in (N.O_DEC64, N.O_DEC128):
+                _, p_, s_ = info.stype
+                if ot == N.O_DEC64:
+                    lo = vals.reshape(info.n_slots, pitch)[s, :n].astype(np.int64)
+                    w = np.stack([lo, lo >> 63], axis=1)
+                else:
+                    w = vals.reshape(info.n_slots, pitch, 2)[s, :n].astype(np.int64)
+                arr = pa.Array.from_buffers(pa.decimal128(p_, s_), n, [valid, pa.py_buffer(np.ascontiguousarray(w).tobytes())])
+            else:
+                dt, typ = {N.O_I32: (np.int32, pa.int32()), N.O_I64: (np.int64, pa.int64()),
+                           N.O_F32: (np.float32, pa.float32()), N.O_F64: (np.float64, pa.float64())}[ot]
+                v = np.ascontiguousarray(vals.reshape(info.n_slots, pitch)[s, :n]).view(np.uint8)
+                v = v.view(np.uint32 if dt in (np.int32, np.float32) else np.uint64)[:n] if v.size else v
+                arr = pa.Array.from_buffers(typ, n, [valid, pa.py_buffer(np.ascontiguousarray(v).tobytes())])
+            out.append(arr)
+        return out
+
+    def to_arrow(self):
+        """The batch as a pyarrow Table in the reference's Spark schema shape: groups -> structs
+        (an inactive segment redefine -> null struct), OCCURS -> lists of the records' element
+        counts (OCCURS DEPENDING ON), generated File_Id / Record_Id / Seg_IdN columns first."""
+        import pyarrow as pa
+        plan = self.plan
+        n = self.n_rec
+        flat: Dict[int, Any] = {}
+
+        def column(ci):
+            if ci not in flat:
+                parts = self._slot_arrays(ci)
+                flat[ci] = parts[0] if len(parts) == 1 else pa.concat_arrays(parts)
+            return flat[ci]
+
+        counts: Dict[int, np.ndarray] = {}
+
+        def count_of(ai):
+            ci = plan.arrays[ai].count_column
+            if ci not in counts:
+                info = plan.columns[ci]
+                v = self.cols[ci]["values"].cpu().numpy().reshape(info.n_slots, -1)[:, :n]
+                counts[ci] = v.reshape(-1).astype(np.int64)   # slot s, record r -> s * n + r
+            return counts[ci]
+
+        seg_active = None
+        if plan.segment_column >= 0:
+            seg_active = self.cols[plan.segment_column]["values"].cpu().numpy()[:n].astype(np.int64)
+
+        def build(node, R, S, in_array):
+            """Array of node's values for instances (record R[i], enclosing-array slot S[i])."""
+            if node.is_array and not in_array:
+                ai = plan.array_of_node[id(node)]
+                m = node.array_max_size
+                cnt = count_of(ai)[S * n + R]
+                j = np.concatenate([np.arange(k) for k in cnt]) if len(cnt) else np.zeros(0, np.int64)
+                R2 = np.repeat(R, cnt)
+                S2 = np.repeat(S, cnt) * m + j
+                child = build(node, R2, S2, True)
+                offs = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
+                return pa.ListArray.from_arrays(pa.array(offs, pa.int32()), child)
+            if isinstance(node, cbk.Group):
+                names, kids = [], []
+                for c in node.children:
+                    if c.is_filler or c.is_child_segment:
+                        continue
+                    if isinstance(c, cbk.Group) or c.is_array or plan.field_of_node.get(id(c)) is not None:
+                        names.append(c.name)
+                        kids.append(build(c, R, S, False))
+                mask = None
+                if node.is_segment_redefine:
+                    si = plan.segment_groups.index(node)
+                    mask = pa.array(seg_active[R] != si if seg_active is not None else np.ones(len(R), bool))
+                return pa.StructArray.from_arrays(kids, names=names, mask=mask)
+            fi = plan.field_of_node[id(node)]
+            arr = column(plan.fields[fi].column)
+            if len(R) == n and not S.any() and np.array_equal(R, np.arange(n)):
+                return arr.slice(0, n)                       # the slot row itself, zero-copy
+            if pa.types.is_string_view(arr.type) or pa.types.is_binary_view(arr.type):
+                # no gather kernel for views in pyarrow: gathered OCCURS elements become large strings
+                arr = arr.cast(pa.large_string() if pa.types.is_string_view(arr.type) else pa.large_binary())
+            return arr.take(pa.array(S * n + R))
+
+        R0 = np.arange(n, dtype=np.int64)
+        S0 = np.zeros(n, dtype=np.int64)
+        names, arrays = [], []
+        if self.generate_record_id:
+            names += ["File_Id", "Record_Id"]
+            arrays += [column(plan.file_id_column), column(plan.record_id_column)]
+        for lv, ci in enumerate(plan.seg_id_columns):
+            names.append(f"Seg_Id{lv}")
+            arrays.append(column(ci))
+        for g in plan.copybook.ast.children:
+            if not isinstance(g, cbk.Group):
+                continue
+            st = build(g, R0, S0, False)
+            if self.collapse_root:
+                for k in range(st.type.num_fields):
+                    names.append(st.type.field(k).name)
+                    arrays.append(st.field(k))
+            else:
+                names.append(g.name)
+                arrays.append(st)
+        return pa.Table.from_arrays(arrays, names=names)
+
     def to_rows(self) -> List[dict]:
         """Rebuild nested rows (RecordHandler.create + applyRecordPostProcessing)."""
         plan = self.plan
