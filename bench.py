@@ -232,7 +232,7 @@ class _VarLen:
     seeded by the entries + (N > 1) one all-gather of the shard's record count, whose exclusive
     prefix is the shard's Record_Id base (cobrix_amd/shard.py record_bases) + decode."""
 
-    def __init__(self, name, n_rec, dev, rank, window, views):
+    def __init__(self, name, n_rec, dev, rank, window, views, lists=True):
         import torch
         from cobrix_amd import synth
         from cobrix_amd.reader import ReaderParameters, VarLenNestedReader
@@ -249,7 +249,7 @@ class _VarLen:
         # segment_id_root only shapes the index (cuts at roots); the decode plan is the C4/C5 one
         self.rd = VarLenNestedReader(cb, ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
                                                           segment_id_redefine_map=segs, window_bytes=window,
-                                                          string_views=views))
+                                                          string_views=views, occurs_lists=lists))
         idx_rd = VarLenNestedReader(cb, ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
                                                          segment_id_levels=["C"], input_split_size_mb=100))
         t0 = time.perf_counter()
@@ -413,6 +413,8 @@ def main():
     ap.add_argument("--window", type=int, default=0, help="LDS window bytes (0 = plan default)")
     ap.add_argument("--strings", default="views", choices=["views", "offsets"],
                     help="string column layout: Arrow string views (one pass) or Arrow large-string offsets")
+    ap.add_argument("--occurs", default="lists", choices=["lists", "slots"],
+                    help="OCCURS DEPENDING ON layout: Arrow lists (present elements) or one slot row per element")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true")
     args = ap.parse_args()
@@ -439,8 +441,10 @@ def main():
 
     progress(f"generating {n_req} records on {dev}")
     views = args.strings == "views"
-    job = (_Fixed if args.workload in ("syn200", "synstr200") else _VarLen)(args.workload, n_req, dev, rank,
-                                                                            args.window, views)
+    if args.workload in ("syn200", "synstr200"):
+        job = _Fixed(args.workload, n_req, dev, rank, args.window, views)
+    else:
+        job = _VarLen(args.workload, n_req, dev, rank, args.window, views, args.occurs == "lists")
     st = torch.cuda.current_stream()
     progress(f"{job.in_bytes / 1e9:.2f} GB generated; allocating columns")
     job.prepare(st)
@@ -491,7 +495,10 @@ def main():
     kind = ctypes.c_int32(0)
     N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
     kname = "cbx_jit_decode (copybook-specialised, hipRTC)" if kind.value == 1 else "cbx::decode_kernel (table-driven)"
-    tag = f"{args.workload}_{args.strings}_{n_rec}"
+    lists = any(c.list_array >= 0 for c in job.rd.plan.columns)
+    if lists:   # the OCCURS list elements: the element-parallel kernel launched right after the decode kernel
+        kname += " + cbx::list_kernel (OCCURS lists; decode_kernel time covers both)"
+    tag = f"{args.workload}_{args.strings}{'' if args.occurs == 'lists' else '_slots'}_{n_rec}"
     traffic, traffic_src = measured_traffic(tag)
     kernel_ms = {"decode_kernel": round(dec_avg_ms, 4),
                  ("post_kernels (deferred-value fixup)" if views else
@@ -528,6 +535,8 @@ def main():
                        "output_columns": job.rd.plan.n_columns, "parallelism": f"dp{world}",
                        "string_layout": "Arrow string views (16 B views + long payloads, one pass)" if views
                        else "Arrow large-string (int64 offsets + payload, scan + placement)",
+                       "occurs_layout": "Arrow lists (present elements only)" if args.occurs == "lists"
+                       else "one slot row per element",
                        "inputs_resident_in_hbm": True},
             "kernel_ms": kernel_ms,
             **({"seeds": f"{len(job.entries)} sparse-index entries from cbx_sparse_index (100 MB, root segments)"}

@@ -71,6 +71,9 @@ struct cbx_plan {
     std::vector<int32_t> col_max_bytes;   // per column: max payload bytes per value
     bool view = false;                    // string columns in the string-view layout
     std::vector<int32_t> segid_cols;      // segment levels with a Seg_Id column
+    std::vector<ListOp> lops;             // list-layout fields (list_kernel), grouped by array
+    ListOp* d_lops = nullptr;
+    int32_t* d_list_len = nullptr;  int64_t list_len_cap = 0;
     // device copies
     Field* d_fields = nullptr;
     DeferSeq* d_defer = nullptr;
@@ -153,6 +156,8 @@ static int upload(T** dst, const T* src, size_t n) {
 }
 
 static bool is_generated(const Field& d) { return d.variant == V_RECORD_ID || d.variant == V_FILE_ID; }
+// elements of list-layout arrays are decoded by the list kernel, not from the staged windows
+static bool is_list(const Field& d) { return (d.flags & CBX_F_LIST) != 0; }
 
 // One element (slot) of a field: static offset and its OCCURS DEPENDING ON conditions.
 struct Elem {
@@ -286,6 +291,7 @@ static void build_contig(cbx_plan* P) {
     int items = 0;
     for (int i = 0; i < (int)P->dfields_h.size(); i++) {
         if (is_generated(P->dfields_h[i])) { gen.push_back(i); continue; }
+        if (is_list(P->dfields_h[i])) continue;
         for (const Elem& e : field_elements(P, i)) { items += e.str; els.push_back(e); }
     }
     if (items > kMaxStrItems) P->contig_ok = false;
@@ -302,6 +308,7 @@ static void build_windowed(cbx_plan* P, int wmax) {
     for (int i = 0; i < (int)P->dfields_h.size(); i++) {
         const Field& d = P->dfields_h[i];
         if (is_generated(d)) { gen.push_back(i); continue; }
+        if (is_list(d)) continue;
         std::vector<Elem> fe = field_elements(P, i);
         if (d.size > wmax) big.insert(big.end(), fe.begin(), fe.end());
         else els.insert(els.end(), fe.begin(), fe.end());
@@ -392,7 +399,7 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
                 P->seq_tile_cap.push_back(((int64_t)kWave * f.size * d.max_utf8 + 15) & ~(int64_t)15);
             }
             P->col_max_bytes[f.column] = f.size * d.max_utf8;
-        } else if (d.variant == V_ZONED16 || d.variant == V_GENERIC) {
+        } else if ((d.variant == V_ZONED16 || d.variant == V_GENERIC) && !(f.flags & CBX_F_LIST)) {
             d.defer = (int)P->hdefer.size();
             for (int s = 0; s < d.n_slots; s++) P->hdefer.push_back(DeferSeq{i, s});
         }
@@ -403,12 +410,30 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     for (int ai = 0; ai < n_arrays; ai++) {
         const cbx_array& ar = arrays[ai];
         if (ar.dependee >= n_fields || ar.max_count <= 0) { delete P; return fail(CBX_E_ARGUMENT, "array " + std::to_string(ai) + ": bad descriptor"); }
+        if (ar.offsets_column >= P->n_columns || (ar.offsets_column >= 0 && (ar.dependee < 0 || ar.n_dims != 0)))
+            { delete P; return fail(CBX_E_ARGUMENT, "array " + std::to_string(ai) + ": list layout needs a top-level OCCURS DEPENDING ON"); }
         if (ar.dependee >= 0) {
             const cbx_field& df = fields[ar.dependee];
             if (!(df.flags & CBX_F_INTEGRAL) || df.n_dims != 0 || df.precision > 18)
                 { delete P; return fail(CBX_E_UNSUPPORTED, "array " + std::to_string(ai) + ": DEPENDING ON source must be a non-array integral field"); }
         }
     }
+    for (int ai = 0; ai < n_arrays; ai++)   // list-layout elements: numeric, one level, the array's segment
+        for (int i = 0; i < n_fields; i++) {
+            const cbx_field& f = fields[i];
+            if (!(f.flags & CBX_F_LIST) || (f.n_dims == 1 && f.dim_array[0] != ai)) continue;
+            if (f.n_dims != 1 || arrays[ai].offsets_column < 0 || is_string_out(f.out_type) || f.segment != arrays[ai].segment)
+                { delete P; return fail(CBX_E_ARGUMENT, "field " + std::to_string(i) + ": CBX_F_LIST needs a numeric element of a list-layout array in its segment"); }
+            ListOp lo{};
+            const int16_t none[CBX_MAX_DIMS] = {0, 0, 0, 0};
+            lo.op = make_numop(P->dfields_h[i], 0, f.offset, none, none, 0);
+            lo.field = i;
+            lo.array = ai;
+            lo.stride = f.dim_stride[0];
+            P->lops.push_back(lo);
+        }
+    if ((int)P->lops.size() != (int)std::count_if(fields, fields + n_fields, [](const cbx_field& f) { return (f.flags & CBX_F_LIST) != 0; }))
+        { delete P; return fail(CBX_E_ARGUMENT, "CBX_F_LIST field outside a list-layout array"); }
     P->seg_col = opts->segment_column;
     if (P->seg_col >= P->n_columns) { delete P; return fail(CBX_E_ARGUMENT, "bad segment column"); }
 
@@ -421,6 +446,7 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
         if (d.variant == V_STRING) P->str_stage = std::max(P->str_stage, kWave * d.size * d.max_utf8);
     P->str_stage = std::min(P->str_stage, kStrStageBytes);
     for (const cbx_field& f : P->hfields) {
+        if (f.flags & CBX_F_LIST) continue;   // the list kernel reads those
         int64_t e = (int64_t)f.offset + f.size;
         for (int k = 0; k < f.n_dims; k++) e += (int64_t)(f.dim_count[k] - 1) * f.dim_stride[k];
         if (f.kind != CBX_K_RECORD_ID && f.kind != CBX_K_FILE_ID)
@@ -469,6 +495,7 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
         (r = upload_set(P->cset)) || (r = upload_set(P->wset)) ||
         (r = upload(&P->d_arrays, P->harrays.data(), P->harrays.size())) ||
         (r = upload(&P->d_defer, P->hdefer.data(), P->hdefer.size())) ||
+        (r = upload(&P->d_lops, P->lops.data(), P->lops.size())) ||
         (r = upload(&P->d_lut, opts->lut, 256))) {
         cbx_plan_destroy(P);
         return r;
@@ -497,6 +524,7 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
     (void)hipFree(P->d_segmap); (void)hipFree(P->d_lut); (void)hipFree(P->d_cols);
     (void)hipFree(P->d_seqcall); (void)hipFree(P->d_str_tot); (void)hipFree(P->d_str_excl); (void)hipFree(P->d_block_sums);
     (void)hipFree(P->d_local); (void)hipFree(P->d_scratch); (void)hipFree(P->d_status); (void)hipFree(P->d_stamps);
+    (void)hipFree(P->d_lops); (void)hipFree(P->d_list_len);
     for (auto& e : P->ev_pool) (void)hipEventDestroy(e);
     for (auto& c : P->ev_calls) for (auto& e : c.e) if (e) (void)hipEventDestroy(e);
     delete P;
@@ -619,7 +647,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.sops = (const CBX_CONST StrOp*)S.d_sops;
     a.gops = (const CBX_CONST GenOp*)S.d_gops;
     a.lds_rows = (a.lds_rows + 15) & ~15;
-    a.lds_counts = ((int)P->harrays.size() * kWave * 4 + 15) & ~15;
+    a.lds_counts = ((int)P->harrays.size() * kWave * 4 + 15) & ~15;   // OCCURS element counts
     // string-view layout: the inline slots (16 bytes per short value) share the area with the long
     // payloads, which it holds for any tile as long as it is at least 16 bytes per lane
     a.str_stage = S.max_str_items > 0 ? (P->view && mode == 0 ? std::max(P->str_stage, 16 * kWave) : P->str_stage) : 0;
@@ -757,6 +785,9 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     int r;
     if (P->n_seq > 0 && (r = grow(&P->d_str_tot, &P->str_tot_cap, (int64_t)P->n_seq * n_tiles, st))) return r;
     a.str_tot = P->d_str_tot;
+    const bool lists = mode == 0 && !P->lops.empty();
+    if (lists && (r = grow(&P->d_list_len, &P->list_len_cap, (int64_t)P->harrays.size() * a.pitch, st))) return r;
+    a.list_len = P->d_list_len;
     const int n_defer = n_defer_seq;
     a.defer_bits = P->d_defer_bits;
     const size_t lds = 1024 + (size_t)kWavesPerBlock * a.lds_wave;
@@ -807,6 +838,12 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         HIP_CHECK(hipModuleLaunchKernel(jfn, (unsigned)grid, 1, 1, kWave * kWavesPerBlock, 1, 1, (unsigned)lds, st, kargs, nullptr));
     } else {
         hipLaunchKernelGGL(decode_kernel, dim3((unsigned)grid), dim3(kWave * kWavesPerBlock), lds, st, a);
+        HIP_CHECK(hipGetLastError());
+    }
+    if (lists) {   // child elements of list-layout arrays, from the lengths and starts the prologue wrote
+        const int64_t lgrid = std::min<int64_t>((n_tiles + kListWaves - 1) / kListWaves, (int64_t)P->num_cus * 8);
+        hipLaunchKernelGGL(list_kernel, dim3((unsigned)lgrid), dim3(kWave * kListWaves), 0, st, a,
+                           (const CBX_CONST ListOp*)P->d_lops, (int32_t)P->lops.size());
         HIP_CHECK(hipGetLastError());
     }
     if (prof) HIP_CHECK(hipEventRecord(ce.e[1], st));

@@ -769,6 +769,20 @@ __device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, c
             }
         }
         s_cnt[ai * kWave + lane] = cnt;
+        if (ar.offsets_column >= 0 && a.mode == 0) {
+            // list layout: the record's present elements (none when the array's segment is not the
+            // record's) get a run of the tile's child region starting at a multiple of 64; the
+            // list kernel decodes them from these starts and lengths
+            const int len = t.active && (ar.segment < 0 || ar.segment == t.seg) ? cnt : 0;
+            uint32_t tot;
+            const uint32_t ex = wave_excl_scan32(((uint32_t)len + 63u) & ~63u, lane, tot);
+            const DevColumn c = ldc(a.cols + ar.offsets_column);
+            const int64_t mpad = (int64_t)((ar.max_count + 63) & ~63);
+            (gp((int64_t*)c.values) + t.tile * kWave)[lane] = t.tile * kWave * mpad + ex;
+            (gp(a.list_len + (int64_t)ai * a.pitch) + t.tile * kWave)[lane] = len;
+            const uint64_t m = __ballot(t.active);
+            if (lane == 0) gp(c.validity)[t.tile] = m;
+        }
         if (a.mode == 0 && ar.count_column >= 0) {
             const DevColumn c = ldc(a.cols + ar.count_column);
             const bool ok = t.active && (ar.segment < 0 || ar.segment == t.seg);

@@ -64,6 +64,16 @@ struct StrCall {
     int64_t tiles_per_buf;    // string-view layout: tiles per Arrow data buffer
 };
 
+// One field of a list-layout OCCURS DEPENDING ON array (CBX_F_LIST): the list kernel decodes its
+// elements k = 0 .. len-1 at op.eo + k * stride.
+struct ListOp {
+    NumOp op;                 // element 0 (fast-path constants of the field)
+    int32_t field;            // field index (byte-loop decoder for wide / deferred forms)
+    int32_t array;            // its array (ListOps of one array are adjacent)
+    int32_t stride;           // bytes between elements
+    int32_t reserved;
+};
+
 // Generated column (File_Id / Record_Id).
 struct GenOp {
     int32_t kind, column, out_type, reserved;
@@ -140,6 +150,7 @@ struct KernelArgs {
     int32_t n_seq;             // string sequences = sum over string fields of n_slots
     uint32_t* str_tot;         // [n_seq][n_tiles] payload bytes of every (sequence, tile)
     int32_t* status;           // [0]: capacity overflow flag
+    int32_t* list_len;         // list-layout arrays: [n_arrays][pitch] present elements per record
     uint64_t* defer_bits;      // [n_defer][n_tiles] values left to the fixup kernel
     // LDS layout (bytes, per wave)
     int32_t lds_rows;          // record image incl. guards

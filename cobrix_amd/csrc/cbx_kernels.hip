@@ -323,6 +323,115 @@ __global__ __launch_bounds__(256) void fixup_kernel(KernelArgs a, const CBX_CONS
 }
 
 // ------------------------------------------------------------------------------------------
+// List layout (CBX_F_LIST): the child elements of OCCURS DEPENDING ON arrays, element-parallel.
+// The decode kernel's prologue left every record's present element count (list_len) and its
+// child start (offsets column, a multiple of 64).  One wave per tile of 64 records takes the
+// tile's records with elements one at a time and their elements 64 per step, lane = element:
+// the loads of adjacent lanes are adjacent bytes, the value stores one contiguous run, and a
+// step's validity is exactly one bitmap word.  The record's bytes are read through a buffer
+// descriptor bounded by the record, so bytes past it read as zeros (elements past the record's
+// end are null, as extractArray's bounds check makes them).  Reference: the OCCURS loop of
+// RecordExtractors.extractRecord (RecordExtractors.scala:66-114) with the element decoders.
+// ------------------------------------------------------------------------------------------
+constexpr int kListWaves = 4;   // waves per workgroup
+constexpr int kListU = 4;       // (element step, field) items per round: loads first
+
+// Dword at byte offset o of the record's descriptor; offsets before the record read as zero.
+__device__ __forceinline__ uint32_t list_dword(__amdgpu_buffer_rsrc_t rs, int o) {
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, o < 0 ? 0x7ffffff0 : o, 0, 0);
+}
+
+// bytes [end - 8, end) of the descriptor as a little-endian u64 (cf. img_le64_ending)
+__device__ __forceinline__ uint64_t list_le64_ending(__amdgpu_buffer_rsrc_t rs, int end) {
+    const int s = end - 8;
+    const int a0 = s & ~3;
+    const uint32_t sh = (uint32_t)s & 3u;
+    const uint32_t d0 = list_dword(rs, a0), d1 = list_dword(rs, a0 + 4), d2 = list_dword(rs, a0 + 8);
+    return ((uint64_t)align_bytes(d2, d1, sh) << 32) | align_bytes(d1, d0, sh);
+}
+
+__global__ __launch_bounds__(kWave * kListWaves) void list_kernel(KernelArgs a, const CBX_CONST ListOp* lops, int32_t n_lops) {
+    const int lane = threadIdx.x % kWave;
+    const int64_t w0 = (int64_t)blockIdx.x * kListWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t nw = (int64_t)gridDim.x * kListWaves;
+    for (int64_t tile = w0; tile < a.n_tiles; tile += nw) {
+        const int64_t rec = tile * kWave + lane;
+        const bool active = rec < a.n_rec;
+        int64_t base = a.base_shift;
+        int avail = 0;
+        if (active) {
+            if (a.rec_off) { base += a.rec_off[rec]; avail = a.rec_len[rec]; }
+            else { base += rec * (int64_t)a.stride; avail = a.stride; }
+        }
+        for (int i0 = 0; i0 < n_lops;) {
+            const int ai = lops[i0].array;
+            int i1 = i0 + 1;
+            while (i1 < n_lops && lops[i1].array == ai) i1++;
+            const int nops = i1 - i0;
+            const DevColumn oc = ldc(a.cols + a.arrays[ai].offsets_column);
+            const int len = active ? a.list_len[(int64_t)ai * a.pitch + rec] : 0;
+            const int64_t start = active ? ((const int64_t*)oc.values)[rec] : 0;
+            for (uint64_t m = __ballot(len > 0); m; m &= m - 1) {
+                const int b = __builtin_ctzll(m);
+                const int rlen = __builtin_amdgcn_readlane(len, b);
+                const int64_t rstart = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(start >> 32), b) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readlane((int)start, b);
+                const int64_t rbase = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(base >> 32), b) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)base, b);
+                const int ravail = __builtin_amdgcn_readlane(avail, b);
+                // descriptor over the record's bytes, from a dword-aligned base
+                const uint64_t addr = (uint64_t)(a.data + rbase);
+                const int bias = (int)(addr & 3);
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)(addr - bias), (short)0, ravail + bias, 0x00020000);
+                const int items = ((rlen + kWave - 1) / kWave) * nops;
+                for (int q0 = 0; q0 < items; q0 += kListU) {
+                    uint64_t r1[kListU], r0[kListU];
+#pragma unroll
+                    for (int u = 0; u < kListU; u++) {
+                        r1[u] = r0[u] = 0;
+                        const int q = q0 + u;
+                        if (q >= items) continue;
+                        const CBX_CONST ListOp* lp = lops + i0 + q % nops;
+                        const int k = (q / nops) * kWave + lane;
+                        const int end = bias + a.start_off + lp->op.eo + k * lp->stride + lp->op.size;
+                        const int v = lp->op.variant;
+                        if (v != V_GENERIC) r1[u] = list_le64_ending(rs, end);
+                        if (v == V_BCD16 || v == V_ZONED16) r0[u] = list_le64_ending(rs, end - 8);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kListU; u++) {
+                        const int q = q0 + u;
+                        if (q >= items) continue;
+                        const CBX_CONST ListOp* lp = lops + i0 + q % nops;
+                        const NumOp op = ldc(&lp->op);
+                        const int c0 = (q / nops) * kWave;
+                        const int k = c0 + lane;
+                        const int eo = a.start_off + op.eo + k * lp->stride;
+                        const bool present = k < rlen;
+                        const bool ok = present && eo + op.size <= ravail;
+                        Val x = null_val();
+                        bool slow = op.variant == V_GENERIC;
+                        if (op.variant == V_BCD8) x = bcd8_raw<0>(op, r1[u]);
+                        else if (op.variant == V_BCD16) x = bcd16_raw<0>(op, r1[u], r0[u]);
+                        else if (op.variant == V_BIN8) x = bin8_raw<0>(op, r1[u]);
+                        else if (op.variant == V_ZONED16) x = zoned16_raw<0>(op, r1[u], r0[u], slow);
+                        else if (op.variant == V_FP) x = fp_raw(op, r1[u]);
+                        if (slow && ok) x = decode_numeric(ldc(a.fields + lp->field), a.data + rbase + eo);
+                        x.valid &= ok;
+                        const DevColumn col = ldc(a.cols + op.column);
+                        if (present) store_value(col, op.out_type, rstart + k, x);
+                        const uint64_t vm = __ballot(x.valid);
+                        gp(col.validity)[(rstart + c0) >> 6] = vm;
+                    }
+                }
+            }
+            i0 = i1;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // RDW framing (RecordHeaderParserRDW.getRecordMetadata + VRLRecordReader.fetchRecordUsingRdwHeaders)
 // One lane per chunk of a seed range walks its header chain; the walk stages the records it finds
 // in a per-chunk region, and one placement pass moves them to their final positions.

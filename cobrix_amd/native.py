@@ -27,6 +27,7 @@ K_FLOAT, K_DOUBLE, K_RECORD_ID, K_FILE_ID = 9, 10, 11, 12
 O_I32, O_I64, O_DEC64, O_DEC128, O_F32, O_F64, O_STRING, O_BINARY = 1, 2, 3, 4, 5, 6, 7, 8
 F_SIGNED, F_BIG_ENDIAN, F_EXPLICIT_DOT, F_INTEGRAL, F_IBM, F_LITTLE_ENDIAN_FP, F_DEPENDEE = (
     0x1, 0x2, 0x4, 0x8, 0x10, 0x20, 0x40)
+F_LIST = 0x80
 TRIM = {"none": 1, "left": 2, "right": 3, "both": 4}
 
 CBX_OK, CBX_E_ARGUMENT, CBX_E_STATE, CBX_E_CAPACITY, CBX_E_HIP, CBX_E_UNSUPPORTED = 0, -1, -2, -3, -4, -5
@@ -39,7 +40,7 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
                     "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text",
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class NativeLibraryError(RuntimeError):
@@ -67,7 +68,7 @@ class CbxField(ctypes.Structure):
 class CbxArray(ctypes.Structure):
     _fields_ = [("max_count", ctypes.c_int32), ("min_count", ctypes.c_int32), ("dependee", ctypes.c_int32),
                 ("segment", ctypes.c_int32), ("count_column", ctypes.c_int32), ("n_dims", ctypes.c_int32),
-                ("parent", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("parent", ctypes.c_int32), ("offsets_column", ctypes.c_int32)]
 
 
 class CbxSegmentMap(ctypes.Structure):

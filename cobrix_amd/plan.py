@@ -36,6 +36,8 @@ class ColumnInfo:
     node: Optional[cbk.Statement] = None
     stype: Tuple[int, int, int] = (0, 0, 0)
     hidden: bool = False           # decoded for a dependency only (e.g. FILLER dependee)
+    list_array: int = -1           # list layout: the OCCURS DEPENDING ON array (child elements)
+    list_mpad: int = 0             # list layout: elements per record slot in a tile region (max rounded to 64)
 
 
 @dataclass
@@ -146,7 +148,7 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
                segment_redefine_map: Optional[Dict[str, str]] = None, generate_record_id: bool = False,
                file_id: int = 0, window_bytes: int = 0, jit_min_records: int = 0,
                segment_levels: Sequence[str] = (), segment_filter: Optional[List[str]] = None,
-               segment_prefix: str = "", string_views: bool = False) -> DecodePlan:
+               segment_prefix: str = "", string_views: bool = False, occurs_lists: bool = False) -> DecodePlan:
     fields: List[N.CbxField] = []
     arrays: List[N.CbxArray] = []
     columns: List[ColumnInfo] = []
@@ -182,6 +184,7 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
             arrays.append(ar)
             array_of_node[id(st)] = ai
             ar.count_column = add_column(kind="count", out_type=N.O_I32, node=st)
+            ar.offsets_column = -1
             pending_arrays.append((ai, st))
             my_dims.append((st.array_max_size, st.data_size, ai))
             if len(my_dims) > N.CBX_MAX_DIMS:
@@ -237,6 +240,23 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
         if not isinstance(q.dtype, cbk.Integral) or q.dtype.precision > 18:
             raise UnsupportedLayout(f"{st.name}: DEPENDING ON a non-integral field (occurs_mappings) is not on the GPU path yet")
         arrays[ai].dependee = field_of_node[id(q)]
+
+    if occurs_lists:
+        # list layout (cobrix_hip.h, CBX_F_LIST): a top-level OCCURS DEPENDING ON array whose elements
+        # are numeric leaves of that one level -- child elements packed per record, absent ones unwritten
+        for ai, ar in enumerate(arrays):
+            if ar.dependee < 0 or ar.n_dims != 0 or any(b.parent == ai for b in arrays):
+                continue
+            members = [f for f in fields if f.n_dims >= 1 and ai in list(f.dim_array)[:f.n_dims]]
+            if not members or any(f.n_dims != 1 or f.out_type in (N.O_STRING, N.O_BINARY) or f.segment != ar.segment
+                                  for f in members):
+                continue
+            mpad = (ar.max_count + 63) // 64 * 64
+            for f in members:
+                f.flags |= N.F_LIST
+                columns[f.column].list_array = ai
+                columns[f.column].list_mpad = mpad
+            ar.offsets_column = add_column(kind="list_offsets", out_type=N.O_I64, node=None)
 
     opts = N.CbxPlanOptions()
     seg_col = -1

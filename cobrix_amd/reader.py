@@ -77,6 +77,9 @@ class ReaderParameters:
     # output layout of string columns: Arrow large-string (offsets, two-pass placement) or Arrow
     # string views (one pass: every value written once by the decode kernel; cobrix_hip.h)
     string_views: bool = False
+    # OCCURS DEPENDING ON arrays of numeric elements in the list layout (child elements packed per
+    # record, absent elements unwritten; cobrix_hip.h CBX_F_LIST) instead of one slot row per element
+    occurs_lists: bool = False
 
 
 @dataclass
@@ -99,11 +102,41 @@ class DecodedBatch:
         self.generate_record_id = generate_record_id
 
     # ---- host views
+    def _list_dense(self, ci: int):
+        """A list-layout column as dense slot rows: (values [n_slots * n_rec (, 2)], validity
+        [n_slots, n_rec]) -- element j of record r at child index offsets[r] + j when j < count[r] (a valid count)."""
+        info = self.plan.columns[ci]
+        ar = self.plan.arrays[info.list_array]
+        n, m = self.n_rec, info.n_slots
+        off = self.cols[ar.offsets_column]["values"].cpu().numpy()[:n].astype(np.int64)
+        cnt = self.cols[ar.count_column]["values"].cpu().numpy()[:n].astype(np.int64)
+        cbits = np.unpackbits(self.cols[ar.count_column]["validity"].cpu().numpy().view(np.uint8), bitorder="little")
+        cnt = np.where(cbits[:n].astype(bool), cnt, 0)   # no elements where the array's segment is inactive
+        child = self.cols[ci]["values"].cpu().numpy()
+        wide = info.out_type == N.O_DEC128
+        if wide:
+            child = child.reshape(-1, 2)
+        bits = np.unpackbits(self.cols[ci]["validity"].cpu().numpy().view(np.uint8), bitorder="little").astype(bool)
+        j = np.arange(m, dtype=np.int64)
+        idx = off[None, :] + j[:, None]                      # [slot, record]
+        present = j[:, None] < cnt[None, :]
+        safe = np.where(present, idx, 0)
+        valid = present & bits[safe]
+        vals = child[safe.reshape(-1)]
+        if wide:
+            vals = np.where(present.reshape(-1)[:, None], vals, 0)
+        else:
+            vals = np.where(present.reshape(-1), vals, 0)
+        return vals, valid
+
     def host_column(self, ci: int) -> Dict[str, Any]:
         c = self.cols[ci]
         info = self.plan.columns[ci]
         pitch = (self.n_rec + 63) // 64
         out: Dict[str, Any] = {"validity": None, "values": None}
+        if info.list_array >= 0:
+            out["values"], out["validity"] = self._list_dense(ci)
+            return out
         vb = c["validity"].cpu().numpy().view(np.uint64)
         bits = np.unpackbits(vb.view(np.uint8), bitorder="little").reshape(info.n_slots, pitch * 64)
         out["validity"] = bits[:, :self.n_rec].astype(bool)
@@ -134,8 +167,18 @@ class DecodedBatch:
         info = self.plan.columns[ci]
         n, pw = self.n_rec, (self.n_rec + 63) // 64
         pitch = 64 * pw
-        vbits = c["validity"].cpu().numpy().view(np.uint64).reshape(info.n_slots, pw)
         ot = info.out_type
+        if info.list_array >= 0:   # list layout: dense slot rows rebuilt from the child elements
+            vals, valid = self._list_dense(ci)
+            dense = np.zeros((info.n_slots, pw * 64), dtype=bool)
+            dense[:, :n] = valid
+            vbits = np.packbits(dense, axis=1, bitorder="little").view(np.uint64).reshape(info.n_slots, pw)
+            vals = vals.reshape(info.n_slots, n, -1) if ot == N.O_DEC128 else vals.reshape(info.n_slots, n)
+            padded = np.zeros((info.n_slots, pitch) + vals.shape[2:], dtype=vals.dtype)
+            padded[:, :n] = vals
+            c = {"values": _HostArray(padded.reshape(-1) if ot != N.O_DEC128 else padded.reshape(-1, 2))}
+        else:
+            vbits = c["validity"].cpu().numpy().view(np.uint64).reshape(info.n_slots, pw)
         out = []
         if "views" in c:
             views = c["views"].cpu().numpy().reshape(info.n_slots, pitch, 16)
@@ -387,6 +430,14 @@ def _alloc_columns(plan: DecodePlan, n_rec: int, slot_capacity: Sequence[int], d
             cstructs[ci].data = c["data"].data_ptr()
             cstructs[ci].data_capacity = cap
             cstructs[ci].data_sizes = c["sizes"].data_ptr()
+        elif info.list_array >= 0:
+            # list layout: child elements, 64 * M per tile (M = max count rounded up to 64)
+            w = N.OUT_WIDTH[info.out_type]
+            dt = {4: torch.int32, 8: torch.int64, 16: torch.int64}[w]
+            n_child = pitch * info.list_mpad
+            c["values"] = torch.zeros(max(1, n_child * (2 if w == 16 else 1)), dtype=dt, device=device)
+            c["validity"] = torch.zeros(max(1, pitch_words * info.list_mpad), dtype=torch.int64, device=device)
+            cstructs[ci].values = c["values"].data_ptr()
         else:
             w = N.OUT_WIDTH[info.out_type]
             dt = {4: torch.int32, 8: torch.int64, 16: torch.int64}[w]
@@ -395,6 +446,18 @@ def _alloc_columns(plan: DecodePlan, n_rec: int, slot_capacity: Sequence[int], d
         cstructs[ci].validity = c["validity"].data_ptr()
         cols.append(c)
     return cols, cstructs
+
+
+class _HostArray:
+    """A numpy array with the tensor method _slot_arrays uses (.cpu().numpy())."""
+    def __init__(self, a):
+        self.a = a
+
+    def cpu(self):
+        return self
+
+    def numpy(self):
+        return self.a
 
 
 def view_geometry(capacity: int, n_tiles: int) -> Tuple[int, int]:
@@ -476,7 +539,8 @@ class _BaseReader:
                                jit_min_records=params.jit_min_records,
                                segment_levels=params.segment_id_levels if var else (),
                                segment_filter=params.segment_id_filter if var else None,
-                               segment_prefix=params.segment_id_prefix, string_views=params.string_views)
+                               segment_prefix=params.segment_id_prefix, string_views=params.string_views,
+                               occurs_lists=params.occurs_lists)
         self.native = NativePlan(self.plan)
 
     @property

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 6
+#define CBX_ABI_VERSION 7
 
 /* status codes */
 #define CBX_OK 0
@@ -85,6 +85,7 @@ enum cbx_out {
 #define CBX_F_IBM 0x10          /* COMP-1/2 in IBM hex float (else IEEE-754) */
 #define CBX_F_LITTLE_ENDIAN_FP 0x20
 #define CBX_F_DEPENDEE 0x40     /* an OCCURS DEPENDING ON source (isDependee) */
+#define CBX_F_LIST 0x80         /* element of a list-layout OCCURS DEPENDING ON array (cbx_array.offsets_column) */
 
 /* string trimming (StringTrimmingPolicy) */
 #define CBX_TRIM_NONE 1
@@ -123,7 +124,8 @@ typedef struct {
     int32_t count_column;  /* output column receiving the per-record element count (int32) */
     int32_t n_dims;        /* enclosing OCCURS levels (outer arrays of this array) */
     int32_t parent;        /* enclosing array index or -1 */
-    int32_t reserved;
+    int32_t offsets_column;/* list layout (fields flagged CBX_F_LIST): output column receiving each
+                              record's int64 child offset, -1 for the slot-major layout */
 } cbx_array;
 
 /* Segment ids (the `segment_field` of a multisegment file) and everything keyed by them:
@@ -185,6 +187,13 @@ typedef struct {
  * n_rec are padding).  data_capacity = cbx_string_bound(...) always suffices; a smaller
  * capacity (e.g. from cbx_string_sizes_*) is honoured: payload never overflows its region, an
  * overflow is reported by cbx_plan_check.
+ *
+ * List layout of an OCCURS DEPENDING ON array (cbx_array.offsets_column >= 0; its fields flagged
+ * CBX_F_LIST, numeric, one OCCURS level; Arrow ListView): a field's `values` / `validity` hold
+ * the CHILD elements -- tile t of 64 records owns elements [t * 64 * M, (t + 1) * 64 * M) with
+ * M = max_count rounded up to 64, record r's elements start at its offsets-column value (a
+ * multiple of 64) and its count column gives their number; absent elements are never written.
+ * values need ceil(n_rec / 64) * 64 * M elements, validity ceil(n_rec / 64) * M words.
  *
  * String-view layout (cbx_plan_options.string_views != 0; Arrow Utf8View / BinaryView): `values`
  * holds n_slots * pitch views of 16 bytes (value (s, r) at view s * pitch + r): int32 length, then

@@ -42,13 +42,13 @@ def gpu_rows(case, **extra):
 
 
 @pytest.mark.parametrize("name", sorted(GC.CASES))
-@pytest.mark.parametrize("jit,views", [(-1, False), (1, False), (-1, True), (1, True)])
-def test_gpu_golden_rows(name, jit, views):
+@pytest.mark.parametrize("jit,views,lists", [(-1, False, False), (1, False, False), (-1, True, True), (1, True, True)])
+def test_gpu_golden_rows(name, jit, views, lists):
     """Both decode kernels (table-driven: jit=-1; copybook-specialised: jit=1), in both string
-    layouts (Arrow offsets / Arrow string views), reproduce the reference's golden rows and the
-    oracle's full row set."""
+    layouts (Arrow offsets / Arrow string views) and both OCCURS DEPENDING ON layouts (slot rows /
+    lists), reproduce the reference's golden rows and the oracle's full row set."""
     case = GC.CASES[name]
-    rd, rows = gpu_rows(case, jit_min_records=jit, string_views=views)
+    rd, rows = gpu_rows(case, jit_min_records=jit, string_views=views, occurs_lists=lists)
     errs = GC.compare(case, rows)
     assert not errs, errs[:10]
     p, var_len = GC.params(case)
@@ -173,6 +173,10 @@ def _norm(v):
 @pytest.mark.parametrize("views", [False, True])
 @pytest.mark.parametrize("name", ["test1", "test5", "test6", "test9_cp037", "test19", "test17a"])
 def test_gpu_arrow_export_matches_rows(name, views):
+    _arrow_vs_rows(name, views)
+
+
+def _arrow_vs_rows(name, views):
     """DecodedBatch.to_arrow (structs, OCCURS DEPENDING ON lists, segment-redefine nulls, views or
     large strings, decimal128) holds exactly the rows to_rows rebuilds."""
     pytest.importorskip("pyarrow")
@@ -180,6 +184,7 @@ def test_gpu_arrow_export_matches_rows(name, views):
     case = GC.CASES[name]
     p, var_len = GC.params(case)
     p.string_views = views
+    p.occurs_lists = views
     data = GC.data_bytes(case)
     rd = (VarLenNestedReader if var_len else FixedLenNestedReader)(GC.copybook_text(case), p)
     batch = rd.read(data) if var_len else rd.decode(data)

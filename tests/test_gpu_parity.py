@@ -253,13 +253,15 @@ def test_synstr200_vs_oracle(n, jit, views):
     assert not errs, errs
 
 
-def test_wide_odo_vs_oracle():
-    """Config C5 (exp3 wide layout, OCCURS 0 TO 2000 DEPENDING ON, segment redefines, RDW)."""
+@pytest.mark.parametrize("lists,jit", [(False, 0), (True, 0), (True, 1)])
+def test_wide_odo_vs_oracle(lists, jit):
+    """Config C5 (exp3 wide layout, OCCURS 0 TO 2000 DEPENDING ON, segment redefines, RDW), the
+    array in slot rows or in the list layout (child elements packed per record)."""
     from cobrix_amd.synth import WIDE_ODO_COPYBOOK, WIDE_ODO_SEGMENTS, wide_odo
     raw_t, hdr = wide_odo(40, seed=5)
     raw = raw_t.numpy().tobytes()
     params = ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
-                              segment_id_redefine_map=WIDE_ODO_SEGMENTS)
+                              segment_id_redefine_map=WIDE_ODO_SEGMENTS, occurs_lists=lists, jit_min_records=jit)
     rd = VarLenNestedReader(WIDE_ODO_COPYBOOK, params)
     t = raw_t.cuda()
     off, ln = rd.frame(t, len(raw))

@@ -12,20 +12,27 @@ import os
 import sys
 
 DECODE_KERNELS = ("cbx::decode_kernel", "cbx_jit_decode")   # table-driven / copybook-specialised
+LIST_KERNEL = "cbx::list_kernel"   # OCCURS lists (dword loads: FETCH_SIZE taken as is)
 root, records = sys.argv[1], int(sys.argv[2])
 names = set()
 vals = collections.defaultdict(float)
 for pas, ctr in (("pmc3", "FETCH_SIZE"), ("pmc4", "WRITE_SIZE")):
     rows = list(csv.DictReader(open(os.path.join(root, pas, "run_counter_collection.csv"))))
-    per = collections.defaultdict(float)
+    per = collections.defaultdict(lambda: collections.defaultdict(float))   # kernel -> dispatch -> KiB
     for r in rows:
-        if r["Kernel_Name"].startswith(DECODE_KERNELS) and r["Counter_Name"] == ctr:
-            per[r["Dispatch_Id"]] += float(r["Counter_Value"])
-            names.add(r["Kernel_Name"].split("(")[0])
-    last = max(per, key=int)          # the measured launch (tools/prof_decode.py --iters 1)
-    vals[ctr] = per[last] * 1024.0
-fetch = 2.0 * vals["FETCH_SIZE"]
-out = {"kernel": "/".join(sorted(names)), "records": records, "fetch_bytes_raw": vals["FETCH_SIZE"],
-       "fetch_bytes": fetch, "write_bytes": vals["WRITE_SIZE"], "traffic_bytes": fetch + vals["WRITE_SIZE"],
-       "note": "FETCH_SIZE doubled (gfx950 counts half of 16-B/lane streaming reads)"}
+        k = r["Kernel_Name"]
+        if (k.startswith(DECODE_KERNELS) or k.startswith(LIST_KERNEL)) and r["Counter_Name"] == ctr:
+            base = k.split("(")[0]
+            per[base][r["Dispatch_Id"]] += float(r["Counter_Value"])
+            names.add(base)
+    for base, d in per.items():
+        last = d[max(d, key=int)] * 1024.0   # the measured launch (the last one)
+        scale = 2.0 if ctr == "FETCH_SIZE" and not base.startswith(LIST_KERNEL) else 1.0
+        vals[ctr] += last * scale
+        vals[ctr + "_raw"] += last
+out = {"kernel": " + ".join(sorted(names)), "records": records, "fetch_bytes_raw": vals["FETCH_SIZE_raw"],
+       "fetch_bytes": vals["FETCH_SIZE"], "write_bytes": vals["WRITE_SIZE"],
+       "traffic_bytes": vals["FETCH_SIZE"] + vals["WRITE_SIZE"],
+       "note": "decode kernel FETCH_SIZE doubled (gfx950 counts half of 16-B/lane streaming reads); "
+               "list kernel (dword loads) as is"}
 print(json.dumps(out))
