@@ -74,6 +74,7 @@ struct cbx_plan {
     std::vector<ListOp> lops;             // list-layout fields (list_kernel), grouped by array
     ListOp* d_lops = nullptr;
     int32_t* d_list_len = nullptr;  int64_t list_len_cap = 0;
+    int32_t* d_list_flag = nullptr; int64_t list_flag_cap = 0;
     // device copies
     Field* d_fields = nullptr;
     DeferSeq* d_defer = nullptr;
@@ -432,6 +433,11 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
             lo.stride = f.dim_stride[0];
             P->lops.push_back(lo);
         }
+    for (ListOp& lo : P->lops) {   // elements are staged from the array's first field byte
+        lo.elem_lo = lo.op.eo;
+        for (const ListOp& o : P->lops)
+            if (o.array == lo.array) lo.elem_lo = std::min(lo.elem_lo, o.op.eo);
+    }
     if ((int)P->lops.size() != (int)std::count_if(fields, fields + n_fields, [](const cbx_field& f) { return (f.flags & CBX_F_LIST) != 0; }))
         { delete P; return fail(CBX_E_ARGUMENT, "CBX_F_LIST field outside a list-layout array"); }
     P->seg_col = opts->segment_column;
@@ -524,7 +530,7 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
     (void)hipFree(P->d_segmap); (void)hipFree(P->d_lut); (void)hipFree(P->d_cols);
     (void)hipFree(P->d_seqcall); (void)hipFree(P->d_str_tot); (void)hipFree(P->d_str_excl); (void)hipFree(P->d_block_sums);
     (void)hipFree(P->d_local); (void)hipFree(P->d_scratch); (void)hipFree(P->d_status); (void)hipFree(P->d_stamps);
-    (void)hipFree(P->d_lops); (void)hipFree(P->d_list_len);
+    (void)hipFree(P->d_lops); (void)hipFree(P->d_list_len); (void)hipFree(P->d_list_flag);
     for (auto& e : P->ev_pool) (void)hipEventDestroy(e);
     for (auto& c : P->ev_calls) for (auto& e : c.e) if (e) (void)hipEventDestroy(e);
     delete P;
@@ -786,8 +792,11 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     if (P->n_seq > 0 && (r = grow(&P->d_str_tot, &P->str_tot_cap, (int64_t)P->n_seq * n_tiles, st))) return r;
     a.str_tot = P->d_str_tot;
     const bool lists = mode == 0 && !P->lops.empty();
-    if (lists && (r = grow(&P->d_list_len, &P->list_len_cap, (int64_t)P->harrays.size() * a.pitch, st))) return r;
+    if (lists && ((r = grow(&P->d_list_len, &P->list_len_cap, (int64_t)P->harrays.size() * a.pitch, st)) ||
+                  (r = grow(&P->d_list_flag, &P->list_flag_cap, n_tiles, st))))
+        return r;
     a.list_len = P->d_list_len;
+    a.list_flag = P->d_list_flag;
     const int n_defer = n_defer_seq;
     a.defer_bits = P->d_defer_bits;
     const size_t lds = 1024 + (size_t)kWavesPerBlock * a.lds_wave;
@@ -842,7 +851,11 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     }
     if (lists) {   // child elements of list-layout arrays, from the lengths and starts the prologue wrote
         const int64_t lgrid = std::min<int64_t>((n_tiles + kListWaves - 1) / kListWaves, (int64_t)P->num_cus * 8);
-        hipLaunchKernelGGL(list_kernel, dim3((unsigned)lgrid), dim3(kWave * kListWaves), 0, st, a,
+        const size_t llds = kListWaves * (2 * kGuard + kListStage);
+        hipLaunchKernelGGL(list_kernel<false>, dim3((unsigned)lgrid), dim3(kWave * kListWaves), llds, st, a,
+                           (const CBX_CONST ListOp*)P->d_lops, (int32_t)P->lops.size());
+        // byte-loop pass over the tiles the first one flagged (deferred zoned forms, wide fields)
+        hipLaunchKernelGGL(list_kernel<true>, dim3((unsigned)lgrid), dim3(kWave * kListWaves), llds, st, a,
                            (const CBX_CONST ListOp*)P->d_lops, (int32_t)P->lops.size());
         HIP_CHECK(hipGetLastError());
     }

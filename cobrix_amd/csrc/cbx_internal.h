@@ -71,7 +71,7 @@ struct ListOp {
     int32_t field;            // field index (byte-loop decoder for wide / deferred forms)
     int32_t array;            // its array (ListOps of one array are adjacent)
     int32_t stride;           // bytes between elements
-    int32_t reserved;
+    int32_t elem_lo;          // offset of the array's first element (lowest eo of its ListOps)
 };
 
 // Generated column (File_Id / Record_Id).
@@ -151,6 +151,7 @@ struct KernelArgs {
     uint32_t* str_tot;         // [n_seq][n_tiles] payload bytes of every (sequence, tile)
     int32_t* status;           // [0]: capacity overflow flag
     int32_t* list_len;         // list-layout arrays: [n_arrays][pitch] present elements per record
+    int32_t* list_flag;        // per tile: the list kernel left elements to its byte-loop pass
     uint64_t* defer_bits;      // [n_defer][n_tiles] values left to the fixup kernel
     // LDS layout (bytes, per wave)
     int32_t lds_rows;          // record image incl. guards

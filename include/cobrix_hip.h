@@ -192,8 +192,12 @@ typedef struct {
  * CBX_F_LIST, numeric, one OCCURS level; Arrow ListView): a field's `values` / `validity` hold
  * the CHILD elements -- tile t of 64 records owns elements [t * 64 * M, (t + 1) * 64 * M) with
  * M = max_count rounded up to 64, record r's elements start at its offsets-column value (a
- * multiple of 64) and its count column gives their number; absent elements are never written.
- * values need ceil(n_rec / 64) * 64 * M elements, validity ceil(n_rec / 64) * M words.
+ * multiple of 64) and its count column gives their number (none where the count is null: the
+ * array's segment is not the record's); the run is padded to a multiple of 64 (padding values
+ * unspecified, validity bits 0) and nothing past it is written.  All CBX_F_LIST fields of an
+ * array share its segment.  values need ceil(n_rec / 64) * 64 * M elements, validity
+ * ceil(n_rec / 64) * M words.  The elements are decoded by a second, element-parallel kernel
+ * (64 consecutive elements of one record per wave step) after the record kernel.
  *
  * String-view layout (cbx_plan_options.string_views != 0; Arrow Utf8View / BinaryView): `values`
  * holds n_slots * pitch views of 16 bytes (value (s, r) at view s * pitch + r): int32 length, then

@@ -276,6 +276,50 @@ def test_wide_odo_vs_oracle(lists, jit):
     assert not errs, errs
 
 
+LIST_COPYBOOK = """
+       01  REC.
+           05  CNT-A         PIC 9(3).
+           05  CNT-B         PIC S9(4) COMP.
+           05  ARR-A OCCURS 0 TO 150 TIMES DEPENDING ON CNT-A.
+               10  A-BCD     PIC S9(5) COMP-3.
+               10  A-BIN     PIC 9(4) COMP.
+               10  A-ZON     PIC S9(3).
+           05  ARR-B OCCURS 1 TO 5 TIMES DEPENDING ON CNT-B.
+               10  B-ZON     PIC S9(18).
+               10  B-WIDE    PIC 9(20)V9(5).
+               10  B-BCD     PIC S9(17)V9(10) COMP-3.
+               10  B-DBL     COMP-2.
+"""
+
+
+@pytest.mark.parametrize("n,jit", [(1, 0), (3001, 0), (3001, 1)])
+def test_list_layout_fixed_vs_oracle(n, jit):
+    """List layout on a fixed-length file: an 8-byte element array (list kernel, LDS-staged element
+    groups, counts 0-170 incl. out-of-range ones) and a 65-byte element array (per-lane loads;
+    zoned, wide DISPLAY, 14-byte COMP-3 and COMP-2 elements) against the oracle."""
+    from test_decode_fuzz import _random_bytes
+    cb = cbk.parse_copybook(LIST_COPYBOOK)
+    leaves = {nm: cb.get_field_by_name(nm) for nm in ("A-BCD", "A-BIN", "A-ZON", "B-ZON", "B-WIDE", "B-BCD", "B-DBL")}
+    rng = np.random.default_rng(n)
+    pool_a = [b"".join(_random_bytes(rng, leaves[k], leaves[k].data_size) for k in ("A-BCD", "A-BIN", "A-ZON"))
+              for _ in range(301)]
+    pool_b = [b"".join(_random_bytes(rng, leaves[k], leaves[k].data_size) for k in ("B-ZON", "B-WIDE", "B-BCD", "B-DBL"))
+              for _ in range(97)]
+    recs = bytearray()
+    for i in range(n):
+        ca = int(rng.integers(0, 171))
+        cb_ = int(rng.integers(0, 8))
+        r = bytearray(("%03d" % ca).encode("cp037")) + cb_.to_bytes(2, "big")
+        r += b"".join(pool_a[(i * 7 + j) % 301] for j in range(150))
+        r += b"".join(pool_b[(i * 3 + j) % 97] for j in range(5))
+        recs += r
+    assert len(recs) == n * cb.record_size
+    rd, batch = _fixed(LIST_COPYBOOK, bytes(recs), occurs_lists=True, jit_min_records=jit)
+    assert sum(c.list_array >= 0 for c in rd.plan.columns) == 7
+    errs = compare_batch(batch, O.decode_fixed(rd.copybook, bytes(recs)))
+    assert not errs, errs
+
+
 @pytest.mark.parametrize("views", [False, True])
 def test_syn200_full_size_sampled_parity(views):
     """The bench's own configuration (C2: 50 M SYN200 records = 10 GB resident in HBM, the
