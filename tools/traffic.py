@@ -12,7 +12,7 @@ import os
 import sys
 
 DECODE_KERNELS = ("cbx::decode_kernel", "cbx_jit_decode")   # table-driven / copybook-specialised
-LIST_KERNEL = "cbx::list_kernel"   # OCCURS lists (dword loads: FETCH_SIZE taken as is)
+LIST_KERNEL = "cbx::list_kernel"   # OCCURS lists ("void cbx::list_kernel<...>", 16-byte LDS-staged loads)
 root, records = sys.argv[1], int(sys.argv[2])
 names = set()
 vals = collections.defaultdict(float)
@@ -21,18 +21,18 @@ for pas, ctr in (("pmc3", "FETCH_SIZE"), ("pmc4", "WRITE_SIZE")):
     per = collections.defaultdict(lambda: collections.defaultdict(float))   # kernel -> dispatch -> KiB
     for r in rows:
         k = r["Kernel_Name"]
-        if (k.startswith(DECODE_KERNELS) or k.startswith(LIST_KERNEL)) and r["Counter_Name"] == ctr:
-            base = k.split("(")[0]
+        base = k.split("(")[0].replace("void ", "", 1)
+        if (base.startswith(DECODE_KERNELS) or base.startswith(LIST_KERNEL)) and r["Counter_Name"] == ctr:
             per[base][r["Dispatch_Id"]] += float(r["Counter_Value"])
             names.add(base)
     for base, d in per.items():
         last = d[max(d, key=int)] * 1024.0   # the measured launch (the last one)
-        scale = 2.0 if ctr == "FETCH_SIZE" and not base.startswith(LIST_KERNEL) else 1.0
+        scale = 2.0 if ctr == "FETCH_SIZE" else 1.0   # both kernels stage with 16-byte loads
         vals[ctr] += last * scale
         vals[ctr + "_raw"] += last
 out = {"kernel": " + ".join(sorted(names)), "records": records, "fetch_bytes_raw": vals["FETCH_SIZE_raw"],
        "fetch_bytes": vals["FETCH_SIZE"], "write_bytes": vals["WRITE_SIZE"],
        "traffic_bytes": vals["FETCH_SIZE"] + vals["WRITE_SIZE"],
-       "note": "decode kernel FETCH_SIZE doubled (gfx950 counts half of 16-B/lane streaming reads); "
-               "list kernel (dword loads) as is"}
+       "note": "FETCH_SIZE doubled (gfx950 counts half of 16-B/lane streaming reads; the decode and list "
+               "kernels stage with 16-byte loads)"}
 print(json.dumps(out))
