@@ -882,11 +882,15 @@ def _add_debug_fields(root: Group, policy: str) -> None:
                 process(c)
                 new_kids.append(c)
             else:
+                # the debug field is field.copy(...) of the original: it keeps the original's
+                # isRedefined (a redefined field's debug twin does not advance the offset either),
+                # while the original itself becomes isRedefined = true (:913-922)
+                was_redefined = c.is_redefined
                 c.is_redefined = True
                 new_kids.append(c)
                 size = c.data_size
                 dbg = Primitive(level=c.level, name=c.name + "_debug", line=c.line,
-                                redefines=c.name, is_redefined=False, occurs=c.occurs, to=c.to,
+                                redefines=c.name, is_redefined=was_redefined, occurs=c.occurs, to=c.to,
                                 depending_on=c.depending_on,
                                 depending_on_handlers=c.depending_on_handlers,
                                 is_filler=c.is_filler, offset=c.offset, data_size=c.data_size,

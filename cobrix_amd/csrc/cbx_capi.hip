@@ -22,6 +22,7 @@
 #include "cbx_kernels.hip"
 #include "cbx_select.h"
 #include "cbx_text.h"
+#include "cbx_hier.h"
 
 using namespace cbx;
 
@@ -1445,8 +1446,10 @@ extern "C" int cbx_sparse_index(cbx_plan* P, const uint8_t* d_data, int64_t n_by
         prm->records_per_entry < 0 || (prm->records_per_entry == 0 && prm->bytes_per_entry <= 0))
         return fail(CBX_E_ARGUMENT, "cbx_sparse_index: invalid arguments");
     *n_entries = 0;
-    const bool hier = prm->hierarchical && P->opts.has_segments && P->opts.segments.n_levels > 0;
-    if (prm->hierarchical && !hier) return fail(CBX_E_ARGUMENT, "cbx_sparse_index: hierarchical cuts need segment levels in the plan");
+    bool root_keys = false;   // level-0 keys: segment_id_level0 / segment_id_root, or a hierarchical file's root ids
+    for (int k = 0; P->opts.has_segments && k < P->opts.segments.n_keys; k++) root_keys |= P->opts.segments.key_level[k] == 0;
+    const bool hier = prm->hierarchical && root_keys;
+    if (prm->hierarchical && !hier) return fail(CBX_E_ARGUMENT, "cbx_sparse_index: hierarchical cuts need level-0 segment keys in the plan");
     const int64_t hh = prm->has_file_header ? 1 : 0;
     std::vector<int64_t> from{0}, recno{0};   // the first mandatory entry
     if (n_rec > 0) {
@@ -1574,5 +1577,99 @@ extern "C" int cbx_sparse_index(cbx_plan* P, const uint8_t* d_data, int64_t n_by
         entries[k].file_id = prm->file_id;
         entries[k].reserved = 0;
     }
+    return CBX_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Hierarchical records (cbx_hier.h): table rows + parent rows, list offsets per child table.
+// ---------------------------------------------------------------------------------------------
+extern "C" int cbx_hier_select(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                               const int32_t* d_rec_len, int64_t n_rec, const cbx_hier_params* prm, cbx_selection* out,
+                               int64_t* d_parent_row, int64_t* table_rows, int64_t* n_rows, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!P || !prm || !out || !n_rows || !table_rows || n_rec < 0 || n_bytes < 0 ||
+        (n_rec > 0 && (!d_data || !d_rec_off || !d_rec_len || !d_parent_row || !out->rec_off || !out->rec_len ||
+                       !out->record_id || !out->segment)))
+        return fail(CBX_E_ARGUMENT, "cbx_hier_select: invalid arguments");
+    if (!P->opts.has_segments) return fail(CBX_E_ARGUMENT, "cbx_hier_select: the plan has no segment map");
+    const int S = prm->n_segments;
+    if (S < 1 || S > kHierMaxSeg) return fail(CBX_E_UNSUPPORTED, "cbx_hier_select: 1 to 16 segments");
+    if (prm->root_segment < 0 || prm->root_segment >= S || prm->parent[prm->root_segment] != -1)
+        return fail(CBX_E_ARGUMENT, "cbx_hier_select: bad root segment");
+    HierArgs a{};
+    a.n_seg = S;
+    a.root = prm->root_segment;
+    for (int s = 0; s < kHierMaxSeg; s++) { a.parent[s] = -1; a.anc[s] = 0; }
+    for (int s = 0; s < S; s++) {
+        const int p = prm->parent[s];
+        if (s != a.root && (p < 0 || p >= S || p == s)) return fail(CBX_E_ARGUMENT, "cbx_hier_select: bad parent segment");
+        a.parent[s] = s == a.root ? -1 : p;
+    }
+    for (int s = 0; s < S; s++) {   // every chain reaches the root; anc = strict non-root ancestors of the parent
+        if (s == a.root) continue;
+        int d = 0;
+        for (int q = a.parent[s]; q != a.root; q = a.parent[q]) {
+            if (q < 0 || ++d > S) return fail(CBX_E_ARGUMENT, "cbx_hier_select: a segment does not reach the root");
+            if (q != a.parent[s]) a.anc[s] |= 1u << q;
+        }
+    }
+    *n_rows = 0;
+    for (int t = 0; t <= S; t++) table_rows[t] = 0;
+    if (n_rec == 0) return CBX_OK;
+    const int64_t n_blk = (n_rec + kHierTile - 1) / kHierTile;   // last-position blocks
+    const int64_t n_eb = (n_rec + 255) / 256;                     // compaction blocks
+    const int64_t n_cnt = (int64_t)(S + 1) * n_eb;
+    const int64_t nb = scan_sums_len(n_cnt + 1);
+    // type, st, tab (n each) | par, row_of (n int64) | blk_lp (n_blk x 16) | cnt (n_cnt + 1 u32) | base (n_cnt + 1) | sums
+    const size_t o_par = ((3 * (size_t)n_rec) + 15) & ~(size_t)15;
+    const size_t o_row = o_par + 8 * (size_t)n_rec;
+    const size_t o_lp = o_row + 8 * (size_t)n_rec;
+    const size_t o_cnt = o_lp + 8 * (size_t)n_blk * kHierMaxSeg;
+    const size_t o_base = (o_cnt + 4 * (size_t)(n_cnt + 1) + 15) & ~(size_t)15;
+    const size_t o_sums = o_base + 8 * (size_t)(n_cnt + 1);
+    AsyncBlock blk(st);
+    HIP_CHECK(hipMallocAsync(&blk.p, o_sums + 8 * (size_t)nb + 64, st));
+    uint8_t* b = (uint8_t*)blk.p;
+    a.data = d_data; a.rec_off = d_rec_off; a.rec_len = d_rec_len; a.n = n_rec;
+    a.m = (const CBX_CONST cbx_segment_map*)P->d_segmap;
+    a.lut = P->d_lut;
+    a.fields = (const CBX_CONST Field*)P->d_fields;
+    a.type = (int8_t*)b; a.st = (int8_t*)b + n_rec; a.tab = (int8_t*)b + 2 * n_rec;
+    a.par = (int64_t*)(b + o_par); a.row_of = (int64_t*)(b + o_row);
+    int64_t* blk_lp = (int64_t*)(b + o_lp);
+    uint32_t* cnt = (uint32_t*)(b + o_cnt);
+    int64_t* base = (int64_t*)(b + o_base);
+    int64_t* sums = (int64_t*)(b + o_sums);
+    HIP_CHECK(hipMemsetAsync(cnt + n_cnt, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(hier_type_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(hier_last_kernel, dim3((unsigned)n_blk), dim3(kHierThreads), 0, st, a, 0, blk_lp);
+    hipLaunchKernelGGL(hier_lp_scan_kernel, dim3(1), dim3(kHierThreads), 0, st, blk_lp, n_blk, (int32_t)S);
+    hipLaunchKernelGGL(hier_last_kernel, dim3((unsigned)n_blk), dim3(kHierThreads), 0, st, a, 1, blk_lp);
+    hipLaunchKernelGGL(hier_chase_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(hier_emit_kernel, dim3((unsigned)n_eb), dim3(256), 0, st, a, 0, n_eb, cnt, (const int64_t*)nullptr,
+                       prm->first_record_id, *out);
+    device_scan(cnt, n_cnt + 1, base, sums, st);
+    hipLaunchKernelGGL(hier_emit_kernel, dim3((unsigned)n_eb), dim3(256), 0, st, a, 1, n_eb, cnt, (const int64_t*)base,
+                       prm->first_record_id, *out);
+    hipLaunchKernelGGL(hier_parent_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, a, d_parent_row);
+    HIP_CHECK(hipGetLastError());
+    std::vector<int64_t> tb(S + 2);
+    for (int t = 0; t <= S; t++)
+        HIP_CHECK(hipMemcpyAsync(&tb[t], base + (int64_t)t * n_eb, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&tb[S + 1], base + n_cnt, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    for (int t = 0; t <= S; t++) table_rows[t] = tb[t + 1] - tb[t];
+    *n_rows = tb[S + 1];
+    return CBX_OK;
+}
+
+extern "C" int cbx_hier_list_offsets(const int64_t* d_parent_row, int64_t child_begin, int64_t n_child, int64_t parent_begin,
+                                     int64_t n_parent, int32_t* d_offsets, void* stream) {
+    if (!d_offsets || child_begin < 0 || n_child < 0 || parent_begin < 0 || n_parent < 0 || (n_child > 0 && !d_parent_row))
+        return fail(CBX_E_ARGUMENT, "cbx_hier_list_offsets: invalid arguments");
+    if (n_child > INT32_MAX) return fail(CBX_E_UNSUPPORTED, "cbx_hier_list_offsets: more than 2^31 - 1 child rows");
+    hipLaunchKernelGGL(hier_offsets_kernel, dim3(blocks_for(n_parent + 1, 256)), dim3(256), 0, (hipStream_t)stream,
+                       d_parent_row, child_begin, n_child, parent_begin, n_parent, d_offsets);
+    HIP_CHECK(hipGetLastError());
     return CBX_OK;
 }

@@ -39,8 +39,9 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_string_bound", "cbx_string_view_geometry", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
                     "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
                     "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text",
-                    "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected")
-ABI_VERSION = 7
+                    "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
+                    "cbx_hier_list_offsets")
+ABI_VERSION = 8
 
 
 class NativeLibraryError(RuntimeError):
@@ -121,6 +122,11 @@ class CbxSelection(ctypes.Structure):
                 ("footer_bytes", ctypes.c_int32)]
 
 
+class CbxHierParams(ctypes.Structure):
+    _fields_ = [("n_segments", ctypes.c_int32), ("root_segment", ctypes.c_int32),
+                ("parent", ctypes.c_int32 * CBX_MAX_SEG_KEYS), ("first_record_id", ctypes.c_int64)]
+
+
 _lib = None
 
 
@@ -161,6 +167,8 @@ def load():
     L.cbx_sparse_index.argtypes = [P, P, i64, P, P, i64, P, P, i64, P, P]
     L.cbx_select_records.argtypes = [P, P, i64, P, P, i64, i32, P, i32, P, P, P]
     L.cbx_decode_selected.argtypes = [P, P, i64, P, i64, i32, P, P]
+    L.cbx_hier_select.argtypes = [P, P, i64, P, P, i64, P, P, P, P, P, P]
+    L.cbx_hier_list_offsets.argtypes = [P, i64, i64, i64, i64, P, P]
     if L.cbx_abi_version() != ABI_VERSION:
         raise NativeLibraryError(f"{LIB_PATH}: ABI {L.cbx_abi_version()} != {ABI_VERSION}; rebuild it")
     _lib = L

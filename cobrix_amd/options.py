@@ -10,8 +10,8 @@ a job switching to it keeps its `spark.read.format("cobol").option(...)` calls:
   * ReaderParameters mapping        SC/source/DefaultSource.scala:141-209
 
 (SC = spark-cobol/src/main/scala/za/co/absa/cobrix/spark/cobol/.)  Options of subsystems outside
-the accelerated path (custom record header parsers / extractors, hierarchical `segment-children`,
-record_length_field, input file name columns) raise UnsupportedOption instead of being dropped.
+the accelerated path (custom record header parsers / extractors, record_length_field, input file
+name columns) raise UnsupportedOption instead of being dropped.
 """
 from __future__ import annotations
 
@@ -99,6 +99,25 @@ def redefine_map(opts: Mapping[str, str]) -> Dict[str, str]:
     return out
 
 
+def segment_redefine_parents(opts: Mapping[str, str]) -> Dict[str, str]:
+    """getSegmentRedefineParents (:433-465): `segment-children:N` = "PARENT => CHILD1,CHILD2" ->
+    child redefine -> parent redefine (transformed identifiers)."""
+    out: Dict[str, str] = {}
+    for k, v in opts.items():
+        if not k.lower().startswith(("segment-children", "segment_children")):
+            continue
+        parts = v.split("=>")
+        if len(parts) != 2:
+            raise ValueError(f"Illegal argument for the 'segment-children' option: '{v}'.")
+        parent = _transform_identifier(parts[0].strip())
+        for child in (_transform_identifier(c.strip()) for c in parts[1].split(",")):
+            if child in out and out[child] != parent:
+                raise ValueError(f"Duplicate child '{child}' for parents {out[child]} and {parent} "
+                                 "specified for 'segment-children' option.")
+            out[child] = parent
+    return out
+
+
 def is_variable_length(opts: Mapping[str, str]) -> bool:
     """parseVariableLengthParameters (:242-290): which options select VarLenNestedReader."""
     if "record_length_field" in opts and ("is_record_sequence" in opts or "is_xcom" in opts):
@@ -123,8 +142,6 @@ def parse_options(options: Mapping[str, object]) -> Tuple[ReaderParameters, bool
     for k, what in UNSUPPORTED.items():
         if k in opts:
             raise UnsupportedOption(f"option '{k}': {what} are not on the GPU path")
-    if any(k.lower().startswith("segment-children") for k in opts):
-        raise UnsupportedOption("option 'segment-children:*': hierarchical records (VarLenHierarchicalIterator) are not on the GPU path")
 
     enc = opts.get("encoding", "")
     if enc == "" or enc.lower() == "ebcdic":
@@ -158,6 +175,11 @@ def parse_options(options: Mapping[str, object]) -> Tuple[ReaderParameters, bool
     seg_field = opts.get("segment_field")
     levels = segment_levels(opts) if seg_field is not None else []
     filt = opts["segment_filter"].split(",") if (seg_field is not None and "segment_filter" in opts) else None
+    parents = segment_redefine_parents(opts)
+    if parents and segment_levels(opts):
+        # CobolParametersParser.validateSparkCobolOptions (:568-574)
+        raise ValueError("Options 'segment-children:*' cannot be used with 'segment_id_level*' or 'segment_id_root' "
+                         "since ID fields generation is not supported for hierarchical records reader.")
     occurs = json.loads(opts.get("occurs_mappings", "{}"))
     non_terminals = [s for s in opts.get("non_terminals", "").split(",") if s]
     p = ReaderParameters(
@@ -186,6 +208,7 @@ def parse_options(options: Mapping[str, object]) -> Tuple[ReaderParameters, bool
         string_trimming_policy=trim.lower(),
         segment_field=seg_field,
         segment_id_redefine_map=redefine_map(opts) if seg_field is not None else {},
+        segment_redefine_parents=parents,
         segment_id_filter=filt,
         segment_id_levels=levels,
         segment_id_prefix=opts.get("segment_id_prefix", "") if seg_field is not None else "",

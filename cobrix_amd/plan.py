@@ -148,7 +148,10 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
                segment_redefine_map: Optional[Dict[str, str]] = None, generate_record_id: bool = False,
                file_id: int = 0, window_bytes: int = 0, jit_min_records: int = 0,
                segment_levels: Sequence[str] = (), segment_filter: Optional[List[str]] = None,
-               segment_prefix: str = "", string_views: bool = False, occurs_lists: bool = False) -> DecodePlan:
+               segment_prefix: str = "", string_views: bool = False, occurs_lists: bool = False,
+               root_keys: Sequence[str] = ()) -> DecodePlan:
+    """root_keys: segment ids of a hierarchical file's root segment (sparse-index cuts at level-0
+    keys, IndexGenerator.scala:89-113, without Seg_IdN columns)."""
     fields: List[N.CbxField] = []
     arrays: List[N.CbxArray] = []
     columns: List[ColumnInfo] = []
@@ -304,7 +307,7 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
                 gname = cbk._transform_identifier(red[key]).upper()
                 matches = [i for i, g in enumerate(seg_groups) if g.name.upper() == gname]
                 sm.key_segment[k] = matches[0] if matches else -1
-            sm.key_level[k] = next((i for i, ids in enumerate(level_sets) if key in ids), -1)
+            sm.key_level[k] = next((i for i, ids in enumerate(level_sets) if key in ids), 0 if key in root_keys else -1)
             sm.key_in_filter[k] = int(seg_filter is not None and key in seg_filter)
             if field_is_int and _CANONICAL_INT.match(key) and -(1 << 63) <= int(key) < (1 << 63):
                 sm.key_is_int[k], sm.key_int[k] = 1, int(key)

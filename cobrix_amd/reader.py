@@ -65,6 +65,8 @@ class ReaderParameters:
     segment_id_filter: Optional[List[str]] = None
     segment_id_levels: List[str] = field(default_factory=list)   # segment_id_level0.. / segment_id_root
     segment_id_prefix: str = ""
+    # segment-children: child segment redefine -> parent (MultisegmentParameters.fieldParentMap)
+    segment_redefine_parents: Dict[str, str] = field(default_factory=dict)
     drop_group_fillers: bool = False
     drop_value_fillers: bool = True
     non_terminals: Sequence[str] = ()
@@ -216,10 +218,11 @@ class DecodedBatch:
             out.append(arr)
         return out
 
-    def to_arrow(self):
-        """The batch as a pyarrow Table in the reference's Spark schema shape: groups -> structs
-        (an inactive segment redefine -> null struct), OCCURS -> lists of the records' element
-        counts (OCCURS DEPENDING ON), generated File_Id / Record_Id / Seg_IdN columns first."""
+    def _arrow_builder(self, extra=None, null_segments: bool = True):
+        """build(node, R, S, in_array): pyarrow array of node's values for the instances (record
+        R[i], enclosing-array slot S[i]) -- groups -> structs (an inactive segment redefine -> null
+        struct when null_segments), OCCURS -> lists of the records' element counts.  extra(node, R)
+        may append (names, arrays) to a group's struct (hierarchical child segments)."""
         import pyarrow as pa
         plan = self.plan
         n = self.n_rec
@@ -242,11 +245,10 @@ class DecodedBatch:
             return counts[ci]
 
         seg_active = None
-        if plan.segment_column >= 0:
+        if plan.segment_column >= 0 and null_segments:
             seg_active = self.cols[plan.segment_column]["values"].cpu().numpy()[:n].astype(np.int64)
 
         def build(node, R, S, in_array):
-            """Array of node's values for instances (record R[i], enclosing-array slot S[i])."""
             if node.is_array and not in_array:
                 ai = plan.array_of_node[id(node)]
                 m = node.array_max_size
@@ -265,8 +267,12 @@ class DecodedBatch:
                     if isinstance(c, cbk.Group) or c.is_array or plan.field_of_node.get(id(c)) is not None:
                         names.append(c.name)
                         kids.append(build(c, R, S, False))
+                if extra is not None:
+                    xn, xa = extra(node, R)
+                    names += xn
+                    kids += xa
                 mask = None
-                if node.is_segment_redefine:
+                if node.is_segment_redefine and null_segments:
                     si = plan.segment_groups.index(node)
                     mask = pa.array(seg_active[R] != si if seg_active is not None else np.ones(len(R), bool))
                 return pa.StructArray.from_arrays(kids, names=names, mask=mask)
@@ -279,6 +285,18 @@ class DecodedBatch:
                 arr = arr.cast(pa.large_string() if pa.types.is_string_view(arr.type) else pa.large_binary())
             return arr.take(pa.array(S * n + R))
 
+        build.column = column
+        return build
+
+    def to_arrow(self):
+        """The batch as a pyarrow Table in the reference's Spark schema shape: groups -> structs
+        (an inactive segment redefine -> null struct), OCCURS -> lists of the records' element
+        counts (OCCURS DEPENDING ON), generated File_Id / Record_Id / Seg_IdN columns first."""
+        import pyarrow as pa
+        plan = self.plan
+        n = self.n_rec
+        build = self._arrow_builder()
+        column = build.column
         R0 = np.arange(n, dtype=np.int64)
         S0 = np.zeros(n, dtype=np.int64)
         names, arrays = [], []
@@ -301,54 +319,54 @@ class DecodedBatch:
                 arrays.append(st)
         return pa.Table.from_arrays(arrays, names=names)
 
-    def to_rows(self) -> List[dict]:
-        """Rebuild nested rows (RecordHandler.create + applyRecordPostProcessing)."""
+    def _host(self, ci: int) -> Dict[str, Any]:
+        cache = self.__dict__.setdefault("_host_cache", {})
+        if ci not in cache:
+            cache[ci] = self.host_column(ci)
+        return cache[ci]
+
+    def cell(self, ci: int, slot: int, r: int):
+        """The Python value of column ci, slot, record r (None when null)."""
+        c = self._host(ci)
+        info = self.plan.columns[ci]
+        if not c["validity"][slot, r]:
+            return None
+        v = slot * self.n_rec + r
+        ot = info.out_type
+        if ot in (N.O_STRING, N.O_BINARY) and "strings" in c:
+            b = c["strings"][slot][r]
+            return b.decode("utf-8") if ot == N.O_STRING else b
+        if ot in (N.O_STRING, N.O_BINARY):
+            off = c["offsets"][slot]
+            b = c["data"][int(off[r]):int(off[r + 1])]
+            return b.decode("utf-8") if ot == N.O_STRING else b
+        x = c["values"][v]
+        if ot == N.O_I32:
+            return int(np.int32(x))
+        if ot == N.O_I64:
+            return int(np.int64(x))
+        if ot == N.O_F32:
+            return np.uint32(x).view(np.float32)
+        if ot == N.O_F64:
+            return np.uint64(x).view(np.float64)
+        if ot == N.O_DEC64:
+            u = int(np.int64(x))
+        else:
+            u = (int(np.int64(x[1])) << 64) | int(np.uint64(x[0]))
+        return Decimal(u).scaleb(-info.stype[2], context=_CTX)
+
+    def _row_builder(self, extra=None, null_segments: bool = True):
+        """walk(group, r, idx): the dict RecordHandler.create builds for a group of record r
+        (idx: enclosing OCCURS indices).  extra(group, r) may add entries (hierarchical children)."""
         plan = self.plan
-        cache: Dict[int, Dict[str, Any]] = {}
-
-        def col(ci):
-            if ci not in cache:
-                cache[ci] = self.host_column(ci)
-            return cache[ci]
-
-        def value(ci: int, slot: int, r: int):
-            c = col(ci)
-            info = plan.columns[ci]
-            if not c["validity"][slot, r]:
-                return None
-            v = slot * self.n_rec + r
-            ot = info.out_type
-            if ot in (N.O_STRING, N.O_BINARY) and "strings" in c:
-                b = c["strings"][slot][r]
-                return b.decode("utf-8") if ot == N.O_STRING else b
-            if ot in (N.O_STRING, N.O_BINARY):
-                off = c["offsets"][slot]
-                b = c["data"][int(off[r]):int(off[r + 1])]
-                return b.decode("utf-8") if ot == N.O_STRING else b
-            x = c["values"][v]
-            if ot == N.O_I32:
-                return int(np.int32(x))
-            if ot == N.O_I64:
-                return int(np.int64(x))
-            if ot == N.O_F32:
-                return np.uint32(x).view(np.float32)
-            if ot == N.O_F64:
-                return np.uint64(x).view(np.float64)
-            if ot == N.O_DEC64:
-                u = int(np.int64(x))
-            else:
-                u = (int(np.int64(x[1])) << 64) | int(np.uint64(x[0]))
-            return Decimal(u).scaleb(-info.stype[2], context=_CTX)
-
-        seg_col = plan.segment_column
+        seg_col = plan.segment_column if null_segments else -1
 
         def walk(g: cbk.Group, r: int, idx: List[Tuple[int, int]]) -> dict:
             d = {}
             for c in g.children:
                 if c.is_array:
                     ai = plan.array_of_node[id(c)]
-                    cnt_col = col(plan.arrays[ai].count_column)
-                    cnt = int(np.int32(cnt_col["values"][r]))
+                    cnt = int(np.int32(self._host(plan.arrays[ai].count_column)["values"][r]))
                     vals = []
                     for i in range(cnt):
                         sub = idx + [(i, c.array_max_size)]
@@ -360,9 +378,9 @@ class DecodedBatch:
                 elif isinstance(c, cbk.Group):
                     if c.is_segment_redefine and seg_col >= 0:
                         si = plan.segment_groups.index(c)
-                        active = int(np.int32(col(seg_col)["values"][r]))
+                        active = int(np.int32(self._host(seg_col)["values"][r]))
                         val = walk(c, r, idx) if active == si else None
-                    elif c.is_segment_redefine:
+                    elif c.is_segment_redefine and null_segments:
                         val = None
                     else:
                         val = walk(c, r, idx)
@@ -370,6 +388,8 @@ class DecodedBatch:
                     val = prim(c, r, idx)
                 if not c.is_filler and not c.is_child_segment:
                     d[c.name] = val
+            if extra is not None:
+                d.update(extra(g, r))
             return d
 
         def prim(p: cbk.Primitive, r: int, idx):
@@ -379,17 +399,23 @@ class DecodedBatch:
             slot = 0
             for i, m in idx:
                 slot = slot * m + i
-            return value(plan.fields[fi].column, slot, r)
+            return self.cell(plan.fields[fi].column, slot, r)
 
+        return walk
+
+    def to_rows(self) -> List[dict]:
+        """Rebuild nested rows (RecordHandler.create + applyRecordPostProcessing)."""
+        plan = self.plan
+        walk = self._row_builder()
         rows = []
         for r in range(self.n_rec):
             recs = [(g.name, walk(g, r, [])) for g in plan.copybook.ast.children if isinstance(g, cbk.Group)]
             row: Dict[str, Any] = {}
             if self.generate_record_id:
-                row["File_Id"] = value(plan.file_id_column, 0, r)
-                row["Record_Id"] = value(plan.record_id_column, 0, r)
+                row["File_Id"] = self.cell(plan.file_id_column, 0, r)
+                row["Record_Id"] = self.cell(plan.record_id_column, 0, r)
             for lv, ci in enumerate(plan.seg_id_columns):
-                row[f"Seg_Id{lv}"] = value(ci, 0, r)
+                row[f"Seg_Id{lv}"] = self.cell(ci, 0, r)
             if self.collapse_root:
                 for _, v in recs:
                     row.update(v)
@@ -510,7 +536,7 @@ def parse_copybook_for(copybook_contents: str, params: ReaderParameters) -> cbk.
         floating_point_format=params.floating_point_format,
         is_utf16_big_endian=params.is_utf16_big_endian, ascii_charset=params.ascii_charset,
         non_terminals=params.non_terminals, occurs_handlers=params.occurs_mappings,
-        debug_fields_policy=params.debug_fields_policy)
+        debug_fields_policy=params.debug_fields_policy, field_parent_map=params.segment_redefine_parents)
 
 
 def reader_schema(cb: cbk.Copybook, params: ReaderParameters, variable_length: bool):
@@ -520,6 +546,139 @@ def reader_schema(cb: cbk.Copybook, params: ReaderParameters, variable_length: b
     levels = len(params.segment_id_levels) if (variable_length and params.segment_field) else 0
     return spark_schema(cb, params.schema_policy == "collapse_root",
                         params.generate_record_id and variable_length, seg_id_levels=levels)
+
+
+def hier_root_keys(cb: cbk.Copybook, params: ReaderParameters) -> List[str]:
+    """CopybookParser.getRootSegmentIds (:751-769): the ids mapped to the segment without a parent."""
+    roots = {g.name for g in cb.all_segment_redefines() if g.parent_segment is None}
+    return [sid for sid, grp in params.segment_id_redefine_map.items() if cbk._transform_identifier(grp) in roots]
+
+
+def check_hierarchical(cb: cbk.Copybook, params: ReaderParameters, plan: DecodePlan) -> None:
+    """What the GPU hierarchical path assumes (cobrix_hip.h cbx_hier_select); anything else is
+    reported, never decoded differently."""
+    if not params.segment_field or not params.segment_id_redefine_map:
+        raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records need segment_field and redefine-segment-id-map")
+    segs = plan.segment_groups
+    if len(segs) > 16:
+        raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: more than 16 segment redefines")
+    if params.start_offset != 0:
+        # extractChildren decodes child segments without the record start offset (:310), the root with it
+        raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records with record_start_offset")
+    ids: Dict[str, List[str]] = {}
+    for sid, grp in params.segment_id_redefine_map.items():
+        ids.setdefault(cbk._transform_identifier(grp), []).append(sid)
+    parents = {g.parent_segment.name for g in segs if g.parent_segment is not None}
+    for g in segs:
+        if g.name in parents and len(ids.get(g.name, [])) > 1:
+            # extractChildren stops a parent's children at a record with the parent's own id: with
+            # several ids per parent segment the lists depend on ids, not types (one record can then
+            # sit under several parents) -- not on the GPU path
+            raise N.CbxError(N.CBX_E_UNSUPPORTED, f"hierarchical records: segment {g.name} has children and "
+                                                  f"{len(ids[g.name])} segment ids")
+
+
+class HierBatch:
+    """Hierarchical records decoded on the GPU (cbx_hier_select + cbx_decode_selected): `flat` holds
+    one decoded row per table row -- table 0 the root records (one per hierarchical record), table
+    1 + s the records of segment s placed in the tree -- and `offsets[s]` the Arrow list offsets of
+    segment s's children over its parent table (cbx_hier_list_offsets)."""
+
+    def __init__(self, flat: DecodedBatch, table_rows: List[int], offsets: Dict[int, np.ndarray],
+                 collapse_root: bool, generate_record_id: bool):
+        self.flat, self.plan = flat, flat.plan
+        self.table_rows = table_rows
+        self.table_base = [int(x) for x in np.concatenate([[0], np.cumsum(table_rows)])]
+        self.offsets = offsets
+        self.collapse_root, self.generate_record_id = collapse_root, generate_record_id
+        self.n_rec = table_rows[0]
+        self.children = {id(g): [c for c in self.plan.segment_groups if c.parent_segment is g]
+                         for g in self.plan.segment_groups}
+
+    def _seg(self, g) -> int:
+        return self.plan.segment_groups.index(g)
+
+    def _parent_base(self, child) -> int:
+        """First row of the table the child's lists run over (roots for children of the root segment)."""
+        p = child.parent_segment
+        return 0 if p.parent_segment is None else self.table_base[1 + self._seg(p)]
+
+    def to_rows(self) -> List[dict]:
+        """getGroupValues + extractChildren + applyRecordPostProcessing (RecordExtractors.scala:298-451)."""
+        plan, flat = self.plan, self.flat
+
+        def extra(g, r):
+            d = {}
+            if not g.is_segment_redefine:
+                return d
+            for c in self.children[id(g)]:
+                s = self._seg(c)
+                off = self.offsets[s]
+                k = r - self._parent_base(c)
+                b = self.table_base[1 + s]
+                d[c.name] = [walk(c, b + j, []) for j in range(int(off[k]), int(off[k + 1]))]
+            return d
+
+        walk = flat._row_builder(extra=extra, null_segments=False)
+        rows = []
+        for r in range(self.n_rec):
+            recs = [(g.name, walk(g, r, [])) for g in plan.copybook.ast.children
+                    if isinstance(g, cbk.Group) and g.parent_segment is None]
+            row: Dict[str, Any] = {}
+            if self.generate_record_id:
+                row["File_Id"] = flat.cell(plan.file_id_column, 0, r)
+                row["Record_Id"] = flat.cell(plan.record_id_column, 0, r)
+            if self.collapse_root:
+                for _, v in recs:
+                    row.update(v)
+            else:
+                row.update({k: v for k, v in recs})
+            rows.append(row)
+        return rows
+
+    def to_arrow(self):
+        """The hierarchical records as a pyarrow Table: each segment's children a list<struct>
+        column inside its struct, built from the table rows and the GPU list offsets."""
+        import pyarrow as pa
+        plan, flat = self.plan, self.flat
+
+        def extra(g, R):
+            if not g.is_segment_redefine:
+                return [], []
+            names, arrays = [], []
+            for c in self.children[id(g)]:
+                s = self._seg(c)
+                off = self.offsets[s]
+                k = R - self._parent_base(c)
+                lo, hi = off[k], off[k + 1]
+                b = self.table_base[1 + s]
+                rows = np.concatenate([np.arange(b + x, b + y) for x, y in zip(lo, hi)]) if len(R) else np.zeros(0, np.int64)
+                child = build(c, rows.astype(np.int64), np.zeros(len(rows), np.int64), False)
+                offs = np.concatenate([[0], np.cumsum(hi - lo)]).astype(np.int32)
+                names.append(c.name)
+                arrays.append(pa.ListArray.from_arrays(pa.array(offs, pa.int32()), child))
+            return names, arrays
+
+        build = flat._arrow_builder(extra=extra, null_segments=False)
+        column = build.column
+        R0 = np.arange(self.n_rec, dtype=np.int64)
+        S0 = np.zeros(self.n_rec, dtype=np.int64)
+        names, arrays = [], []
+        if self.generate_record_id:
+            names += ["File_Id", "Record_Id"]
+            arrays += [column(plan.file_id_column).slice(0, self.n_rec), column(plan.record_id_column).slice(0, self.n_rec)]
+        for g in plan.copybook.ast.children:
+            if not isinstance(g, cbk.Group) or g.parent_segment is not None:
+                continue
+            st = build(g, R0, S0, False)
+            if self.collapse_root:
+                for k in range(st.type.num_fields):
+                    names.append(st.type.field(k).name)
+                    arrays.append(st.field(k))
+            else:
+                names.append(g.name)
+                arrays.append(st)
+        return pa.Table.from_arrays(arrays, names=names)
 
 
 class _BaseReader:
@@ -533,6 +692,8 @@ class _BaseReader:
         var = self.VARIABLE_LENGTH
         # the fixed-length reader only uses the redefine map (FixedLenNestedRowIterator.scala:50-70);
         # segment levels, filter and record ids belong to the variable-length iterator
+        self.hierarchical = var and self.copybook.is_hierarchical
+        root_keys = hier_root_keys(self.copybook, params) if self.hierarchical else ()
         self.plan = build_plan(self.copybook, segment_field=params.segment_field,
                                segment_redefine_map=params.segment_id_redefine_map or None,
                                generate_record_id=params.generate_record_id and var, window_bytes=params.window_bytes,
@@ -540,7 +701,9 @@ class _BaseReader:
                                segment_levels=params.segment_id_levels if var else (),
                                segment_filter=params.segment_id_filter if var else None,
                                segment_prefix=params.segment_id_prefix, string_views=params.string_views,
-                               occurs_lists=params.occurs_lists)
+                               occurs_lists=params.occurs_lists, root_keys=root_keys)
+        if self.hierarchical:
+            check_hierarchical(self.copybook, params, self.plan)
         self.native = NativePlan(self.plan)
 
     @property
@@ -710,7 +873,8 @@ class VarLenNestedReader(_BaseReader):
             prm.bytes_per_entry, prm.subtract_size = 100 * 1024 * 1024, 0   # Constants.defaultIndexEntrySizeMB
         prm.header_bytes = self.header_bytes()
         prm.has_file_header = int(self.has_file_header())
-        prm.hierarchical = int(bool(p.segment_field) and bool(p.segment_id_levels))
+        # segmentLevelIds.nonEmpty || fieldParentMap.nonEmpty (VarLenNestedReader.scala:151-155)
+        prm.hierarchical = int(bool(p.segment_field) and (bool(p.segment_id_levels) or self.hierarchical))
         prm.file_id = file_id
         return prm
 
@@ -824,11 +988,61 @@ class VarLenNestedReader(_BaseReader):
         off, ln = self.frame_fixed(t, n_bytes)
         return off, ln, n_bytes
 
+    def read_hierarchical(self, d_data, n_bytes: int, rec_off, rec_len, file_id: int = 0, first_record_id: int = 0,
+                          stream=None) -> HierBatch:
+        """VarLenHierarchicalIterator over framed records (GPU): cbx_hier_select -> cbx_decode_selected ->
+        cbx_hier_list_offsets per child segment.  Index entries are cut at root records, so reading the
+        whole stream at once gives the rows (and Record_Ids) of reading entry by entry."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream()
+        sp = ctypes.c_void_p(st.cuda_stream)
+        L = N.load()
+        n = int(rec_off.numel())
+        dev = d_data.device
+        segs = self.plan.segment_groups
+        prm = N.CbxHierParams()
+        prm.n_segments = len(segs)
+        prm.root_segment = next(i for i, g in enumerate(segs) if g.parent_segment is None)
+        for i in range(N.CBX_MAX_SEG_KEYS):
+            prm.parent[i] = -1
+        for i, g in enumerate(segs):
+            prm.parent[i] = segs.index(g.parent_segment) if g.parent_segment is not None else -1
+        prm.first_record_id = first_record_id
+        sel = {"rec_off": torch.empty(max(1, n), dtype=torch.int64, device=dev),
+               "rec_len": torch.empty(max(1, n), dtype=torch.int32, device=dev),
+               "record_id": torch.empty(max(1, n), dtype=torch.int64, device=dev),
+               "segment": torch.empty(max(1, n), dtype=torch.int32, device=dev)}
+        parent_row = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+        cs = N.CbxSelection()
+        for k in ("rec_off", "rec_len", "record_id", "segment"):
+            setattr(cs, k, sel[k].data_ptr())
+        cs.file_id = file_id
+        rows = (ctypes.c_int64 * (len(segs) + 1))()
+        n_rows = ctypes.c_int64(0)
+        N.check(L.cbx_hier_select(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(), rec_len.data_ptr(), n,
+                                  ctypes.byref(prm), ctypes.byref(cs), parent_row.data_ptr(), rows, ctypes.byref(n_rows), sp))
+        table_rows = [int(x) for x in rows]
+        sel["n"], sel["struct"] = n_rows.value, cs
+        flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
+        base = np.concatenate([[0], np.cumsum(table_rows)]).astype(np.int64)
+        offsets: Dict[int, np.ndarray] = {}
+        for s, g in enumerate(segs):
+            if g.parent_segment is None:
+                continue
+            ps = segs.index(g.parent_segment)
+            pb, pn = (0, table_rows[0]) if g.parent_segment.parent_segment is None else (int(base[1 + ps]), table_rows[1 + ps])
+            o = torch.empty(pn + 1, dtype=torch.int32, device=dev)
+            N.check(L.cbx_hier_list_offsets(parent_row.data_ptr(), int(base[1 + s]), table_rows[1 + s], pb, pn, o.data_ptr(), sp))
+            offsets[s] = o.cpu().numpy()
+        return HierBatch(flat, table_rows, offsets, self.collapse_root, self.params.generate_record_id)
+
     def read(self, data: bytes, file_id: int = 0) -> DecodedBatch:
         """A whole file, as the reference reads it: sparse-index entries (when index generation
         applies) each read by its own VarLenNestedIterator, concatenated in file order."""
         t = self._device_file(data)
         off, ln, vb = self.frame_file(t, len(data))
+        if self.hierarchical:
+            return self.read_hierarchical(t, vb, off, ln, file_id)
         entries = None
         if self.index_generation_needed() and not self.params.is_text:
             entries = self.generate_index(t, len(data), off, ln, file_id)

@@ -47,23 +47,30 @@ class SparkField:
     stype: Tuple[int, int, int] = (0, 0, 0)
 
 
-def _parse_group(g: Group) -> SparkField:
+def _parse_group(g: Group, redefines: List[Group]) -> SparkField:
+    """parseGroup (:116-139): child segments are skipped where they sit and appended, as arrays of
+    structs, to the group named as their parent (getChildSegments, :175-192)."""
     kids: List[SparkField] = []
     for c in g.children:
         if c.is_filler:
             continue
         if isinstance(c, Group):
             if c.parent_segment is None:
-                kids.append(_parse_group(c))
+                kids.append(_parse_group(c, redefines))
         else:
             kids.append(SparkField(c.name, "primitive", c, c.is_array, None, spark_type(c)))
+    for seg in redefines:
+        if seg.parent_segment is not None and seg.parent_segment.name.upper() == g.name.upper():
+            child = _parse_group(seg, redefines)
+            kids.append(SparkField(seg.name, "struct", seg, True, child.children))
     return SparkField(g.name, "struct", g, g.is_array, kids)
 
 
 def spark_schema(cb: Copybook, collapse_root: bool, generate_record_id: bool = False,
                  seg_id_levels: int = 0, input_file_name_field: str = "") -> List[SparkField]:
     """CobolSchema.createSparkSchema (SC/schema/CobolSchema.scala:77-113)."""
-    records = [_parse_group(r) for r in cb.ast.children if isinstance(r, Group)]
+    redefines = cb.all_segment_redefines()
+    records = [_parse_group(r, redefines) for r in cb.ast.children if isinstance(r, Group)]
     fields: List[SparkField] = []
     if collapse_root:
         for r in records:

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 7
+#define CBX_ABI_VERSION 8
 
 /* status codes */
 #define CBX_OK 0
@@ -148,7 +148,8 @@ typedef struct {
     int32_t key_len[CBX_MAX_SEG_KEYS];
     uint16_t key[CBX_MAX_SEG_KEYS][CBX_MAX_SEG_KEY_LEN];  /* UTF-16 code units */
     int32_t key_segment[CBX_MAX_SEG_KEYS];   /* redefine segment the key activates, -1 none */
-    int32_t key_level[CBX_MAX_SEG_KEYS];     /* first segment_id_level listing the key, -1 none */
+    int32_t key_level[CBX_MAX_SEG_KEYS];     /* first segment_id_level listing the key (0 also for a hierarchical
+                                                file's root ids: index cuts, no Seg_Id column), -1 none */
     int32_t key_in_filter[CBX_MAX_SEG_KEYS]; /* 1: listed in segment_filter */
     int32_t key_is_int[CBX_MAX_SEG_KEYS];    /* integral segment field: key is a canonical integer */
     int64_t key_int[CBX_MAX_SEG_KEYS];
@@ -362,6 +363,42 @@ int cbx_select_records(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, c
  * (SegmentIdAccumulator.getSegmentLevelId: prefix_fileId_rootRecordId[_L<level>_<counter>]). */
 int cbx_decode_selected(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const cbx_selection* sel,
                         int64_t n_rec, int32_t start_offset, cbx_column* columns, void* stream);
+
+/* ---- hierarchical records (`segment-children`) ----
+ *
+ * Replaces VarLenHierarchicalIterator + the structure walk of RecordExtractors.extractHierarchicalRecord
+ * (CP/reader/iterator/VarLenHierarchicalIterator.scala:43-162, RecordExtractors.scala:211-385): the
+ * framed records of a stream are grouped by root segment (records before the first root dropped) and
+ * each record is placed under its parent instance (extractChildren's rule, :298-322: the children of
+ * type C of a parent p are the C records after p up to the first record of p's segment or of one of
+ * its ancestors).  Requires one segment id per segment that has children (the host checks it; the
+ * reference's rule then depends on types only) and at most 16 segments.
+ *
+ * Output: one cbx_selection of rows in table order -- table 0 = the root records (one row per
+ * hierarchical record, Record_Id = first_record_id + the index of the next root record or n_rec,
+ * VarLenHierarchicalIterator.scala:107-133), then table 1 + s = the records of segment s placed in
+ * the tree, each table in record order (Record_Id = first_record_id + record index, unused by the
+ * reference).  parent_row[row] = the row of the record's parent instance (-1 for roots).  Decode
+ * the rows with cbx_decode_selected (segment = the record's own segment: its redefine decodes); the
+ * list of segment-C children of every parent row is a contiguous run of table 1 + C
+ * (cbx_hier_list_offsets).  table_rows (host, n_segments + 1 entries) receives the row count per
+ * table.  Output arrays need capacity n_rec. */
+typedef struct {
+    int32_t n_segments;               /* segment redefines (cbx_field.segment / key_segment indices) */
+    int32_t root_segment;             /* the segment without a parent */
+    int32_t parent[CBX_MAX_SEG_KEYS]; /* parent segment of each segment, -1 for the root */
+    int64_t first_record_id;          /* startRecordId of the stream (entry.record_index) */
+} cbx_hier_params;
+
+int cbx_hier_select(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                    const int32_t* d_rec_len, int64_t n_rec, const cbx_hier_params* params, cbx_selection* out,
+                    int64_t* d_parent_row, int64_t* table_rows, int64_t* n_rows, void* stream);
+
+/* Arrow list offsets (int32, n_parent + 1 entries) of one child table over its parent table:
+ * offsets[k] = rows of the child table [child_begin, child_begin + n_child) whose parent row is
+ * below parent_begin + k.  Asynchronous on `stream`. */
+int cbx_hier_list_offsets(const int64_t* d_parent_row, int64_t child_begin, int64_t n_child, int64_t parent_begin,
+                          int64_t n_parent, int32_t* d_offsets, void* stream);
 
 /* Text record framing (is_text = true) on the GPU: replaces TextRecordExtractor
  * (cobol-parser/.../reader/extractors/raw/TextRecordExtractor.scala:26-108, chosen by

@@ -904,7 +904,7 @@ static int extract_array(walk_ctx* c, int nid, int use_offset) {
 static int extract_value(walk_ctx* c, int nid, int use_offset) {
     const ora_node* f = &c->nodes[nid];
     if (f->kind == ORA_GROUP) {
-        if (f->is_segment_redefine && f->name_upper_id != c->active_seg) {
+        if (f->is_segment_redefine && c->active_seg != ORA_ALL_SEGMENTS && f->name_upper_id != c->active_seg) {
             ora_event* e = new_event(c);
             if (e) { e->node = nid; e->kind = ORA_EV_SEGNULL; e->slot = cur_slot(c); }
             return f->actual_size;

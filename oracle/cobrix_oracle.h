@@ -77,6 +77,9 @@ typedef struct {
 
 /* Decode one record (RecordExtractors.extractRecord). Returns 0 on success, <0 on error
  * (-1 event buffer full, -2 heap full, -3 non-integral dependee). */
+/* active_segment_upper_id = ORA_ALL_SEGMENTS: every segment redefine is decoded (no nulls) -- the
+ * hierarchical walk decodes each segment group from its own record (RecordExtractors.scala:298-322) */
+#define ORA_ALL_SEGMENTS (-3)
 int ora_extract_record(const ora_node* nodes, int32_t root, const ora_handler* handlers,
                        const ora_options* opt, const uint8_t* data, int32_t data_len,
                        int32_t offset_bytes, int32_t active_segment_upper_id, uint32_t rec,

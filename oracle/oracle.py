@@ -48,6 +48,7 @@ class OraOptions(ctypes.Structure):
 EVENT_DTYPE = np.dtype([("rec", "<u4"), ("node", "<i4"), ("kind", "<i4"), ("isnull", "<i4"),
                         ("slot", "<i4"), ("stype", "<i4"), ("lo", "<i8"), ("hi", "<i8")])
 EV_VALUE, EV_ARRAY, EV_SEGNULL = 1, 2, 3
+ORA_ALL_SEGMENTS = -3   # cobrix_oracle.h
 
 _TRIM = {"none": 1, "left": 2, "right": 3, "both": 4}
 _FP = {"IBM": 0, "IBM_LE": 1, "IEEE754": 2, "IEEE754_LE": 3}
@@ -247,13 +248,16 @@ def decode_fixed(cb: cbk.Copybook, data: bytes, record_size: Optional[int] = Non
 def decode_records(cb: cbk.Copybook, records: Sequence[bytes], start_offset: int = 0,
                    variable_size_occurs: bool = False, active_segments: Optional[Sequence[Optional[str]]] = None,
                    ast: Optional[OracleAst] = None) -> OracleResult:
-    """Decode a list of variable-length record payloads (VarLenNestedIterator.fetchNext)."""
+    """Decode a list of variable-length record payloads (VarLenNestedIterator.fetchNext).
+    active_segments: per record the active segment redefine (others decode to null), or "*" for
+    every segment redefine decoded (the hierarchical reader)."""
     ast = ast or OracleAst(cb)
     ast.opts.variable_size_occurs = int(variable_size_occurs)
     n_rec = len(records)
     ev_cap = max(1, n_rec * ast.max_events_per_record())
     ev = np.zeros(ev_cap, dtype=EVENT_DTYPE)
-    heap_cap = max(64, sum(len(r) for r in records) * 3 + 64 * n_rec + 64)
+    alts = 1 + (len(cb.all_segment_redefines()) if active_segments == "*" else 0)   # every alternative decodes
+    heap_cap = max(64, sum(len(r) for r in records) * 3 * alts + 64 * n_rec + 64)
     heap = np.zeros(heap_cap, dtype=np.uint8)
     n_ev = ctypes.c_int64(0)
     hl = ctypes.c_int64(0)
@@ -261,7 +265,9 @@ def decode_records(cb: cbk.Copybook, records: Sequence[bytes], start_offset: int
     for i, rec in enumerate(records):
         buf = np.frombuffer(rec, dtype=np.uint8) if len(rec) else np.zeros(1, np.uint8)
         act = -1
-        if active_segments is not None and active_segments[i]:
+        if active_segments == "*":
+            act = ORA_ALL_SEGMENTS
+        elif active_segments is not None and active_segments[i]:
             act = ast.names.get(active_segments[i].upper(), -2)
         r = L.ora_extract_record(ctypes.addressof(ast.nodes), 0, ctypes.addressof(ast.handlers),
                                  ctypes.addressof(ast.opts), _ptr(buf), len(rec), start_offset, act, i,

@@ -14,6 +14,9 @@ SC = spark-cobol/src/main/scala/za/co/absa/cobrix/spark/cobol/):
   * VarLenNestedIterator (filter, root-reached, redefine map, Record_Id)
                                               CP/reader/iterator/VarLenNestedIterator.scala:80-147
   * SegmentIdAccumulator (Seg_IdN)            CP/reader/iterator/SegmentIdAccumulator.scala:19-86
+  * VarLenHierarchicalIterator + extractHierarchicalRecord (segment-children)
+                                              CP/reader/iterator/VarLenHierarchicalIterator.scala:43-162,
+                                              CP/reader/extractors/record/RecordExtractors.scala:211-385
   * applyRecordPostProcessing                 CP/reader/extractors/record/RecordExtractors.scala:409-451
   * CobolScanners.buildScanForVarLenIndex     SC/source/scanners/CobolScanners.scala:38-55
 
@@ -179,8 +182,11 @@ def sparse_index(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
     if split_records is None and split_mb is not None and not (1 <= split_mb <= 2000):
         raise ValueError(f"Invalid input split size of {split_mb} MB.")
     seg_reader = FieldReader(cb, cb.get_field_by_name(p.segment_field)) if p.segment_field else None
-    is_hier = bool(p.segment_id_levels)   # segmentLevelIds.nonEmpty || fieldParentMap.nonEmpty
+    parents = getattr(p, "segment_redefine_parents", {}) or {}
+    is_hier = bool(p.segment_id_levels) or bool(parents)   # segmentLevelIds.nonEmpty || fieldParentMap.nonEmpty
     root_id = p.segment_id_levels[0] if p.segment_id_levels else ""
+    if parents and p.segment_id_redefine_map:   # VarLenNestedReader.getRootSegmentId (:298-309)
+        root_id = next(iter(root_segment_ids(cb, p)), "")
     root_ids = root_id.split(",")
     really_hier = seg_reader is not None and is_hier
     split_by_size = split_records is None and split_mb is not None
@@ -219,6 +225,13 @@ def sparse_index(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
         byte_index += record_size
         bytes_in_chunk += record_size
     return index
+
+
+def root_segment_ids(cb: cbk.Copybook, p) -> List[str]:
+    """CopybookParser.getRootSegmentIds (:751-769): ids mapped to a redefine without a parent."""
+    parents = getattr(p, "segment_redefine_parents", {}) or {}
+    roots = set(parents.values()) - set(parents)
+    return [sid for sid, grp in p.segment_id_redefine_map.items() if grp in roots]
 
 
 def index_generation_needed(p) -> bool:
@@ -307,9 +320,163 @@ def var_len_records(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
     return out
 
 
+def raw_records(cb: cbk.Copybook, data: bytes, p, e: Entry) -> List[Tuple[str, bytes]]:
+    """VRLRecordReader over one entry's bounded stream: (segment id, payload) of every valid record."""
+    rp = header_parser(cb, p)
+    seg_reader = FieldReader(cb, cb.get_field_by_name(p.segment_field)) if p.segment_field else None
+    n_bytes = e.offset_to - e.offset_from if e.offset_to > 0 else 0
+    s = Stream(data, e.offset_from, n_bytes)
+    out = []
+    while True:
+        valid, eof, rec = False, False, b""
+        while not valid and not eof:
+            hdr = s.next(rp.header_length)
+            n, valid = rp.metadata(hdr, s.offset, s.size)
+            if n > 0:
+                rec = s.next(n)
+            else:
+                eof = True
+        if eof:
+            return out
+        out.append((_trim(seg_reader.segment_id(rec, p.start_offset)) if seg_reader else "", rec))
+
+
+def _full_record(res, r_events_pos: int, groups: Dict[int, Any]):
+    """Walk one record's event stream like O.rows, keeping every group's dict -- child segments
+    included -- keyed by id(group) (the values getGroupValues reads)."""
+    ast = res.ast
+    ev = res.events
+    heap = res.heap
+    pos = r_events_pos
+
+    def dec_value(st, e):
+        v = O.event_value(e, heap)
+        if v is not None and int(e["stype"]) == ST_DECIMAL:
+            v = PyDecimal(v).scaleb(-spark_type(st)[2])
+        return v
+
+    def walk(g) -> dict:
+        nonlocal pos
+        d = {}
+        for c in g.children:
+            if c.is_array:
+                cnt = int(ev[pos]["lo"])
+                pos += 1
+                vals = []
+                for _ in range(cnt):
+                    if isinstance(c, cbk.Group):
+                        vals.append(walk(c))
+                    else:
+                        vals.append(dec_value(c, ev[pos]))
+                        pos += 1
+                val: Any = vals
+            elif isinstance(c, cbk.Group):
+                val = walk(c)
+                groups[id(c)] = val
+            else:
+                val = dec_value(c, ev[pos])
+                pos += 1
+            if not c.is_filler:
+                d[c.name] = val
+        return d
+
+    tops = []
+    for g in ast.cb.ast.children:
+        v = walk(g)
+        groups[id(g)] = v
+        tops.append((g, v))
+    return pos, tops
+
+
+def hier_rows(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
+              entries: Optional[List[Entry]] = None) -> List[dict]:
+    """VarLenHierarchicalIterator (:83-160) per index entry + extractHierarchicalRecord (:211-385)
+    + applyRecordPostProcessing.  Every record is decoded whole (no segment-redefine nulls: the
+    hierarchical walk decodes each segment from its own record at the segment's offset)."""
+    if entries is None:
+        entries = sparse_index(cb, data, p, file_id) if index_generation_needed(p) else [Entry(0, -1, file_id, 0)]
+    red = p.segment_id_redefine_map
+    roots = set(root_segment_ids(cb, p))
+    redefines = cb.all_segment_redefines()
+    children = {g.name: [c for c in redefines if c.parent_segment is not None and c.parent_segment.name == g.name]
+                for g in redefines}
+    out: List[dict] = []
+    for e in entries:
+        raw = raw_records(cb, data, p, e)
+        res = O.decode_records(cb, [r for _, r in raw], start_offset=p.start_offset, active_segments="*")
+        pos = 0
+        decoded = []   # per record: {id(group): dict}
+        tops_of = []
+        for _ in raw:
+            gm: Dict[int, Any] = {}
+            pos, tops = _full_record(res, pos, gm)
+            decoded.append(gm)
+            tops_of.append(tops)
+
+        def group_values(group, vals: dict, seg_idx: List[int], cur: int, parent_ids: List[str]) -> dict:
+            d = {}
+            for c in group.children:
+                if c.is_filler or c.is_child_segment:
+                    continue
+                v = vals[c.name]
+                if isinstance(c, cbk.Group):
+                    v = [group_values(c, x, seg_idx, cur, parent_ids) for x in v] if c.is_array else \
+                        group_values(c, v, seg_idx, cur, parent_ids)
+                d[c.name] = v
+            if group.is_segment_redefine:
+                for ch in children[group.name]:
+                    d[ch.name] = extract_children(ch, seg_idx, cur + 1, parent_ids)
+            return d
+
+        def extract_children(field, seg_idx: List[int], cur: int, parent_ids: List[str]) -> list:
+            kids = []
+            i = cur
+            while i < len(seg_idx):
+                sid = raw[seg_idx[i]][0]
+                if red.get(sid, "") == field.name:
+                    kids.append(group_values(field, decoded[seg_idx[i]][id(field)], seg_idx, i, [sid] + parent_ids))
+                elif sid in parent_ids:
+                    break
+                i += 1
+            return kids
+
+        def emit(seg_idx: List[int], record_id: int):
+            r0 = seg_idx[0]
+            recs = [(g, group_values(g, v, seg_idx, 0, [raw[r0][0]])) for g, v in tops_of[r0]
+                    if isinstance(g, cbk.Group) and g.parent_segment is None]
+            row: Dict[str, Any] = {}
+            if p.generate_record_id:
+                row["File_Id"] = e.file_id
+                row["Record_Id"] = record_id
+            if p.schema_policy == "collapse_root":
+                for _, v in recs:
+                    row.update(v)
+            else:
+                row.update({g.name: v for g, v in recs})
+            out.append(row)
+
+        record_index = e.record_index
+        fetched: List[int] = []
+        for i, (sid, _) in enumerate(raw):
+            if sid in roots:
+                if fetched:
+                    emit(fetched, record_index)
+                    fetched = []
+                fetched.append(i)
+            elif fetched:
+                fetched.append(i)
+            record_index += 1
+        if fetched:
+            emit(fetched, record_index)
+    return out
+
+
 def var_len_rows(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
                  entries: Optional[List[Entry]] = None) -> List[dict]:
-    """Rows of a variable-length read (extractRecord + applyRecordPostProcessing)."""
+    """Rows of a variable-length read (extractRecord + applyRecordPostProcessing); hierarchical
+    copybooks go through VarLenHierarchicalIterator (SC/reader/VarLenNestedReader.scala:55-81)."""
+    if cb.is_hierarchical:
+        return hier_rows(cb, data, p, file_id, entries)
     recs = var_len_records(cb, data, p, file_id, entries)
     res = O.decode_records(cb, [r.payload for r in recs], start_offset=p.start_offset,
                            active_segments=[r.active_segment for r in recs] if p.segment_id_redefine_map else None)

@@ -194,6 +194,44 @@ CASES: Dict[str, Dict[str, Any]] = {
                              "redefine-segment-id-map:7": "CONTRACT => 7"},
                     expected="test17_expected/test17b.txt", schema="test17_expected/test17b_schema.json",
                     sort=("File_Id", "Record_Id"), take=300),
+    **{name: dict(spec="SCT/source/integration/Test17HierarchicalSpec.scala:118-193",
+                  copybook="test17_hierarchical.cob", data="test17/HIERARCHICAL.DATA.RDW.dat",
+                  options={"pedantic": "true", "is_record_sequence": "true", "generate_record_id": "true",
+                           "schema_retention_policy": "collapse_root", "segment_field": "SEGMENT_ID",
+                           "redefine_segment_id_map:1": "COMPANY => 1", "redefine-segment-id-map:2": "DEPT => 2",
+                           "redefine-segment-id-map:3": "EMPLOYEE => 3", "redefine-segment-id-map:4": "OFFICE => 4",
+                           "redefine-segment-id-map:5": "CUSTOMER => 5", "redefine-segment-id-map:6": "CONTACT => 6",
+                           "redefine-segment-id-map:7": "CONTRACT => 7",
+                           "segment-children:1": "COMPANY => DEPT,CUSTOMER",
+                           "segment-children:2": "DEPT => EMPLOYEE,OFFICE",
+                           "segment-children:3": "CUSTOMER => CONTACT,CONTRACT", **extra},
+                  expected="test17_expected/test17c.txt", schema="test17_expected/test17c_schema.json",
+                  sort=("File_Id", "Record_Id"), take=60, count=50)
+       for name, extra in (("test17c", {}), ("test17c_split", {"input_split_records": "5"}))},
+    **{name: dict(spec="SCT/source/integration/Test17HierarchicalSpec.scala:196-262",
+                  copybook="test4_copybook.cob", data="test4_data/COMP.DETAILS.SEP30.DATA.dat",
+                  options={"encoding": "ascii", "is_record_sequence": "true", "segment_field": "SEGMENT_ID",
+                           "redefine_segment_id_map:1": "STATIC-DETAILS => C", "redefine-segment-id-map:2": "CONTACTS => P",
+                           "segment-children:1": "STATIC-DETAILS => CONTACTS", "generate_record_id": "true",
+                           "schema_retention_policy": "collapse_root", **extra},
+                  expected="test17_expected/test17d.txt", schema="test17_expected/test17d_schema.json",
+                  sort=("File_Id", "Record_Id"), take=60)
+       for name, extra in (("test17d", {}), ("test17d_split", {"input_split_records": "5"}))},
+    "test17e": dict(spec="SCT/source/integration/Test17HierarchicalSpec.scala:264-290",
+                    copybook="test4_copybook.cob", data="test4_data/COMP.DETAILS.SEP30.DATA.dat",
+                    options={"encoding": "ascii", "is_record_sequence": "true", "segment_field": "SEGMENT_ID",
+                             "redefine_segment_id_map:1": "STATIC-DETAILS => C", "redefine-segment-id-map:2": "CONTACTS => P",
+                             "segment-children:1": "STATIC-DETAILS => CONTACTS"},
+                    expected="test17_expected/test17e.txt", schema="test17_expected/test17e_schema.json",
+                    sort=("COMPANY_DETAILS.COMPANY_ID",), take=60),
+    "test17f": dict(spec="SCT/source/integration/Test17HierarchicalSpec.scala:292-321",
+                    copybook="test4_copybook.cob", data="test4_data/COMP.DETAILS.SEP30.DATA.dat",
+                    options={"encoding": "ascii", "is_record_sequence": "true", "segment_field": "SEGMENT_ID",
+                             "redefine_segment_id_map:1": "STATIC-DETAILS => C", "redefine-segment-id-map:2": "CONTACTS => P",
+                             "segment-children:1": "STATIC-DETAILS => CONTACTS", "generate_record_id": "true",
+                             "schema_retention_policy": "collapse_root", "debug": "true"},
+                    expected="test17_expected/test17f.txt", schema="test17_expected/test17f_schema.json",
+                    sort=("File_Id", "Record_Id"), take=60),
     "test19": dict(spec="SCT/source/integration/Test19DisplayNumParsingSpec.scala:32-75",
                    copybook="test19_display_num.cob", data="test19_display_num/data.dat",
                    options={"pedantic": "true", "generate_record_id": "true", "schema_retention_policy": "collapse_root"},
@@ -239,10 +277,12 @@ def load_json_values(path: str) -> List[Any]:
 
 
 def _sort_key(row: dict, cols) -> tuple:
-    """Spark orderBy ascending: nulls first."""
+    """Spark orderBy ascending: nulls first; a dotted column is a struct field."""
     key = []
     for c in cols:
-        v = row.get(c)
+        v: Any = row
+        for part in c.split("."):
+            v = v.get(part) if isinstance(v, dict) else None
         key.append((0, 0) if v is None else (1, v))
     return tuple(key)
 
@@ -270,5 +310,7 @@ def expected_rows(case) -> List[Any]:
 
 
 def compare(case, rows: List[dict]) -> List[str]:
+    if "count" in case and len(rows) != case["count"]:   # df.count asserted by the spec
+        return [f"{len(rows)} rows, the spec asserts {case['count']}"]
     rows = spark_order(rows, case.get("sort"))[: case.get("take", len(rows))]
     return G.compare_rows(rows, expected_rows(case), na_fill=case.get("na_fill", False))

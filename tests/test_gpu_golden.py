@@ -171,7 +171,7 @@ def _norm(v):
 
 
 @pytest.mark.parametrize("views", [False, True])
-@pytest.mark.parametrize("name", ["test1", "test5", "test6", "test9_cp037", "test19", "test17a"])
+@pytest.mark.parametrize("name", ["test1", "test5", "test6", "test9_cp037", "test19", "test17a", "test17c", "test17d", "test17e", "test17f"])
 def test_gpu_arrow_export_matches_rows(name, views):
     _arrow_vs_rows(name, views)
 

@@ -1,0 +1,147 @@
+"""Hierarchical records (`segment-children`, VarLenHierarchicalIterator + extractHierarchicalRecord)
+through the HIP path (cbx_hier_select / cbx_decode_selected / cbx_hier_list_offsets) against the
+oracle's literal restatement (oracle/reader_oracle.py hier_rows), on synthetic streams that break
+every rule of the tree walk: children before the first root, grandchildren whose parent is missing,
+siblings interleaved with cousins, unknown segment ids, short records.  The reference's own
+hierarchical goldens (test17c-f) run in test_gpu_golden.py.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+import goldens as G  # noqa: E402
+
+from oracle import reader_oracle as RO  # noqa: E402
+
+OPTS = {"is_record_sequence": "true", "generate_record_id": "true", "schema_retention_policy": "collapse_root",
+        "segment_field": "SEGMENT_ID",
+        "redefine_segment_id_map:1": "COMPANY => 1", "redefine-segment-id-map:2": "DEPT => 2",
+        "redefine-segment-id-map:3": "EMPLOYEE => 3", "redefine-segment-id-map:4": "OFFICE => 4",
+        "redefine-segment-id-map:5": "CUSTOMER => 5", "redefine-segment-id-map:6": "CONTACT => 6",
+        "redefine-segment-id-map:7": "CONTRACT => 7",
+        "segment-children:1": "COMPANY => DEPT,CUSTOMER", "segment-children:2": "DEPT => EMPLOYEE,OFFICE",
+        "segment-children:3": "CUSTOMER => CONTACT,CONTRACT"}
+
+_EBCDIC_TEXT = bytes([0x40] * 4) + bytes(range(0xC1, 0xCA)) + bytes(range(0xD1, 0xDA)) + bytes(range(0xF0, 0xFA))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def hier_stream(n: int, seed: int, tree_like: float = 0.8) -> bytes:
+    """n RDW records of the test17 layout: mostly tree-ordered segments (company, departments with
+    employees / offices, customers with contacts / contracts), with a share of random ids (0-9,
+    incl. ids no redefine maps) and lengths from 1 byte to the full record."""
+    rnd = random.Random(seed)
+    seq = []
+    while len(seq) < n:
+        if rnd.random() < tree_like:
+            seq.append(1)
+            for _ in range(rnd.randint(0, 3)):
+                if rnd.random() < 0.5:
+                    seq.append(2)
+                    seq += [rnd.choice((3, 4)) for _ in range(rnd.randint(0, 4))]
+                else:
+                    seq.append(5)
+                    seq += [rnd.choice((6, 7)) for _ in range(rnd.randint(0, 4))]
+        else:
+            seq += [rnd.randint(0, 9) for _ in range(rnd.randint(1, 6))]
+    out = bytearray()
+    for sid in seq[:n]:
+        ln = 108 if rnd.random() < 0.8 else rnd.randint(1, 108)
+        body = bytes([0xF0 + sid]) + bytes(rnd.choice(_EBCDIC_TEXT) if rnd.random() < 0.9 else rnd.randrange(256)
+                                            for _ in range(ln - 1))
+        out += bytes([0, 0, ln & 0xFF, ln >> 8]) + body[:ln]
+    return bytes(out)
+
+
+def _reader(extra=None, **params):
+    import dataclasses
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import VarLenNestedReader
+    p, var_len = parse_options({**OPTS, **(extra or {})})
+    assert var_len
+    p = dataclasses.replace(p, **params)
+    return VarLenNestedReader(G.read("test17_hierarchical.cob").decode("latin-1"), p), p
+
+
+@pytest.mark.parametrize("seed,n,tree_like", [(1, 200, 1.0), (2, 3000, 0.8), (3, 3000, 0.3), (4, 20000, 0.9)])
+@pytest.mark.parametrize("views", [False, True])
+def test_hier_synthetic_vs_oracle(seed, n, tree_like, views):
+    raw = hier_stream(n, seed, tree_like)
+    for jit in (-1, 1):
+        rd, p = _reader(string_views=views, jit_min_records=jit)
+        rows = rd.read(raw, file_id=4).to_rows()
+        exp = RO.var_len_rows(rd.copybook, raw, p, file_id=4)
+        assert len(rows) == len(exp)
+        bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
+        assert not bad, (jit, bad[:5], rows[bad[0]], exp[bad[0]])
+
+
+def test_hier_entries_cut_at_roots():
+    """With input_split_records the reference reads each index entry (cut at root records) with its
+    own iterator; the GPU reads the stream once -- same rows, same Record_Ids."""
+    raw = hier_stream(5000, 7, 0.7)
+    rd, p = _reader({"input_split_records": "37"})
+    t = rd._device_file(raw)
+    off, ln, _ = rd.frame_file(t, len(raw))
+    ents = rd.generate_index(t, len(raw), off, ln)
+    exp_ents = RO.sparse_index(rd.copybook, raw, p)
+    assert [(e.offset_from, e.offset_to, e.record_index) for e in ents] == \
+        [(e.offset_from, e.offset_to, e.record_index) for e in exp_ents]
+    assert len(ents) > 10
+    rows = rd.read(raw).to_rows()
+    assert rows == RO.var_len_rows(rd.copybook, raw, p)
+
+
+def test_hier_arrow_matches_rows():
+    pytest.importorskip("pyarrow")
+    raw = hier_stream(3000, 9, 0.8)
+    rd, _ = _reader(string_views=True)
+    batch = rd.read(raw)
+    table = batch.to_arrow()
+    table.validate(full=True)
+    assert table.num_rows == len(batch.to_rows())
+    from test_gpu_golden import _norm
+    assert _norm(table.to_pylist()) == _norm(batch.to_rows())
+
+
+def test_hier_empty_and_rootless():
+    rd, p = _reader()
+    assert rd.read(b"").to_rows() == []
+    recs = bytearray()   # no root record: every record is dropped
+    for sid in (2, 3, 5, 6, 9, 0):
+        recs += bytes([0, 0, 10, 0]) + bytes([0xF0 + sid]) + b"\x40" * 9
+    assert rd.read(bytes(recs)).to_rows() == RO.var_len_rows(rd.copybook, bytes(recs), p) == []
+
+
+def test_hier_unsupported_layouts():
+    from cobrix_amd import native as N
+    with pytest.raises(N.CbxError):   # a parent segment with two ids
+        _reader({"redefine-segment-id-map:2": "DEPT => 2,8"})
+    with pytest.raises(N.CbxError):
+        _reader({"record_start_offset": "2"})
+
+
+def test_hier_record_id_is_next_root():
+    """Record_Id of a hierarchical record = the index of the next root record (or the record count
+    for the last one): VarLenHierarchicalIterator.scala:107-133."""
+    recs = bytearray()
+    for sid in (3, 1, 2, 3, 1, 5, 1):
+        recs += bytes([0, 0, 20, 0]) + bytes([0xF0 + sid]) + b"\xC1" * 19
+    rd, p = _reader()
+    rows = rd.read(bytes(recs)).to_rows()
+    assert [r["Record_Id"] for r in rows] == [4, 6, 7]
+    assert rows == RO.var_len_rows(rd.copybook, bytes(recs), p)
+    assert [len(r["COMPANY"]["DEPT"]) for r in rows] == [1, 0, 0]
+    assert len(rows[0]["COMPANY"]["DEPT"][0]["EMPLOYEE"]) == 1

@@ -12,13 +12,14 @@ def main():
     ap.add_argument("--records", type=int, default=5_000_000)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--window", type=int, default=0)
+    ap.add_argument("--offsets", action="store_true", help="large-string layout instead of string views (bench default)")
     a = ap.parse_args()
     import torch
     from cobrix_amd import native as N
     from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters, _alloc_columns, string_capacity
     from cobrix_amd.synth import SYN200_COPYBOOK, syn200
     rec = syn200(a.records, device="cuda").view(-1)
-    rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters(window_bytes=a.window))
+    rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters(window_bytes=a.window, string_views=not a.offsets, occurs_lists=True))
     L = N.load()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     cols, cs = _alloc_columns(rd.plan, a.records, string_capacity(rd.native, a.records), rec.device)
