@@ -23,6 +23,7 @@
 #include "cbx_select.h"
 #include "cbx_text.h"
 #include "cbx_hier.h"
+#include "cbx_walk.h"
 
 using namespace cbx;
 
@@ -115,6 +116,17 @@ struct cbx_plan {
     int last_kind = 0;
     int32_t* d_status = nullptr;
     int num_cus = 256;
+    // record walk (cbx_plan_set_walk, cbx_walk.h)
+    bool walk = false;
+    int32_t walk_root = 0, walk_var = 0, walk_n_handlers = 0;
+    cbx_walk_node* d_wnodes = nullptr;
+    cbx_walk_array* d_warr = nullptr;
+    cbx_walk_handler* d_whand = nullptr;
+    int64_t* d_wslot_base = nullptr;    // per column: first string-slot index
+    int64_t* d_wtile_bytes = nullptr;   // per column: view tile bytes
+    int64_t n_str_slots = 0;
+    uint32_t* d_wcursor = nullptr; int64_t wcursor_cap = 0;
+    int32_t fid_col = -1, rid_col = -1;
     // profiling: HIP events around the decode kernel and the post passes of every call (no sync)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;     // free events
@@ -532,6 +544,8 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
     (void)hipFree(P->d_seqcall); (void)hipFree(P->d_str_tot); (void)hipFree(P->d_str_excl); (void)hipFree(P->d_block_sums);
     (void)hipFree(P->d_local); (void)hipFree(P->d_scratch); (void)hipFree(P->d_status); (void)hipFree(P->d_stamps);
     (void)hipFree(P->d_lops); (void)hipFree(P->d_list_len); (void)hipFree(P->d_list_flag);
+    (void)hipFree(P->d_wnodes); (void)hipFree(P->d_warr); (void)hipFree(P->d_whand); (void)hipFree(P->d_wslot_base);
+    (void)hipFree(P->d_wtile_bytes); (void)hipFree(P->d_wcursor);
     for (auto& e : P->ev_pool) (void)hipEventDestroy(e);
     for (auto& c : P->ev_calls) for (auto& e : c.e) if (e) (void)hipEventDestroy(e);
     delete P;
@@ -884,6 +898,48 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     return CBX_OK;
 }
 
+// The record walk (cbx_walk.h): one lane per record, data-dependent offsets.
+static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hipStream_t st) {
+    const int64_t n_tiles = (c.n_rec + kWave - 1) / kWave;
+    for (int i = 0; i < P->n_columns; i++) {
+        if (!P->col_is_string[i] || c.n_rec == 0) continue;
+        const int64_t need = n_tiles * view_tile_bytes(P, i);
+        if (!columns[i].values || !columns[i].data || columns[i].data_capacity < need)
+            return fail(CBX_E_CAPACITY, "column " + std::to_string(i) + ": string-view buffers of cbx_string_bound required");
+    }
+    if (c.n_rec == 0) return CBX_OK;
+    P->h_cols.resize(P->n_columns);
+    for (int i = 0; i < P->n_columns; i++) {
+        DevColumn d{};
+        d.values = columns[i].values; d.validity = columns[i].validity; d.offsets = columns[i].offsets;
+        d.data = columns[i].data; d.capacity = columns[i].data_capacity; d.sizes = columns[i].data_sizes;
+        P->h_cols[i] = d;
+    }
+    HIP_CHECK(hipMemcpyAsync(P->d_cols, P->h_cols.data(), sizeof(DevColumn) * P->n_columns, hipMemcpyHostToDevice, st));
+    int r;
+    const int64_t nc = std::max<int64_t>(1, P->n_str_slots * n_tiles);
+    if ((r = grow(&P->d_wcursor, &P->wcursor_cap, nc, st))) return r;
+    HIP_CHECK(hipMemsetAsync(P->d_wcursor, 0, sizeof(uint32_t) * nc, st));
+    WalkArgs a{};
+    a.data = c.data; a.data_len = c.data_len; a.rec_off = c.rec_off; a.rec_len = c.rec_len; a.n_rec = c.n_rec;
+    a.stride = c.stride; a.start_off = c.start_off; a.first_record_id = c.first_record_id;
+    a.rec_id = c.rec_id; a.rec_seg = c.rec_seg; a.file_id = c.file_id >= 0 ? c.file_id : P->opts.file_id;
+    a.var_occurs = P->walk_var; a.n_tiles = n_tiles; a.pitch = n_tiles * kWave;
+    a.nodes = (const CBX_CONST cbx_walk_node*)P->d_wnodes; a.root = P->walk_root;
+    a.warr = (const CBX_CONST cbx_walk_array*)P->d_warr;
+    a.handlers = (const CBX_CONST cbx_walk_handler*)P->d_whand; a.n_handlers = P->walk_n_handlers;
+    a.arrays = (const CBX_CONST cbx_array*)P->d_arrays; a.fields = (const CBX_CONST Field*)P->d_fields;
+    a.cols = (const CBX_CONST DevColumn*)P->d_cols;
+    a.segmap = P->opts.has_segments ? (const CBX_CONST cbx_segment_map*)P->d_segmap : nullptr;
+    a.lut = P->d_lut; a.seg_col = P->seg_col; a.fid_col = P->fid_col; a.rid_col = P->rid_col;
+    a.str_slot_base = P->d_wslot_base; a.cursors = P->d_wcursor; a.tile_bytes = P->d_wtile_bytes; a.status = P->d_status;
+    const int64_t grid = std::min<int64_t>((c.n_rec + 255) / 256, (int64_t)P->num_cus * 8);
+    hipLaunchKernelGGL(walk_kernel, dim3((unsigned)grid), dim3(256), 0, st, a);
+    HIP_CHECK(hipGetLastError());
+    P->last_kind = 2;
+    return CBX_OK;
+}
+
 static int decode_common(cbx_plan* P, const CallShape& c, cbx_column* columns, int64_t* sizes_only, hipStream_t st) {
     if (!P || !c.data || c.n_rec < 0 || c.start_off < 0) return fail(CBX_E_ARGUMENT, "invalid decode arguments");
     if (!sizes_only && !columns) return fail(CBX_E_ARGUMENT, "columns required");
@@ -909,6 +965,7 @@ static int decode_common(cbx_plan* P, const CallShape& c, cbx_column* columns, i
         }
         return CBX_OK;
     }
+    if (P->walk) return walk_launch(P, c, columns, st);
     for (int i = 0; i < P->n_columns; i++) {
         if (!P->col_is_string[i] || c.n_rec == 0) continue;
         if (P->view) {
@@ -1671,5 +1728,87 @@ extern "C" int cbx_hier_list_offsets(const int64_t* d_parent_row, int64_t child_
     hipLaunchKernelGGL(hier_offsets_kernel, dim3(blocks_for(n_parent + 1, 256)), dim3(256), 0, (hipStream_t)stream,
                        d_parent_row, child_begin, n_child, parent_begin, n_parent, d_offsets);
     HIP_CHECK(hipGetLastError());
+    return CBX_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The record walk: node tables (cbx_plan_set_walk) and VarOccursRecordExtractor framing.
+// ---------------------------------------------------------------------------------------------
+extern "C" int cbx_plan_set_walk(cbx_plan* P, const cbx_walk_node* nodes, int32_t n_nodes, int32_t root,
+                                 const cbx_walk_array* arrays, const cbx_walk_handler* handlers, int32_t n_handlers,
+                                 int32_t variable_size_occurs) {
+    if (!P || !nodes || n_nodes <= 0 || root < 0 || root >= n_nodes || n_handlers < 0 || (n_handlers > 0 && !handlers) ||
+        (!P->harrays.empty() && !arrays))
+        return fail(CBX_E_ARGUMENT, "cbx_plan_set_walk: invalid arguments");
+    const int nf = (int)P->dfields_h.size(), na = (int)P->harrays.size();
+    for (int i = 0; i < n_nodes; i++) {
+        const cbx_walk_node& n = nodes[i];
+        if ((n.kind != CBX_W_GROUP && n.kind != CBX_W_PRIM) || n.next >= n_nodes || n.child >= n_nodes || n.field >= nf ||
+            n.array >= na || n.dep_slot >= kWalkDeps || (n.kind == CBX_W_PRIM && n.data_size <= 0))
+            return fail(CBX_E_ARGUMENT, "cbx_plan_set_walk: bad node " + std::to_string(i));
+    }
+    for (int i = 0; i < na; i++)
+        if (arrays[i].dep_slot >= kWalkDeps || arrays[i].h_begin < 0 || arrays[i].h_end > n_handlers || arrays[i].h_begin > arrays[i].h_end)
+            return fail(CBX_E_ARGUMENT, "cbx_plan_set_walk: bad array " + std::to_string(i));
+    for (int i = 0; i < n_handlers; i++)
+        if (handlers[i].key_len < 0 || handlers[i].key_len > 64) return fail(CBX_E_ARGUMENT, "cbx_plan_set_walk: bad handler");
+    if (P->walk) return fail(CBX_E_STATE, "cbx_plan_set_walk: the plan already walks");
+    std::vector<int64_t> slot_base(P->n_columns, 0), tile_bytes(P->n_columns, 0);
+    int64_t ns = 0;
+    for (int c = 0; c < P->n_columns; c++) {
+        if (!P->col_is_string[c]) continue;
+        if (!P->view) return fail(CBX_E_UNSUPPORTED, "cbx_plan_set_walk: string columns need the string-view layout");
+        slot_base[c] = ns;
+        ns += P->col_slots[c];
+        tile_bytes[c] = view_tile_bytes(P, c);
+    }
+    int r;
+    if ((r = upload(&P->d_wnodes, nodes, n_nodes)) || (r = upload(&P->d_warr, arrays, na)) ||
+        (r = upload(&P->d_whand, handlers, n_handlers)) || (r = upload(&P->d_wslot_base, slot_base.data(), slot_base.size())) ||
+        (r = upload(&P->d_wtile_bytes, tile_bytes.data(), tile_bytes.size())))
+        return r;
+    for (const Field& d : P->dfields_h) {
+        if (d.variant == V_FILE_ID) P->fid_col = d.column;
+        if (d.variant == V_RECORD_ID) P->rid_col = d.column;
+    }
+    P->n_str_slots = ns;
+    P->walk_root = root;
+    P->walk_var = variable_size_occurs != 0;
+    P->walk_n_handlers = n_handlers;
+    P->walk = true;
+    return CBX_OK;
+}
+
+extern "C" int cbx_frame_var_occurs(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, int64_t first_offset,
+                                    int64_t* d_rec_off, int32_t* d_rec_len, int64_t capacity, int64_t* n_records,
+                                    int64_t* virtual_bytes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!P || !n_records || !virtual_bytes || n_bytes < 0 || first_offset < 0 || capacity < 0 ||
+        (n_bytes > 0 && !d_data) || (capacity > 0 && (!d_rec_off || !d_rec_len)))
+        return fail(CBX_E_ARGUMENT, "cbx_frame_var_occurs: invalid arguments");
+    if (!P->walk) return fail(CBX_E_STATE, "cbx_frame_var_occurs: the plan has no walk tables (cbx_plan_set_walk)");
+    *n_records = 0;
+    *virtual_bytes = n_bytes;
+    if (first_offset >= n_bytes) return CBX_OK;
+    WalkArgs a{};
+    a.data = d_data;
+    a.nodes = (const CBX_CONST cbx_walk_node*)P->d_wnodes; a.root = P->walk_root;
+    a.warr = (const CBX_CONST cbx_walk_array*)P->d_warr;
+    a.handlers = (const CBX_CONST cbx_walk_handler*)P->d_whand; a.n_handlers = P->walk_n_handlers;
+    a.arrays = (const CBX_CONST cbx_array*)P->d_arrays; a.fields = (const CBX_CONST Field*)P->d_fields;
+    a.lut = P->d_lut;
+    AsyncBlock blk(st);
+    HIP_CHECK(hipMallocAsync(&blk.p, 3 * sizeof(int64_t), st));
+    int64_t* d_out = (int64_t*)blk.p;
+    HIP_CHECK(hipMemsetAsync(d_out, 0, 3 * sizeof(int64_t), st));
+    hipLaunchKernelGGL(walk_frame_kernel, dim3(1), dim3(1), 0, st, a, first_offset, n_bytes, capacity, d_rec_off, d_rec_len, d_out);
+    HIP_CHECK(hipGetLastError());
+    int64_t h[3] = {0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(h, d_out, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (h[2] < 0) return fail(CBX_E_UNSUPPORTED, "cbx_frame_var_occurs: copybook nesting deeper than the walk's frame stack");
+    *n_records = h[0];
+    *virtual_bytes = std::max(n_bytes, h[1]);
+    if (h[0] > capacity) return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(h[0]));
     return CBX_OK;
 }

@@ -9,6 +9,12 @@
 
 #include "cbx_internal.h"
 
+// Diagnostic builds only (tools/build_variant.py --diag N): bit 0 drops the numeric validity /
+// deferral stores, bit 1 the numeric value stores -- to price the stores.  The product build is 0.
+#ifndef CBX_DIAG
+#define CBX_DIAG 0
+#endif
+
 namespace cbx {
 
 // Exclusive scan of a 32-bit value over the wave with DPP row shifts (Hillis-Steele inside
@@ -201,13 +207,58 @@ __device__ __forceinline__ void store_w(void* values, int64_t tile, int lane, co
     else (gp((u32x4*)values) + tile * kWave)[lane] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
 }
 
+// Where a numeric op's validity / deferral word of a tile goes.  DirectSink: a wave ballot stored
+// by every lane to its address (8 bytes per (op, tile)).  VWords: gathered in lanes over a run of
+// kVRun consecutive tiles and stored 64 bytes at a time (VWords::flush) -- one 8-byte store per
+// (word, tile) cost the SYN200 kernel a fifth of its time (4.78 -> 3.85 ms without them, measured).
+struct DirectSink {
+    __device__ __forceinline__ void valid(const NumCall& c, int, int64_t tile, uint64_t m) const { gp(c.validity)[tile] = m; }
+    __device__ __forceinline__ void defer(const NumCall& c, int, int64_t tile, uint64_t m) const {
+        if (c.defer) gp(c.defer)[tile] = m;
+    }
+};
+
+constexpr int kVRun = 8;   // consecutive tiles per run of a wave (the words of 8 tiles = 64 bytes)
+
+// NV VGPR pairs: word w of the run's tile j sits in lane 8 (w % 8) + j of pair w / 8.  Validity
+// words are numbered by op (NNUM ops), deferral words follow (NNUM + deferral sequence).  Every
+// index is a compile-time constant after inlining (specialised kernels), so the pairs stay in
+// registers.
+template <int NV, int NNUM>
+struct VWords {
+    uint32_t lo[NV], hi[NV];
+    int j;   // the current tile's place in its run
+    __device__ __forceinline__ void put(int w, uint64_t m) {
+        // v_writelane: the wave-uniform word from SGPRs into one lane (a lane compare + select per
+        // word costs ~20 VGPRs more: 174 -> 191, below 3 waves per SIMD).  The lane select goes
+        // through M0: with both operands in SGPRs gfx950 rejects the instruction (constant bus).
+        const int reg = w >> 3, ln = ((w & 7) << 3) | j;
+        const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)m), mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
+        asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(lo[reg]) : "s"(mlo), "s"(ln) : "m0");
+        asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(hi[reg]) : "s"(mhi), "s"(ln) : "m0");
+    }
+    __device__ __forceinline__ void valid(const NumCall&, int i, int64_t, uint64_t m) { put(i, m); }
+    __device__ __forceinline__ void defer(const NumCall&, int d, int64_t, uint64_t m) { if (d >= 0) put(NNUM + d, m); }
+    // the run starting at tile t0: lanes 8k..8k+7 of pair r store word 8r + k of its tiles (64 B)
+    __device__ __forceinline__ void flush(const KernelArgs& a, int n_words, int64_t t0, int lane) {
+        const int jj = lane & 7;
+#pragma unroll
+        for (int r = 0; r < NV; r++) {
+            const int w = 8 * r + (lane >> 3);
+            if (w < n_words && t0 + jj < a.n_tiles) {
+                uint64_t* p = w < NNUM ? a.ncall[w].validity : a.defer_bits + (int64_t)(w - NNUM) * a.n_tiles;
+                gp(p)[t0 + jj] = ((uint64_t)hi[r] << 32) | lo[r];
+            }
+        }
+    }
+};
+
 // One batch of numeric ops (same decoder variant V, output width W).  Decoding is branch-free
 // per lane: every lane reads its (clamped) element and computes, the bounds / segment / OCCURS
-// conditions only select validity.  The validity (and deferral) word of each op is a wave
-// ballot stored by every lane to the same address.
-template <int V, int W, bool kOdo, bool kGlobal>
+// conditions only select validity.  The validity (and deferral) word of each op goes to the sink.
+template <int V, int W, bool kOdo, bool kGlobal, typename Sink>
 __device__ __forceinline__ void num_one(const KernelArgs& a, const NumOp& op, int i, const TileCtx& t,
-                                        bool ok, uint64_t r1, uint64_t r0, const int32_t* s_cnt, int lane) {
+                                        bool ok, uint64_t r1, uint64_t r0, const int32_t* s_cnt, int lane, Sink& sk) {
     if (op.segment >= 0) ok &= op.segment == t.seg;
     if (kOdo) ok &= odo_present(a.nops + i, op.n_odo, s_cnt, lane);
     Val x = null_val();
@@ -224,13 +275,10 @@ __device__ __forceinline__ void num_one(const KernelArgs& a, const NumOp& op, in
     }
     const NumCall c = ldc(a.ncall + i);
     // every lane stores (slot rows are padded to 64 * n_tiles values): no exec-mask branches
-    store_w<W>(c.values, t.tile, lane, x, op.out_type);
+    if (!(CBX_DIAG & 2)) store_w<W>(c.values, t.tile, lane, x, op.out_type);
     const uint64_t m = __ballot(x.valid);
-    gp(c.validity)[t.tile] = m;
-    if (V == V_ZONED16 || V == V_GENERIC || kGlobal) {
-        const uint64_t dm = __ballot(defer);
-        if (c.defer) gp(c.defer)[t.tile] = dm;
-    }
+    if (!(CBX_DIAG & 1)) sk.valid(c, i, t.tile, m);
+    if ((V == V_ZONED16 || V == V_GENERIC || kGlobal) && !(CBX_DIAG & 1)) sk.defer(c, op.defer, t.tile, __ballot(defer));
 }
 
 // One batch of numeric ops (same decoder variant V, output width W), four ops per step: the
@@ -244,6 +292,7 @@ __device__ __forceinline__ void num_batch(const KernelArgs& a, const Batch& b, c
     constexpr bool kWide = V == V_BCD16 || V == V_ZONED16;   // two 8-byte reads per element
     constexpr bool kRead = !(kGlobal || V == V_GENERIC);
     const int lim = t.active ? t.avail - a.start_off : -1;   // element must end within the record
+    DirectSink ds;
     constexpr int U = 4;
     int i = b.begin;
     for (; i + U <= b.end; i += U) {
@@ -262,7 +311,7 @@ __device__ __forceinline__ void num_batch(const KernelArgs& a, const Batch& b, c
             }
         }
 #pragma unroll
-        for (int u = 0; u < U; u++) num_one<V, W, kOdo, kGlobal>(a, op[u], i + u, t, ok[u], r1[u], r0[u], s_cnt, lane);
+        for (int u = 0; u < U; u++) num_one<V, W, kOdo, kGlobal>(a, op[u], i + u, t, ok[u], r1[u], r0[u], s_cnt, lane, ds);
     }
     for (; i < b.end; i++) {
         const NumOp op = ldc(a.nops + i);
@@ -273,7 +322,7 @@ __device__ __forceinline__ void num_batch(const KernelArgs& a, const Batch& b, c
             r1 = img_le64_ending(src, end);
             if (kWide) r0 = img_le64_ending(src, end - 8);
         }
-        num_one<V, W, kOdo, kGlobal>(a, op, i, t, ok, r1, r0, s_cnt, lane);
+        num_one<V, W, kOdo, kGlobal>(a, op, i, t, ok, r1, r0, s_cnt, lane, ds);
     }
 }
 
@@ -349,9 +398,9 @@ __device__ __forceinline__ void run_batch(const KernelArgs& a, const Batch& b, c
 
 // A group of N <= 4 numeric ops with the op records known at compile time (the specialised
 // kernels of cbx_jit.h): the interpreter's batch step with every descriptor field folded.
-template <int V, int W, bool kOdo, int N>
+template <int V, int W, bool kOdo, int N, typename Sink>
 __device__ __forceinline__ void num_group(const KernelArgs& a, const NumOp (&op)[N], int i0, const TileCtx& t,
-                                          const uint8_t* src, uint32_t rec_addr, const int32_t* s_cnt, int lane) {
+                                          const uint8_t* src, uint32_t rec_addr, const int32_t* s_cnt, int lane, Sink& sk) {
     constexpr bool kWide = V == V_BCD16 || V == V_ZONED16;
     constexpr bool kRead = V != V_GENERIC;
     const int lim = t.active ? t.avail - a.start_off : -1;
@@ -368,7 +417,7 @@ __device__ __forceinline__ void num_group(const KernelArgs& a, const NumOp (&op)
         }
     }
 #pragma unroll
-    for (int u = 0; u < N; u++) num_one<V, W, kOdo, false>(a, op[u], i0 + u, t, ok[u], r1[u], r0[u], s_cnt, lane);
+    for (int u = 0; u < N; u++) num_one<V, W, kOdo, false>(a, op[u], i0 + u, t, ok[u], r1[u], r0[u], s_cnt, lane, sk);
 }
 
 // String-view layout (cbx_plan_options.string_views): the element's Arrow view -- length, then the
@@ -850,10 +899,26 @@ __device__ __forceinline__ WaveLds wave_lds(const KernelArgs& a, uint8_t* smem, 
 // the next tile's loads are issued between the two parts instead of before both -- the
 // specialised kernel puts a layout's string elements in `pre` when it also has numerics, so the
 // string phase's register peak does not stack on the prefetch registers.
+// Tile order of a wave: grid-stride over single tiles, or -- for a body that gathers its words
+// over runs (Body::kWords > 0, VWords) -- over runs of kVRun consecutive tiles.
+template <typename Body>
+__device__ __forceinline__ int64_t first_tile(int64_t wave) { return Body::kWords > 0 ? wave * kVRun : wave; }
+template <typename Body>
+__device__ __forceinline__ int64_t next_tile(int64_t tile, int64_t tstep) {
+    if (Body::kWords == 0) return tile + tstep;
+    return ((tile + 1) % kVRun) ? tile + 1 : tile + 1 + (tstep - 1) * kVRun;
+}
+// end of the tile's run: the body's gathered words go out
+template <typename Body>
+__device__ __forceinline__ void run_end(const KernelArgs& a, Body& body, int64_t tile, int lane) {
+    if (Body::kWords > 0 && (((tile + 1) % kVRun) == 0 || tile + 1 >= a.n_tiles)) body.flush(a, tile - tile % kVRun, lane);
+}
+
 template <int KP, int kPro, bool kLate, typename Body>
 __device__ __forceinline__ void contig_loop(const KernelArgs& a, const WaveLds& l, int64_t tile, int64_t tstep,
-                                            int lane, const Body& body) {
+                                            int lane, Body body) {
     uint4 buf[KP];
+    tile = first_tile<Body>(tile);
     if (tile < a.n_tiles) contig_issue<KP>(a, contig_span(a, tile), lane, buf);
     Stamps st;
     st.init();
@@ -862,7 +927,8 @@ __device__ __forceinline__ void contig_loop(const KernelArgs& a, const WaveLds& 
         contig_store<KP>(a, sp, lane, buf, l.img);
         wave_sync_lds();
         st.mark(0);   // staging: wait for the prefetched loads + LDS writes
-        const int64_t next = tile + tstep;
+        const int64_t next = next_tile<Body>(tile, tstep);
+        body.begin(tile);
         // issued even past the last tile (a span of no chunks: every offset out of range, no
         // access), so the buffer is always redefined here and never live across the decode
         if (!kLate) contig_issue<KP>(a, contig_span(a, next), lane, buf);
@@ -874,6 +940,7 @@ __device__ __forceinline__ void contig_loop(const KernelArgs& a, const WaveLds& 
         body.pre(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
         if (kLate) contig_issue<KP>(a, contig_span(a, next), lane, buf);
         body.post(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
+        run_end(a, body, tile, lane);
         wave_sync_lds();
         st.mark(5);   // end of tile
         tile = next;
@@ -941,19 +1008,20 @@ __device__ __forceinline__ void span_store(const ContigSpan& sp, int lane, const
 
 template <int KP, int kPro, bool kLate, typename Body>
 __device__ __forceinline__ void span_loop(const KernelArgs& a, const WaveLds& l, int64_t tile, int64_t tstep,
-                                          int lane, const Body& body) {
+                                          int lane, Body body) {
+    tile = first_tile<Body>(tile);
     if (tile >= a.n_tiles) return;
     uint4 buf[KP];
     int64_t off_c, off_n;
     int32_t len_c, len_n;
     span_recs(a, tile, lane, off_c, len_c);
-    span_recs(a, tile + tstep, lane, off_n, len_n);
+    span_recs(a, next_tile<Body>(tile, tstep), lane, off_n, len_n);
     ContigSpan sp_c = span_of<KP>(a, tile, off_c, len_c);
     contig_issue<KP>(a, sp_c, lane, buf);
     Stamps st;
     st.init();
     while (tile < a.n_tiles) {
-        const int64_t next = tile + tstep;
+        const int64_t next = next_tile<Body>(tile, tstep);
         const ContigSpan sp = sp_c;
         const int64_t off = off_c;
         const int32_t len = len_c;
@@ -962,7 +1030,8 @@ __device__ __forceinline__ void span_loop(const KernelArgs& a, const WaveLds& l,
         sp_c = span_of<KP>(a, next, off_n, len_n);
         off_c = off_n;
         len_c = len_n;
-        span_recs(a, next + tstep, lane, off_n, len_n);
+        span_recs(a, next_tile<Body>(next, tstep), lane, off_n, len_n);
+        body.begin(tile);
         TileCtx t;
         t.tile = tile;
         t.rec = tile * kWave + lane;
@@ -989,6 +1058,7 @@ __device__ __forceinline__ void span_loop(const KernelArgs& a, const WaveLds& l,
         body.pre(a, t, (const uint8_t*)l.img, rec_addr, l, lane, st);
         if (kLate) contig_issue<KP>(a, sp_c, lane, buf);
         body.post(a, t, (const uint8_t*)l.img, rec_addr, l, lane, st);
+        run_end(a, body, tile, lane);
         wave_sync_lds();
         st.mark(5);
         tile = next;

@@ -29,6 +29,9 @@ namespace cbx {
 
 // Interpreter body of the contiguous loop: the plan's windows, read from the tables at run time.
 struct InterpBody {
+    static constexpr int kWords = 0;   // validity words stored per tile (DirectSink)
+    __device__ __forceinline__ void begin(int64_t) {}
+    __device__ __forceinline__ void flush(const KernelArgs&, int64_t, int) {}
     __device__ __forceinline__ void post(const KernelArgs&, const TileCtx&, const uint8_t*, uint32_t, const WaveLds&, int,
                                          Stamps&) const {}
     __device__ __forceinline__ void pre(const KernelArgs& a, const TileCtx& t, const uint8_t* img,

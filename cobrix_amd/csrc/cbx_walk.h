@@ -1,0 +1,391 @@
+// cbx_walk.h -- the record walk with data-dependent offsets: RecordExtractors.extractRecord
+// restated per lane (CP/reader/extractors/record/RecordExtractors.scala:49-183) for the layouts
+// the static-offset kernels cannot express:
+//   * variable_size_occurs = true: an OCCURS DEPENDING ON array consumes only its present
+//     elements, so every later field moves with the data (:109-113);
+//   * DEPENDING ON a field inside an OCCURS (each element carries the count of a nested array);
+//   * DEPENDING ON a string field through occurs_mappings (dependingOnHandlers, :70-74);
+// and VarOccursRecordExtractor's record lengths (CP/reader/extractors/raw/VarOccursRecordExtractor.scala:30-154).
+// Included by cbx_capi.hip.
+//
+// One lane walks one record through the copybook's node table (cbx_walk_node: DFS order with
+// child / sibling links) with an explicit frame stack, keeps the dependFields map as a small
+// per-lane table of dependee slots (one per DEPENDING ON name, Left(int) or Right(handler key)),
+// decodes each primitive with the byte-loop decoders straight from HBM and writes it to its
+// (column, slot, record) place; validity bits are OR-ed in with atomics (lanes of a wave diverge:
+// no ballot).  String columns use the string-view layout: a value longer than 12 bytes takes its
+// place in its tile's region through a per-(column slot, tile) cursor.  Records are independent,
+// so the walk is data-parallel; within a record it is the reference's sequence, which is the point.
+#pragma once
+
+namespace cbx {
+
+constexpr int kWalkDepth = 16;     // group / OCCURS nesting levels
+constexpr int kWalkDeps = 8;       // DEPENDING ON names (dependee slots)
+
+struct WalkArgs {
+    const uint8_t* data;
+    int64_t data_len;
+    const int64_t* rec_off;           // framed records (nullptr: fixed stride)
+    const int32_t* rec_len;
+    int64_t n_rec;
+    int32_t stride, start_off;
+    int64_t first_record_id;
+    const int64_t* rec_id;            // selection: per-record Record_Id
+    const int32_t* rec_seg;           // selection: per-record active segment
+    int32_t file_id;
+    int32_t var_occurs;               // variable_size_occurs
+    int64_t n_tiles, pitch;
+    const CBX_CONST cbx_walk_node* nodes;
+    int32_t root;                     // the AST root node (a group whose children are the records)
+    const CBX_CONST cbx_walk_array* warr;
+    const CBX_CONST cbx_walk_handler* handlers;
+    int32_t n_handlers;
+    const CBX_CONST cbx_array* arrays;
+    const CBX_CONST Field* fields;
+    const CBX_CONST DevColumn* cols;
+    const CBX_CONST cbx_segment_map* segmap;
+    const uint32_t* lut;
+    int32_t seg_col, fid_col, rid_col;
+    const int64_t* str_slot_base;     // per column: index of its slot 0 among the string column slots
+    uint32_t* cursors;                // [string column slots][n_tiles] payload bytes used in the tile region
+    const int64_t* tile_bytes;        // per column: view region bytes per tile
+    int32_t* status;
+};
+
+struct WalkFrame {
+    int32_t node;     // group (children loop) or OCCURS node (elements loop)
+    int32_t elems;    // 1: the elements of node (an OCCURS node), 0: node's children
+    int32_t cur;      // group: current child; array: current element
+    int32_t cnt;      // array: present elements
+    int32_t start;    // offset where the node began
+    int32_t off;      // running offset
+    int32_t slot;     // slot of the node's values (array: the enclosing slot)
+};
+
+// A dependee slot: kind 0 unseen, 1 Left(int), 2 Right(string) -> v = handler key index + 1 (0: a
+// string no handler lists)
+struct WalkDep { int32_t kind, v; };
+
+__device__ __forceinline__ uint32_t walk_lut(const WalkArgs& a, int kind, uint32_t b) {
+    return kind == CBX_K_STRING_ASCII ? ascii_lut(b) : a.lut[b];
+}
+
+__device__ __forceinline__ void walk_set_valid(uint64_t* validity, int64_t word, int lane) {
+    atomicOr((unsigned long long*)(validity + word), 1ull << lane);
+}
+
+// extractArray's element count (:66-81)
+__device__ __forceinline__ int walk_count(const WalkArgs& a, int ai, const WalkDep* dep) {
+    const cbx_array ar = ldc(a.arrays + ai);
+    const cbx_walk_array wa = ldc(a.warr + ai);
+    int v = ar.max_count;
+    if (wa.dep_slot >= 0) {
+        const WalkDep d = dep[wa.dep_slot];
+        if (d.kind == 1) v = d.v;
+        else if (d.kind == 2) {   // dependingOnHandlers.getOrElse(s, arraySize)
+            for (int h = wa.h_begin; h < wa.h_end; h++)
+                { const cbx_walk_handler hd = ldc(a.handlers + h); if (hd.key_id + 1 == d.v) { v = hd.value; break; } }
+        }
+    }
+    return (v >= ar.min_count && v <= ar.max_count) ? v : ar.max_count;
+}
+
+// One primitive element at record offset `off` (relative to the decode base).
+__device__ void walk_prim(const WalkArgs& a, const cbx_walk_node& nd, int off, int slot, const uint8_t* rec, int avail,
+                          int64_t r, int lane, WalkDep* dep) {
+    const bool decoded = nd.field >= 0;
+    Field f{};
+    if (decoded) f = ldc(a.fields + nd.field);
+    const int size = nd.data_size;
+    const int o = a.start_off + off;
+    const int64_t tile = r / kWave;
+    const bool is_str = decoded && (f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII || f.kind == CBX_K_HEX ||
+                                    f.kind == CBX_K_RAW || f.kind == CBX_K_UTF16_BE || f.kind == CBX_K_UTF16_LE);
+    if (is_str) {
+        // Primitive.decodeTypeValue (:102-128): offset past the end -> null, else truncated
+        if (o > avail) return;
+        const int n = o + size <= avail ? size : avail - o;
+        const uint8_t* p = rec + o;
+        auto lutf = [&](uint32_t b) { return walk_lut(a, f.kind, b); };
+        const StrSpan sp = string_span(f.kind, f.trim, p, n, lutf);
+        const DevColumn c = ldc(a.cols + f.column);
+        const int len = sp.utf8_len;
+        uint8_t inl[16] = {0};
+        u32x4 view;
+        view.x = (uint32_t)len;
+        if (len <= 12) {
+            string_write(f.kind, p, sp, inl, lutf);
+            view.y = inl[0] | (uint32_t)inl[1] << 8 | (uint32_t)inl[2] << 16 | (uint32_t)inl[3] << 24;
+            view.z = inl[4] | (uint32_t)inl[5] << 8 | (uint32_t)inl[6] << 16 | (uint32_t)inl[7] << 24;
+            view.w = inl[8] | (uint32_t)inl[9] << 8 | (uint32_t)inl[10] << 16 | (uint32_t)inl[11] << 24;
+        } else {
+            const int64_t tb = a.tile_bytes[f.column];
+            const int64_t tpb = (int64_t(1) << 30) / (tb < 16 ? 16 : tb);
+            const int64_t cs = a.str_slot_base[f.column] + slot;
+            const uint32_t at = atomicAdd(a.cursors + cs * a.n_tiles + tile, (uint32_t)len);
+            if ((int64_t)at + len > tb) { atomicOr(a.status, 1); return; }
+            uint8_t* dst = c.data + (int64_t)slot * c.capacity + tile * tb + at;
+            string_write(f.kind, p, sp, dst, lutf);
+            view.y = dst[0] | (uint32_t)dst[1] << 8 | (uint32_t)dst[2] << 16 | (uint32_t)dst[3] << 24;
+            const int64_t b = tile / tpb;
+            view.z = (uint32_t)b;
+            view.w = (uint32_t)((tile - b * tpb) * tb + at);
+        }
+        ((u32x4*)c.values)[(int64_t)slot * a.pitch + r] = view;
+        walk_set_valid(c.validity, (int64_t)slot * a.n_tiles + tile, lane);
+        if (nd.dep_slot >= 0) {   // Right(s): the handler key it equals (occurs_mappings)
+            int key = 0;
+            uint8_t buf[64];
+            if (len <= 64) {
+                string_write(f.kind, p, sp, buf, lutf);
+                for (int h = 0; h < a.n_handlers && key == 0; h++) {
+                    const cbx_walk_handler hd = ldc(a.handlers + h);
+                    bool eq = hd.key_len == len;
+                    for (int i = 0; eq && i < len; i++) eq = hd.key[i] == buf[i];
+                    if (eq) key = hd.key_id + 1;
+                }
+            }
+            dep[nd.dep_slot] = WalkDep{2, key};
+        }
+        return;
+    }
+    if (!decoded) return;   // a FILLER that nothing depends on
+    if (o + size > avail) return;   // numeric past the end -> null
+    const uint8_t* p = rec + o;
+    const Val x = decode_numeric(f, p);
+    if (!x.valid) return;   // null: dependFields keeps its previous entry (:126-134)
+    const DevColumn c = ldc(a.cols + f.column);
+    const int w = f.out_type == CBX_O_I32 || f.out_type == CBX_O_F32 ? 4 : f.out_type == CBX_O_DEC128 ? 16 : 8;
+    const int64_t at = (int64_t)slot * a.pitch + r;
+    if (w == 4) ((uint32_t*)c.values)[at] = (uint32_t)x.lo;
+    else if (w == 8) ((uint64_t*)c.values)[at] = x.lo;
+    else ((u32x4*)c.values)[at] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
+    walk_set_valid(c.validity, (int64_t)slot * a.n_tiles + tile, lane);
+    if (nd.dep_slot >= 0) {   // Left(Number.intValue)
+        const Val dv = decode_count_int(f, p);
+        if (dv.valid) dep[nd.dep_slot] = WalkDep{1, (int32_t)dv.lo};
+    }
+}
+
+// The walk of one record (extractRecord's getGroupValues / extractArray / extractValue).
+// seg: the active segment redefine (-1 none).
+__device__ void walk_record(const WalkArgs& a, const uint8_t* rec, int avail, int seg, int64_t r, int lane) {
+    WalkFrame st[kWalkDepth];
+    WalkDep dep[kWalkDeps];
+    for (int i = 0; i < kWalkDeps; i++) dep[i] = WalkDep{0, 0};
+    int sp = 0;
+    st[0] = WalkFrame{a.root, 0, ldc(a.nodes + a.root).child, 0, 0, 0, 0};
+    int last_size = 0;   // size consumed by the frame just popped
+    bool popped = false;
+    while (sp >= 0) {
+        WalkFrame& fr = st[sp];
+        const cbx_walk_node nd = ldc(a.nodes + fr.node);
+        if (fr.elems) {   // the elements of an OCCURS node
+            if (popped) {   // a group element finished
+                fr.off += last_size;
+                fr.cur++;
+                popped = false;
+            }
+            if (fr.cur < fr.cnt) {
+                const int slot = fr.slot * ldc(a.arrays + nd.array).max_count + fr.cur;
+                if (nd.kind == CBX_W_GROUP) {
+                    if (sp + 1 >= kWalkDepth) { atomicOr(a.status, 2); return; }
+                    st[sp + 1] = WalkFrame{fr.node, 0, nd.child, 0, fr.off, fr.off, slot};
+                    sp++;
+                    continue;
+                }
+                walk_prim(a, nd, fr.off, slot, rec, avail, r, lane, dep);
+                fr.off += nd.data_size;
+                fr.cur++;
+                continue;
+            }
+            // extractArray's consumed size: the elements walked, or the static size (:109-113)
+            last_size = a.var_occurs ? fr.off - fr.start : nd.actual_size;
+            sp--;
+            popped = true;
+            continue;
+        }
+        // a group's children (the group node itself, or one element of an OCCURS group)
+        if (popped) {   // a child group / array finished: advance by its size (getGroupValues, :144-160)
+            const cbx_walk_node ch = ldc(a.nodes + fr.cur);
+            if (!(ch.flags & CBX_W_REDEFINED)) fr.off += (ch.array < 0 && (ch.flags & CBX_W_REDEFINES)) ? ch.actual_size : last_size;
+            fr.cur = ch.next;
+            popped = false;
+        }
+        if (fr.cur < 0) {   // the group is done
+            last_size = fr.off - fr.start;
+            sp--;
+            popped = true;
+            continue;
+        }
+        const int ci = fr.cur;
+        const cbx_walk_node ch = ldc(a.nodes + ci);
+        if (ch.array >= 0) {   // an OCCURS node: its element count, then its elements
+            const int cnt = walk_count(a, ch.array, dep);
+            const int ccol = ldc(a.arrays + ch.array).count_column;
+            if (ccol >= 0) {
+                const DevColumn c = ldc(a.cols + ccol);
+                ((int32_t*)c.values)[(int64_t)fr.slot * a.pitch + r] = cnt;
+                walk_set_valid(c.validity, (int64_t)fr.slot * a.n_tiles + r / kWave, lane);
+            }
+            if (sp + 1 >= kWalkDepth) { atomicOr(a.status, 2); return; }
+            st[sp + 1] = WalkFrame{ci, 1, 0, cnt, fr.off, fr.off, fr.slot};
+            sp++;
+            continue;
+        }
+        if (ch.kind == CBX_W_GROUP) {
+            if (ch.segment >= 0 && ch.segment != seg) {   // inactive segment redefine: null, full size (:119-121)
+                last_size = ch.actual_size;
+                popped = true;
+                continue;
+            }
+            if (sp + 1 >= kWalkDepth) { atomicOr(a.status, 2); return; }
+            st[sp + 1] = WalkFrame{ci, 0, ch.child, 0, fr.off, fr.off, fr.slot};
+            sp++;
+            continue;
+        }
+        walk_prim(a, ch, fr.off, fr.slot, rec, avail, r, lane, dep);
+        if (!(ch.flags & CBX_W_REDEFINED)) fr.off += ch.actual_size;
+        fr.cur = ch.next;
+    }
+}
+
+__global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n_rec; r += (int64_t)gridDim.x * blockDim.x) {
+        int64_t base;
+        int avail;
+        if (a.rec_off) { base = a.rec_off[r]; avail = a.rec_len[r]; }
+        else { base = r * (int64_t)a.stride; avail = a.stride; }
+        const uint8_t* rec = a.data + base;
+        int seg = -1;
+        if (a.rec_seg) seg = a.rec_seg[r];
+        else if (a.segmap) {
+            const int k = segment_key(a.segmap, a.lut, a.fields, rec, avail, a.start_off);
+            if (k >= 0) seg = a.segmap->key_segment[k];
+        }
+        const int64_t tile = r / kWave;
+        if (a.seg_col >= 0) {
+            const DevColumn c = ldc(a.cols + a.seg_col);
+            ((int32_t*)c.values)[r] = seg;
+            walk_set_valid(c.validity, tile, lane);
+        }
+        if (a.fid_col >= 0) {
+            const DevColumn c = ldc(a.cols + a.fid_col);
+            ((int32_t*)c.values)[r] = a.file_id;
+            walk_set_valid(c.validity, tile, lane);
+        }
+        if (a.rid_col >= 0) {
+            const DevColumn c = ldc(a.cols + a.rid_col);
+            ((int64_t*)c.values)[r] = a.rec_id ? a.rec_id[r] : a.first_record_id + r;
+            walk_set_valid(c.validity, tile, lane);
+        }
+        walk_record(a, rec, avail, seg, r, lane);
+    }
+}
+
+// ---- VarOccursRecordExtractor: record lengths by walking each record's dependees ----
+// extractVarOccursRecordBytes (:52-136): a walk with no decoding besides the dependees, every
+// non-redefined field advancing by its walked size; the record is the walked prefix of the stream
+// (a short read at the end is zero-filled: the record may reach past n_bytes).  Sequential in the
+// stream (a record starts where the previous one ends): one thread.
+__device__ int walk_length(const WalkArgs& a, const uint8_t* rec, int avail) {
+    WalkFrame st[kWalkDepth];
+    WalkDep dep[kWalkDeps];
+    for (int i = 0; i < kWalkDeps; i++) dep[i] = WalkDep{0, 0};
+    int sp = 0;
+    st[0] = WalkFrame{a.root, 0, ldc(a.nodes + a.root).child, 0, 0, 0, 0};
+    int last_size = 0;
+    bool popped = false;
+    uint8_t zb[64];
+    while (sp >= 0) {
+        WalkFrame& fr = st[sp];
+        const cbx_walk_node nd = ldc(a.nodes + fr.node);
+        if (fr.elems) {
+            if (popped) { fr.off += last_size; fr.cur++; popped = false; }
+            if (fr.cur < fr.cnt) {
+                if (nd.kind == CBX_W_GROUP) {
+                    if (sp + 1 >= kWalkDepth) return -1;
+                    st[sp + 1] = WalkFrame{fr.node, 0, nd.child, 0, fr.off, fr.off, 0};
+                    sp++;
+                    continue;
+                }
+                fr.off += nd.data_size * (fr.cnt - fr.cur);   // primitive elements: dataSize * count
+                fr.cur = fr.cnt;
+                continue;
+            }
+            last_size = fr.off - fr.start;
+            sp--;
+            popped = true;
+            continue;
+        }
+        if (popped) {   // extractGroup (:111-131): every non-redefined field advances by its walked size
+            const cbx_walk_node ch = ldc(a.nodes + fr.cur);
+            if (!(ch.flags & CBX_W_REDEFINED)) fr.off += last_size;
+            fr.cur = ch.next;
+            popped = false;
+        }
+        if (fr.cur < 0) { last_size = fr.off - fr.start; sp--; popped = true; continue; }
+        const int ci = fr.cur;
+        const cbx_walk_node ch = ldc(a.nodes + ci);
+        if (ch.array >= 0) {
+            const int cnt = walk_count(a, ch.array, dep);
+            if (sp + 1 >= kWalkDepth) return -1;
+            st[sp + 1] = WalkFrame{ci, 1, 0, cnt, fr.off, fr.off, 0};
+            sp++;
+            continue;
+        }
+        if (ch.kind == CBX_W_GROUP) {
+            if (sp + 1 >= kWalkDepth) return -1;
+            st[sp + 1] = WalkFrame{ci, 0, ch.child, 0, fr.off, fr.off, 0};
+            sp++;
+            continue;
+        }
+        if (ch.dep_slot >= 0 && ch.field >= 0) {   // a dependee: decoded from the (zero-filled) bytes
+            const Field f = ldc(a.fields + ch.field);
+            const int size = ch.actual_size < 64 ? ch.actual_size : 64;
+            for (int i = 0; i < size; i++) zb[i] = fr.off + i < avail ? rec[fr.off + i] : 0;
+            if (f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII) {
+                auto lutf = [&](uint32_t b) { return walk_lut(a, f.kind, b); };
+                const StrSpan s = string_span(f.kind, f.trim, zb, size, lutf);
+                uint8_t buf[64];
+                int key = 0;
+                if (s.utf8_len <= 64) {
+                    string_write(f.kind, zb, s, buf, lutf);
+                    for (int h = 0; h < a.n_handlers && key == 0; h++) {
+                        const cbx_walk_handler hd = ldc(a.handlers + h);
+                        bool eq = hd.key_len == s.utf8_len;
+                        for (int i = 0; eq && i < s.utf8_len; i++) eq = hd.key[i] == buf[i];
+                        if (eq) key = hd.key_id + 1;
+                    }
+                }
+                dep[ch.dep_slot] = WalkDep{2, key};
+            } else {
+                const Val dv = decode_count_int(f, zb);
+                if (dv.valid) dep[ch.dep_slot] = WalkDep{1, (int32_t)dv.lo};
+            }
+        }
+        if (!(ch.flags & CBX_W_REDEFINED)) fr.off += ch.actual_size;
+        fr.cur = ch.next;
+    }
+    return last_size;
+}
+
+__global__ void walk_frame_kernel(WalkArgs a, int64_t first, int64_t n_bytes, int64_t capacity, int64_t* rec_off,
+                                  int32_t* rec_len, int64_t* out /* [0] records, [1] end of the last record */) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    int64_t pos = first, k = 0;
+    while (pos < n_bytes) {   // hasNext: offset < size
+        const int64_t left = n_bytes - pos;
+        const int len = walk_length(a, a.data + pos, left < 0x7fffffff ? (int)left : 0x7fffffff);
+        if (len <= 0) { out[2] = len < 0 ? -1 : 0; break; }
+        if (k < capacity) { rec_off[k] = pos; rec_len[k] = len; }
+        k++;
+        pos += len;
+    }
+    out[0] = k;
+    out[1] = pos;
+}
+
+}  // namespace cbx

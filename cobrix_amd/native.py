@@ -40,8 +40,8 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
                     "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text",
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
-                    "cbx_hier_list_offsets")
-ABI_VERSION = 8
+                    "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs")
+ABI_VERSION = 9
 
 
 class NativeLibraryError(RuntimeError):
@@ -122,6 +122,25 @@ class CbxSelection(ctypes.Structure):
                 ("footer_bytes", ctypes.c_int32)]
 
 
+W_GROUP, W_PRIM = 0, 1
+W_REDEFINED, W_REDEFINES = 0x1, 0x2
+
+
+class CbxWalkNode(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("kind", "next", "child", "field", "array", "flags", "data_size",
+                                                "actual_size", "segment", "dep_slot")]
+
+
+class CbxWalkArray(ctypes.Structure):
+    _fields_ = [("dep_slot", ctypes.c_int32), ("h_begin", ctypes.c_int32), ("h_end", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class CbxWalkHandler(ctypes.Structure):
+    _fields_ = [("key_id", ctypes.c_int32), ("key_len", ctypes.c_int32), ("value", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("key", ctypes.c_uint8 * 64)]
+
+
 class CbxHierParams(ctypes.Structure):
     _fields_ = [("n_segments", ctypes.c_int32), ("root_segment", ctypes.c_int32),
                 ("parent", ctypes.c_int32 * CBX_MAX_SEG_KEYS), ("first_record_id", ctypes.c_int64)]
@@ -167,8 +186,12 @@ def load():
     L.cbx_sparse_index.argtypes = [P, P, i64, P, P, i64, P, P, i64, P, P]
     L.cbx_select_records.argtypes = [P, P, i64, P, P, i64, i32, P, i32, P, P, P]
     L.cbx_decode_selected.argtypes = [P, P, i64, P, i64, i32, P, P]
-    L.cbx_hier_select.argtypes = [P, P, i64, P, P, i64, P, P, P, P, P, P]
-    L.cbx_hier_list_offsets.argtypes = [P, i64, i64, i64, i64, P, P]
+    for name, at in (("cbx_hier_select", [P, P, i64, P, P, i64, P, P, P, P, P, P]),
+                     ("cbx_hier_list_offsets", [P, i64, i64, i64, i64, P, P]),
+                     ("cbx_plan_set_walk", [P, P, i32, i32, P, P, i32, i32]),
+                     ("cbx_frame_var_occurs", [P, P, i64, i64, P, P, i64, P, P, P])):
+        if hasattr(L, name):   # (diagnostic builds of older revisions lack the newest entry points)
+            getattr(L, name).argtypes = at
     if L.cbx_abi_version() != ABI_VERSION:
         raise NativeLibraryError(f"{LIB_PATH}: ABI {L.cbx_abi_version()} != {ABI_VERSION}; rebuild it")
     _lib = L

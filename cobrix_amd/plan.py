@@ -27,6 +27,10 @@ class UnsupportedLayout(ValueError):
     """The layout uses a feature outside the GPU path (reported, never silently degraded)."""
 
 
+class NeedsWalk(UnsupportedLayout):
+    """The static-offset kernels cannot express the layout; the record walk can (build_plan(walk=True))."""
+
+
 @dataclass
 class ColumnInfo:
     index: int
@@ -54,6 +58,7 @@ class DecodePlan:
     record_id_column: int = -1
     file_id_column: int = -1
     seg_id_columns: List[int] = field(default_factory=list)   # Seg_Id0.. string columns
+    walk: Optional["WalkTables"] = None                          # record-walk tables (cbx_plan_set_walk)
 
     @property
     def n_columns(self) -> int:
@@ -149,9 +154,11 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
                file_id: int = 0, window_bytes: int = 0, jit_min_records: int = 0,
                segment_levels: Sequence[str] = (), segment_filter: Optional[List[str]] = None,
                segment_prefix: str = "", string_views: bool = False, occurs_lists: bool = False,
-               root_keys: Sequence[str] = ()) -> DecodePlan:
+               root_keys: Sequence[str] = (), walk: bool = False, variable_size_occurs: bool = False) -> DecodePlan:
     """root_keys: segment ids of a hierarchical file's root segment (sparse-index cuts at level-0
-    keys, IndexGenerator.scala:89-113, without Seg_IdN columns)."""
+    keys, IndexGenerator.scala:89-113, without Seg_IdN columns).  walk: the plan decodes through the
+    record walk (cbx_walk.h) -- count columns of nested OCCURS get one slot per enclosing element,
+    dependees inside OCCURS and string dependees (occurs_mappings) are allowed, no list layout."""
     fields: List[N.CbxField] = []
     arrays: List[N.CbxArray] = []
     columns: List[ColumnInfo] = []
@@ -186,7 +193,10 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
             ar.parent = dims[-1][2] if dims else -1
             arrays.append(ar)
             array_of_node[id(st)] = ai
-            ar.count_column = add_column(kind="count", out_type=N.O_I32, node=st)
+            outer = 1
+            for (cnt, _, _) in dims:
+                outer *= cnt
+            ar.count_column = add_column(kind="count", out_type=N.O_I32, node=st, n_slots=outer if walk else 1)
             ar.offsets_column = -1
             pending_arrays.append((ai, st))
             my_dims.append((st.array_max_size, st.data_size, ai))
@@ -238,13 +248,13 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
         q = cand[0]
         if walk_order[id(q)] > walk_order[id(st)]:
             continue  # decoded after the array -> not yet in dependFields -> arrayMaxSize
-        if q.__dict__.get("_cbx_in_array"):
-            raise UnsupportedLayout(f"{st.name}: DEPENDING ON {q.name} inside an OCCURS is not on the GPU path yet")
-        if not isinstance(q.dtype, cbk.Integral) or q.dtype.precision > 18:
-            raise UnsupportedLayout(f"{st.name}: DEPENDING ON a non-integral field (occurs_mappings) is not on the GPU path yet")
+        if q.__dict__.get("_cbx_in_array") or not isinstance(q.dtype, cbk.Integral) or q.dtype.precision > 18:
+            if not walk:   # a count per enclosing element / a string dependee: the record walk
+                raise NeedsWalk(f"{st.name}: DEPENDING ON {q.name} (inside an OCCURS or not integral)")
+            continue
         arrays[ai].dependee = field_of_node[id(q)]
 
-    if occurs_lists:
+    if occurs_lists and not walk:
         # list layout (cobrix_hip.h, CBX_F_LIST): a top-level OCCURS DEPENDING ON array whose elements
         # are numeric leaves of that one level -- child elements packed per record, absent ones unwritten
         for ai, ar in enumerate(arrays):
@@ -343,8 +353,85 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
     lut = utf8_lut(ascii_charset_table(cb.ascii_charset) if _charset_strings(cb) else lut_for(cb.code_page))
     for i in range(256):
         opts.lut[i] = int(lut[i])
-    return DecodePlan(cb, fields, arrays, columns, opts, field_of_node, array_of_node, seg_groups,
+    plan = DecodePlan(cb, fields, arrays, columns, opts, field_of_node, array_of_node, seg_groups,
                       seg_col, rid_col, fid_col, seg_id_cols)
+    if walk:
+        plan.walk = walk_tables(plan, variable_size_occurs, has_segments=bool(red))
+    return plan
+
+
+@dataclass
+class WalkTables:
+    nodes: List[N.CbxWalkNode]
+    arrays: List[N.CbxWalkArray]
+    handlers: List[N.CbxWalkHandler]
+    root: int
+    variable_size_occurs: bool
+
+
+def walk_tables(plan: DecodePlan, variable_size_occurs: bool, has_segments: bool) -> WalkTables:
+    """The copybook as cbx_walk_node records (DFS, child / sibling links): what extractRecord walks
+    (RecordExtractors.scala:49-183), with each DEPENDING ON name a dependee slot (dependFields) and
+    each array's occurs_mappings handlers (dependingOnHandlers)."""
+    cb = plan.copybook
+    nodes: List[N.CbxWalkNode] = []
+    dep_slots: Dict[str, int] = {}
+    stmts: List[cbk.Statement] = []
+
+    def slot_of(name: str) -> int:
+        if name not in dep_slots:
+            if len(dep_slots) >= 8:
+                raise UnsupportedLayout("more than 8 DEPENDING ON names")
+            dep_slots[name] = len(dep_slots)
+        return dep_slots[name]
+
+    def add(st: cbk.Statement) -> int:
+        i = len(nodes)
+        nd = N.CbxWalkNode()
+        nodes.append(nd)
+        stmts.append(st)
+        is_group = isinstance(st, cbk.Group)
+        nd.kind = N.W_GROUP if is_group else N.W_PRIM
+        nd.next = nd.child = -1
+        nd.field = -1 if is_group else plan.field_of_node.get(id(st), -1)
+        nd.array = plan.array_of_node.get(id(st), -1) if st.is_array else -1
+        nd.flags = (N.W_REDEFINED if st.is_redefined else 0) | (N.W_REDEFINES if st.redefines is not None else 0)
+        nd.data_size, nd.actual_size = st.data_size, st.actual_size
+        nd.segment = plan.segment_groups.index(st) if (is_group and st.is_segment_redefine and has_segments) else -1
+        nd.dep_slot = slot_of(st.name) if (not is_group and st.is_dependee) else -1
+        if is_group:
+            prev = -1
+            for c in st.children:
+                ci = add(c)
+                if prev < 0:
+                    nodes[i].child = ci
+                else:
+                    nodes[prev].next = ci
+                prev = ci
+        return i
+
+    root = add(cb.ast)
+    arrays: List[N.CbxWalkArray] = []
+    handlers: List[N.CbxWalkHandler] = []
+    key_ids: Dict[str, int] = {}
+    for ai in range(len(plan.arrays)):
+        st = next(s for s in stmts if plan.array_of_node.get(id(s)) == ai)
+        wa = N.CbxWalkArray()
+        wa.dep_slot = dep_slots.get(st.depending_on, -1) if st.depending_on is not None else -1
+        wa.h_begin = len(handlers)
+        for key, value in st.depending_on_handlers.items():
+            kb = key.encode("utf-8")
+            if len(kb) > 64:
+                raise UnsupportedLayout("occurs_mappings key longer than 64 bytes")
+            h = N.CbxWalkHandler()
+            h.key_id = key_ids.setdefault(key, len(key_ids))
+            h.key_len, h.value = len(kb), int(value)
+            for j, b in enumerate(kb):
+                h.key[j] = b
+            handlers.append(h)
+        wa.h_end = len(handlers)
+        arrays.append(wa)
+    return WalkTables(nodes, arrays, handlers, root, variable_size_occurs)
 
 
 def _iter_prims(g: cbk.Group):
@@ -369,6 +456,14 @@ class NativePlan:
                                len(plan.arrays), ctypes.byref(plan.options), ctypes.byref(h))
         N.check(rc)
         self.handle = h
+        w = plan.walk
+        if w is not None:
+            self._wnodes = (N.CbxWalkNode * len(w.nodes))(*w.nodes)
+            self._warr = (N.CbxWalkArray * max(1, len(w.arrays)))(*w.arrays)
+            self._whand = (N.CbxWalkHandler * max(1, len(w.handlers)))(*w.handlers)
+            N.check(L.cbx_plan_set_walk(h, ctypes.addressof(self._wnodes), len(w.nodes), w.root,
+                                        ctypes.addressof(self._warr), ctypes.addressof(self._whand), len(w.handlers),
+                                        int(w.variable_size_occurs)))
 
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:

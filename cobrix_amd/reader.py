@@ -20,7 +20,7 @@ import numpy as np
 
 from . import copybook as cbk
 from . import native as N
-from .plan import DecodePlan, NativePlan, build_plan
+from .plan import DecodePlan, NativePlan, NeedsWalk, build_plan
 from .schema import ST_DECIMAL, spark_schema
 
 _CTX = Context(prec=200)
@@ -252,7 +252,7 @@ class DecodedBatch:
             if node.is_array and not in_array:
                 ai = plan.array_of_node[id(node)]
                 m = node.array_max_size
-                cnt = count_of(ai)[S * n + R]
+                cnt = count_of(ai)[(S if plan.columns[plan.arrays[ai].count_column].n_slots > 1 else 0) * n + R]
                 j = np.concatenate([np.arange(k) for k in cnt]) if len(cnt) else np.zeros(0, np.int64)
                 R2 = np.repeat(R, cnt)
                 S2 = np.repeat(S, cnt) * m + j
@@ -364,9 +364,16 @@ class DecodedBatch:
         def walk(g: cbk.Group, r: int, idx: List[Tuple[int, int]]) -> dict:
             d = {}
             for c in g.children:
+                if c.is_child_segment:
+                    continue   # never in a row (hierarchical children come from `extra`)
                 if c.is_array:
                     ai = plan.array_of_node[id(c)]
-                    cnt = int(np.int32(self._host(plan.arrays[ai].count_column)["values"][r]))
+                    cci = plan.arrays[ai].count_column
+                    cs = 0   # a count per enclosing element (record-walk plans)
+                    if plan.columns[cci].n_slots > 1:
+                        for i, m in idx:
+                            cs = cs * m + i
+                    cnt = int(np.int32(self._host(cci)["values"][cs * self.n_rec + r]))
                     vals = []
                     for i in range(cnt):
                         sub = idx + [(i, c.array_max_size)]
@@ -687,21 +694,34 @@ class _BaseReader:
     def __init__(self, copybook_contents: str, params: ReaderParameters):
         self.params = params
         self.copybook = parse_copybook_for(copybook_contents, params)
-        if params.variable_size_occurs:
-            raise N.CbxError(N.CBX_E_UNSUPPORTED, "variable_size_occurs=true is not on the GPU path yet")
         var = self.VARIABLE_LENGTH
         # the fixed-length reader only uses the redefine map (FixedLenNestedRowIterator.scala:50-70);
         # segment levels, filter and record ids belong to the variable-length iterator
         self.hierarchical = var and self.copybook.is_hierarchical
         root_keys = hier_root_keys(self.copybook, params) if self.hierarchical else ()
-        self.plan = build_plan(self.copybook, segment_field=params.segment_field,
-                               segment_redefine_map=params.segment_id_redefine_map or None,
-                               generate_record_id=params.generate_record_id and var, window_bytes=params.window_bytes,
-                               jit_min_records=params.jit_min_records,
-                               segment_levels=params.segment_id_levels if var else (),
-                               segment_filter=params.segment_id_filter if var else None,
-                               segment_prefix=params.segment_id_prefix, string_views=params.string_views,
-                               occurs_lists=params.occurs_lists, root_keys=root_keys)
+
+        def plan(walk: bool):
+            # the record walk (cbx_walk.h) writes string columns as views
+            return build_plan(self.copybook, segment_field=params.segment_field,
+                              segment_redefine_map=params.segment_id_redefine_map or None,
+                              generate_record_id=params.generate_record_id and var, window_bytes=params.window_bytes,
+                              jit_min_records=params.jit_min_records,
+                              segment_levels=params.segment_id_levels if var else (),
+                              segment_filter=params.segment_id_filter if var else None,
+                              segment_prefix=params.segment_id_prefix, string_views=params.string_views or walk,
+                              occurs_lists=params.occurs_lists, root_keys=root_keys, walk=walk,
+                              variable_size_occurs=params.variable_size_occurs)
+
+        # variable_size_occurs, DEPENDING ON inside an OCCURS, string dependees: the record walk
+        walk = bool(params.variable_size_occurs)
+        if not walk:
+            try:
+                self.plan = plan(False)
+            except NeedsWalk:
+                walk = True
+        if walk:
+            self.plan = plan(True)
+        self.walk = walk
         if self.hierarchical:
             check_hierarchical(self.copybook, params, self.plan)
         self.native = NativePlan(self.plan)
@@ -972,16 +992,39 @@ class VarLenNestedReader(_BaseReader):
 
     def _device_file(self, data: bytes):
         torch = _torch()
-        extra = self.copybook.record_size + 2 + 16 if self.params.is_text else 0
+        # zero fill past the data: text windows and VarOccursRecordExtractor's short last record
+        extra = self.copybook.record_size + 2 + 16 if (self.params.is_text or self.var_occurs_extractor()) else 0
         t = torch.zeros(max(16, len(data) + extra), dtype=torch.uint8, device="cuda")
         if len(data):
             t[: len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
         return t
 
+    def frame_var_occurs(self, d_data, n_bytes: int, stream=None):
+        """VarOccursRecordExtractor (GPU, sequential walk) -> (rec_off, rec_len, virtual_bytes): the
+        last record may reach past n_bytes into the reference's zero fill (d_data holds zeros there)."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream()
+        cap = max(1, n_bytes)
+        off = torch.empty(cap, dtype=torch.int64, device=d_data.device)
+        ln = torch.empty(cap, dtype=torch.int32, device=d_data.device)
+        n = ctypes.c_int64(0)
+        vb = ctypes.c_int64(0)
+        N.check(N.load().cbx_frame_var_occurs(self.native.handle, d_data.data_ptr(), n_bytes, 0, off.data_ptr(), ln.data_ptr(),
+                                               cap, ctypes.byref(n), ctypes.byref(vb), ctypes.c_void_p(st.cuda_stream)))
+        return off[: n.value], ln[: n.value], vb.value
+
+    def var_occurs_extractor(self) -> bool:
+        """VarLenNestedReader.recordExtractor (:60-78): VarOccursRecordExtractor for variable-size
+        OCCURS without RDW headers (no custom extractor / header parser / length field here)."""
+        p = self.params
+        return p.variable_size_occurs and not p.is_record_sequence and not p.is_text
+
     def frame_file(self, t, n_bytes: int):
         """(rec_off, rec_len, bytes the records are decoded against) of a whole file."""
         if self.params.is_text:
             return self.frame_text(t, n_bytes)
+        if self.var_occurs_extractor():
+            return self.frame_var_occurs(t, n_bytes)
         if self.params.is_record_sequence:
             off, ln = self.frame(t, n_bytes)
             return off, ln, n_bytes
@@ -1052,8 +1095,8 @@ class VarLenNestedReader(_BaseReader):
     def decode(self, data: bytes, seeds: Optional[Sequence[int]] = None, first_record_id: int = 0) -> DecodedBatch:
         """Frame + decode as one entry (no selection stage)."""
         t = self._device_file(data)
-        if self.params.is_text:
-            off, ln, vb = self.frame_text(t, len(data))
+        if self.params.is_text or self.var_occurs_extractor():
+            off, ln, vb = self.frame_file(t, len(data))
             return self.decode_device(t, vb, off, ln, first_record_id)
         off, ln = self.frame(t, len(data), seeds) if self.params.is_record_sequence else self.frame_fixed(t, len(data))
         return self.decode_device(t, len(data), off, ln, first_record_id)

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 8
+#define CBX_ABI_VERSION 9
 
 /* status codes */
 #define CBX_OK 0
@@ -274,6 +274,7 @@ int cbx_plan_set_profiling(cbx_plan* plan, int32_t enable);
 int cbx_plan_kernel_times(cbx_plan* plan, float* decode_ms, float* post_ms, int32_t max_calls, int32_t* n_calls);
 
 /* Which decode kernel the plan's last decode call ran: *kind = 0 the table-driven kernel,
+ * 2 the record walk (cbx_plan_set_walk),
  * 1 the copybook-specialised kernel.  If specialisation was attempted and failed, *kind = 0 and
  * the reason is in cbx_last_error() (the call itself succeeded on the table-driven kernel). */
 int cbx_plan_kernel_kind(cbx_plan* plan, int32_t* kind);
@@ -363,6 +364,59 @@ int cbx_select_records(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, c
  * (SegmentIdAccumulator.getSegmentLevelId: prefix_fileId_rootRecordId[_L<level>_<counter>]). */
 int cbx_decode_selected(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const cbx_selection* sel,
                         int64_t n_rec, int32_t start_offset, cbx_column* columns, void* stream);
+
+/* ---- the record walk with data-dependent offsets ----
+ *
+ * Layouts the static-offset tables above cannot express run through a per-record walk of the
+ * copybook (RecordExtractors.extractRecord restated per lane, cbx_walk.h): variable_size_occurs =
+ * true (an OCCURS DEPENDING ON array consumes only its present elements, RecordExtractors.scala:
+ * 109-113), DEPENDING ON a field inside an OCCURS, DEPENDING ON a string field through
+ * occurs_mappings (dependingOnHandlers).  cbx_plan_set_walk attaches the copybook's node table to a
+ * plan; every later decode call on the plan walks.  Output columns are as above, with two
+ * differences: a count column of an array nested in OCCURS has one slot per enclosing element
+ * (n_slots = product of the enclosing max counts), and string columns must use the string-view
+ * layout.  Requires zeroed validity buffers. */
+#define CBX_W_GROUP 0
+#define CBX_W_PRIM 1
+#define CBX_W_REDEFINED 0x1   /* isRedefined: the node does not advance the offset */
+#define CBX_W_REDEFINES 0x2   /* redefines another node: a group advances by its static size */
+typedef struct {
+    int32_t kind;          /* CBX_W_GROUP / CBX_W_PRIM */
+    int32_t next, child;   /* next sibling, first child (groups); -1 none */
+    int32_t field;         /* primitive: cbx_field index, -1 when not decoded (FILLER) */
+    int32_t array;         /* OCCURS node: cbx_array index, -1 */
+    int32_t flags;         /* CBX_W_* */
+    int32_t data_size;     /* bytes per element (binaryProperties.dataSize) */
+    int32_t actual_size;   /* bytes of the whole node (binaryProperties.actualSize) */
+    int32_t segment;       /* group: segment redefine index, -1 */
+    int32_t dep_slot;      /* DEPENDING ON source: its dependee slot (one per name, < 8), -1 */
+} cbx_walk_node;
+typedef struct {
+    int32_t dep_slot;      /* dependee slot of the array's DEPENDING ON name, -1: fixed OCCURS */
+    int32_t h_begin, h_end;/* its occurs_mappings handlers (cbx_walk_handler range) */
+    int32_t reserved;
+} cbx_walk_array;
+typedef struct {
+    int32_t key_id;        /* distinct key strings share an id */
+    int32_t key_len;       /* UTF-8 bytes */
+    int32_t value;         /* element count the key stands for */
+    int32_t reserved;
+    uint8_t key[64];
+} cbx_walk_handler;
+
+int cbx_plan_set_walk(cbx_plan* plan, const cbx_walk_node* nodes, int32_t n_nodes, int32_t root,
+                      const cbx_walk_array* arrays, const cbx_walk_handler* handlers, int32_t n_handlers,
+                      int32_t variable_size_occurs);
+
+/* VarOccursRecordExtractor (CP/reader/extractors/raw/VarOccursRecordExtractor.scala:30-154): record
+ * boundaries of a file whose record size follows from its OCCURS DEPENDING ON values (no RDW, no
+ * length field), from first_offset on.  A record starts where the previous one ends, so the walk is
+ * sequential (one device thread: a latency-bound path).  A short read at the end is zero-filled by
+ * the reference: the last record may reach past n_bytes, up to *virtual_bytes (the buffer must hold
+ * zeros there before decoding).  Needs a plan with cbx_plan_set_walk. */
+int cbx_frame_var_occurs(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, int64_t first_offset,
+                         int64_t* d_rec_off, int32_t* d_rec_len, int64_t capacity, int64_t* n_records,
+                         int64_t* virtual_bytes, void* stream);
 
 /* ---- hierarchical records (`segment-children`) ----
  *

@@ -14,6 +14,7 @@ SC = spark-cobol/src/main/scala/za/co/absa/cobrix/spark/cobol/):
   * VarLenNestedIterator (filter, root-reached, redefine map, Record_Id)
                                               CP/reader/iterator/VarLenNestedIterator.scala:80-147
   * SegmentIdAccumulator (Seg_IdN)            CP/reader/iterator/SegmentIdAccumulator.scala:19-86
+  * VarOccursRecordExtractor                  CP/reader/extractors/raw/VarOccursRecordExtractor.scala:30-154
   * VarLenHierarchicalIterator + extractHierarchicalRecord (segment-children)
                                               CP/reader/iterator/VarLenHierarchicalIterator.scala:43-162,
                                               CP/reader/extractors/record/RecordExtractors.scala:211-385
@@ -232,6 +233,86 @@ def root_segment_ids(cb: cbk.Copybook, p) -> List[str]:
     parents = getattr(p, "segment_redefine_parents", {}) or {}
     roots = set(parents.values()) - set(parents)
     return [sid for sid, grp in p.segment_id_redefine_map.items() if grp in roots]
+
+
+def var_occurs_records(cb: cbk.Copybook, data: bytes) -> List[bytes]:
+    """VarOccursRecordExtractor.next over the whole stream (:37-154): each record is the walked
+    prefix of the stream -- OCCURS DEPENDING ON counts from the dependees read so far (dependFields,
+    string dependees through dependingOnHandlers), every non-redefined field advancing by its walked
+    size -- zero-filled when the stream ends early; a record starts where the previous ended."""
+    fields = {}
+
+    def has_var_occurs(g) -> bool:
+        for c in g.children:
+            if isinstance(c, cbk.Group):
+                if has_var_occurs(c):
+                    return True
+            elif c.is_dependee:
+                return True
+        return False
+
+    max_size = cb.record_size
+    out: List[bytes] = []
+    pos = 0
+    ast = O.OracleAst(cb)
+    var = has_var_occurs(cb.ast)
+    while pos < len(data):   # hasNext: offset < size
+        if not var:
+            out.append(data[pos:pos + max_size])
+            pos += max_size
+            continue
+        buf = bytearray(max_size)
+        got = [0]
+        dep: Dict[str, Any] = {}
+
+        def ensure(n: int):
+            need = n - got[0]
+            if need > 0:
+                chunk = data[pos + got[0]:pos + n]
+                if len(chunk) > 0:
+                    buf[got[0]:got[0] + len(chunk)] = chunk
+                    got[0] = n
+
+        def extract_array(f, off: int) -> int:
+            size = f.array_max_size
+            if f.depending_on is not None:
+                v = dep.get(f.depending_on, ("L", size))
+                n = v[1] if v[0] == "L" else f.depending_on_handlers.get(v[1], size)
+                size = n if f.array_min_size <= n <= f.array_max_size else f.array_max_size
+            o = off
+            if isinstance(f, cbk.Group):
+                for _ in range(size):
+                    o += extract_group(o, f)
+            else:
+                o += f.data_size * size
+            return o - off
+
+        def extract_value(f, off: int) -> int:
+            if isinstance(f, cbk.Group):
+                return extract_group(off, f)
+            if f.is_dependee:
+                ensure(off + f.actual_size)
+                v = FieldReader(cb, f).value(bytes(buf), off - f.offset)
+                if v is not None:
+                    dep[f.name] = ("R", v) if isinstance(v, str) else ("L", int(v))
+            return f.actual_size
+
+        def extract_group(off: int, g) -> int:
+            o = off
+            for c in g.children:
+                size = extract_array(c, o) if c.is_array else extract_value(c, o)
+                if not c.is_redefined:
+                    o += size
+            return o - off
+
+        nxt = 0
+        for rec in cb.ast.children:
+            nxt += extract_group(nxt, rec)
+        ensure(nxt)
+        out.append(bytes(buf[:nxt]))
+        pos += nxt
+    del fields, ast
+    return out
 
 
 def index_generation_needed(p) -> bool:
@@ -477,8 +558,14 @@ def var_len_rows(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
     copybooks go through VarLenHierarchicalIterator (SC/reader/VarLenNestedReader.scala:55-81)."""
     if cb.is_hierarchical:
         return hier_rows(cb, data, p, file_id, entries)
-    recs = var_len_records(cb, data, p, file_id, entries)
+    if p.variable_size_occurs and not p.is_record_sequence and not p.is_text:
+        # VarOccursRecordExtractor framing (VarLenNestedReader.recordExtractor, :60-78); one index entry
+        payloads = var_occurs_records(cb, data)
+        recs = [VarRecord(b, i, [], None) for i, b in enumerate(payloads)]
+    else:
+        recs = var_len_records(cb, data, p, file_id, entries)
     res = O.decode_records(cb, [r.payload for r in recs], start_offset=p.start_offset,
+                           variable_size_occurs=p.variable_size_occurs,
                            active_segments=[r.active_segment for r in recs] if p.segment_id_redefine_map else None)
     body = O.rows(res, collapse_root=p.schema_policy == "collapse_root")
     rows = []

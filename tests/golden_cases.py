@@ -232,6 +232,15 @@ CASES: Dict[str, Dict[str, Any]] = {
                              "schema_retention_policy": "collapse_root", "debug": "true"},
                     expected="test17_expected/test17f.txt", schema="test17_expected/test17f_schema.json",
                     sort=("File_Id", "Record_Id"), take=60),
+    "test21": dict(spec="SCT/source/integration/Test21VariableOccurs.scala:70-95",
+                   copybook="test21_copybook.cob", data="test21_data/data.dat",
+                   options={"encoding": "ascii", "variable_size_occurs": "true"},
+                   expected="test21_expected/test21.txt", schema="test21_expected/test21_schema.json", take=60),
+    "test25": dict(spec="SCT/source/integration/Test25OccursMappings.scala:106-131",
+                   copybook="test25_copybook.cob", data="test25_data/data.dat",
+                   options={"encoding": "ascii", "variable_size_occurs": "true",
+                            "occurs_mappings": '{"DETAIL1":{"A":0,"B":1},"DETAIL2":{"A":1,"B":2}}'},
+                   expected="test25_expected/test25.txt", schema="test25_expected/test25_schema.json", take=60),
     "test19": dict(spec="SCT/source/integration/Test19DisplayNumParsingSpec.scala:32-75",
                    copybook="test19_display_num.cob", data="test19_display_num/data.dat",
                    options={"pedantic": "true", "generate_record_id": "true", "schema_retention_policy": "collapse_root"},

@@ -68,3 +68,15 @@ def test_sparse_index_known_answer_python_restatement():
     is_root = [1 if G.java_trim(raw[o:o + 5].decode("cp037")) == "C" else 0 for o in off]
     c_idx = O.sparse_index(raw, records_per_entry=10, is_root=is_root)
     assert [(e.offset_from, e.offset_to, e.record_index) for e in idx] == c_idx
+
+
+@pytest.mark.parametrize("name,records", [
+    ("test21", [b"0", b"10", b"12AB", b"21A2BC", b"21A1B"]),   # Test21VariableOccurs.scala:38-60
+    ("test25", [b"1AX", b"2BXYZ"]),                            # Test25OccursMappings.scala:52-79
+])
+def test_var_occurs_record_extractor_known_answer(name, records):
+    """VarOccursRecordExtractor splits the stream into the records the reference's unit tests list."""
+    case = GC.CASES[name]
+    p, _ = GC.params(case)
+    cb = parse_copybook_for(GC.copybook_text(case), p)
+    assert RO.var_occurs_records(cb, GC.data_bytes(case)) == records

@@ -191,3 +191,20 @@ def _arrow_vs_rows(name, views):
     table = batch.to_arrow()
     table.validate(full=True)
     assert _norm(table.to_pylist()) == _norm(batch.to_rows())
+
+
+@pytest.mark.parametrize("name,lengths", [("test21", [1, 2, 4, 6, 5]), ("test25", [3, 5])])
+def test_gpu_var_occurs_framing(name, lengths):
+    """cbx_frame_var_occurs against the reference's VarOccursRecordExtractor unit tests
+    (Test21VariableOccurs.scala:38-60, Test25OccursMappings.scala:52-79)."""
+    from cobrix_amd.reader import VarLenNestedReader
+    case = GC.CASES[name]
+    p, _ = GC.params(case)
+    data = GC.data_bytes(case)
+    rd = VarLenNestedReader(GC.copybook_text(case), p)
+    assert rd.walk
+    t = rd._device_file(data)
+    off, ln, vb = rd.frame_file(t, len(data))
+    assert ln.cpu().tolist() == lengths
+    assert off.cpu().tolist() == [sum(lengths[:i]) for i in range(len(lengths))]
+    assert vb == max(len(data), sum(lengths))

@@ -1,0 +1,153 @@
+"""The record walk (cbx_walk.h: extractRecord with data-dependent offsets, one lane per record)
+against the oracle: variable_size_occurs = true over RDW records and over VarOccursRecordExtractor
+framing, DEPENDING ON inside an OCCURS, string dependees through occurs_mappings, short records.
+The reference's own goldens for these layouts (test21, test25) run in test_gpu_golden.py."""
+from __future__ import annotations
+
+import random
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from oracle import reader_oracle as RO  # noqa: E402
+
+NESTED = """
+       01  REC.
+           05  SEG         PIC X(1).
+           05  N-OUT       PIC 9(1).
+           05  OUTER       OCCURS 0 TO 3 TIMES DEPENDING ON N-OUT.
+               10  N-IN    PIC 9(1).
+               10  KIND    PIC X(2).
+               10  INNER   OCCURS 1 TO 4 TIMES DEPENDING ON N-IN.
+                   15  AMT   PIC S9(5) COMP-3.
+                   15  NAME  PIC X(3).
+           05  TAIL-NUM    PIC 9(4) COMP.
+           05  TAIL-TXT    PIC X(6).
+"""
+
+MAPPED = """
+       01  REC.
+           05  ID          PIC 9(2).
+           05  CODE        PIC X(2).
+           05  ITEMS       OCCURS 0 TO 3 TIMES DEPENDING ON CODE.
+               10  V       PIC X(3).
+           05  AFTER       PIC 9(3).
+"""
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _ebcdic(s: str) -> bytes:
+    return s.encode("cp037")
+
+
+def nested_record(rnd: random.Random, var_size: bool) -> bytes:
+    """One NESTED record: counts sometimes out of range or non-numeric (the reference then takes the
+    maximum), the arrays' bytes as the layout variant lays them out."""
+    n_out = rnd.choice([0, 1, 2, 3, 3, 7])
+    b = bytearray(_ebcdic(rnd.choice("ABC")))
+    b += bytes([0xF0 + n_out]) if rnd.random() < 0.95 else b"\x40"
+    eff_out = n_out if 0 <= n_out <= 3 else 3
+    for i in range(3):
+        if var_size and i >= eff_out:
+            break
+        n_in = rnd.choice([1, 2, 3, 4, 0, 9])
+        b += bytes([0xF0 + n_in])
+        b += _ebcdic(rnd.choice(["AA", "BB", "  ", "ZZ"]))
+        eff_in = n_in if 1 <= n_in <= 4 else 4
+        for j in range(4):
+            if var_size and j >= eff_in:
+                break
+            dg = [int(c) for c in f"{rnd.randrange(100000):05d}"]
+            sign = rnd.choice([0x0C, 0x0D, 0x0F, 0x0A])   # 0x0A: a bad sign nibble -> null
+            b += bytes([dg[0] << 4 | dg[1], dg[2] << 4 | dg[3], dg[4] << 4 | sign])
+            b += _ebcdic(rnd.choice(["ABC", "X  ", "   ", "Q1 "]))
+    b += rnd.randrange(65536).to_bytes(2, "big")
+    b += _ebcdic(rnd.choice(["TAIL  ", "T", "      "]).ljust(6))
+    cut = len(b) if rnd.random() < 0.85 else rnd.randint(1, len(b))
+    return bytes(b[:cut])
+
+
+def rdw_file(recs) -> bytes:
+    return b"".join(bytes([0, 0, len(r) & 0xFF, len(r) >> 8]) + r for r in recs)
+
+
+def _reader(copybook: str, options: dict, **params):
+    import dataclasses
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import VarLenNestedReader
+    p, var_len = parse_options(options)
+    assert var_len
+    p = dataclasses.replace(p, **params)
+    return VarLenNestedReader(copybook, p), p
+
+
+@pytest.mark.parametrize("var_size", [True, False])
+def test_walk_nested_odo_rdw_vs_oracle(var_size):
+    rnd = random.Random(5 + var_size)
+    raw = rdw_file([nested_record(rnd, var_size) for _ in range(3000)])
+    opts = {"is_record_sequence": "true", "variable_size_occurs": str(var_size).lower(), "generate_record_id": "true"}
+    rd, p = _reader(NESTED, opts)
+    assert rd.walk
+    rows = rd.read(raw, file_id=1).to_rows()
+    exp = RO.var_len_rows(rd.copybook, raw, p, file_id=1)
+    assert len(rows) == len(exp) == 3000
+    bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
+    assert not bad, (bad[:5], rows[bad[0]], exp[bad[0]])
+
+
+def test_walk_var_occurs_extractor_vs_oracle():
+    """No RDW: VarOccursRecordExtractor framing on the GPU (sequential walk), then the walk decode."""
+    rnd = random.Random(11)
+    raw = b"".join(nested_record(rnd, True) for _ in range(400))
+    rd, p = _reader(NESTED, {"variable_size_occurs": "true"})
+    rows = rd.read(raw).to_rows()
+    exp = RO.var_len_rows(rd.copybook, raw, p)
+    assert len(rows) == len(exp) > 300
+    bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
+    assert not bad, (bad[:5], rows[bad[0]], exp[bad[0]])
+
+
+@pytest.mark.parametrize("var_size", [True, False])
+def test_walk_string_dependee_occurs_mappings(var_size):
+    rnd = random.Random(3)
+    recs = []
+    for i in range(2000):
+        code = rnd.choice(["A ", "B ", "C ", "ZZ", "  "])
+        n = {"A ": 0, "B ": 1, "C ": 3}.get(code, 3)
+        body = f"{i % 100:02d}{code}" + "".join(rnd.choice(["abc", "XYZ", "   "]) for _ in range(n if var_size else 3)) + f"{i % 1000:03d}"
+        recs.append(body.encode("cp037"))
+    raw = rdw_file(recs)
+    opts = {"is_record_sequence": "true", "variable_size_occurs": str(var_size).lower(),
+            "occurs_mappings": '{"ITEMS":{"A":0,"B":1,"C":3}}'}
+    rd, p = _reader(MAPPED, opts)
+    assert rd.walk
+    rows = rd.read(raw).to_rows()
+    exp = RO.var_len_rows(rd.copybook, raw, p)
+    assert rows == exp
+
+
+@pytest.mark.parametrize("policy", ["hex", "raw"])
+def test_debug_fields_vs_oracle(policy):
+    """HEX / RAW debug fields (debug = true | raw, CopybookParser.addDebugFields) on the test1 layout."""
+    import goldens as G
+    from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters
+    from oracle import oracle as O
+    from parity import compare_batch
+    cb_text = G.read("test1_copybook.cob").decode("latin-1")
+    data = G.read("test1_data", "example.bin")
+    for jit in (-1, 1):
+        rd = FixedLenNestedReader(cb_text, ReaderParameters(schema_policy="collapse_root", debug_fields_policy=policy,
+                                                            jit_min_records=jit))
+        b = rd.decode(data)
+        errs = compare_batch(b, O.decode_fixed(rd.copybook, data))
+        assert not errs, errs[:5]
+        rows = b.to_rows()
+        assert rows == RO.fixed_len_rows(rd.copybook, data, rd.params)

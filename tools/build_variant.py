@@ -1,7 +1,9 @@
 """Build the library from another git revision as cobrix_amd/libcobrix_hip_<name>.so (A/B timing
 within one GPU call: CBX_LIB_VARIANT=<name> python bench.py ...).  Diagnostic; never shipped.
 
-Usage: python tools/build_variant.py <git rev> <name>
+Usage: python tools/build_variant.py <git rev | .> <name> [-DMACRO=value ...]
+("." builds the working tree; -D defines go to hipcc, e.g. -DCBX_DIAG=1 for cbx_device.h's store
+diagnostics, which the specialised kernels inherit through cbx_jit.h.)
 """
 import os
 import subprocess
@@ -14,11 +16,15 @@ sys.path.insert(0, ROOT)
 
 def main():
     rev, name = sys.argv[1], sys.argv[2]
+    defines = [x for x in sys.argv[3:] if x.startswith("-D")]
     import __graft_entry__ as G
     with tempfile.TemporaryDirectory() as d:
-        arch = subprocess.run(["git", "archive", rev, "cobrix_amd/csrc", "include"], cwd=ROOT, check=True,
-                              capture_output=True).stdout
-        subprocess.run(["tar", "-x", "-C", d], input=arch, check=True)
+        if rev == ".":
+            subprocess.run(["cp", "-r", os.path.join(ROOT, "cobrix_amd"), os.path.join(ROOT, "include"), d], check=True)
+        else:
+            arch = subprocess.run(["git", "archive", rev, "cobrix_amd/csrc", "include"], cwd=ROOT, check=True,
+                                  capture_output=True).stdout
+            subprocess.run(["tar", "-x", "-C", d], input=arch, check=True)
         csrc = os.path.join(d, "cobrix_amd", "csrc")
         inc = os.path.join(d, "include")
         G.JIT_HEADERS = (("cobrix_hip.h", os.path.join(inc, "cobrix_hip.h")),
@@ -29,7 +35,7 @@ def main():
         G._write_jit_bundle()
         out = os.path.join(ROOT, "cobrix_amd", f"libcobrix_hip_{name}.so")
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                        "-I" + inc, "-I" + csrc, "-o", out, os.path.join(csrc, "cbx_capi.hip"), "-lhiprtc"], check=True)
+                        "-I" + inc, "-I" + csrc, *defines, "-o", out, os.path.join(csrc, "cbx_capi.hip"), "-lhiprtc"], check=True)
         print(out)
 
 
