@@ -951,13 +951,14 @@ class Copybook:
 
     def __init__(self, ast: Group, *, code_page: str = "common", string_trimming: str = "both",
                  floating_point_format: str = "IBM", is_utf16_big_endian: bool = True,
-                 ascii_charset: str = ""):
+                 ascii_charset: str = "", data_encoding: str = EBCDIC):
         self.ast = ast
         self.code_page = code_page
         self.string_trimming = string_trimming
         self.floating_point_format = floating_point_format
         self.is_utf16_big_endian = is_utf16_big_endian
         self.ascii_charset = ascii_charset
+        self.data_encoding = data_encoding
 
     # Copybook.getRecordSize (Copybook.scala:33-35)
     @property
@@ -1084,4 +1085,5 @@ def parse_copybook(contents: str, *, data_encoding: str = EBCDIC, drop_group_fil
     _calculate_non_filler_sizes(root)
     return Copybook(root, code_page=code_page, string_trimming=string_trimming,
                     floating_point_format=floating_point_format,
-                    is_utf16_big_endian=is_utf16_big_endian, ascii_charset=ascii_charset)
+                    is_utf16_big_endian=is_utf16_big_endian, ascii_charset=ascii_charset,
+                    data_encoding=data_encoding)

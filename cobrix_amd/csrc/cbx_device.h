@@ -232,7 +232,8 @@ struct VWords {
         // v_writelane: the wave-uniform word from SGPRs into one lane (a lane compare + select per
         // word costs ~20 VGPRs more: 174 -> 191, below 3 waves per SIMD).  The lane select goes
         // through M0: with both operands in SGPRs gfx950 rejects the instruction (constant bus).
-        const int reg = w >> 3, ln = ((w & 7) << 3) | j;
+        const int reg = w >> 3;
+        const int ln = __builtin_amdgcn_readfirstlane(((w & 7) << 3) | j);   // provably uniform: an SGPR
         const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)m), mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
         asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(lo[reg]) : "s"(mlo), "s"(ln) : "m0");
         asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(hi[reg]) : "s"(mhi), "s"(ln) : "m0");

@@ -284,9 +284,8 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
         if not isinstance(sf, cbk.Primitive):
             raise UnsupportedLayout("segment field must be a primitive field")
         field_is_int = isinstance(sf.dtype, cbk.Integral) and sf.dtype.precision <= 18
-        if not field_is_int and not (isinstance(sf.dtype, cbk.AlphaNumeric) and
-                                     (sf.dtype.enc == cbk.EBCDIC or (sf.dtype.enc == cbk.ASCII and _charset_strings(cb)))):
-            raise UnsupportedLayout("segment field must be an EBCDIC (or charset ASCII) string or an integral field")
+        if not field_is_int and not (isinstance(sf.dtype, cbk.AlphaNumeric) and sf.dtype.enc in (cbk.EBCDIC, cbk.ASCII)):
+            raise UnsupportedLayout("segment field must be an EBCDIC / ASCII string or an integral field")
         if sf.is_array:
             raise UnsupportedLayout("segment field must not be an OCCURS array")
         keys = segment_keys(red, levels, seg_filter)
@@ -350,7 +349,16 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
     opts.segment_column = seg_col
     opts.jit_min_records = jit_min_records
     opts.string_views = 1 if string_views else 0
-    lut = utf8_lut(ascii_charset_table(cb.ascii_charset) if _charset_strings(cb) else lut_for(cb.code_page))
+    # the byte table: the code page (EBCDIC), the charset (ASCII wrapper), or for a US-ASCII copybook
+    # decodeAsciiString's own mapping (bytes < 32 and >= 128 -> ' ') -- its strings decode through
+    # ascii_lut on the device; the table serves the segment-id match (segment_key)
+    if _charset_strings(cb):
+        table = ascii_charset_table(cb.ascii_charset)
+    elif cb.data_encoding == cbk.ASCII:
+        table = [b if 32 <= b < 128 else 0x20 for b in range(256)]
+    else:
+        table = lut_for(cb.code_page)
+    lut = utf8_lut(table)
     for i in range(256):
         opts.lut[i] = int(lut[i])
     plan = DecodePlan(cb, fields, arrays, columns, opts, field_of_node, array_of_node, seg_groups,
