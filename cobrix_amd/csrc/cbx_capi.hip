@@ -471,10 +471,10 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
         if (f.kind != CBX_K_RECORD_ID && f.kind != CBX_K_FILE_ID)
             P->rec_extent = std::max(P->rec_extent, (int)std::min<int64_t>(e, 1 << 30));
     }
-    if (P->view)   // the register path (fields of <= kStrFastBytes) always stages its tile's long payloads
+    if (P->view)   // the register path (fields of <= kStrFastBytes) composes in lane-private slots (str_view_fast)
         for (const Field& d : P->dfields_h)
             if (d.variant == V_STRING && d.size <= kStrFastBytes && (d.kind == CBX_K_STRING || d.kind == CBX_K_STRING_ASCII))
-                P->str_stage = std::max(P->str_stage, kWave * d.size * d.max_utf8);
+                P->str_stage = std::max(P->str_stage, kWave * str_lane_slot(d.size, d.max_utf8));
 
     // ---- segment map: keys to UTF-8, Seg_IdN string columns
     cbx_segment_map sm = opts->segments;
@@ -553,7 +553,8 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
 
 // String-view layout: bytes of a slot region owned by one tile (the tile's payload bound, 16-aligned)
 // and tiles per Arrow data buffer (buffers of at most 1 GiB, a whole number of tiles each).
-static int64_t view_tile_bytes(const cbx_plan* P, int c) { return ((int64_t)kWave * P->col_max_bytes[c] + 15) & ~(int64_t)15; }
+// a tile's region: 64 payloads of the column's widest value, each at a 4-byte-aligned position
+static int64_t view_tile_bytes(const cbx_plan* P, int c) { return ((int64_t)kWave * ((P->col_max_bytes[c] + 3) & ~3) + 15) & ~(int64_t)15; }
 static int64_t view_tiles_per_buf(int64_t tile_bytes) { return std::max<int64_t>(1, (int64_t(1) << 30) / std::max<int64_t>(16, tile_bytes)); }
 
 extern "C" int cbx_string_bound(const cbx_plan* P, int64_t n_rec, int64_t* out_bytes) {
@@ -1195,6 +1196,15 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     return CBX_OK;
 }
 
+namespace {
+struct AsyncBlock {   // one hipMallocAsync block, freed (stream-ordered) when the scope ends
+    void* p = nullptr;
+    hipStream_t st;
+    explicit AsyncBlock(hipStream_t s) : st(s) {}
+    ~AsyncBlock() { if (p) (void)hipFreeAsync(p, st); }
+};
+}  // namespace
+
 // Text framing (is_text): cbx_text.h.  Needs d_data readable up to n_bytes; records past n_bytes
 // (the reference's zero fill, cbx_text.h) require the caller's buffer to hold zeros up to
 // *virtual_bytes (at most n_bytes + record_size + 2).
@@ -1220,12 +1230,14 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
                            (const int64_t*)sums, out);
     };
     auto sums_len = [](int64_t n) { return (n + kScanTile - 1) / kScanTile; };
-    uint32_t* d_cnt = nullptr;
-    int64_t* d_base = nullptr;
-    int64_t* d_sums = nullptr;
-    HIP_CHECK(hipMallocAsync((void**)&d_cnt, sizeof(uint32_t) * (nch + 1), st));
-    HIP_CHECK(hipMallocAsync((void**)&d_base, sizeof(int64_t) * (nch + 1), st));
-    HIP_CHECK(hipMallocAsync((void**)&d_sums, sizeof(int64_t) * sums_len(nch + 1), st));
+    // stream-ordered temporaries, each released when its scope ends (every return path)
+    AsyncBlock b_cnt(st), b_base(st), b_sums(st), b_lf(st), b_eol(st), b_scnt(st), b_sbase(st), b_big(st), b_sums2(st);
+    HIP_CHECK(hipMallocAsync(&b_cnt.p, sizeof(uint32_t) * (nch + 1), st));
+    HIP_CHECK(hipMallocAsync(&b_base.p, sizeof(int64_t) * (nch + 1), st));
+    HIP_CHECK(hipMallocAsync(&b_sums.p, sizeof(int64_t) * sums_len(nch + 1), st));
+    uint32_t* d_cnt = (uint32_t*)b_cnt.p;
+    int64_t* d_base = (int64_t*)b_base.p;
+    int64_t* d_sums = (int64_t*)b_sums.p;
     HIP_CHECK(hipMemsetAsync(d_cnt + nch, 0, sizeof(uint32_t), st));
     const unsigned cblocks = (unsigned)((nch + 3) / 4);   // 4 waves per block, one chunk each
     hipLaunchKernelGGL(text_lf_kernel, dim3(cblocks), dim3(256), 0, st, d_data, n_bytes, nch, 0, d_cnt,
@@ -1234,18 +1246,15 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     int64_t n_lf = 0;
     HIP_CHECK(hipMemcpyAsync(&n_lf, d_base + nch, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    int64_t* d_lf = nullptr;
-    HIP_CHECK(hipMallocAsync((void**)&d_lf, sizeof(int64_t) * (n_lf + 1), st));
+    HIP_CHECK(hipMallocAsync(&b_lf.p, sizeof(int64_t) * (n_lf + 1), st));
+    int64_t* d_lf = (int64_t*)b_lf.p;
     hipLaunchKernelGGL(text_lf_kernel, dim3(cblocks), dim3(256), 0, st, d_data, n_bytes, nch, 1, d_cnt,
                        (const int64_t*)d_base, d_lf);
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipFreeAsync(d_cnt, st));
-    HIP_CHECK(hipFreeAsync(d_base, st));
-    HIP_CHECK(hipFreeAsync(d_sums, st));
     // line-ending length before every segment (scan of per-segment maps, cbx_text.h)
     const int64_t n_eol_tiles = (n_lf + 1 + kEolTile - 1) / kEolTile;
-    uint8_t* d_eol = nullptr;   // [n_eol_tiles] tile maps | [n_lf + 1] f before each segment
-    HIP_CHECK(hipMallocAsync((void**)&d_eol, n_eol_tiles + n_lf + 1 + 16, st));
+    HIP_CHECK(hipMallocAsync(&b_eol.p, n_eol_tiles + n_lf + 1 + 16, st));
+    uint8_t* d_eol = (uint8_t*)b_eol.p;   // [n_eol_tiles] tile maps | [n_lf + 1] f before each segment
     uint8_t* d_fb = d_eol + n_eol_tiles;
     hipLaunchKernelGGL(text_eol_kernel, dim3((unsigned)n_eol_tiles), dim3(kEolThreads), 0, st, d_data, (const int64_t*)d_lf,
                        n_lf, M, 0, d_eol, (const uint8_t*)nullptr, (uint8_t*)nullptr);
@@ -1255,14 +1264,15 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
     HIP_CHECK(hipGetLastError());
     // pass 2: records per segment (n_lf line-ended segments + the tail) -> bases -> records
     const int64_t nseg = n_lf + 1;
-    uint32_t* d_scnt = nullptr;
-    int64_t* d_sbase = nullptr;   // [nseg + 1] bases, then the tail's final start
-    HIP_CHECK(hipMallocAsync((void**)&d_scnt, sizeof(uint32_t) * (nseg + 1), st));
-    HIP_CHECK(hipMallocAsync((void**)&d_sbase, sizeof(int64_t) * (nseg + 2), st));
-    unsigned long long* d_big = nullptr;   // [0] count of segments with many forced records, [1..] their indices
-    HIP_CHECK(hipMallocAsync((void**)&d_big, sizeof(unsigned long long) * (1 + kBigSegCap), st));
+    HIP_CHECK(hipMallocAsync(&b_scnt.p, sizeof(uint32_t) * (nseg + 1), st));
+    HIP_CHECK(hipMallocAsync(&b_sbase.p, sizeof(int64_t) * (nseg + 2), st));
+    HIP_CHECK(hipMallocAsync(&b_big.p, sizeof(unsigned long long) * (1 + kBigSegCap), st));
+    HIP_CHECK(hipMallocAsync(&b_sums2.p, sizeof(int64_t) * sums_len(nseg + 1), st));
+    uint32_t* d_scnt = (uint32_t*)b_scnt.p;
+    int64_t* d_sbase = (int64_t*)b_sbase.p;   // [nseg + 1] bases, then the tail's final start
+    unsigned long long* d_big = (unsigned long long*)b_big.p;   // [0] count of segments with many forced records, [1..] their indices
+    d_sums = (int64_t*)b_sums2.p;
     HIP_CHECK(hipMemsetAsync(d_big, 0, sizeof(unsigned long long), st));
-    HIP_CHECK(hipMallocAsync((void**)&d_sums, sizeof(int64_t) * sums_len(nseg + 1), st));
     HIP_CHECK(hipMemsetAsync(d_scnt + nseg, 0, sizeof(uint32_t), st));
     const unsigned sblocks = (unsigned)((nseg + 255) / 256);
     hipLaunchKernelGGL(text_seg_kernel, dim3(sblocks), dim3(256), 0, st, d_data, n_bytes, (const int64_t*)d_lf, n_lf,
@@ -1292,12 +1302,6 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
             HIP_CHECK(hipGetLastError());
         }
     }
-    HIP_CHECK(hipFreeAsync(d_scnt, st));
-    HIP_CHECK(hipFreeAsync(d_sbase, st));
-    HIP_CHECK(hipFreeAsync(d_sums, st));
-    HIP_CHECK(hipFreeAsync(d_lf, st));
-    HIP_CHECK(hipFreeAsync(d_big, st));
-    HIP_CHECK(hipFreeAsync(d_eol, st));
     if (rc) { HIP_CHECK(hipStreamSynchronize(st)); return rc; }
     // the virtual length: the window that first reached past the data (record start s_k, the
     // first with s_k + M >= n_bytes) was marked full (ensureBytesRead, :98-107)
@@ -1333,12 +1337,6 @@ extern "C" int cbx_frame_text(const uint8_t* d_data, int64_t n_bytes, int32_t re
 // index (cbx_select.h).  Temporaries are stream-ordered allocations released on every exit path.
 // ---------------------------------------------------------------------------------------------
 namespace {
-struct AsyncBlock {   // one hipMallocAsync block, freed (stream-ordered) when the scope ends
-    void* p = nullptr;
-    hipStream_t st;
-    explicit AsyncBlock(hipStream_t s) : st(s) {}
-    ~AsyncBlock() { if (p) (void)hipFreeAsync(p, st); }
-};
 
 // exclusive scan of n uint32 values into int64 out (cbx_kernels.hip scan passes); sums: nb int64
 void device_scan(const uint32_t* in, int64_t n, int64_t* out, int64_t* sums, hipStream_t st) {

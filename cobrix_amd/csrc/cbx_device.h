@@ -9,8 +9,9 @@
 
 #include "cbx_internal.h"
 
-// Diagnostic builds only (tools/build_variant.py --diag N): bit 0 drops the numeric validity /
-// deferral stores, bit 1 the numeric value stores -- to price the stores.  The product build is 0.
+// Diagnostic builds only (tools/build_variant.py . NAME -DCBX_DIAG=N): bit 0 drops the numeric
+// validity / deferral stores, bit 1 the numeric value stores, bit 2 has one lane store a word (not
+// all 64) -- to price the stores.  The product build is 0.
 #ifndef CBX_DIAG
 #define CBX_DIAG 0
 #endif
@@ -212,19 +213,23 @@ __device__ __forceinline__ void store_w(void* values, int64_t tile, int lane, co
 // kVRun consecutive tiles and stored 64 bytes at a time (VWords::flush) -- one 8-byte store per
 // (word, tile) cost the SYN200 kernel a fifth of its time (4.78 -> 3.85 ms without them, measured).
 struct DirectSink {
-    __device__ __forceinline__ void valid(const NumCall& c, int, int64_t tile, uint64_t m) const { gp(c.validity)[tile] = m; }
-    __device__ __forceinline__ void defer(const NumCall& c, int, int64_t tile, uint64_t m) const {
-        if (c.defer) gp(c.defer)[tile] = m;
+    __device__ __forceinline__ void valid(const NumCall& c, int, int64_t tile, uint64_t m) const {
+        if (!(CBX_DIAG & 4) || __builtin_amdgcn_mbcnt_lo(~0u, 0u) == 0) gp(c.validity)[tile] = m;   // (diag 4: one lane stores)
     }
+    __device__ __forceinline__ void defer(const NumCall& c, int, int64_t tile, uint64_t m) const {
+        if (c.defer && (!(CBX_DIAG & 4) || __builtin_amdgcn_mbcnt_lo(~0u, 0u) == 0)) gp(c.defer)[tile] = m;
+    }
+    __device__ __forceinline__ void svalid(const StrCall& c, int, int64_t tile, uint64_t m) const { gp(c.validity)[tile] = m; }
 };
 
 constexpr int kVRun = 8;   // consecutive tiles per run of a wave (the words of 8 tiles = 64 bytes)
 
 // NV VGPR pairs: word w of the run's tile j sits in lane 8 (w % 8) + j of pair w / 8.  Validity
-// words are numbered by op (NNUM ops), deferral words follow (NNUM + deferral sequence).  Every
+// words are numbered by op (NNUM ops), deferral words follow (NNUM + deferral sequence, NDEF of
+// them), then the string elements' validity words (NNUM + NDEF + string op).  Every
 // index is a compile-time constant after inlining (specialised kernels), so the pairs stay in
 // registers.
-template <int NV, int NNUM>
+template <int NV, int NNUM, int NDEF = 0>
 struct VWords {
     uint32_t lo[NV], hi[NV];
     int j;   // the current tile's place in its run
@@ -240,6 +245,7 @@ struct VWords {
     }
     __device__ __forceinline__ void valid(const NumCall&, int i, int64_t, uint64_t m) { put(i, m); }
     __device__ __forceinline__ void defer(const NumCall&, int d, int64_t, uint64_t m) { if (d >= 0) put(NNUM + d, m); }
+    __device__ __forceinline__ void svalid(const StrCall&, int i, int64_t, uint64_t m) { put(NNUM + NDEF + i, m); }
     // the run starting at tile t0: lanes 8k..8k+7 of pair r store word 8r + k of its tiles (64 B)
     __device__ __forceinline__ void flush(const KernelArgs& a, int n_words, int64_t t0, int lane) {
         const int jj = lane & 7;
@@ -247,7 +253,9 @@ struct VWords {
         for (int r = 0; r < NV; r++) {
             const int w = 8 * r + (lane >> 3);
             if (w < n_words && t0 + jj < a.n_tiles) {
-                uint64_t* p = w < NNUM ? a.ncall[w].validity : a.defer_bits + (int64_t)(w - NNUM) * a.n_tiles;
+                uint64_t* p = w < NNUM ? a.ncall[w].validity
+                            : w < NNUM + NDEF ? a.defer_bits + (int64_t)(w - NNUM) * a.n_tiles
+                                              : a.scall[w - NNUM - NDEF].validity;
                 gp(p)[t0 + jj] = ((uint64_t)hi[r] << 32) | lo[r];
             }
         }
@@ -429,16 +437,18 @@ __device__ __forceinline__ void num_group(const KernelArgs& a, const NumOp (&op)
 // front of the long ones (one scan places both: every lane takes 16 bytes or its length, so the
 // area a plan sizes for 64 values of the field -- at least 1 KiB -- holds the tile) and into the
 // view.  One pass, no scan across tiles, no placement kernel.
-__device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrOp& op, const StrCall& c, const TileCtx& t,
+template <typename Sink>
+__device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrOp& op, int i, const StrCall& c, const TileCtx& t,
                                                  const StrSpan& sp, bool ok, bool fast, const uint32_t (&ev)[kStrFastBytes],
-                                                 const uint8_t* sp_src, const uint32_t* s_lut, uint8_t* s_str, int lane) {
+                                                 const uint8_t* sp_src, const uint32_t* s_lut, uint8_t* s_str, int lane,
+                                                 Sink& sk) {
     const int len = ok ? sp.utf8_len : 0;
     const bool lng = len > 12;
     // one scan: short slots counted above bit 20, long payload bytes below (<= 64 * 96 bytes)
     uint32_t both;
     const uint32_t exb = wave_excl_scan32(lng ? (uint32_t)len : (1u << 20), lane, both);
     const uint32_t ex = exb & 0xFFFFFu, tot = both & 0xFFFFFu, n_short = both >> 20;
-    gp(c.validity)[t.tile] = __ballot(ok);
+    sk.svalid(c, i, t.tile, __ballot(ok));
     auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
     uint8_t* s_short = s_str + 16 * (exb >> 20);   // this lane's inline bytes
     uint8_t* s_long = s_str + 16 * n_short;        // the tile's long payloads, packed (16-aligned)
@@ -483,22 +493,118 @@ __device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrO
     wave_sync_lds();   // the staging area is reused by the next element
 }
 
+// Lane-private LDS slot of a register-path element in the view layout: its UTF-8 bytes (<= size *
+// width) + the bytes written past them (<= 3).
+__host__ __device__ constexpr int str_lane_slot(int size, int width) { return (size * width + 3 + 15) & ~15; }
+
+// The view layout's register-path string element (fields of <= kStrFastBytes EBCDIC / ASCII bytes,
+// StringDecoders.decodeEbcdicString / decodeAsciiString + StringTools.trim*): every byte's LUT
+// entry once, the trim range from the entries' trim bits, then the UTF-8 bytes written at running
+// positions into the lane's own LDS slot -- a byte outside the range adds no length, so its writes
+// land where the next kept byte's go, or past the end.  No cross-lane staging and no wave barrier:
+// the lane builds its view from its slot, and a long payload (> 12 bytes) goes from registers to the
+// tile's region at a 4-byte-aligned packed position (exact dword counts, so lanes never overlap).
+template <typename Sink>
+__device__ __forceinline__ void str_view_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp, int i,
+                                              const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
+                                              const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
+                                              uint8_t* s_str, int lane, Sink& sk) {
+    bool el = t.active && (op.segment < 0 || op.segment == t.seg);
+    if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
+    const int o = a.start_off + op.eo;
+    const bool ok = el && o <= t.avail;
+    const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
+    uint32_t w[8], ev[kStrFastBytes];
+    img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
+    lut_entries32(w, op.size, [&](uint32_t b) { return str_lut(op.kind, s_lut, b); }, ev);
+    uint32_t tm = 0;   // bit j: byte j trimmable (entry bit 31)
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++)
+        if (j < op.size) tm |= (ev[j] >> 31) << j;
+    const uint32_t keep = ~tm & bits_below(n);
+    int b = 0, e = n;
+    if (op.trim == CBX_TRIM_LEFT || op.trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;
+    if (op.trim == CBX_TRIM_RIGHT || op.trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
+    const uint32_t range = bits_below(e) & ~bits_below(b);
+    const int width = op.pad;
+    uint8_t* slot = s_str + lane * str_lane_slot(op.size, width);
+    uint32_t pos = 0;
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++) {
+        if (j < op.size) {
+            const uint32_t ej = ev[j];
+            uint8_t* p = slot + pos;
+            p[0] = (uint8_t)ej;
+            if (width > 1) p[1] = (uint8_t)(ej >> 8);
+            if (width > 2) p[2] = (uint8_t)(ej >> 16);
+            pos += ((ej >> 24) & 3u) & (uint32_t)__builtin_amdgcn_sbfe((int)range, j, 1);
+        }
+    }
+    const int len = (int)pos;
+    slot[len] = 0; slot[len + 1] = 0; slot[len + 2] = 0;   // the partial dword's tail
+    constexpr int kNC = (kStrFastBytes * 3 + 15) / 16;
+    u32x4 q[kNC];
+#pragma unroll
+    for (int k = 0; k < kNC; k++)
+        if (16 * k < op.size * width) q[k] = ((const u32x4*)slot)[k];
+    sk.svalid(c, i, t.tile, __ballot(ok));
+    const bool lng = len > 12;
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32(lng ? (uint32_t)(len + 3) & ~3u : 0u, lane, tot);
+    u32x4 v;
+    if (!lng) {
+        v = u32x4{(uint32_t)len, len > 0 ? q[0].x : 0u, len > 4 ? q[0].y : 0u, len > 8 ? q[0].z : 0u};
+    } else {
+        typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+        typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+        CBX_GLOBAL uint8_t* dst = gp(c.scratch + t.tile * c.tile_cap + ex);
+        const int n4 = (len + 3) >> 2;
+#pragma unroll
+        for (int k = 0; k < kNC; k++) {
+            if (16 * k < op.size * width) {
+                const int r = n4 - 4 * k;
+                CBX_GLOBAL uint8_t* d = dst + 16 * k;
+                if (r >= 4) {
+                    *(CBX_GLOBAL u32x4a*)d = u32x4a{q[k].x, q[k].y, q[k].z, q[k].w};
+                } else if (r >= 2) {
+                    *(CBX_GLOBAL u32x2a*)d = u32x2a{q[k].x, q[k].y};
+                    if (r == 3) ((CBX_GLOBAL uint32_t*)d)[2] = q[k].z;
+                } else if (r == 1) {
+                    *(CBX_GLOBAL uint32_t*)d = q[k].x;
+                }
+            }
+        }
+        const int64_t tb = t.tile / c.tiles_per_buf;
+        v = u32x4{(uint32_t)len, q[0].x, (uint32_t)tb, (uint32_t)((t.tile - tb * c.tiles_per_buf) * c.tile_cap + ex)};
+    }
+    (gp((u32x4*)c.views) + t.tile * kWave)[lane] = v;
+}
+
 // One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):
 // span + tile-local scan; the tile's payload is staged contiguously in LDS and copied with
 // dword stores to the tile's scratch region; the tile-local start of every value and the
 // tile's byte total are recorded for the compaction kernel, which places tiles after a
 // device-wide scan of the totals (two-pass string offsets, no cross-tile waiting).
-template <bool kView>
+template <bool kView, typename Sink = DirectSink>
 __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
                                             const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
                                             const uint8_t* src, uint32_t rec_addr, bool global,
-                                            const uint32_t* s_lut, uint8_t* s_str, int lane) {
+                                            const uint32_t* s_lut, uint8_t* s_str, int lane, int i = 0,
+                                            Sink* sk = nullptr) {
     const bool fast = sop_fast(op, global);
+    if (kView && fast) {
+        DirectSink ds;
+        if (sk) str_view_fast(a, op, opp, i, c, t, s_cnt, src, rec_addr, s_lut, s_str, lane, *sk);
+        else str_view_fast(a, op, opp, i, c, t, s_cnt, src, rec_addr, s_lut, s_str, lane, ds);
+        return;
+    }
     bool ok;
     uint32_t ev[kStrFastBytes];
     const StrSpan sp = sop_span(a, op, opp, t, s_cnt, lane, src, rec_addr, s_lut, ok, fast, ev);
     if (kView) {   // decode mode only: the view layout has no sizes pre-pass (cbx_string_bound)
-        str_view_element(a, op, c, t, sp, ok, fast, ev, src + rec_addr + (uint32_t)op.eo, s_lut, s_str, lane);
+        DirectSink ds;
+        if (sk) str_view_element(a, op, i, c, t, sp, ok, fast, ev, src + rec_addr + (uint32_t)op.eo, s_lut, s_str, lane, *sk);
+        else str_view_element(a, op, i, c, t, sp, ok, fast, ev, src + rec_addr + (uint32_t)op.eo, s_lut, s_str, lane, ds);
         return;
     }
     uint32_t tot;
