@@ -555,7 +555,12 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
 // and tiles per Arrow data buffer (buffers of at most 1 GiB, a whole number of tiles each).
 // a tile's region: 64 payloads of the column's widest value, each at a 4-byte-aligned position
 static int64_t view_tile_bytes(const cbx_plan* P, int c) { return ((int64_t)kWave * ((P->col_max_bytes[c] + 3) & ~3) + 15) & ~(int64_t)15; }
-static int64_t view_tiles_per_buf(int64_t tile_bytes) { return std::max<int64_t>(1, (int64_t(1) << 30) / std::max<int64_t>(16, tile_bytes)); }
+// whole tiles per data buffer: the largest power of two fitting 1 GiB (the kernels split a tile
+// index into buffer and position by a shift)
+static int64_t view_tiles_per_buf(int64_t tile_bytes) {
+    const int64_t n = std::max<int64_t>(1, (int64_t(1) << 30) / std::max<int64_t>(16, tile_bytes));
+    return int64_t(1) << (63 - __builtin_clzll((unsigned long long)n));
+}
 
 extern "C" int cbx_string_bound(const cbx_plan* P, int64_t n_rec, int64_t* out_bytes) {
     if (!P || n_rec < 0 || !out_bytes) return fail(CBX_E_ARGUMENT, "cbx_string_bound: invalid arguments");

@@ -437,6 +437,15 @@ __device__ __forceinline__ void num_group(const KernelArgs& a, const NumOp (&op)
 // front of the long ones (one scan places both: every lane takes 16 bytes or its length, so the
 // area a plan sizes for 64 values of the field -- at least 1 KiB -- holds the tile) and into the
 // view.  One pass, no scan across tiles, no placement kernel.
+// Data buffer of a tile and a position in it (tiles_per_buf is a power of two: a shift, not a
+// 64-bit division per element).
+__device__ __forceinline__ uint32_t view_buf(int64_t tile, const StrCall& c) {
+    return (uint32_t)(tile >> __builtin_ctzll((unsigned long long)c.tiles_per_buf));
+}
+__device__ __forceinline__ uint32_t view_pos(int64_t tile, const StrCall& c, uint32_t ex) {
+    return (uint32_t)((tile & (c.tiles_per_buf - 1)) * c.tile_cap + ex);
+}
+
 template <typename Sink>
 __device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrOp& op, int i, const StrCall& c, const TileCtx& t,
                                                  const StrSpan& sp, bool ok, bool fast, const uint32_t (&ev)[kStrFastBytes],
@@ -486,11 +495,22 @@ __device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrO
             const CBX_GLOBAL uint8_t* g = gp(region + ex);
             pre = (uint32_t)g[0] | (uint32_t)g[1] << 8 | (uint32_t)g[2] << 16 | (uint32_t)g[3] << 24;
         }
-        const int64_t tb = t.tile / c.tiles_per_buf;
-        v = u32x4{(uint32_t)len, pre, (uint32_t)tb, (uint32_t)((t.tile - tb * c.tiles_per_buf) * c.tile_cap + ex)};
+        v = u32x4{(uint32_t)len, pre, view_buf(t.tile, c), view_pos(t.tile, c, ex)};
     }
     (gp((u32x4*)c.views) + t.tile * kWave)[lane] = v;
     wave_sync_lds();   // the staging area is reused by the next element
+}
+
+// (byte k of w) * 4: the byte offset of its 4-byte LUT entry, one SDWA shift
+__device__ __forceinline__ uint32_t byte_x4(uint32_t w, int k) {
+    uint32_t r;
+    switch (k) {
+    case 0: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w)); break;
+    case 1: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w)); break;
+    case 2: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w)); break;
+    default: asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w)); break;
+    }
+    return r;
 }
 
 // Lane-private LDS slot of a register-path element in the view layout: its UTF-8 bytes (<= size *
@@ -516,7 +536,17 @@ __device__ __forceinline__ void str_view_fast(const KernelArgs& a, const StrOp& 
     const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
     uint32_t w[8], ev[kStrFastBytes];
     img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
+#ifndef CBX_STR_NO_SDWA
+    if (op.kind == CBX_K_STRING) {   // code page: LDS entries, byte offsets straight from the image dwords
+#pragma unroll
+        for (int j = 0; j < kStrFastBytes; j++)
+            ev[j] = j < op.size ? *(const uint32_t*)((const uint8_t*)s_lut + byte_x4(w[j >> 2], j & 3)) : 0u;
+    } else {
+        lut_entries32(w, op.size, [&](uint32_t b) { return ascii_lut(b); }, ev);
+    }
+#else
     lut_entries32(w, op.size, [&](uint32_t b) { return str_lut(op.kind, s_lut, b); }, ev);
+#endif
     uint32_t tm = 0;   // bit j: byte j trimmable (entry bit 31)
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++)
@@ -528,19 +558,20 @@ __device__ __forceinline__ void str_view_fast(const KernelArgs& a, const StrOp& 
     const uint32_t range = bits_below(e) & ~bits_below(b);
     const int width = op.pad;
     uint8_t* slot = s_str + lane * str_lane_slot(op.size, width);
-    uint32_t pos = 0;
+    uint8_t* p = slot;
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++) {
         if (j < op.size) {
             const uint32_t ej = ev[j];
-            uint8_t* p = slot + pos;
+            // byte stores: one unaligned 2-byte LDS store instead made SYNSTR200 2.8x slower (6.54 ->
+            // 18.3 ms, measured)
             p[0] = (uint8_t)ej;
             if (width > 1) p[1] = (uint8_t)(ej >> 8);
             if (width > 2) p[2] = (uint8_t)(ej >> 16);
-            pos += ((ej >> 24) & 3u) & (uint32_t)__builtin_amdgcn_sbfe((int)range, j, 1);
+            p += ((ej >> 24) & 3u) & (uint32_t)__builtin_amdgcn_sbfe((int)range, j, 1);
         }
     }
-    const int len = (int)pos;
+    const int len = (int)(p - slot);
     slot[len] = 0; slot[len + 1] = 0; slot[len + 2] = 0;   // the partial dword's tail
     constexpr int kNC = (kStrFastBytes * 3 + 15) / 16;
     u32x4 q[kNC];
@@ -574,8 +605,7 @@ __device__ __forceinline__ void str_view_fast(const KernelArgs& a, const StrOp& 
                 }
             }
         }
-        const int64_t tb = t.tile / c.tiles_per_buf;
-        v = u32x4{(uint32_t)len, q[0].x, (uint32_t)tb, (uint32_t)((t.tile - tb * c.tiles_per_buf) * c.tile_cap + ex)};
+        v = u32x4{(uint32_t)len, q[0].x, view_buf(t.tile, c), view_pos(t.tile, c, ex)};
     }
     (gp((u32x4*)c.views) + t.tile * kWave)[lane] = v;
 }

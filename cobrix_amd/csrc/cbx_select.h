@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void segid_view_kernel(SegIdArgs a, u32x4* vie
         if (j < k) w[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
     u32x4 v{n, w[0], w[1], w[2]};
     if (n > 12) {
-        const int64_t tb = tile / tiles_per_buf;
+        const int64_t tb = tile >> __builtin_ctzll((unsigned long long)tiles_per_buf);   // a power of two
         v.z = (uint32_t)tb;
         v.w = (uint32_t)((tile - tb * tiles_per_buf) * tile_bytes + ex);
     }

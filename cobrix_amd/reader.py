@@ -495,12 +495,13 @@ class _HostArray:
 
 def view_geometry(capacity: int, n_tiles: int) -> Tuple[int, int]:
     """String-view layout: (tile_bytes, buffer_bytes) of a slot region of `capacity` bytes for
-    n_tiles tiles (cbx_string_bound's capacity; buffers of whole tiles, at most 1 GiB each --
-    cbx_string_view_geometry)."""
+    n_tiles tiles (cbx_string_bound's capacity; buffers of a power-of-two number of whole tiles,
+    at most 1 GiB each unless one tile is larger -- cbx_string_view_geometry)."""
     if n_tiles <= 0 or capacity <= 0:
         return 0, 0
     tb = capacity // n_tiles
-    return tb, max(1, (1 << 30) // max(16, tb)) * tb
+    tpb = max(1, (1 << 30) // max(16, tb))
+    return tb, (1 << (tpb.bit_length() - 1)) * tb
 
 
 def decode_views(views: np.ndarray, data: bytes, buffer_bytes: int, region: int) -> List[bytes]:

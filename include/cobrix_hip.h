@@ -206,7 +206,8 @@ typedef struct {
  * data-buffer index and an int32 offset into that buffer.  `data` holds n_slots regions of
  * data_capacity bytes; a region is cut into data buffers of buffer_bytes (the last one shorter):
  * buffer k of slot s starts at data + s * data_capacity + k * buffer_bytes
- * (cbx_string_view_geometry).  Every tile of 64 records owns tile_bytes of its slot's region,
+ * (cbx_string_view_geometry: a power-of-two number of whole tiles, at most 1 GiB unless one tile
+ * is larger).  Long payloads start at 4-byte-aligned positions of their tile.  Every tile of 64 records owns tile_bytes of its slot's region,
  * so a value is written once, where the decode kernel produces it -- no scan over the batch and
  * no placement pass.  data_capacity must be at least ceil(n_rec / 64) * tile_bytes
  * (cbx_string_bound returns that in this layout; a smaller one fails the call with

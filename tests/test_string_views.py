@@ -36,8 +36,10 @@ def _views(values, tile_bytes, buffer_bytes):
 
 
 def test_view_geometry_rule():
-    # tile_bytes = capacity / tiles; buffers hold floor(1 GiB / tile_bytes) whole tiles
-    assert view_geometry(781_250 * 2560, 781_250) == (2560, (2 ** 30 // 2560) * 2560)
+    # tile_bytes = capacity / tiles; buffers hold a power-of-two number of whole tiles (<= 1 GiB)
+    # 2**30 // 2560 = 419,430 tiles fit; the buffer takes the largest power of two of them
+    assert view_geometry(781_250 * 2560, 781_250) == (2560, 262_144 * 2560)
+    assert view_geometry(64 * 4096, 64) == (4096, 2 ** 30)
     assert view_geometry(0, 10) == (0, 0)
     tb, bb = view_geometry(3 * (2 ** 30 + 16), 3)
     assert tb == 2 ** 30 + 16 and bb == tb   # a tile larger than 1 GiB is its own buffer
