@@ -514,8 +514,12 @@ __device__ __forceinline__ uint32_t byte_x4(uint32_t w, int k) {
 }
 
 // Lane-private LDS slot of a register-path element in the view layout: its UTF-8 bytes (<= size *
-// width) + the bytes written past them (<= 3).
-__host__ __device__ constexpr int str_lane_slot(int size, int width) { return (size * width + 3 + 15) & ~15; }
+// width) + the bytes written past them (<= 3), rounded to 8 bytes with an odd count of 8-byte
+// words -- lanes at the same position fall on different banks (2-way at most for the byte stores;
+// the 8-byte read-backs conflict-free), where a 16-byte multiple put lanes 8 apart on one bank.
+__host__ __device__ constexpr int str_lane_slot(int size, int width) {
+    return (((size * width + 3 + 7) >> 3) | 1) << 3;
+}
 
 // The view layout's register-path string element (fields of <= kStrFastBytes EBCDIC / ASCII bytes,
 // StringDecoders.decodeEbcdicString / decodeAsciiString + StringTools.trim*): every byte's LUT
@@ -576,8 +580,13 @@ __device__ __forceinline__ void str_view_fast(const KernelArgs& a, const StrOp& 
     constexpr int kNC = (kStrFastBytes * 3 + 15) / 16;
     u32x4 q[kNC];
 #pragma unroll
-    for (int k = 0; k < kNC; k++)
-        if (16 * k < op.size * width) q[k] = ((const u32x4*)slot)[k];
+    for (int k = 0; k < kNC; k++) {
+        if (16 * k < op.size * width) {   // 8-byte reads (the slot is 8-byte aligned)
+            const uint2 lo = ((const uint2*)slot)[2 * k];
+            const uint2 hi = 16 * k + 8 < op.size * width ? ((const uint2*)slot)[2 * k + 1] : make_uint2(0u, 0u);
+            q[k] = u32x4{lo.x, lo.y, hi.x, hi.y};
+        }
+    }
     sk.svalid(c, i, t.tile, __ballot(ok));
     const bool lng = len > 12;
     uint32_t tot;
