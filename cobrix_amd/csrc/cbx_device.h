@@ -528,44 +528,41 @@ __host__ __device__ constexpr int str_lane_slot(int size, int width) {
 // land where the next kept byte's go, or past the end.  No cross-lane staging and no wave barrier:
 // the lane builds its view from its slot, and a long payload (> 12 bytes) goes from registers to the
 // tile's region at a 4-byte-aligned packed position (exact dword counts, so lanes never overlap).
-template <typename Sink>
-__device__ __forceinline__ void str_view_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp, int i,
-                                              const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
-                                              const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
-                                              uint8_t* s_str, int lane, Sink& sk) {
-    bool el = t.active && (op.segment < 0 || op.segment == t.seg);
-    if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
-    const int o = a.start_off + op.eo;
-    const bool ok = el && o <= t.avail;
-    const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
+constexpr int kStrNC = (kStrFastBytes * 3 + 15) / 16;   // 16-byte words of a lane slot's read-back
+
+// The lane's field of a register-path view element: bytes [eo, eo + n) of its record (n <= size
+// <= smax; smax bounds the unrolled loops), composed in the lane's slot and read back into q.
+// Returns the UTF-8 length.
+__device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, int smax, int eo, int n, bool ok,
+                                                const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
+                                                uint8_t* s_str, int lane, u32x4 (&q)[kStrNC]) {
     uint32_t w[8], ev[kStrFastBytes];
-    img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
+    img_bytes32(src, rec_addr + (ok ? (uint32_t)eo : 0u), smax, w);
 #ifndef CBX_STR_NO_SDWA
-    if (op.kind == CBX_K_STRING) {   // code page: LDS entries, byte offsets straight from the image dwords
+    if (kind == CBX_K_STRING) {   // code page: LDS entries, byte offsets straight from the image dwords
 #pragma unroll
         for (int j = 0; j < kStrFastBytes; j++)
-            ev[j] = j < op.size ? *(const uint32_t*)((const uint8_t*)s_lut + byte_x4(w[j >> 2], j & 3)) : 0u;
+            ev[j] = j < smax ? *(const uint32_t*)((const uint8_t*)s_lut + byte_x4(w[j >> 2], j & 3)) : 0u;
     } else {
-        lut_entries32(w, op.size, [&](uint32_t b) { return ascii_lut(b); }, ev);
+        lut_entries32(w, smax, [&](uint32_t b) { return ascii_lut(b); }, ev);
     }
 #else
-    lut_entries32(w, op.size, [&](uint32_t b) { return str_lut(op.kind, s_lut, b); }, ev);
+    lut_entries32(w, smax, [&](uint32_t b) { return str_lut(kind, s_lut, b); }, ev);
 #endif
     uint32_t tm = 0;   // bit j: byte j trimmable (entry bit 31)
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++)
-        if (j < op.size) tm |= (ev[j] >> 31) << j;
+        if (j < smax) tm |= (ev[j] >> 31) << j;
     const uint32_t keep = ~tm & bits_below(n);
     int b = 0, e = n;
-    if (op.trim == CBX_TRIM_LEFT || op.trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;
-    if (op.trim == CBX_TRIM_RIGHT || op.trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
+    if (trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;
+    if (trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
     const uint32_t range = bits_below(e) & ~bits_below(b);
-    const int width = op.pad;
-    uint8_t* slot = s_str + lane * str_lane_slot(op.size, width);
+    uint8_t* slot = s_str + lane * str_lane_slot(smax, width);
     uint8_t* p = slot;
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++) {
-        if (j < op.size) {
+        if (j < smax) {
             const uint32_t ej = ev[j];
             // byte stores: one unaligned 2-byte LDS store instead made SYNSTR200 2.8x slower (6.54 ->
             // 18.3 ms, measured)
@@ -577,46 +574,108 @@ __device__ __forceinline__ void str_view_fast(const KernelArgs& a, const StrOp& 
     }
     const int len = (int)(p - slot);
     slot[len] = 0; slot[len + 1] = 0; slot[len + 2] = 0;   // the partial dword's tail
-    constexpr int kNC = (kStrFastBytes * 3 + 15) / 16;
-    u32x4 q[kNC];
 #pragma unroll
-    for (int k = 0; k < kNC; k++) {
-        if (16 * k < op.size * width) {   // 8-byte reads (the slot is 8-byte aligned)
+    for (int k = 0; k < kStrNC; k++) {
+        if (16 * k < smax * width) {   // 8-byte reads (the slot is 8-byte aligned)
             const uint2 lo = ((const uint2*)slot)[2 * k];
-            const uint2 hi = 16 * k + 8 < op.size * width ? ((const uint2*)slot)[2 * k + 1] : make_uint2(0u, 0u);
+            const uint2 hi = 16 * k + 8 < smax * width ? ((const uint2*)slot)[2 * k + 1] : make_uint2(0u, 0u);
             q[k] = u32x4{lo.x, lo.y, hi.x, hi.y};
         }
     }
+    return len;
+}
+
+// A long payload (len > 12) from registers to dst (4-byte aligned): exact dword count.
+__device__ __forceinline__ void str_store_long(CBX_GLOBAL uint8_t* dst, int len, int cap, const u32x4 (&q)[kStrNC]) {
+    typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+    const int n4 = (len + 3) >> 2;
+#pragma unroll
+    for (int k = 0; k < kStrNC; k++) {
+        if (16 * k < cap) {
+            const int r = n4 - 4 * k;
+            CBX_GLOBAL uint8_t* d = dst + 16 * k;
+            if (r >= 4) {
+                *(CBX_GLOBAL u32x4a*)d = u32x4a{q[k].x, q[k].y, q[k].z, q[k].w};
+            } else if (r >= 2) {
+                *(CBX_GLOBAL u32x2a*)d = u32x2a{q[k].x, q[k].y};
+                if (r == 3) ((CBX_GLOBAL uint32_t*)d)[2] = q[k].z;
+            } else if (r == 1) {
+                *(CBX_GLOBAL uint32_t*)d = q[k].x;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ u32x4 str_short_view(int len, const u32x4 (&q)[kStrNC]) {
+    return u32x4{(uint32_t)len, len > 0 ? q[0].x : 0u, len > 4 ? q[0].y : 0u, len > 8 ? q[0].z : 0u};
+}
+
+template <typename Sink>
+__device__ __forceinline__ void str_view_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp, int i,
+                                              const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
+                                              const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
+                                              uint8_t* s_str, int lane, Sink& sk) {
+    bool el = t.active && (op.segment < 0 || op.segment == t.seg);
+    if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
+    const int o = a.start_off + op.eo;
+    const bool ok = el && o <= t.avail;
+    const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
+    u32x4 q[kStrNC];
+    const int len = str_lane_compose(op.kind, op.trim, op.pad, op.size, op.eo, n, ok, src, rec_addr, s_lut, s_str, lane, q);
     sk.svalid(c, i, t.tile, __ballot(ok));
     const bool lng = len > 12;
     uint32_t tot;
     const uint32_t ex = wave_excl_scan32(lng ? (uint32_t)(len + 3) & ~3u : 0u, lane, tot);
     u32x4 v;
     if (!lng) {
-        v = u32x4{(uint32_t)len, len > 0 ? q[0].x : 0u, len > 4 ? q[0].y : 0u, len > 8 ? q[0].z : 0u};
+        v = str_short_view(len, q);
     } else {
-        typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
-        typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
-        CBX_GLOBAL uint8_t* dst = gp(c.scratch + t.tile * c.tile_cap + ex);
-        const int n4 = (len + 3) >> 2;
-#pragma unroll
-        for (int k = 0; k < kNC; k++) {
-            if (16 * k < op.size * width) {
-                const int r = n4 - 4 * k;
-                CBX_GLOBAL uint8_t* d = dst + 16 * k;
-                if (r >= 4) {
-                    *(CBX_GLOBAL u32x4a*)d = u32x4a{q[k].x, q[k].y, q[k].z, q[k].w};
-                } else if (r >= 2) {
-                    *(CBX_GLOBAL u32x2a*)d = u32x2a{q[k].x, q[k].y};
-                    if (r == 3) ((CBX_GLOBAL uint32_t*)d)[2] = q[k].z;
-                } else if (r == 1) {
-                    *(CBX_GLOBAL uint32_t*)d = q[k].x;
-                }
-            }
-        }
+        str_store_long(gp(c.scratch + t.tile * c.tile_cap + ex), len, op.size * op.pad, q);
         v = u32x4{(uint32_t)len, q[0].x, view_buf(t.tile, c), view_pos(t.tile, c, ex)};
     }
     (gp((u32x4*)c.views) + t.tile * kWave)[lane] = v;
+}
+
+// Two register-path view elements of mutually exclusive segment redefines (the same record bytes
+// read as fields of different segments, e.g. exp2's STATIC-DETAILS / CONTACTS) in one pass: each
+// lane composes the field of its record's segment, so the tile pays the byte loop once for the
+// pair (the longer field's).  The specialised kernel pairs them (cbx_jit.h: same kind, trim and
+// code page, no OCCURS); each column gets its validity word, the lane's view where its record holds
+// the field and a null view elsewhere; one wave scan places both columns' long payloads (16-bit
+// halves: a tile's payload per column is < 64 KiB).
+template <typename Sink>
+__device__ __forceinline__ void str_view_pair(const KernelArgs& a, const StrOp& A, int ia, const StrCall& ca,
+                                              const StrOp& B, int ib, const StrCall& cb, const TileCtx& t,
+                                              const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
+                                              uint8_t* s_str, int lane, Sink& sk) {
+    const bool sa = t.seg == A.segment;
+    const int eo = sa ? A.eo : B.eo, size = sa ? A.size : B.size;
+    const int smax = A.size > B.size ? A.size : B.size;
+    const int o = a.start_off + eo;
+    const bool ok = t.active && (sa || t.seg == B.segment) && o <= t.avail;
+    const int n = ok ? (size < t.avail - o ? size : t.avail - o) : 0;
+    u32x4 q[kStrNC];
+    const int len = str_lane_compose(A.kind, A.trim, A.pad, smax, eo, n, ok, src, rec_addr, s_lut, s_str, lane, q);
+    sk.svalid(ca, ia, t.tile, __ballot(ok && sa));
+    sk.svalid(cb, ib, t.tile, __ballot(ok && !sa));
+    const bool lng = len > 12;
+    uint32_t tot;
+    const uint32_t r4 = lng ? (uint32_t)(len + 3) & ~3u : 0u;
+    const uint32_t exb = wave_excl_scan32(sa ? r4 : r4 << 16, lane, tot);
+    const uint32_t ex = sa ? exb & 0xFFFFu : exb >> 16;
+    u32x4 v;
+    if (!lng) {
+        v = str_short_view(len, q);
+    } else {
+        CBX_GLOBAL uint8_t* dst = sa ? gp(ca.scratch + t.tile * ca.tile_cap + ex) : gp(cb.scratch + t.tile * cb.tile_cap + ex);
+        str_store_long(dst, len, smax * A.pad, q);
+        v = sa ? u32x4{(uint32_t)len, q[0].x, view_buf(t.tile, ca), view_pos(t.tile, ca, ex)}
+               : u32x4{(uint32_t)len, q[0].x, view_buf(t.tile, cb), view_pos(t.tile, cb, ex)};
+    }
+    const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+    (gp((u32x4*)ca.views) + t.tile * kWave)[lane] = sa ? v : z;
+    (gp((u32x4*)cb.views) + t.tile * kWave)[lane] = sa ? z : v;
 }
 
 // One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):

@@ -628,7 +628,14 @@ struct RdwStep {
 };
 
 __device__ __forceinline__ uint32_t rdw_header(const RdwArgs& a, int64_t pos) {
-    // 4 bytes at any alignment (caller guarantees pos + 4 <= n_bytes)
+    // 4 bytes at any alignment (caller guarantees pos + 4 <= n_bytes): the two dwords around them
+    // (two loads per header instead of four byte loads -- the walks' lanes hit 64 different lines
+    // per instruction), byte loads only where the second dword would pass the end of the input
+    // (dwords aligned in memory: the one holding data[pos] starts at most 3 bytes before it, in the
+    // same page as the input's first byte when pos < 4)
+    const uintptr_t u = (uintptr_t)(a.data + pos);
+    const uint32_t* q = (const uint32_t*)(u & ~(uintptr_t)3);
+    if ((const uint8_t*)q + 8 <= a.data + a.n_bytes) return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(u & 3));
     uint32_t w = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) w |= (uint32_t)a.data[pos + j] << (8 * j);

@@ -399,7 +399,9 @@ def _var_decode_vs_oracle(raw: bytes, views: bool, **kw):
 def test_var_span_kernel_vs_oracle(views):
     """The specialised span kernel (variable-length tiles staged by byte span, span_loop) on the C4
     layout, and on records of 1-3,000 bytes where many tiles overflow the span staging and fall
-    back to record-by-record windows (short records: trailing fields null / truncated)."""
+    back to record-by-record windows (short records: trailing fields null / truncated).  In the
+    view layout the C and P string fields are decoded in pairs (str_view_pair): lanes of either
+    segment, of neither, and short records in one pass."""
     from cobrix_amd.synth import rdw_narrow
     raw = rdw_narrow(20_000, seed=21)[0].numpy().tobytes()
     rd, errs = _var_decode_vs_oracle(raw, views, jit_min_records=1)
@@ -409,7 +411,8 @@ def test_var_span_kernel_vs_oracle(views):
     for i in range(5000):
         ln = int(rng.integers(1, 3000)) if rng.random() < 0.2 else int(rng.integers(1, 90))
         payload = bytearray(rng.integers(0x40, 0xFA, ln, dtype=np.uint8).tobytes())
-        payload[:5] = (b"\xC3" if i % 3 else b"\xD7") + b"\x40" * 4   # segment id C / P (cp037)
+        # segment id C / P (cp037), or X: a segment with no redefine (all its redefine fields null)
+        payload[:5] = (b"\xE7" if i % 7 == 0 else b"\xC3" if i % 3 else b"\xD7") + b"\x40" * 4
         payload = payload[:ln]
         body += bytes([0, 0, ln & 0xFF, ln >> 8]) + bytes(payload)
     rd, errs = _var_decode_vs_oracle(bytes(body), views, jit_min_records=1)
