@@ -62,6 +62,7 @@ struct cbx_plan {
     } cset, wset;
     bool contig_ok = true;       // every string element fits the single contiguous window
     int str_stage = 16;          // LDS payload staging bytes per wave
+    bool view_staged = false;    // view layout: some string field takes the staged byte-loop path
     cbx_plan_options opts;
     int n_columns = 0;
     int seg_col = -1;
@@ -461,8 +462,23 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     if (wmax > kMaxWindowBytes) wmax = kMaxWindowBytes;
     build_contig(P);
     build_windowed(P, wmax);
-    for (const Field& d : P->dfields_h)
-        if (d.variant == V_STRING) P->str_stage = std::max(P->str_stage, kWave * d.size * d.max_utf8);
+    // string staging per wave: the byte-loop / large-string paths stage a tile's payload (kWave *
+    // size * max_utf8, capped); the view layout's register path composes multi-byte code pages in
+    // lane slots (str_view_fast) and single-byte ones in registers (no LDS at all)
+    int slots = 0;
+    if (P->view) P->str_stage = 0;
+    for (const Field& d : P->dfields_h) {
+        if (d.variant != V_STRING) continue;
+        const bool fast = d.size <= kStrFastBytes && (d.kind == CBX_K_STRING || d.kind == CBX_K_STRING_ASCII);
+        if (P->view && fast) {
+            // (env CBX_STR_NO_SHIFT: single-byte pages through the slots too -- A/B runs; the
+            // specialised kernel then compiles the slot path for them, cbx_jit.h)
+            if (d.max_utf8 > 1 || getenv("CBX_STR_NO_SHIFT")) slots = std::max(slots, kWave * str_lane_slot(d.size, d.max_utf8));
+        } else {
+            P->str_stage = std::max(P->str_stage, kWave * d.size * d.max_utf8);
+            P->view_staged |= P->view;
+        }
+    }
     P->str_stage = std::min(P->str_stage, kStrStageBytes);
     for (const cbx_field& f : P->hfields) {
         if (f.flags & CBX_F_LIST) continue;   // the list kernel reads those
@@ -471,10 +487,7 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
         if (f.kind != CBX_K_RECORD_ID && f.kind != CBX_K_FILE_ID)
             P->rec_extent = std::max(P->rec_extent, (int)std::min<int64_t>(e, 1 << 30));
     }
-    if (P->view)   // the register path (fields of <= kStrFastBytes) composes in lane-private slots (str_view_fast)
-        for (const Field& d : P->dfields_h)
-            if (d.variant == V_STRING && d.size <= kStrFastBytes && (d.kind == CBX_K_STRING || d.kind == CBX_K_STRING_ASCII))
-                P->str_stage = std::max(P->str_stage, kWave * str_lane_slot(d.size, d.max_utf8));
+    P->str_stage = std::max(P->str_stage, slots);
 
     // ---- segment map: keys to UTF-8, Seg_IdN string columns
     cbx_segment_map sm = opts->segments;
@@ -677,7 +690,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.lds_counts = ((int)P->harrays.size() * kWave * 4 + 15) & ~15;   // OCCURS element counts
     // string-view layout: the inline slots (16 bytes per short value) share the area with the long
     // payloads, which it holds for any tile as long as it is at least 16 bytes per lane
-    a.str_stage = S.max_str_items > 0 ? (P->view && mode == 0 ? std::max(P->str_stage, 16 * kWave) : P->str_stage) : 0;
+    a.str_stage = S.max_str_items > 0 ? (P->view && mode == 0 && P->view_staged ? std::max(P->str_stage, 16 * kWave) : P->str_stage) : 0;
     // per-lane dump slots for the branch-free string stores (a shared slot serialises the wave's
     // LDS stores) -- unless the extra 4 * kWave bytes per wave cost a resident workgroup per CU
     // (wide windowed layouts sit close to the LDS limit; C5 decode 49.7 -> 62.1 ms with them)

@@ -535,6 +535,49 @@ constexpr int kStrNC = (kStrFastBytes * 3 + 15) / 16;   // 16-byte words of a la
 // Returns the UTF-8 length.
 __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, int smax, int eo, int n, bool ok,
                                                 const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
+                                                uint8_t* s_str, int lane, u32x4 (&q)[kStrNC]);
+
+// Single-byte code pages: the kept bytes [b, e) are the mapped bytes shifted down by b -- packed
+// into dwords, a 3-stage dword shift by b / 4 and one byte align, in registers (no LDS).
+__device__ __forceinline__ int str_lane_shift(int smax, const uint32_t (&ev)[kStrFastBytes], int b, int e,
+                                              u32x4 (&q)[kStrNC]) {
+    uint32_t s[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        uint32_t v = 0;
+        if (k < 8) {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (4 * k + u < smax) v |= (ev[4 * k + u] & 0xFFu) << (8 * u);
+        }
+        s[k] = v;
+    }
+    // the stages as bit blends on sbfe masks (0 / ~0): written as selects, the compiler turned the
+    // network into a lane-indexed array in scratch
+    const int qd = b >> 2;
+    const uint32_t m4 = (uint32_t)__builtin_amdgcn_sbfe(qd, 2, 1), m2 = (uint32_t)__builtin_amdgcn_sbfe(qd, 1, 1),
+                   m1 = (uint32_t)__builtin_amdgcn_sbfe(qd, 0, 1);
+#pragma unroll
+    for (int k = 0; k < 12; k++) s[k] = (s[k + 4] & m4) | (s[k] & ~m4);
+#pragma unroll
+    for (int k = 0; k < 10; k++) s[k] = (s[k + 2] & m2) | (s[k] & ~m2);
+#pragma unroll
+    for (int k = 0; k < 9; k++) s[k] = (s[k + 1] & m1) | (s[k] & ~m1);
+    const int len = e - b;
+    uint32_t o[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t x = __builtin_amdgcn_alignbyte(s[k + 1], s[k], (uint32_t)(b & 3));
+        const int r = len - 4 * k;   // bytes of this dword inside the value
+        o[k] = r >= 4 ? x : r <= 0 ? 0u : x & ((1u << (8 * r)) - 1u);
+    }
+    q[0] = u32x4{o[0], o[1], o[2], o[3]};   // <= 32 bytes: the other words are never read (cap)
+    q[1] = u32x4{o[4], o[5], o[6], o[7]};
+    return len;
+}
+
+__device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, int smax, int eo, int n, bool ok,
+                                                const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
                                                 uint8_t* s_str, int lane, u32x4 (&q)[kStrNC]) {
     uint32_t w[8], ev[kStrFastBytes];
     img_bytes32(src, rec_addr + (ok ? (uint32_t)eo : 0u), smax, w);
@@ -557,6 +600,9 @@ __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, i
     int b = 0, e = n;
     if (trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;
     if (trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
+#ifndef CBX_STR_NO_SHIFT
+    if (width == 1) return str_lane_shift(smax, ev, b, e, q);
+#endif
     const uint32_t range = bits_below(e) & ~bits_below(b);
     uint8_t* slot = s_str + lane * str_lane_slot(smax, width);
     uint8_t* p = slot;
