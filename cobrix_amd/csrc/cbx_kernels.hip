@@ -803,9 +803,45 @@ __device__ __forceinline__ RdwChunk rdw_chunk(const RdwChunkArgs& c, int64_t k) 
 // First q in [s, e) that starts a strictly plausible chain.  A strict header has two zero bytes
 // (LE: bytes 0-1, BE: bytes 2-3), so only zero-byte pairs are candidates: the chunk is scanned
 // a dword at a time with an exact zero-byte mask, and the chain test runs on candidates only.
+__device__ __forceinline__ uint32_t zero_bytes4(uint32_t x) {   // bit j: byte j of x is zero
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
 __device__ int64_t rdw_strict_scan(const RdwArgs& a, int64_t s, int64_t e, int64_t re) {
     const int64_t off = a.p.big_endian ? 2 : 0;
     const int64_t p0 = s + off, p1 = e + off;          // pair start positions [p0, p1)
+    if (((uintptr_t)a.data & 15) == 0) {
+        // 16 bytes per step with the next 16 prefetched: a chunk of long records (C5: 16 KB) is
+        // scanned for kilobytes before its first header, and the scan is a chain of loads
+        int64_t w = p0 & ~(int64_t)15;
+        auto load = [&](int64_t q) -> uint4 {
+            if (q + 16 <= a.n_bytes) return *(const uint4*)(a.data + q);
+            uint32_t d[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};   // past the end: not zero
+            for (int j = 0; j < 16 && q + j < a.n_bytes; j++)
+                d[j >> 2] = (d[j >> 2] & ~(0xFFu << (8 * (j & 3)))) | ((uint32_t)a.data[q + j] << (8 * (j & 3)));
+            return make_uint4(d[0], d[1], d[2], d[3]);
+        };
+        uint4 cur = w < a.n_bytes ? load(w) : make_uint4(1u, 1u, 1u, 1u);
+        uint32_t carry = 0;                             // byte w-1 is zero
+        for (; w < p1 && w < a.n_bytes; w += 16) {
+            const uint4 nxt = w + 16 < p1 && w + 16 < a.n_bytes ? load(w + 16) : make_uint4(1u, 1u, 1u, 1u);
+            const uint32_t zb = zero_bytes4(cur.x) | zero_bytes4(cur.y) << 4 | zero_bytes4(cur.z) << 8 | zero_bytes4(cur.w) << 12;
+            // pairs starting at w-1 .. w+14 (bit i <-> position w - 1 + i)
+            uint32_t pairs = (carry & zb) | ((zb & (zb >> 1)) << 1);
+            carry = zb >> 15;
+            while (pairs) {
+                const int i = __builtin_ctz(pairs);
+                pairs &= pairs - 1;
+                const int64_t p = w - 1 + i;
+                if (p < p0 || p >= p1) continue;
+                const int64_t q = p - off;
+                if (rdw_plausible(a, q, re, true)) return q;
+            }
+            cur = nxt;
+        }
+        return -1;
+    }
     uint32_t carry = 0;                                 // byte w-1 is zero
     for (int64_t w = p0 & ~(int64_t)3; w < p1 && w < a.n_bytes; w += 4) {
         uint32_t zb = 0;                                // bit j: byte w + j is zero
