@@ -817,9 +817,10 @@ __device__ int64_t rdw_strict_scan(const RdwArgs& a, int64_t s, int64_t e, int64
         int64_t w = p0 & ~(int64_t)15;
         auto load = [&](int64_t q) -> uint4 {
             if (q + 16 <= a.n_bytes) return *(const uint4*)(a.data + q);
-            uint32_t d[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};   // past the end: not zero
-            for (int j = 0; j < 16 && q + j < a.n_bytes; j++)
-                d[j >> 2] = (d[j >> 2] & ~(0xFFu << (8 * (j & 3)))) | ((uint32_t)a.data[q + j] << (8 * (j & 3)));
+            uint32_t d[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < 16; j++)   // past the end: 1, not a zero byte
+                d[j >> 2] |= (q + j < a.n_bytes ? (uint32_t)a.data[q + j] : 1u) << (8 * (j & 3));
             return make_uint4(d[0], d[1], d[2], d[3]);
         };
         uint4 cur = w < a.n_bytes ? load(w) : make_uint4(1u, 1u, 1u, 1u);
