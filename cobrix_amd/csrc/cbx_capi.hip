@@ -674,7 +674,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         // conflicts on the per-lane dword reads (gcd(stride_dw, 32) >= 4); 2-way is cheaper
         // than the dword scatter padding costs
         const int g = std::__gcd(sdw, 32);
-        a.cpitch = 4 * (g >= 4 ? ((sdw & 1) ? sdw : sdw + 1) : sdw);
+        a.cpitch = 4 * ((g >= 4 || (g == 2 && getenv("CBX_PAD_ROWS"))) ? ((sdw & 1) ? sdw : sdw + 1) : sdw);   // env: A/B
         a.inv_stride_dw = 1.0f / (float)sdw;
         a.lds_rows = kGuard + kWave * a.cpitch + 16 + kGuard;
     } else {
