@@ -1,30 +1,40 @@
 """Benchmark: GPU decode of the BASELINE.json configs (default: config C2, SYN200 numeric mix).
 
 `python bench.py --gpus N --steps K --warmup W [--workload syn200|synstr200|rdw_narrow|wide_odo]`
--- one rank per GPU (torchrun for N > 1); each rank decodes its own shard of records already
-resident in HBM (weak scaling: records are independent, shards need no data-path collective;
-fixed-length shards know their Record_Id base statically, variable-length shards get it from one
-RCCL all-gather of their framed record counts per step).  Rank 0 prints ONE JSON line.
+-- one rank per GPU.  With N > 1 and no torchrun environment, bench.py starts the N ranks itself
+(`python -m torch.distributed.run --nproc-per-node N ... bench.py`, before anything touches a GPU)
+and exits with their status; under torchrun (the driver's launch) it checks WORLD_SIZE == N.
+Rank 0 prints ONE JSON line.
+
+Shards, weak scaling -- the per-GPU work is fixed as N grows:
+  fixed-length (C2, C3): rank r decodes records [r n, (r + 1) n) of an N n-record job; the
+      Record_Id base r n is static, there is no collective on the data path;
+  variable-length (C4, C5): ONE RDW file of N blocks (block b generated with seed + b) is indexed
+      once at setup (GPU framing + cbx_sparse_index, untimed like the reference's index job); rank r
+      takes the contiguous run of index entries shard.entry_shards gives it (balanced by bytes) and
+      keeps only those bytes.  A step frames the run from its entries' offsets, all-gathers the
+      run's record count on the device (RCCL, int64 per rank), and decodes with the exclusive
+      prefix as its Record_Id base -- a device pointer (cbx_plan_set_record_base), no host read.
 
 A step = one full decode of the shard through the C ABI:
-  fixed-length (C2 syn200, C3 synstr200): `cbx_decode_fixed` -- decode kernel (numerics and
-      strings; with the default --strings views every string value is written once, into an Arrow
-      string view + its tile's data region) + fixup kernel for deferred values (--strings offsets:
-      Arrow large-string offsets, + string scan and placement kernels);
-  variable-length (C4 rdw_narrow, C5 wide_odo): `cbx_frame_rdw` (GPU RDW offset discovery seeded
-      by the sparse-index entries cbx_sparse_index cut at setup, 100 MB at root segments) +
-      `cbx_decode_var` (segment redefines, ODO); for N > 1 one all-gather of the shard's record count
-      between framing and decode gives its Record_Id base.
+  fixed-length: `cbx_decode_fixed` -- decode kernel + fixup of deferred values (+ string scan and
+      placement in the large-string layout);
+  variable-length: `cbx_frame_rdw` (RDW offset discovery seeded by the shard's index entries) +
+      `cbx_decode_var`.
 
-roofline: algorithmic bytes (input record bytes + every output buffer byte of the
-layout produced -- validity bits, values, 16-byte string views + the payload of views longer than
-12 bytes, or int64 offsets + payload) of one decode-kernel launch / its average duration, measured
-with HIP events recorded by the library on the launch stream over the timed steps
-(cbx_plan_kernel_times).
+roofline: algorithmic bytes = input bytes + for every output value its Arrow
+width (int32 4, int64 8, decimal <= 18 digits 8, <= 38 16, float 4, double 8), 1 validity bit per
+value, strings as UTF-8 payload + a 4-byte offset per value, OCCURS DEPENDING ON lists as a 4-byte
+offset per list; absent ODO elements count nothing.  The layout actually written (16-byte string
+views, int64 offsets, count / segment columns) is reported as `layout_overhead` beside it, never in
+`achieved`.  achieved = algorithmic bytes / the decode kernel's average duration (HIP events recorded
+by the library on the launch stream over the timed steps, cbx_plan_kernel_times); the rocprofv3
+summary of the same command is committed under profiles/ (tools/gpu_r03.sh).
 
-end_to_end (fixed-length workloads, N = 1 view per rank): the same shard streamed from pinned host
-memory -- H2D copies of 2.5M-record chunks on a copy stream overlapped with the decode of the
-previous chunk on the decode stream (double-buffered) -- reported beside `value`, never as it.
+end_to_end (N = 1): the same shard streamed from pinned host memory -- fixed-length: 2.5 M-record
+chunks; variable-length: pieces of whole index entries (their offsets seed the framing of the
+piece) -- H2D on a copy stream overlapped with the framing / decode of the previous piece on the
+decode stream (double-buffered); reported beside `value`, never as it.
 """
 from __future__ import annotations
 
@@ -39,27 +49,109 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_MEASURED_GBS = 6300.0  # achievable (MI355X_MICROARCH.md, HBM)
 METRIC = "decoded input GB/s + records/s, fixed-len COMP-3 mix, 1-8 MI355X; % HBM peak"
 
 
-def algorithmic_bytes(plan, n_rec: int, in_bytes: int, payload_bytes: int, present=None) -> int:
-    """input bytes + every output buffer byte one decode writes (payload_bytes: the
-    string payload written to data buffers -- all of it in the offsets layout, the values longer
-    than 12 bytes in the view layout).  present[column]: elements that exist (OCCURS DEPENDING ON:
-    the records' element counts) -- absent elements are not algorithmic output, whatever the
-    slot-major layout writes for them."""
+# ------------------------------------------------------------------------------------------------
+# SURVEY.md 8(d) byte counts
+# ------------------------------------------------------------------------------------------------
+def _valid_mask(c, n_slots: int, n_rec: int):
+    """Validity bits of the n_rec records of every slot row as a bool tensor [n_slots, n_rec]."""
+    import torch
+    pw = (n_rec + 63) // 64
+    b = c["validity"][: n_slots * pw].view(torch.uint8).view(n_slots, pw * 8)
+    bits = (b.unsqueeze(-1) >> torch.arange(8, device=b.device, dtype=torch.uint8)) & 1
+    return bits.view(n_slots, pw * 64)[:, :n_rec].bool()
+
+
+def string_payload(plan, cols, n_rec: int) -> dict:
+    """Per string column: UTF-8 payload bytes of the batch's values (all of them, whatever the layout:
+    the view lengths, or the offsets layout's per-slot sizes)."""
+    import torch
     from cobrix_amd import native as N
-    total = in_bytes + payload_bytes
-    views = bool(plan.options.string_views)
-    present = present or {}
-    for info in plan.columns:
-        n = present.get(info.index, n_rec * info.n_slots)
-        total += (n + 7) // 8                                   # validity bits
-        if info.out_type in (N.O_STRING, N.O_BINARY):
-            total += 16 * n if views else 8 * (n + info.n_slots)   # views / int64 offsets (n_rec + 1 per slot)
+    out = {}
+    pitch = 64 * ((n_rec + 63) // 64)
+    for ci, info in enumerate(plan.columns):
+        if info.out_type not in (N.O_STRING, N.O_BINARY):
+            continue
+        c = cols[ci]
+        if "sizes" in c:
+            out[ci] = int(c["sizes"].sum().item())
+        elif "views" in c:
+            ln = c["views"].view(-1, pitch, 16)[:, :n_rec, :4].contiguous().view(torch.int32).view(info.n_slots, n_rec)
+            out[ci] = int((ln.to(torch.int64) * _valid_mask(c, info.n_slots, n_rec)).sum().item())
+        elif "offsets32" in c:
+            offs = c["offsets32"].view(info.n_slots, pitch + 1)
+            out[ci] = int((offs[:, n_rec].to(torch.int64) - offs[:, 0].to(torch.int64)).sum().item())
+    return out
+
+
+def present_elements(plan, cols, n_rec: int):
+    """Per value column under one OCCURS DEPENDING ON level: the elements the records hold (the sum
+    of the array's valid counts); columns under fixed OCCURS or deeper nesting keep every slot."""
+    import torch
+    out = {}
+    for f in plan.fields:
+        if f.n_dims != 1:
+            continue
+        ar = plan.arrays[f.dim_array[0]]
+        if ar.dependee < 0 or ar.count_column < 0:
+            continue
+        cnt = cols[ar.count_column]["values"][:n_rec].to(dtype=torch.int64)
+        if ar.segment >= 0 and plan.segment_column >= 0:   # arrays of an inactive segment redefine are absent
+            seg = cols[plan.segment_column]["values"][:n_rec]
+            cnt = cnt * (seg == ar.segment)
+        out[f.column] = int(cnt.sum().item())
+    return out
+
+
+def algorithmic_bytes(plan, n_rec: int, in_bytes: int, payload: dict, present: dict) -> int:
+    """input + Arrow output bytes (see the module docstring), independent of the layout
+    the library writes."""
+    from cobrix_amd import native as N
+    total = in_bytes
+    for ci, info in enumerate(plan.columns):
+        n = present.get(ci, n_rec * info.n_slots)
+        if info.kind == "count":
+            # one list per (record, enclosing slot): a 4-byte offset + a validity bit
+            total += 4 * n + (n + 7) // 8
+        elif info.kind in ("list_offsets", "segment"):
+            continue                     # the list offsets are the count's; the segment index is the structs' bit
+        elif info.out_type in (N.O_STRING, N.O_BINARY):
+            total += 4 * n + payload.get(ci, 0) + (n + 7) // 8
+        else:
+            total += n * N.OUT_WIDTH[info.out_type] + (n + 7) // 8
+    total += len(plan.segment_groups) * ((n_rec + 7) // 8)   # validity of each segment-redefine struct
+    return total
+
+
+def layout_bytes(plan, cols, n_rec: int, in_bytes: int, payload: dict, present: dict) -> int:
+    """Bytes the chosen layout writes for the same batch (views / int64 offsets / count, list-offset
+    and segment columns, padded list runs): the algorithmic count plus the layout's overhead."""
+    from cobrix_amd import native as N
+    total = in_bytes
+    pitch = 64 * ((n_rec + 63) // 64)
+    for ci, info in enumerate(plan.columns):
+        c = cols[ci]
+        n = n_rec * info.n_slots if info.list_array < 0 else present.get(ci, n_rec * info.n_slots)
+        total += (n + 7) // 8
+        if "views" in c:
+            total += 16 * n + _long_view_payload(c, info.n_slots, n_rec, pitch)
+        elif "offsets" in c:
+            total += 8 * (n + info.n_slots) + payload.get(ci, 0)
+        elif "offsets32" in c:
+            total += 4 * (n + info.n_slots) + payload.get(ci, 0)
         else:
             total += n * N.OUT_WIDTH[info.out_type]
     return total
+
+
+def _long_view_payload(c, n_slots: int, n_rec: int, pitch: int) -> int:
+    import torch
+    ln = c["views"].view(-1, pitch, 16)[:, :n_rec, :4].contiguous().view(torch.int32).view(n_slots, n_rec)
+    ln = ln * _valid_mask(c, n_slots, n_rec)
+    return int(torch.where(ln > 12, ln, 0).to(torch.int64).sum().item())
 
 
 def _round_key(path: str):
@@ -71,7 +163,7 @@ def _round_key(path: str):
 
 def measured_traffic(tag: str):
     """HBM bytes per decode-kernel launch from the newest committed rocprofv3 FETCH_SIZE/WRITE_SIZE
-    passes of this configuration (tools/gpu_profile.sh -> profiles/<round tag>/traffic_<tag>.json)."""
+    passes of this configuration (tools/gpu_r03.sh -> profiles/<round tag>/traffic_<tag>.json)."""
     import glob
     found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_{tag}.json")), key=_round_key)
     if not found:
@@ -85,31 +177,39 @@ def measured_traffic(tag: str):
 # workloads
 # ------------------------------------------------------------------------------------------------
 WORKLOADS = {
-    "syn200": dict(records=50_000_000, config="C2",
+    "syn200": dict(records=50_000_000, config="C2", strings="views",
                    desc="SYN200: fixed-length 200-byte EBCDIC records, numeric mix (COMP, COMP-3, zoned DISPLAY "
                         "overpunch, IBM COMP-2, cp037 X(18)) -- BASELINE config C2",
                    data="synthetic (cobrix_amd/synth.py SYN200, seed 20261015+rank, 0.5% malformed numerics)"),
-    "synstr200": dict(records=50_000_000, config="C3",
-                      desc="SYNSTR200: fixed-length 200-byte records, 10 x PIC X(20) cp037 -> UTF-8, trim both, "
-                           "Arrow string offsets -- BASELINE config C3",
+    "synstr200": dict(records=50_000_000, config="C3", strings="views",
+                      desc="SYNSTR200: fixed-length 200-byte records, 10 x PIC X(20) cp037 -> UTF-8, trim both "
+                           "-- BASELINE config C3",
                       data="synthetic (cobrix_amd/synth.py SYNSTR200: lengths 0-20, 25% accented, 10% leading "
                            "spaces, 1% control bytes)"),
-    "rdw_narrow": dict(records=150_000_000, config="C4",
-                       desc="RDW multisegment file, exp2/test5 layout (C 68 B / P 64 B records, segment redefines), "
-                            "GPU RDW offset discovery seeded every 100 MB + var-len decode -- BASELINE config C4",
-                       data="synthetic (cobrix_amd/synth.py rdw_narrow, 35% root segments)"),
-    "wide_odo": dict(records=770_000, config="C5",
+    "rdw_narrow": dict(records=150_000_000, config="C4", strings="views",
+                       desc="RDW multisegment file, exp2/test5 layout (C 68 B / P 64 B records, segment redefines, "
+                            "File_Id + Record_Id), GPU RDW offset discovery seeded by sparse-index entries + var-len "
+                            "decode -- BASELINE config C4",
+                       data="synthetic (cobrix_amd/synth.py rdw_narrow, 35% root segments; one file of N blocks)"),
+    "wide_odo": dict(records=770_000, config="C5", strings="views",
                      desc="Wide multisegment RDW file (exp3 layout + OCCURS 0 TO 2000 DEPENDING ON, 16,070 B roots, "
-                          "64 B children) -- BASELINE config C5 (per-GPU shard of the 8-GPU job)",
-                     data="synthetic (cobrix_amd/synth.py wide_odo, element counts uniform 0-2000, 0-4 children)"),
+                          "64 B children, File_Id + Record_Id) -- BASELINE config C5 (per-GPU shard of the 8-GPU job)",
+                     data="synthetic (cobrix_amd/synth.py wide_odo, element counts uniform 0-2000, 0-4 children; "
+                          "one file of N blocks)"),
+}
+
+STRING_LAYOUTS = {
+    "views": "Arrow string views (16 B views + long payloads, one pass)",
+    "offsets": "Arrow large-string (int64 offsets + payload)",
 }
 
 
 class _Fixed:
-    def __init__(self, name, n_rec, dev, rank, window, views):
+    def __init__(self, name, n_rec, dev, rank, window, strings):
         import torch
         from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters
         from cobrix_amd import synth
+        views = strings == "views"
         if name == "syn200":
             cb, self.stride = synth.SYN200_COPYBOOK, synth.SYN200_RECORD_SIZE
             self.rec = synth.syn200(n_rec, seed=20261015 + rank, device=dev).view(-1)
@@ -122,6 +222,7 @@ class _Fixed:
         self.rd = FixedLenNestedReader(cb, params)
         self.n_rec, self.in_bytes, self.dev = n_rec, n_rec * self.stride, dev
         self.record_base = rank * n_rec
+        self.shard_note = f"records [{rank} n, {rank + 1} n) of the job, Record_Id base static"
 
     def prepare(self, stream):
         from cobrix_amd import native as N
@@ -135,6 +236,9 @@ class _Fixed:
         # fixed-length shards: rank r holds records [r n, (r + 1) n) -- the Record_Id base is static
         N.check(self.L.cbx_decode_fixed(self.h, self.rec.data_ptr(), self.n_rec, self.stride, 0, self.record_base,
                                         self.cs, self.stream))
+        return None
+
+    def verify(self, world):
         return None
 
     def end_to_end(self, chunk_rec: int = 2_500_000, passes: int = 2):
@@ -185,81 +289,98 @@ class _Fixed:
                 "how": f"{n_chunks} chunks of {chunk_rec} records: pinned-host H2D on a copy stream overlapped with "
                        "cbx_decode_fixed of the previous chunk (double-buffered), per rank"}
 
-    def payload(self):
-        return _payload(self.cols, self.n_rec)
 
-
-def present_elements(plan, cols, n_rec: int):
-    """Per value column under one OCCURS DEPENDING ON level: the elements the records hold (the sum
-    of the array's count column); columns under fixed OCCURS or deeper nesting keep every slot."""
+def _frame_rdw(L, data, n_bytes, seeds, prm, cap, dev, stream):
+    """cbx_frame_rdw into fresh (offsets, lengths) tensors of `cap` records -> (off, len, n)."""
     import torch
-    out = {}
-    for f in plan.fields:
-        if f.n_dims != 1:
-            continue
-        ar = plan.arrays[f.dim_array[0]]
-        if ar.dependee < 0 or ar.count_column < 0:
-            continue
-        cnt = cols[ar.count_column]["values"][:n_rec].to(dtype=torch.int64)
-        if ar.segment >= 0 and plan.segment_column >= 0:   # arrays of an inactive segment redefine are absent
-            seg = cols[plan.segment_column]["values"][:n_rec]
-            cnt = cnt * (seg == ar.segment)
-        out[f.column] = int(cnt.sum().item())
-    return out
-
-
-def _payload(cols, n_rec: int) -> int:
-    """String payload bytes the last decode wrote to data buffers: per-slot sizes (offsets layout)
-    or the lengths of views longer than 12 bytes (view layout)."""
-    import torch
-    tot = 0
-    for c in cols:
-        if "sizes" in c:
-            tot += int(c["sizes"].sum().item())
-        elif "views" in c:
-            pitch = 64 * ((n_rec + 63) // 64)
-            ln = c["views"].view(-1, pitch, 16)[:, :n_rec].reshape(-1, 16)[:, :4].contiguous().view(torch.int32).view(-1)
-            tot += int(torch.where(ln > 12, ln, 0).to(torch.int64).sum().item())
-    return tot
+    from cobrix_amd import native as N
+    off = torch.empty(max(1, cap), dtype=torch.int64, device=dev)
+    ln = torch.empty(max(1, cap), dtype=torch.int32, device=dev)
+    sd = (ctypes.c_int64 * len(seeds))(*seeds)
+    n = ctypes.c_int64(0)
+    N.check(L.cbx_frame_rdw(data.data_ptr(), n_bytes, sd, len(seeds), ctypes.byref(prm), off.data_ptr(),
+                            ln.data_ptr(), cap, ctypes.byref(n), stream))
+    return off, ln, n.value
 
 
 class _VarLen:
-    """C4 / C5: one file (per rank: its shard, a contiguous run of the global file's index entries).
+    """C4 / C5: one RDW file of `world` blocks; this rank keeps the bytes of its run of index entries.
 
-    Setup (untimed, as the reference's index pass is a separate Spark job): the shard is framed
-    once on the GPU from its start and cut into sparse-index entries by cbx_sparse_index (100 MB
-    entries at root segments); the entries' offsets seed every step's framing.  A step = RDW framing
-    seeded by the entries + (N > 1) one all-gather of the shard's record count, whose exclusive
-    prefix is the shard's Record_Id base (cobrix_amd/shard.py record_bases) + decode."""
+    Setup (untimed, as the reference's index pass is a separate Spark job): the file is framed on the
+    GPU (the block starts are known record boundaries and seed the walk with the file start) and cut
+    into sparse-index entries by cbx_sparse_index (`seed_mb`: the 100 MB default, reset at each entry,
+    or a 32 MB block size, subtracted -- VarLenNestedReader.scala:237-243) at root segments.  A step =
+    RDW framing of the run seeded by its entries + (N > 1) one device all-gather of the run's record
+    count, whose exclusive prefix is the run's Record_Id base + decode."""
 
-    def __init__(self, name, n_rec, dev, rank, window, views, lists=True):
+    def __init__(self, name, n_rec, dev, rank, world, window, strings, lists=True, seed_mb=100):
         import torch
+        from cobrix_amd import native as N
         from cobrix_amd import synth
         from cobrix_amd.reader import ReaderParameters, VarLenNestedReader
+        from cobrix_amd.shard import entry_shards
         if name == "rdw_narrow":
-            self.raw, hdr = synth.rdw_narrow_large(n_rec, seed=20261016 + rank, device=dev)
+            gen = lambda b: synth.rdw_narrow_large(n_rec, seed=20261016 + b, device=dev)  # noqa: E731
             cb, segs = synth.RDW_NARROW_COPYBOOK, synth.RDW_NARROW_SEGMENTS
         else:
-            self.raw, hdr = synth.wide_odo(n_rec, seed=20261018 + rank, device=dev)
+            gen = lambda b: synth.wide_odo(n_rec, seed=20261018 + b, device=dev)  # noqa: E731
             cb, segs = synth.WIDE_ODO_COPYBOOK, synth.WIDE_ODO_SEGMENTS
-        self.in_bytes = int(self.raw.numel())
-        self.n_expected = int(hdr.numel())
-        del hdr
+        self.dev, self.world, self.rank = dev, world, rank
+        L = N.load()
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        # the file: blocks 0..world-1 back to back (sizes first, then generated in place: bounded memory)
+        if world == 1:
+            full, hdr = gen(0)
+            starts, n_total = [0], int(hdr.numel())
+            del hdr
+        else:
+            sizes, counts = [], []
+            for b in range(world):
+                o, h = gen(b)
+                sizes.append(int(o.numel()))
+                counts.append(int(h.numel()))
+                del o, h
+            starts = [sum(sizes[:b]) for b in range(world)]
+            full = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
+            for b in range(world):
+                o, _ = gen(b)
+                full[starts[b]:starts[b] + sizes[b]].copy_(o)
+                del o
+            n_total = sum(counts)
         torch.cuda.synchronize()
+        total_bytes = int(full.numel())
+        opts = dict(is_record_sequence=True, segment_field="SEGMENT-ID", segment_id_redefine_map=segs,
+                    window_bytes=window, string_views=strings == "views", occurs_lists=lists, generate_record_id=True)
+        self.rd = VarLenNestedReader(cb, ReaderParameters(**opts))
         # segment_id_root only shapes the index (cuts at roots); the decode plan is the C4/C5 one
-        self.rd = VarLenNestedReader(cb, ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
-                                                          segment_id_redefine_map=segs, window_bytes=window,
-                                                          string_views=views, occurs_lists=lists))
-        idx_rd = VarLenNestedReader(cb, ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
-                                                         segment_id_levels=["C"], input_split_size_mb=100))
+        ip = dict(is_record_sequence=True, segment_field="SEGMENT-ID", segment_id_levels=["C"])
+        if seed_mb != 100:
+            ip["hdfs_default_block_size_mb"] = seed_mb     # a block size: subtracted (VarLenNestedReader.scala:237-243)
+        idx_rd = VarLenNestedReader(cb, ReaderParameters(**ip))
+        self.prm = self.rd.rdw_params()
         t0 = time.perf_counter()
-        off, ln = idx_rd.frame(self.raw, self.in_bytes)
-        self.entries = idx_rd.generate_index(self.raw, self.in_bytes, off, ln)
+        off, ln, nf = _frame_rdw(L, full, total_bytes, starts, self.prm, n_total + 1, dev, st)
+        if nf != n_total:
+            raise RuntimeError(f"setup framing found {nf} records, the generator wrote {n_total}")
+        entries = idx_rd.generate_index(full, total_bytes, off[:nf], ln[:nf])
         torch.cuda.synchronize()
         self.index_ms = (time.perf_counter() - t0) * 1e3
-        self.seeds = [e.offset_from for e in self.entries]
-        del off, ln, idx_rd
-        self.dev = dev
+        k0, k1 = entry_shards(entries, total_bytes, world)[rank]
+        lo = entries[k0].offset_from if k0 < len(entries) else total_bytes
+        hi = entries[k1].offset_from if k1 < len(entries) else total_bytes
+        hdr_off = off[:nf] - 4                               # RDW header offsets of the framed records
+        self.expected_base = int(torch.searchsorted(hdr_off, torch.tensor([lo], device=dev)).item())
+        self.n_expected = int(torch.searchsorted(hdr_off, torch.tensor([hi], device=dev)).item()) - self.expected_base
+        self.raw = full[lo:hi].clone() if world > 1 else full
+        self.in_bytes = hi - lo
+        self.seeds = [e.offset_from - lo for e in entries[k0:k1]] or [0]
+        self.n_entries_file, self.entry_run = len(entries), (k0, k1)
+        self.seed_mb = seed_mb
+        del full, off, ln, hdr_off, idx_rd
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        self.shard_note = (f"entries [{k0}, {k1}) of the file's {len(entries)} ({seed_mb} MB index), bytes "
+                           f"[{lo}, {hi}) of {total_bytes}; Record_Id base from a device all-gather of record counts")
 
     def prepare(self, stream):
         import torch
@@ -270,37 +391,118 @@ class _VarLen:
         self.off = torch.empty(self.cap, dtype=torch.int64, device=self.dev)
         self.ln = torch.empty(self.cap, dtype=torch.int32, device=self.dev)
         self.sd = (ctypes.c_int64 * len(self.seeds))(*self.seeds)
-        self.prm = self.rd.rdw_params()
         self.nfr = ctypes.c_int64(0)
         self.n_rec = self.n_expected
         self.cols, self.cs = _alloc_columns(self.rd.plan, self.n_rec, string_capacity(self.rd.native, self.n_rec),
                                             self.dev)
         self.fr0, self.fr1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        self.record_base = 0
+        # the run's Record_Id base lives on the device: the decode kernels read it (cbx_plan_set_record_base)
+        self.base = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.gathered = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
+        N.check(self.L.cbx_plan_set_record_base(self.h, self.base.data_ptr()))
 
     def step(self, world=1):
+        import torch.distributed as dist
         from cobrix_amd import native as N
-        from cobrix_amd.shard import record_bases
         self.fr0.record()
         N.check(self.L.cbx_frame_rdw(self.raw.data_ptr(), self.in_bytes, self.sd, len(self.seeds),
                                      ctypes.byref(self.prm), self.off.data_ptr(), self.ln.data_ptr(), self.cap,
                                      ctypes.byref(self.nfr), self.stream))
         self.fr1.record()
         if self.nfr.value != self.n_expected:
-            raise RuntimeError(f"framing found {self.nfr.value} records, generator wrote {self.n_expected}")
-        if world > 1:
-            self.record_base, _ = record_bases(self.nfr.value)     # Record_Id base of this shard
+            raise RuntimeError(f"framing found {self.nfr.value} records, the index run holds {self.n_expected}")
+        if world > 1:   # Record_Id base = exclusive prefix of the ranks' counts, computed on the device
+            self.count.fill_(self.nfr.value)
+            dist.all_gather_into_tensor(self.gathered, self.count)
+            self.base.copy_(self.gathered[: self.rank].sum().view(1))
         N.check(self.L.cbx_decode_var(self.h, self.raw.data_ptr(), self.in_bytes, self.off.data_ptr(),
-                                      self.ln.data_ptr(), self.n_rec, 0, self.record_base, self.cs, self.stream))
+                                      self.ln.data_ptr(), self.n_rec, 0, 0, self.cs, self.stream))
         return (self.fr0, self.fr1)
 
-    def end_to_end(self):
-        return None
+    def verify(self, world):
+        """After timing: the device base equals the records before this run in the setup framing, and
+        the Record_Id column starts there."""
+        import torch
+        got = int(self.base.item()) if world > 1 else 0
+        rid = self.cols[self.rd.plan.record_id_column]["values"][: max(1, self.n_rec)]
+        first = int(rid[0].item()) if self.n_rec else got
+        last = int(rid[self.n_rec - 1].item()) if self.n_rec else got - 1
+        torch.cuda.synchronize()
+        ok = got == self.expected_base and first == got and last == got + self.n_rec - 1
+        return {"record_id_base": got, "expected": self.expected_base, "ok": ok}
 
-    def payload(self):
-        return _payload(self.cols, self.n_rec)
+    def end_to_end(self, entries_per_piece: int = 4, passes: int = 2):
+        """H2D of the run in pieces of whole index entries (pinned host), each framed from its entries'
+        offsets and decoded while the next piece is copied (two streams, double-buffered)."""
+        import torch
+        from cobrix_amd import native as N
+        from cobrix_amd.reader import _alloc_columns, string_capacity
+        host = torch.empty(self.in_bytes, dtype=torch.uint8, pin_memory=True)
+        host.copy_(self.raw)
+        bounds = self.seeds[::entries_per_piece] + [self.in_bytes]
+        pieces = [(bounds[i], bounds[i + 1], [s - bounds[i] for s in self.seeds if bounds[i] <= s < bounds[i + 1]])
+                  for i in range(len(bounds) - 1)]
+        # records per piece from the timed framing (the same seeds give the same boundaries)
+        offs = self.off[: self.n_rec] - 4
+        cnt = [int(torch.searchsorted(offs, torch.tensor([b], device=self.dev)).item()) for b in bounds]
+        max_rec = max(cnt[i + 1] - cnt[i] for i in range(len(pieces)))
+        max_bytes = max(b - a for a, b, _ in pieces)
+        bufs = [torch.empty(max_bytes, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        outs = [_alloc_columns(self.rd.plan, max_rec, string_capacity(self.rd.native, max_rec), self.dev)
+                for _ in range(2)]
+        fo = [(torch.empty(max_rec + 1, dtype=torch.int64, device=self.dev),
+               torch.empty(max_rec + 1, dtype=torch.int32, device=self.dev)) for _ in range(2)]
+        cp, dc = torch.cuda.Stream(self.dev), torch.cuda.Stream(self.dev)
+        done = [torch.cuda.Event() for _ in range(2)]
+        copied = [torch.cuda.Event() for _ in range(2)]
+        for e in done:
+            e.record(dc)
+        dstream = ctypes.c_void_p(dc.cuda_stream)
+        N.check(self.L.cbx_plan_set_record_base(self.h, None))
+        nfr = ctypes.c_int64(0)
+
+        def run():
+            rbase = 0
+            for i, (a, b, sd) in enumerate(pieces):
+                k = i % 2
+                cp.wait_event(done[k])
+                with torch.cuda.stream(cp):
+                    bufs[k][: b - a].copy_(host[a:b], non_blocking=True)
+                copied[k].record(cp)
+                dc.wait_event(copied[k])
+                seeds = (ctypes.c_int64 * len(sd))(*sd)
+                N.check(self.L.cbx_frame_rdw(bufs[k].data_ptr(), b - a, seeds, len(sd), ctypes.byref(self.prm),
+                                             fo[k][0].data_ptr(), fo[k][1].data_ptr(), max_rec + 1, ctypes.byref(nfr),
+                                             dstream))
+                N.check(self.L.cbx_decode_var(self.h, bufs[k].data_ptr(), b - a, fo[k][0].data_ptr(),
+                                              fo[k][1].data_ptr(), nfr.value, 0, rbase, outs[k][1], dstream))
+                rbase += nfr.value
+                done[k].record(dc)
+            return rbase
+
+        run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            n = run()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / passes
+        N.check(self.L.cbx_plan_check(self.h, dstream))
+        N.check(self.L.cbx_plan_set_record_base(self.h, self.base.data_ptr()))
+        if n != self.n_rec:
+            raise RuntimeError(f"end-to-end pieces framed {n} records, expected {self.n_rec}")
+        del host
+        return {"value": round(self.in_bytes / dt / 1e9, 3), "unit": "GB/s", "records_per_s": round(self.n_rec / dt, 1),
+                "ms_per_pass": round(dt * 1e3, 3),
+                "how": f"{len(pieces)} pieces of {entries_per_piece} index entries ({self.seed_mb} MB): pinned-host "
+                       "H2D on a copy stream overlapped with cbx_frame_rdw (seeded by the piece's entries) + "
+                       "cbx_decode_var of the previous piece (double-buffered), per rank"}
 
 
+# ------------------------------------------------------------------------------------------------
+# CPU baseline (the oracle restatement; the reference's JVM path is not runnable here)
+# ------------------------------------------------------------------------------------------------
 def _probe_reference_jvm():
     """the reference CPU path runs only where a JVM + Spark + a Cobrix jar exist."""
     import shutil
@@ -311,15 +513,23 @@ def _probe_reference_jvm():
         " -- the reference Cobrix/Spark CPU path cannot run here; the oracle restatement is timed instead"
 
 
-def _cpu_threads() -> int:
-    """Host cores of this GPU's share: a 1-GPU box exposes the whole machine in nproc but allots 16
-    CPUs per GPU (CBX_CPU_THREADS overrides)."""
-    return int(os.environ.get("CBX_CPU_THREADS", str(min(16, os.cpu_count() or 1))))
+def _cpu_counts():
+    """(nproc = CPUs this process may run on, the cgroup CPU quota or None)."""
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    return nproc, quota
 
 
 def _cpu_baseline(workload: str, seconds: float = 10.0):
     """The oracle (scalar C restatement of the reference decoders) on a bounded sample of the same
-    workload, at 1 thread and at the GPU's host-core share (threads over record chunks: ctypes
+    workload, at 1 thread and at N = nproc threads (capped at 64; threads over record chunks: ctypes
     releases the GIL inside the C calls).  For RDW workloads the header walk stays sequential, as
     the reference's index pass is per file (IndexGenerator.scala:61-120); decode is split."""
     import threading
@@ -390,16 +600,76 @@ def _cpu_baseline(workload: str, seconds: float = 10.0):
     n = int(min(max(n0 / max(dt, 1e-9) * seconds, n0), 6_000_000 if workload != "wide_odo" else 60_000))
     data, fr, t_frame, _ = make(n, 100)
     dt1, nrec = timed(data, fr, t_frame, 1)
-    T = _cpu_threads()
+    nproc, quota = _cpu_counts()
+    T = int(os.environ.get("CBX_CPU_THREADS", str(min(64, nproc))))
     dtT, _ = timed(data, fr, t_frame, T)
     unit_n = {"syn200": "SYN200 records", "synstr200": "SYNSTR200 records", "rdw_narrow": "RDW records",
               "wide_odo": "root records (+ children)"}[workload]
     return {"value": round(len(data) / dtT / 1e9, 6), "unit": "GB/s", "cores": T, "kind": "port",
             "value_1_core": round(len(data) / dt1 / 1e9, 6),
+            "nproc": nproc, "cgroup_cpu_quota": quota,
             "sample": f"{n} {unit_n} ({len(data) / 1e6:.1f} MB, {nrec} records) through oracle/cobrix_oracle.c "
                       f"(restatement of extractRecord + decoders{'' if fixed else '; RDW header walk sequential'}): "
-                      f"{dt1:.1f} s at 1 thread, {dtT:.2f} s at {T} threads",
+                      f"{dt1:.1f} s at 1 thread, {dtT:.2f} s at N = {T} threads (nproc {nproc}"
+                      f"{'' if quota is None else f', cgroup quota {quota:g} CPUs'})",
             "reference_jvm": _probe_reference_jvm()}
+
+
+# ------------------------------------------------------------------------------------------------
+# launcher
+# ------------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start n ranks of this script under torch.distributed.run (one process per GPU) and return
+    their exit status.  Called before anything initialises a GPU in this process."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def _dry_run(args, world, rank):
+    """CPU plumbing of the multi-rank job (gloo): launcher, process group, the per-step count
+    all-gather and the barrier + max-over-ranks timing -- no decode (the product path needs a GPU)."""
+    import torch
+    import torch.distributed as dist
+    from cobrix_amd.shard import global_bases
+    if world > 1:
+        dist.init_process_group("gloo")
+    n_local = 1000 + 7 * rank
+    bases = []
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rb, _, tot = global_bases(n_local) if world > 1 else (torch.tensor(0), None, torch.tensor([n_local]))
+        bases.append(int(rb))
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.barrier()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    expect = sum(1000 + 7 * r for r in range(rank))
+    ok = all(b == expect for b in bases)
+    gathered = [None] * world
+    if world > 1:
+        dist.all_gather_object(gathered, {"rank": rank, "ok": ok, "base": bases[-1] if bases else None})
+    else:
+        gathered = [{"rank": 0, "ok": ok, "base": 0}]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": float(t.item()) / max(1, args.steps) * 1e3,
+                          "dry_run": True, "ranks": gathered}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if all(g["ok"] for g in gathered) else 1
 
 
 def main():
@@ -411,22 +681,33 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="records per GPU (root records for wide_odo); "
                                                            "0 = the workload's default")
     ap.add_argument("--window", type=int, default=0, help="LDS window bytes (0 = plan default)")
-    ap.add_argument("--strings", default="views", choices=["views", "offsets"],
-                    help="string column layout: Arrow string views (one pass) or Arrow large-string offsets")
+    ap.add_argument("--strings", default="", choices=["", "views", "offsets"],
+                    help="string column layout (default per workload): Arrow string views or large-string offsets")
     ap.add_argument("--occurs", default="lists", choices=["lists", "slots"],
                     help="OCCURS DEPENDING ON layout: Arrow lists (present elements) or one slot row per element")
+    ap.add_argument("--seed-mb", type=int, default=100, choices=[100, 32],
+                    help="var-len index entry size: 100 MB default (reset) or a 32 MB block size (subtracted)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true")
+    ap.add_argument("--dry-run", action="store_true", help="CPU plumbing only (gloo): launcher, all-gather, timing")
     args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE {world} != --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        sys.exit(_dry_run(args, world, rank))
 
     import torch
     import torch.distributed as dist
 
     from cobrix_amd import native as N
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -434,19 +715,20 @@ def main():
 
     W = WORKLOADS[args.workload]
     n_req = args.records or W["records"]
+    strings = args.strings or W["strings"]
 
     def progress(msg):
         if rank == 0:
             print(f"[bench {args.workload}] {msg}", file=sys.stderr, flush=True)
 
-    progress(f"generating {n_req} records on {dev}")
-    views = args.strings == "views"
+    progress(f"generating {n_req} records per GPU on {dev} (world {world})")
     if args.workload in ("syn200", "synstr200"):
-        job = _Fixed(args.workload, n_req, dev, rank, args.window, views)
+        job = _Fixed(args.workload, n_req, dev, rank, args.window, strings)
     else:
-        job = _VarLen(args.workload, n_req, dev, rank, args.window, views, args.occurs == "lists")
+        job = _VarLen(args.workload, n_req, dev, rank, world, args.window, strings, args.occurs == "lists",
+                      args.seed_mb)
     st = torch.cuda.current_stream()
-    progress(f"{job.in_bytes / 1e9:.2f} GB generated; allocating columns")
+    progress(f"{job.in_bytes / 1e9:.2f} GB on this rank; allocating columns")
     job.prepare(st)
     progress("warm-up")
     L, h = job.L, job.h
@@ -481,38 +763,48 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    check = job.verify(world)
 
     n_rec = job.n_rec
-    payload = job.payload()
+    plan = job.rd.plan
+    # job totals: every rank's input bytes and records (var-len runs differ in size)
+    tot = torch.tensor([job.in_bytes, n_rec], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    job_bytes, job_recs = float(tot[0].item()), float(tot[1].item())
     steps = args.steps
     ms_per_step = elapsed / steps * 1e3
-    gbs = job.in_bytes * world / (elapsed / steps) / 1e9
-    recs_per_s = n_rec * world / (elapsed / steps)
-    alg = algorithmic_bytes(job.rd.plan, n_rec, job.in_bytes, payload, present_elements(job.rd.plan, job.cols, n_rec))
+    gbs = job_bytes / (elapsed / steps) / 1e9
+    recs_per_s = job_recs / (elapsed / steps)
+    present = present_elements(plan, job.cols, n_rec)
+    payload = string_payload(plan, job.cols, n_rec)
+    alg = algorithmic_bytes(plan, n_rec, job.in_bytes, payload, present)
+    lay = layout_bytes(plan, job.cols, n_rec, job.in_bytes, payload, present)
     dec_avg_ms = sum(dec[: nc.value]) / max(1, nc.value)
     fix_avg_ms = sum(fix[: nc.value]) / max(1, nc.value)
     achieved = alg / (dec_avg_ms * 1e-3) / 1e9
     kind = ctypes.c_int32(0)
     N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
-    kname = "cbx_jit_decode (copybook-specialised, hipRTC)" if kind.value == 1 else "cbx::decode_kernel (table-driven)"
-    lists = any(c.list_array >= 0 for c in job.rd.plan.columns)
+    kname = {1: "cbx_jit_decode (copybook-specialised, hipRTC)", 2: "cbx::walk_kernel (record walk)"}.get(
+        kind.value, "cbx::decode_kernel (table-driven)")
+    lists = any(c.list_array >= 0 for c in plan.columns)
     if lists:   # the OCCURS list elements: the element-parallel kernel launched right after the decode kernel
         kname += " + cbx::list_kernel (OCCURS lists; decode_kernel time covers both)"
-    tag = f"{args.workload}_{args.strings}{'' if args.occurs == 'lists' else '_slots'}_{n_rec}"
+    tag = f"{args.workload}_{strings}{'' if args.occurs == 'lists' else '_slots'}_{n_rec}"
     traffic, traffic_src = measured_traffic(tag)
-    kernel_ms = {"decode_kernel": round(dec_avg_ms, 4),
-                 ("post_kernels (deferred-value fixup)" if views else
-                  "post_kernels (deferred-value fixup, string scan + placement)"): round(fix_avg_ms, 4)}
+    kernel_ms = {"decode_kernel": round(dec_avg_ms, 4), "post_kernels": round(fix_avg_ms, 4)}
+    fms = None
     if frame_ev:
         fms = sum(a.elapsed_time(b) for a, b in frame_ev) / len(frame_ev)
         kernel_ms["rdw_framing (cbx_frame_rdw incl. count readback)"] = round(fms, 4)
-    if hasattr(job, "entries"):
-        kernel_ms["sparse_index_setup (untimed: frame + cbx_sparse_index, once)"] = round(job.index_ms, 3)
+    if hasattr(job, "index_ms"):
+        kernel_ms["sparse_index_setup (untimed: frame + cbx_sparse_index of the whole file, once)"] = round(job.index_ms, 3)
     e2e = None
     if not args.no_end_to_end and world == 1:
         progress("end-to-end (pinned host -> HBM) pass")
         e2e = job.end_to_end()
     progress("cpu baseline" if not args.no_cpu_baseline and world == 1 else "done")
+    kernels_sum = dec_avg_ms + fix_avg_ms + (fms or 0.0)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -531,20 +823,24 @@ def main():
             "data": W["data"],
             "config": {"workload": W["desc"], "baseline_config": W["config"],
                        "records_per_gpu": n_rec, "input_bytes_per_gpu": job.in_bytes,
-                       "input_gb_per_gpu": round(job.in_bytes / 1e9, 3),
-                       "output_columns": job.rd.plan.n_columns, "parallelism": f"dp{world}",
-                       "string_layout": "Arrow string views (16 B views + long payloads, one pass)" if views
-                       else "Arrow large-string (int64 offsets + payload, scan + placement)",
+                       "input_gb_per_gpu": round(job.in_bytes / 1e9, 3), "job_input_bytes": int(job_bytes),
+                       "output_columns": plan.n_columns, "parallelism": f"dp{world}",
+                       "shard": job.shard_note,
+                       "string_layout": STRING_LAYOUTS[strings],
                        "occurs_layout": "Arrow lists (present elements only)" if args.occurs == "lists"
                        else "one slot row per element",
                        "inputs_resident_in_hbm": True},
             "kernel_ms": kernel_ms,
-            **({"seeds": f"{len(job.entries)} sparse-index entries from cbx_sparse_index (100 MB, root segments)"}
-               if hasattr(job, "entries") else {}),
+            "step_vs_kernels": round(ms_per_step / kernels_sum, 3) if kernels_sum > 0 else None,
+            **({"seeds": f"{len(job.seeds)} sparse-index entries of this rank's run ({args.seed_mb} MB, root segments)",
+                "record_id_check": check} if hasattr(job, "seeds") else {}),
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "algorithmic_bytes_per_launch": alg, "traffic": traffic,
-                         "traffic_source": traffic_src},
+                         "frac_of_measured_peak": round(achieved / HBM_MEASURED_GBS, 4),
+                         "algorithmic_bytes_per_launch": alg,
+                         "layout_bytes_per_launch": lay, "layout_overhead": lay - alg,
+                         "timing": "HIP events on the launch stream (cbx_plan_kernel_times), average of the timed steps",
+                         "traffic": traffic, "traffic_source": traffic_src},
         }
         if e2e is not None:
             out["end_to_end"] = e2e
@@ -553,6 +849,9 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if check is not None and not check["ok"]:
+        print(f"[bench] Record_Id base check failed on rank {rank}: {check}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -125,6 +125,7 @@ struct cbx_plan {
     cbx_walk_handler* d_whand = nullptr;
     int64_t* d_wslot_base = nullptr;    // per column: first string-slot index
     int64_t* d_wtile_bytes = nullptr;   // per column: view tile bytes
+    const int64_t* d_rec_base = nullptr;   // caller's device Record_Id base (cbx_plan_set_record_base)
     int64_t n_str_slots = 0;
     uint32_t* d_wcursor = nullptr; int64_t wcursor_cap = 0;
     int32_t fid_col = -1, rid_col = -1;
@@ -570,8 +571,15 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
 static int64_t view_tile_bytes(const cbx_plan* P, int c) { return ((int64_t)kWave * ((P->col_max_bytes[c] + 3) & ~3) + 15) & ~(int64_t)15; }
 // whole tiles per data buffer: the largest power of two fitting 1 GiB (the kernels split a tile
 // index into buffer and position by a shift)
+// (CBX_VIEW_BUFFER_BYTES lowers the 1 GiB cap: tests of multi-buffer regions on small inputs;
+// reader.view_geometry reads the same variable)
+static int64_t view_buffer_cap() {
+    const char* e = getenv("CBX_VIEW_BUFFER_BYTES");
+    const int64_t v = e ? atoll(e) : 0;
+    return v >= 16 && v < (int64_t(1) << 30) ? v : (int64_t(1) << 30);
+}
 static int64_t view_tiles_per_buf(int64_t tile_bytes) {
-    const int64_t n = std::max<int64_t>(1, (int64_t(1) << 30) / std::max<int64_t>(16, tile_bytes));
+    const int64_t n = std::max<int64_t>(1, view_buffer_cap() / std::max<int64_t>(16, tile_bytes));
     return int64_t(1) << (63 - __builtin_clzll((unsigned long long)n));
 }
 
@@ -635,6 +643,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.stride = c.stride;
     a.start_off = c.start_off;
     a.first_record_id = c.first_record_id;
+    a.rec_id_base = P->d_rec_base;
     a.rec_id = c.rec_id;
     a.rec_seg = c.rec_seg;
     a.file_id = c.file_id >= 0 ? c.file_id : P->opts.file_id;
@@ -941,7 +950,7 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
     HIP_CHECK(hipMemsetAsync(P->d_wcursor, 0, sizeof(uint32_t) * nc, st));
     WalkArgs a{};
     a.data = c.data; a.data_len = c.data_len; a.rec_off = c.rec_off; a.rec_len = c.rec_len; a.n_rec = c.n_rec;
-    a.stride = c.stride; a.start_off = c.start_off; a.first_record_id = c.first_record_id;
+    a.stride = c.stride; a.start_off = c.start_off; a.first_record_id = c.first_record_id; a.rec_id_base = P->d_rec_base;
     a.rec_id = c.rec_id; a.rec_seg = c.rec_seg; a.file_id = c.file_id >= 0 ? c.file_id : P->opts.file_id;
     a.var_occurs = P->walk_var; a.n_tiles = n_tiles; a.pitch = n_tiles * kWave;
     a.nodes = (const CBX_CONST cbx_walk_node*)P->d_wnodes; a.root = P->walk_root;
@@ -1012,6 +1021,12 @@ extern "C" int cbx_plan_check(cbx_plan* P, void* stream) {
         HIP_CHECK(hipMemset(P->d_status, 0, sizeof(int32_t)));
         return fail(CBX_E_CAPACITY, "a string column's payload exceeded its data_capacity (size it with cbx_string_bound or cbx_string_sizes_*)");
     }
+    return CBX_OK;
+}
+
+extern "C" int cbx_plan_set_record_base(cbx_plan* P, const int64_t* d_base) {
+    if (!P) return fail(CBX_E_ARGUMENT, "cbx_plan_set_record_base: invalid plan");
+    P->d_rec_base = d_base;
     return CBX_OK;
 }
 
@@ -1769,14 +1784,15 @@ extern "C" int cbx_plan_set_walk(cbx_plan* P, const cbx_walk_node* nodes, int32_
     for (int i = 0; i < n_handlers; i++)
         if (handlers[i].key_len < 0 || handlers[i].key_len > 64) return fail(CBX_E_ARGUMENT, "cbx_plan_set_walk: bad handler");
     if (P->walk) return fail(CBX_E_STATE, "cbx_plan_set_walk: the plan already walks");
-    std::vector<int64_t> slot_base(P->n_columns, 0), tile_bytes(P->n_columns, 0);
+    std::vector<int64_t> slot_base(P->n_columns, 0), tile_bytes(2 * (size_t)P->n_columns, 0);   // [tile bytes, tiles per buffer]
     int64_t ns = 0;
     for (int c = 0; c < P->n_columns; c++) {
         if (!P->col_is_string[c]) continue;
         if (!P->view) return fail(CBX_E_UNSUPPORTED, "cbx_plan_set_walk: string columns need the string-view layout");
         slot_base[c] = ns;
         ns += P->col_slots[c];
-        tile_bytes[c] = view_tile_bytes(P, c);
+        tile_bytes[2 * c] = view_tile_bytes(P, c);
+        tile_bytes[2 * c + 1] = view_tiles_per_buf(tile_bytes[2 * c]);
     }
     int r;
     if ((r = upload(&P->d_wnodes, nodes, n_nodes)) || (r = upload(&P->d_warr, arrays, na)) ||

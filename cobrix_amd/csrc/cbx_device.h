@@ -793,7 +793,8 @@ __device__ __forceinline__ void decode_generated(const KernelArgs& a, const Wind
         const GenOp g = ldc(a.gops + i);
         const DevColumn col = ldc(a.cols + g.column);
         // Record_Id: the selection's per-record ids (cbx_decode_selected), else first_record_id + r
-        const int64_t rid = (kSel && a.rec_id) ? (t.active ? a.rec_id[t.rec] : 0) : a.first_record_id + t.rec;
+        const int64_t rid = (kSel && a.rec_id) ? (t.active ? a.rec_id[t.rec] : 0)
+                                               : a.first_record_id + (a.rec_id_base ? *a.rec_id_base : 0) + t.rec;
         Val x{g.kind == CBX_K_RECORD_ID ? (uint64_t)rid : (uint64_t)(int64_t)a.file_id, 0, true};
         if (t.active) store_value(col, g.out_type, t.rec, x);
         const uint64_t m = __ballot(t.active);

@@ -116,6 +116,7 @@ struct KernelArgs {
     int32_t start_off;         // record_start_offset
     int64_t first_record_id;
     const int64_t* rec_id;     // per-record Record_Id (selected records), nullptr: first_record_id + r
+    const int64_t* rec_id_base;// device int64 added to first_record_id (cbx_plan_set_record_base), nullptr: 0
     const int32_t* rec_seg;    // per-record active segment (selected records), nullptr: from segmap
     int32_t file_id;
     int32_t mode;              // 0 decode, 1 string sizes only

@@ -413,7 +413,7 @@ __global__ __launch_bounds__(64) void idx_walk_kernel(IdxArgs a, const int64_t* 
                 if (f > 0) lo = lo + (int64_t)(f - 1) * step + 1;
                 break;
             }
-            lo = lo + 64 * step;
+            lo = lo + 63 * step + 1;          // every rank up to lo + 63 step was probed and missed
             if (lo >= n_cand) { hi = n_cand; break; }
             step *= 64;
         }

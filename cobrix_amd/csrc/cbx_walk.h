@@ -31,6 +31,7 @@ struct WalkArgs {
     int64_t n_rec;
     int32_t stride, start_off;
     int64_t first_record_id;
+    const int64_t* rec_id_base;       // device int64 added to first_record_id (cbx_plan_set_record_base), nullptr: 0
     const int64_t* rec_id;            // selection: per-record Record_Id
     const int32_t* rec_seg;           // selection: per-record active segment
     int32_t file_id;
@@ -49,7 +50,7 @@ struct WalkArgs {
     int32_t seg_col, fid_col, rid_col;
     const int64_t* str_slot_base;     // per column: index of its slot 0 among the string column slots
     uint32_t* cursors;                // [string column slots][n_tiles] payload bytes used in the tile region
-    const int64_t* tile_bytes;        // per column: view region bytes per tile
+    const int64_t* tile_bytes;        // per column: view region bytes per tile, tiles per data buffer
     int32_t* status;
 };
 
@@ -91,9 +92,11 @@ __device__ __forceinline__ int walk_count(const WalkArgs& a, int ai, const WalkD
     return (v >= ar.min_count && v <= ar.max_count) ? v : ar.max_count;
 }
 
-// One primitive element at record offset `off` (relative to the decode base).
+// One primitive element at record offset `off` (relative to the decode base).  `element`: an
+// element of a primitive OCCURS -- extractArray decodes those with decodeTypeValue, which never
+// touches dependFields (RecordExtractors.scala:96-107), so they update no dependee.
 __device__ void walk_prim(const WalkArgs& a, const cbx_walk_node& nd, int off, int slot, const uint8_t* rec, int avail,
-                          int64_t r, int lane, WalkDep* dep) {
+                          int64_t r, int lane, WalkDep* dep, bool element) {
     const bool decoded = nd.field >= 0;
     Field f{};
     if (decoded) f = ldc(a.fields + nd.field);
@@ -120,21 +123,20 @@ __device__ void walk_prim(const WalkArgs& a, const cbx_walk_node& nd, int off, i
             view.z = inl[4] | (uint32_t)inl[5] << 8 | (uint32_t)inl[6] << 16 | (uint32_t)inl[7] << 24;
             view.w = inl[8] | (uint32_t)inl[9] << 8 | (uint32_t)inl[10] << 16 | (uint32_t)inl[11] << 24;
         } else {
-            const int64_t tb = a.tile_bytes[f.column];
-            const int64_t tpb = (int64_t(1) << 30) / (tb < 16 ? 16 : tb);
+            const int64_t tb = a.tile_bytes[2 * f.column];
+            const int64_t tpb = a.tile_bytes[2 * f.column + 1];   // a power of two (view_tiles_per_buf)
             const int64_t cs = a.str_slot_base[f.column] + slot;
             const uint32_t at = atomicAdd(a.cursors + cs * a.n_tiles + tile, (uint32_t)len);
             if ((int64_t)at + len > tb) { atomicOr(a.status, 1); return; }
             uint8_t* dst = c.data + (int64_t)slot * c.capacity + tile * tb + at;
             string_write(f.kind, p, sp, dst, lutf);
             view.y = dst[0] | (uint32_t)dst[1] << 8 | (uint32_t)dst[2] << 16 | (uint32_t)dst[3] << 24;
-            const int64_t b = tile / tpb;
-            view.z = (uint32_t)b;
-            view.w = (uint32_t)((tile - b * tpb) * tb + at);
+            view.z = (uint32_t)(tile >> __builtin_ctzll((unsigned long long)tpb));
+            view.w = (uint32_t)((tile & (tpb - 1)) * tb + at);
         }
         ((u32x4*)c.values)[(int64_t)slot * a.pitch + r] = view;
         walk_set_valid(c.validity, (int64_t)slot * a.n_tiles + tile, lane);
-        if (nd.dep_slot >= 0) {   // Right(s): the handler key it equals (occurs_mappings)
+        if (nd.dep_slot >= 0 && !element) {   // Right(s): the handler key it equals (occurs_mappings)
             int key = 0;
             uint8_t buf[64];
             if (len <= 64) {
@@ -162,7 +164,7 @@ __device__ void walk_prim(const WalkArgs& a, const cbx_walk_node& nd, int off, i
     else if (w == 8) ((uint64_t*)c.values)[at] = x.lo;
     else ((u32x4*)c.values)[at] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
     walk_set_valid(c.validity, (int64_t)slot * a.n_tiles + tile, lane);
-    if (nd.dep_slot >= 0) {   // Left(Number.intValue)
+    if (nd.dep_slot >= 0 && !element) {   // Left(Number.intValue)
         const Val dv = decode_count_int(f, p);
         if (dv.valid) dep[nd.dep_slot] = WalkDep{1, (int32_t)dv.lo};
     }
@@ -195,7 +197,7 @@ __device__ void walk_record(const WalkArgs& a, const uint8_t* rec, int avail, in
                     sp++;
                     continue;
                 }
-                walk_prim(a, nd, fr.off, slot, rec, avail, r, lane, dep);
+                walk_prim(a, nd, fr.off, slot, rec, avail, r, lane, dep, true);
                 fr.off += nd.data_size;
                 fr.cur++;
                 continue;
@@ -245,7 +247,7 @@ __device__ void walk_record(const WalkArgs& a, const uint8_t* rec, int avail, in
             sp++;
             continue;
         }
-        walk_prim(a, ch, fr.off, fr.slot, rec, avail, r, lane, dep);
+        walk_prim(a, ch, fr.off, fr.slot, rec, avail, r, lane, dep, false);
         if (!(ch.flags & CBX_W_REDEFINED)) fr.off += ch.actual_size;
         fr.cur = ch.next;
     }
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
         }
         if (a.rid_col >= 0) {
             const DevColumn c = ldc(a.cols + a.rid_col);
-            ((int64_t*)c.values)[r] = a.rec_id ? a.rec_id[r] : a.first_record_id + r;
+            ((int64_t*)c.values)[r] = a.rec_id ? a.rec_id[r] : a.first_record_id + (a.rec_id_base ? *a.rec_id_base : 0) + r;
             walk_set_valid(c.validity, tile, lane);
         }
         walk_record(a, rec, avail, seg, r, lane);

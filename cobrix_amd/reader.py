@@ -12,6 +12,7 @@ The GPU decodes a whole batch (split / partition) per call instead of one record
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 from decimal import Context, Decimal
 from typing import Any, Dict, Iterator, List, Optional, Sequence, Tuple
@@ -241,7 +242,11 @@ class DecodedBatch:
             if ci not in counts:
                 info = plan.columns[ci]
                 v = self.cols[ci]["values"].cpu().numpy().reshape(info.n_slots, -1)[:, :n]
-                counts[ci] = v.reshape(-1).astype(np.int64)   # slot s, record r -> s * n + r
+                # an invalid count cell (an array inside an inactive segment redefine the record walk
+                # skips) holds no element count: no elements, as in _list_dense
+                vb = np.unpackbits(self.cols[ci]["validity"].cpu().numpy().view(np.uint8), bitorder="little")
+                ok = vb.reshape(info.n_slots, -1)[:, :n].astype(bool)
+                counts[ci] = np.where(ok, v, 0).reshape(-1).astype(np.int64)   # slot s, record r -> s * n + r
             return counts[ci]
 
         seg_active = None
@@ -500,7 +505,9 @@ def view_geometry(capacity: int, n_tiles: int) -> Tuple[int, int]:
     if n_tiles <= 0 or capacity <= 0:
         return 0, 0
     tb = capacity // n_tiles
-    tpb = max(1, (1 << 30) // max(16, tb))
+    cap = int(os.environ.get("CBX_VIEW_BUFFER_BYTES", "0") or 0)   # tests: multi-buffer regions (cbx_capi.hip)
+    cap = cap if 16 <= cap < (1 << 30) else (1 << 30)
+    tpb = max(1, cap // max(16, tb))
     return tb, (1 << (tpb.bit_length() - 1)) * tb
 
 

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 9
+#define CBX_ABI_VERSION 10
 
 /* status codes */
 #define CBX_OK 0
@@ -261,6 +261,14 @@ int cbx_decode_var(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const
 int cbx_string_sizes_var(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
                          const int32_t* d_rec_len, int64_t n_rec, int32_t start_offset,
                          int64_t* out_sizes, void* stream);
+
+/* Multi-GPU shards of one variable-length file: d_base is a device int64 (e.g. the
+ * exclusive prefix of the ranks' framed record counts, all-gathered on the device) that every later
+ * decode call of the plan adds to its first_record_id when it writes Record_Id -- the shard's base
+ * never visits the host.  NULL clears it.  The pointer must stay valid while calls are in flight.
+ * Replaces the startingRecordIndex a Spark task passes to VarLenNestedReader.getRowIterator
+ * (SC/reader/VarLenNestedReader.scala:52-81). */
+int cbx_plan_set_record_base(cbx_plan* plan, const int64_t* d_base);
 
 /* Synchronise `stream` and report device-side errors of the plan's earlier decode calls
  * (CBX_E_CAPACITY: a string payload exceeded data_capacity). */

@@ -113,6 +113,10 @@ _SYN_OPTS = {"is_record_sequence": "true", "segment_field": "SEGMENT_ID"}
     ({"segment_id_root": "C"}, {"bytes_per_entry": 300_000, "subtract_size": 0}, 40_000),
     ({"input_split_records": "100", "segment_id_root": "C", "file_start_offset": "100", "file_end_offset": "120"},
      None, 5_000),                                                                     # file header / footer
+    # split gaps of ~4,100-4,160 candidates: the galloping walk's second probe round (step 64) must
+    # resume right after its last probe (lo + 63 step + 1), not 64 step further on
+    ({"input_split_records": "11770", "segment_id_root": "C"}, None, 90_000),
+    ({"segment_id_root": "C"}, {"bytes_per_entry": 780_000, "subtract_size": 0}, 90_000),
 ])
 def test_gpu_sparse_index_modes(extra, override, n):
     from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow

@@ -153,3 +153,119 @@ def test_debug_fields_vs_oracle(policy):
         assert not errs, errs[:5]
         rows = b.to_rows()
         assert rows == RO.fixed_len_rows(rd.copybook, data, rd.params)
+
+
+LONGSTR = """
+       01  REC.
+           05  N-OUT       PIC 9(1).
+           05  OUTER       OCCURS 0 TO 3 TIMES DEPENDING ON N-OUT.
+               10  NAME    PIC X(24).
+           05  TAIL-TXT    PIC X(30).
+"""
+
+
+def test_walk_long_strings_multi_buffer(monkeypatch):
+    """Long (> 12 byte) strings of the record walk land in Arrow data buffers of a power-of-two
+    number of tiles, like the other view writers: with a 64 KiB buffer cap every slot region spans
+    several buffers (view index = tile >> log2(tiles per buffer))."""
+    monkeypatch.setenv("CBX_VIEW_BUFFER_BYTES", str(65536))
+    rnd = random.Random(17)
+    recs = []
+    for _ in range(6000):
+        n = rnd.choice([0, 1, 2, 3])
+        b = bytes([0xF0 + n])
+        for _ in range(n):
+            b += _ebcdic("".join(rnd.choice("ABCDEFGHIJ KLMNOP") for _ in range(24)))
+        b += _ebcdic(("TAIL" + "x" * rnd.randrange(26)).ljust(30))
+        recs.append(b)
+    raw = rdw_file(recs)
+    opts = {"is_record_sequence": "true", "variable_size_occurs": "true"}
+    rd, p = _reader(LONGSTR, opts)
+    assert rd.walk
+    batch = rd.read(raw)
+    ci = next(i for i, c in enumerate(batch.cols) if "buffer_bytes" in c)
+    assert batch.cols[ci]["capacity"] > 2 * batch.cols[ci]["buffer_bytes"]
+    rows = batch.to_rows()
+    exp = RO.var_len_rows(rd.copybook, raw, p)
+    assert len(rows) == len(exp) == 6000
+    bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
+    assert not bad, (bad[:5], rows[bad[0]], exp[bad[0]])
+
+
+SEGODO = """
+       01  REC.
+           05  SEG         PIC X(1).
+           05  A-PART.
+               10  NA      PIC 9(1).
+               10  AITEMS  OCCURS 0 TO 4 TIMES DEPENDING ON NA.
+                   15  AV  PIC S9(3) COMP-3.
+           05  B-PART REDEFINES A-PART.
+               10  NB      PIC 9(1).
+               10  BITEMS  OCCURS 0 TO 2 TIMES DEPENDING ON NB.
+                   15  BV  PIC X(4).
+"""
+
+
+def test_walk_segment_redefine_odo_to_arrow():
+    """to_arrow of a record-walk batch whose OCCURS DEPENDING ON arrays sit inside segment
+    redefines: the walk leaves the inactive redefine's count cells unwritten (invalid), which must
+    give no list elements rather than garbage counts."""
+    pytest.importorskip("pyarrow")
+    rnd = random.Random(23)
+    recs = []
+    for _ in range(3000):
+        if rnd.random() < 0.5:
+            n = rnd.randrange(5)
+            b = _ebcdic("A") + bytes([0xF0 + n]) + b"".join(bytes([rnd.randrange(10) << 4 | rnd.randrange(10),
+                                                                  rnd.randrange(10) << 4 | 0x0C]) for _ in range(n))
+        else:
+            n = rnd.randrange(3)
+            b = _ebcdic("B") + bytes([0xF0 + n]) + b"".join(_ebcdic(rnd.choice(["ab  ", "WXYZ", "    "])) for _ in range(n))
+        recs.append(b)
+    raw = rdw_file(recs)
+    opts = {"is_record_sequence": "true", "variable_size_occurs": "true", "segment_field": "SEG",
+            "redefine_segment_id_map:0": "A-PART => A", "redefine_segment_id_map:1": "B-PART => B"}
+    rd, p = _reader(SEGODO, opts)
+    assert rd.walk
+    batch = rd.read(raw)
+    # count cells the walk does not write hold whatever the allocator left: make that visible
+    for ar in batch.plan.arrays:
+        c = batch.cols[ar.count_column]
+        if ar.segment >= 0:
+            vb = c["validity"].cpu().numpy().view("uint8")
+            import numpy as np
+            bits = np.unpackbits(vb, bitorder="little")[: batch.n_rec].astype(bool)
+            c["values"][: batch.n_rec][torch.from_numpy(~bits).to(c["values"].device)] = 1_000_000
+    table = batch.to_arrow()
+    table.validate(full=True)
+    rows = batch.to_rows()
+    from test_gpu_golden import _norm
+    assert _norm(table.to_pylist()) == _norm(rows)
+    assert rows == RO.var_len_rows(rd.copybook, raw, p)
+
+
+ELEMDEP = """
+       01  REC.
+           05  CNT         PIC 9(1) OCCURS 2 TIMES.
+           05  ITEMS       OCCURS 0 TO 3 TIMES DEPENDING ON CNT.
+               10  V       PIC X(2).
+           05  AFTER       PIC 9(2).
+"""
+
+
+@pytest.mark.parametrize("var_size", [True, False])
+def test_walk_primitive_array_element_is_no_dependee(var_size):
+    """A DEPENDING ON name that is an element of a primitive OCCURS: extractArray decodes those
+    elements with decodeTypeValue and never records them in dependFields (RecordExtractors.scala:96-107),
+    so the array keeps its maximum size."""
+    rnd = random.Random(31)
+    recs = []
+    for i in range(500):
+        body = f"{rnd.randrange(4)}{rnd.randrange(4)}" + "".join(rnd.choice(["ab", "XY", "  "]) for _ in range(3)) + f"{i % 100:02d}"
+        recs.append(body.encode("cp037"))
+    raw = rdw_file(recs)
+    rd, p = _reader(ELEMDEP, {"is_record_sequence": "true", "variable_size_occurs": str(var_size).lower()})
+    assert rd.walk
+    rows = rd.read(raw).to_rows()
+    exp = RO.var_len_rows(rd.copybook, raw, p)
+    assert rows == exp

@@ -123,3 +123,35 @@ def test_varlen_shards_record_ids_gloo():
     assert res[0][1] == res[1][1] == 1000
     assert len(res[0][2]) > 100 and len(res[1][2]) > 100
     assert split == whole
+
+
+def test_bench_launcher_two_ranks_gloo():
+    """`bench.py --gpus 2` with no torchrun environment starts its own 2 ranks (torch.distributed.run,
+    127.0.0.1); --dry-run keeps them on the CPU (gloo): process group, the per-step record-count
+    all-gather (exclusive prefix = each rank's Record_Id base), barrier + max-over-ranks timing, and
+    ONE JSON line from rank 0 reporting both ranks."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                              "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3",
+                        "--warmup", "0"], capture_output=True, text=True, timeout=180, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["dry_run"]
+    assert sorted((g["rank"], g["base"], g["ok"]) for g in out["ranks"]) == [(0, 0, True), (1, 1000, True)]
+
+
+def test_bench_rejects_world_mismatch():
+    """Under a torchrun environment whose WORLD_SIZE differs from --gpus, bench.py exits non-zero."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert r.returncode == 2 and "WORLD_SIZE 1 != --gpus 2" in r.stderr

@@ -85,8 +85,19 @@ def test_alloc_columns_view_layout(monkeypatch):
         assert c["views"].numel() == 16 * 64 * tiles and "offsets" not in c
         assert s.values == c["views"].data_ptr() and s.offsets is None and s.data_capacity == caps[0]
         assert c["tile_bytes"] == 64 * 20
-    # accounting: input + validity + 16-byte views + long payload
-    assert algorithmic_bytes(plan, n, 200 * n, 777) == 200 * n + 777 + 10 * ((n + 7) // 8 + 16 * n)
+    # SURVEY.md 8(d) accounting, whatever the layout: input + validity + a 4-byte offset per value +
+    # the whole UTF-8 payload
+    pay = {ci: 1000 + ci for ci in range(10)}
+    assert algorithmic_bytes(plan, n, 200 * n, pay, {}) == 200 * n + sum(pay.values()) + 10 * ((n + 7) // 8 + 4 * n)
+    from bench import layout_bytes, string_payload
+    # views: lengths of valid values only; the layout writes 16-byte views + payloads over 12 bytes
+    ln = torch.tensor([5, 13, 0, 20], dtype=torch.int32)
+    cols[0]["views"].view(-1, 16)[:4, :4] = ln.view(torch.uint8).view(4, 4)
+    cols[0]["validity"][0] = 0b1011                      # value 2 null (length 0 anyway), value 3 valid
+    got = string_payload(plan, cols, n)
+    assert got[0] == 5 + 13 + 20 and all(got[ci] == 0 for ci in range(1, 10))
+    lay = layout_bytes(plan, cols, n, 200 * n, got, {})
+    assert lay == 200 * n + 10 * ((n + 7) // 8 + 16 * n) + 13 + 20
 
 
 def test_present_elements_counts_only_live_odo_elements():
@@ -108,7 +119,7 @@ def test_present_elements_counts_only_live_odo_elements():
     pres = present_elements(plan, cols, n)
     odo_cols = {f.column for f in plan.fields if f.n_dims == 1}
     assert set(pres) == odo_cols and all(v == 10 + 7 + 0 for v in pres.values())
-    full = algorithmic_bytes(plan, n, 0, 0)
-    live = algorithmic_bytes(plan, n, 0, 0, pres)
+    full = algorithmic_bytes(plan, n, 0, {}, {})
+    live = algorithmic_bytes(plan, n, 0, {}, pres)
     per = sum(4 * (n * plan.columns[c].n_slots - pres[c]) for c in odo_cols)
     assert full - live >= per

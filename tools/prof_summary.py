@@ -1,0 +1,92 @@
+"""Summary of one workload's round-3 GPU evidence (tools/gpu_r03.sh): the bench JSON line, the
+rocprofv3 kernel trace of the SAME process and the PMC passes of a 1-step run.
+
+* per kernel: calls, rocprof average over all calls, and the average over the timed steps only (the
+  last `steps` dispatches; the warm-up dispatches run first);
+* roofline recomputed from the trace: algorithmic bytes (from the bench line) / the traced average
+  of the decode kernel over the timed steps, next to the bench's HIP-event figure;
+* HBM traffic per launch: FETCH_SIZE (KiB) x 2 for the kernels that read with 16-byte-per-lane
+  streaming loads (MI355X_MICROARCH.md, HBM: gfx950 counts half of those), WRITE_SIZE as is, each
+  from the last dispatch of the kernel in the pass;
+* SQ counters per launch of each cbx kernel (the last dispatch).
+Usage: prof_summary.py <workload dir> -> JSON on stdout."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+D = sys.argv[1]
+STAGED16 = ("cbx_jit_decode", "cbx::decode_kernel", "cbx::list_kernel")   # 16-byte/lane staged reads
+
+
+def base(name: str) -> str:
+    n = name.split("(")[0].replace("void ", "", 1)
+    return n.split("<")[0] if n.startswith("cbx::") else n
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(os.path.join(D, pattern), recursive=True):
+        out += list(csv.DictReader(open(f)))
+    return out
+
+
+bench = json.loads([ln for ln in open(os.path.join(D, "bench.json")) if ln.startswith("{")][-1])
+steps = bench["steps"]
+trace = rows("trace/**/run_kernel_trace.csv")
+per = collections.defaultdict(list)
+for r in sorted(trace, key=lambda r: int(r["Start_Timestamp"])):
+    per[base(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+kernels = {}
+for k, d in per.items():
+    if not (k.startswith("cbx") or "cbx" in k):
+        continue
+    timed = d[-steps:] if len(d) >= steps else d
+    kernels[k] = {"calls": len(d), "avg_ms_all": round(sum(d) / len(d), 4), "avg_ms_timed_steps": round(sum(timed) / len(timed), 4),
+                  "max_ms": round(max(d), 4)}
+
+dec = [k for k in kernels if k.startswith("cbx_jit_decode") or k == "cbx::decode_kernel" or k == "cbx::walk_kernel"]
+alg = bench["roofline"]["algorithmic_bytes_per_launch"]
+check = {}
+if dec:
+    k = dec[0]
+    t = kernels[k]["avg_ms_timed_steps"]
+    if "cbx::list_kernel" in kernels:      # the bench's decode time covers the record and the list kernel
+        t += kernels["cbx::list_kernel"]["avg_ms_timed_steps"]
+    frac = alg / (t * 1e-3) / 1e9 / bench["roofline"]["peak"]
+    check = {"kernel": k + (" + cbx::list_kernel" if "cbx::list_kernel" in kernels else ""), "rocprof_ms": round(t, 4),
+             "hip_event_ms": bench["kernel_ms"]["decode_kernel"], "frac_rocprof": round(frac, 4),
+             "frac_bench": bench["roofline"]["frac"],
+             "agree_within": round(abs(frac - bench["roofline"]["frac"]) / bench["roofline"]["frac"], 4)}
+
+pmc = collections.defaultdict(lambda: collections.defaultdict(dict))   # kernel -> counter -> dispatch -> value
+for i in range(1, 9):
+    for r in rows(f"pmc{i}/**/run_counter_collection.csv"):
+        k = base(r["Kernel_Name"])
+        if "cbx" not in k:
+            continue
+        d = pmc[k][r["Counter_Name"]]
+        d[int(r["Dispatch_Id"])] = d.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+counters, traffic = {}, {}
+for k, cs in pmc.items():
+    last = {c: v[max(v)] for c, v in cs.items()}
+    counters[k] = {c: int(v) for c, v in sorted(last.items())}
+    if "FETCH_SIZE" in last or "WRITE_SIZE" in last:
+        f = last.get("FETCH_SIZE", 0.0) * 1024.0
+        w = last.get("WRITE_SIZE", 0.0) * 1024.0
+        scale = 2.0 if k.startswith(STAGED16) else 1.0
+        traffic[k] = {"fetch_bytes_raw": int(f), "fetch_bytes": int(f * scale), "write_bytes": int(w),
+                      "traffic_bytes": int(f * scale + w), "fetch_scale": scale}
+    if "SQ_LDS_BANK_CONFLICT" in last and last.get("SQ_ACTIVE_INST_LDS"):
+        counters[k]["lds_conflict_per_active_lds"] = round(last["SQ_LDS_BANK_CONFLICT"] / last["SQ_ACTIVE_INST_LDS"], 3)
+    if last.get("SQ_WAVE_CYCLES"):
+        counters[k]["wait_any_frac"] = round(last.get("SQ_WAIT_ANY", 0) / last["SQ_WAVE_CYCLES"], 3)
+dec_traffic = sum(v["traffic_bytes"] for k, v in traffic.items() if k.startswith(STAGED16))
+print(json.dumps({"workload": bench["config"]["workload"][:60], "records": bench["config"]["records_per_gpu"],
+                  "bench": {k: bench[k] for k in ("value", "ms_per_step", "kernel_ms", "roofline", "hbm_frac_step")},
+                  "kernels": kernels, "check": check, "traffic": traffic,
+                  "decode_traffic_bytes": dec_traffic or None,
+                  "decode_traffic_over_algorithmic": round(dec_traffic / alg, 3) if dec_traffic else None,
+                  "counters": counters}, indent=1))
