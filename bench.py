@@ -181,7 +181,7 @@ WORKLOADS = {
                    desc="SYN200: fixed-length 200-byte EBCDIC records, numeric mix (COMP, COMP-3, zoned DISPLAY "
                         "overpunch, IBM COMP-2, cp037 X(18)) -- BASELINE config C2",
                    data="synthetic (cobrix_amd/synth.py SYN200, seed 20261015+rank, 0.5% malformed numerics)"),
-    "synstr200": dict(records=50_000_000, config="C3", strings="views",
+    "synstr200": dict(records=50_000_000, config="C3", strings="offsets",
                       desc="SYNSTR200: fixed-length 200-byte records, 10 x PIC X(20) cp037 -> UTF-8, trim both "
                            "-- BASELINE config C3",
                       data="synthetic (cobrix_amd/synth.py SYNSTR200: lengths 0-20, 25% accented, 10% leading "
@@ -200,8 +200,13 @@ WORKLOADS = {
 
 STRING_LAYOUTS = {
     "views": "Arrow string views (16 B views + long payloads, one pass)",
-    "offsets": "Arrow large-string (int64 offsets + payload)",
+    "offsets": "Arrow Utf8 (int32 offsets + payload: count pass, device scan, written once in place)",
+    "large": "Arrow large-string (int64 offsets + payload: scratch, scan, placement pass)",
 }
+
+
+def _layout_params(strings: str) -> dict:
+    return {"string_views": strings == "views", "string_utf8": strings == "offsets"}
 
 
 class _Fixed:
@@ -209,15 +214,15 @@ class _Fixed:
         import torch
         from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters
         from cobrix_amd import synth
-        views = strings == "views"
+        lay = _layout_params(strings)
         if name == "syn200":
             cb, self.stride = synth.SYN200_COPYBOOK, synth.SYN200_RECORD_SIZE
             self.rec = synth.syn200(n_rec, seed=20261015 + rank, device=dev).view(-1)
-            params = ReaderParameters(window_bytes=window, string_views=views)
+            params = ReaderParameters(window_bytes=window, **lay)
         else:
             cb, self.stride = synth.SYNSTR200_COPYBOOK, synth.SYNSTR200_RECORD_SIZE
             self.rec = synth.synstr200(n_rec, seed=20261017 + rank, device=dev).view(-1)
-            params = ReaderParameters(window_bytes=window, ebcdic_code_page="cp037", string_views=views)
+            params = ReaderParameters(window_bytes=window, ebcdic_code_page="cp037", **lay)
         torch.cuda.synchronize()
         self.rd = FixedLenNestedReader(cb, params)
         self.n_rec, self.in_bytes, self.dev = n_rec, n_rec * self.stride, dev
@@ -350,7 +355,7 @@ class _VarLen:
         torch.cuda.synchronize()
         total_bytes = int(full.numel())
         opts = dict(is_record_sequence=True, segment_field="SEGMENT-ID", segment_id_redefine_map=segs,
-                    window_bytes=window, string_views=strings == "views", occurs_lists=lists, generate_record_id=True)
+                    window_bytes=window, occurs_lists=lists, generate_record_id=True, **_layout_params(strings))
         self.rd = VarLenNestedReader(cb, ReaderParameters(**opts))
         # segment_id_root only shapes the index (cuts at roots); the decode plan is the C4/C5 one
         ip = dict(is_record_sequence=True, segment_field="SEGMENT-ID", segment_id_levels=["C"])
@@ -681,8 +686,9 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="records per GPU (root records for wide_odo); "
                                                            "0 = the workload's default")
     ap.add_argument("--window", type=int, default=0, help="LDS window bytes (0 = plan default)")
-    ap.add_argument("--strings", default="", choices=["", "views", "offsets"],
-                    help="string column layout (default per workload): Arrow string views or large-string offsets")
+    ap.add_argument("--strings", default="", choices=["", "views", "offsets", "large"],
+                    help="string column layout (default per workload): Arrow string views, Arrow Utf8 offsets "
+                         "(in place after a count pass) or Arrow large-string offsets (placement pass)")
     ap.add_argument("--occurs", default="lists", choices=["lists", "slots"],
                     help="OCCURS DEPENDING ON layout: Arrow lists (present elements) or one slot row per element")
     ap.add_argument("--seed-mb", type=int, default=100, choices=[100, 32],
@@ -787,6 +793,8 @@ def main():
     N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
     kname = {1: "cbx_jit_decode (copybook-specialised, hipRTC)", 2: "cbx::walk_kernel (record walk)"}.get(
         kind.value, "cbx::decode_kernel (table-driven)")
+    if strings == "offsets" and any(c.out_type in (N.O_STRING, N.O_BINARY) for c in plan.columns):
+        kname = "Utf8 count pass (cbx_jit_count) + device scan + " + kname + " (decode_kernel time covers all three)"
     lists = any(c.list_array >= 0 for c in plan.columns)
     if lists:   # the OCCURS list elements: the element-parallel kernel launched right after the decode kernel
         kname += " + cbx::list_kernel (OCCURS lists; decode_kernel time covers both)"

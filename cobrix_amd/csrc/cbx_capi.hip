@@ -73,6 +73,7 @@ struct cbx_plan {
     std::vector<int32_t> col_slots;       // per column: slots
     std::vector<int32_t> col_max_bytes;   // per column: max payload bytes per value
     bool view = false;                    // string columns in the string-view layout
+    bool packed = false;                  // string columns in the Arrow Utf8 layout (count pass + one decode pass)
     std::vector<int32_t> segid_cols;      // segment levels with a Seg_Id column
     std::vector<ListOp> lops;             // list-layout fields (list_kernel), grouped by array
     ListOp* d_lops = nullptr;
@@ -110,8 +111,10 @@ struct cbx_plan {
     int64_t jit_min = 262144;
     // specialised kernels: [0] windowed op set, [kp] contiguous op set with kp chunks per lane,
     // [kPre + 1 + kp] the contiguous op set over variable-length spans (span_loop)
-    bool jit_tried[2 * kPre + 2] = {};
-    hipFunction_t jit_fn[2 * kPre + 2] = {};
+    // specialised kernels: [0, kPre] contiguous decode by prefetch depth, kPre + 1 + kp span decode,
+    // 2 (kPre + 1) + kp the Utf8 layout's contiguous count pass
+    bool jit_tried[3 * kPre + 3] = {};
+    hipFunction_t jit_fn[3 * kPre + 3] = {};
     int rec_extent = 0;          // bytes past the decode base that any field (any OCCURS element) reaches
     std::string jit_error;
     int last_kind = 0;
@@ -372,7 +375,10 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     if (const char* e = getenv("CBX_JIT"))
         if (e[0] == '0') P->jit_min = -1;   // operator switch: table-driven kernel only
     P->n_columns = opts->n_columns;
-    P->view = opts->string_views != 0;
+    if (opts->string_views < 0 || opts->string_views > 2)
+        { delete P; return fail(CBX_E_ARGUMENT, "cbx_plan_create: string_views must be 0, 1 or 2"); }
+    P->view = opts->string_views == 1;
+    P->packed = opts->string_views == 2;
     if (P->n_columns <= 0) { delete P; return fail(CBX_E_ARGUMENT, "cbx_plan_create: n_columns must be positive"); }
     P->hfields.assign(fields, fields + n_fields);
     if (n_arrays) P->harrays.assign(arrays, arrays + n_arrays);
@@ -648,7 +654,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.rec_seg = c.rec_seg;
     a.file_id = c.file_id >= 0 ? c.file_id : P->opts.file_id;
     a.mode = mode;
-    a.str_view = P->view ? 1 : 0;
+    a.str_view = P->view ? 1 : P->packed ? 2 : 0;
     // staging mode
     const int sdw = c.stride / 4;
     const bool contig = !c.rec_off && P->contig_ok && c.stride > 0 && c.stride % 4 == 0 && a.base_shift % 4 == 0 &&
@@ -731,7 +737,14 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // column table + per-op address tables: stream-ordered uploads from pageable host memory
     // (staged by the runtime, so the host vectors are free again when the call returns)
     const int n_defer_seq = (int)P->hdefer.size();
-    if (mode == 0 && P->n_seq > 0 && !P->view) {
+    if (mode == 0 && P->n_seq > 0 && P->packed) {   // the count pass's scan target, before the call tables point at it
+        const int64_t n = (int64_t)P->n_seq * n_tiles;
+        int rr;
+        if ((rr = grow(&P->d_str_excl, &P->str_excl_cap, n, st)) ||
+            (rr = grow(&P->d_block_sums, &P->block_sums_cap, (n + kScanTile - 1) / kScanTile, st)))
+            return rr;
+    }
+    if (mode == 0 && P->n_seq > 0 && !P->view && !P->packed) {
         int rr;
         P->h_seq_scratch.resize(P->n_seq);
         int64_t scratch = 0;
@@ -784,6 +797,12 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                 sc.scratch = col.data + (int64_t)op.slot * col.data_capacity;
                 sc.views = (uint8_t*)col.values + (int64_t)op.slot * a.pitch * 16;
                 sc.tiles_per_buf = view_tiles_per_buf(sc.tile_cap);
+            } else if (P->packed) {   // Arrow Utf8: int32 offsets (pitch + 1 per slot) + the slot's region
+                sc.local = (uint32_t*)((int32_t*)col.offsets + (int64_t)op.slot * (a.pitch + 1));
+                sc.scratch = col.data + (int64_t)op.slot * col.data_capacity;
+                sc.tile_cap = col.data_capacity;
+                sc.excl = P->d_str_excl + (int64_t)op.seq * n_tiles;
+                sc.size = col.data_sizes ? col.data_sizes + op.slot : nullptr;
             } else {
                 sc.local = P->d_local + (int64_t)op.seq * a.pitch;
                 sc.scratch = P->d_scratch + P->h_seq_scratch[op.seq];
@@ -791,7 +810,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
             }
             P->h_scall[i] = sc;
         }
-        P->h_seqcall.resize(P->view ? 0 : P->n_seq);   // placement pass only in the offsets layout
+        P->h_seqcall.resize(P->view || P->packed ? 0 : P->n_seq);   // placement pass only in the large-string layout
         for (int q = 0; q < (int)P->h_seqcall.size(); q++) {
             const Field& d = P->dfields_h[P->seq_field[q]];
             const cbx_column& col = columns[d.column];
@@ -807,7 +826,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
             sq.tile_cap = (int32_t)P->seq_tile_cap[q];
             P->h_seqcall[q] = sq;
         }
-        if (P->n_seq > 0 && !P->view)
+        if (P->n_seq > 0 && !P->view && !P->packed)
             HIP_CHECK(hipMemcpyAsync(P->d_seqcall, P->h_seqcall.data(), sizeof(SeqCall) * P->n_seq, hipMemcpyHostToDevice, st));
         if (P->h_ncall.size() > P->ncall_cap) {
             HIP_CHECK(hipStreamSynchronize(st));
@@ -885,6 +904,43 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
         HIP_CHECK(hipEventRecord(ce.e[0], st));
     }
+    if (mode == 0 && P->packed && P->n_seq > 0 && !contig) {
+        // Arrow Utf8 layout, windowed / span-staged records: the table-driven count pass (a mode-1
+        // call: tile payload totals + their scan), timed with the decode
+        const int kind = P->last_kind;
+        if ((r = launch(P, c, columns, 1, st))) return r;
+        P->last_kind = kind;
+    } else if (mode == 0 && P->packed && P->n_seq > 0) {
+        // Arrow Utf8 layout: the count pass (tile payload totals) and their scan, so the decode writes
+        // every offset and payload byte once, at its final place (timed with the decode)
+        KernelArgs ac = a;
+        ac.mode = 1;
+        hipFunction_t cfn = nullptr;
+        if (contig && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
+            const int k = 2 * (kPre + 1) + contig_kp(sdw);
+            if (!P->jit_tried[k]) {
+                P->jit_tried[k] = true;
+                std::string err;
+                P->jit_fn[k] = jit_get(jit_source(true, contig_kp(sdw), jit_pro(P), false, S.win, S.nops, S.batches, S.sops, false, true),
+                                       &err, "cbx_jit_count");
+            }
+            cfn = P->jit_fn[k];
+        }
+        int cocc = 0;
+        const hipError_t ce2 = cfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, cfn, kWave * kWavesPerBlock, lds)
+                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, decode_kernel, kWave * kWavesPerBlock, lds);
+        int cbpc = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / lds));
+        if (ce2 == hipSuccess && cocc > 0) cbpc = std::min(cbpc, cocc);
+        const int64_t cgrid = std::min<int64_t>(blocks_needed, (int64_t)P->num_cus * cbpc);
+        if (cfn) {
+            void* kargs[] = {&ac};
+            HIP_CHECK(hipModuleLaunchKernel(cfn, (unsigned)cgrid, 1, 1, kWave * kWavesPerBlock, 1, 1, (unsigned)lds, st, kargs, nullptr));
+        } else {
+            hipLaunchKernelGGL(decode_kernel, dim3((unsigned)cgrid), dim3(kWave * kWavesPerBlock), lds, st, ac);
+            HIP_CHECK(hipGetLastError());
+        }
+        if ((r = string_scan(P, n_tiles, st))) return r;
+    }
     if (jfn) {
         void* kargs[] = {&a};
         HIP_CHECK(hipModuleLaunchKernel(jfn, (unsigned)grid, 1, 1, kWave * kWavesPerBlock, 1, 1, (unsigned)lds, st, kargs, nullptr));
@@ -909,7 +965,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                            (const CBX_CONST DeferSeq*)P->d_defer, n_defer);
         HIP_CHECK(hipGetLastError());
     }
-    if (P->n_seq > 0 && !(P->view && mode == 0)) {
+    if (P->n_seq > 0 && !((P->view || P->packed) && mode == 0)) {
         if ((r = string_scan(P, n_tiles, st))) return r;
         if (mode == 0) {
             const unsigned gx = (unsigned)((n_tiles + kPlaceWaves * kPlaceTiles - 1) / (kPlaceWaves * kPlaceTiles));
@@ -1063,6 +1119,9 @@ extern "C" int cbx_plan_specialize(cbx_plan* P, char* source, int64_t source_cap
         std::vector<char> code;
         std::string err;
         if (!jit_compile(src, &code, &err)) return fail(CBX_E_HIP, err);
+        if (P->packed && P->contig_ok && P->n_seq > 0 &&   // the Utf8 layout's count pass too
+            !jit_compile(jit_source(true, kPre, jit_pro(P), false, S.win, S.nops, S.batches, S.sops, false, true), &code, &err))
+            return fail(CBX_E_HIP, err);
     }
     return CBX_OK;
 }
@@ -1455,6 +1514,17 @@ extern "C" int cbx_select_records(cbx_plan* P, const uint8_t* d_data, int64_t n_
     return CBX_OK;
 }
 
+namespace cbx {
+// Utf8 layout: int64 offsets of a scanned column narrowed to Arrow's int32 (overflow -> status)
+__global__ void narrow_offsets_kernel(const int64_t* in, int64_t n, int32_t* out, int32_t* status) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t v = in[i];
+    if (v > 0x7fffffffll) atomicOr(status, 1);
+    out[i] = (int32_t)v;
+}
+}  // namespace cbx
+
 extern "C" int cbx_decode_selected(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, const cbx_selection* sel,
                                    int64_t n_rec, int32_t start_offset, cbx_column* columns, void* stream) {
     hipStream_t st = (hipStream_t)stream;
@@ -1487,25 +1557,31 @@ extern "C" int cbx_decode_selected(cbx_plan* P, const uint8_t* d_data, int64_t n
             continue;
         }
         if (n_rec == 0) {
-            HIP_CHECK(hipMemsetAsync(col.offsets, 0, sizeof(int64_t), st));
+            HIP_CHECK(hipMemsetAsync(col.offsets, 0, P->packed ? sizeof(int32_t) : sizeof(int64_t), st));
             if (col.data_sizes) HIP_CHECK(hipMemsetAsync(col.data_sizes, 0, sizeof(int64_t), st));
             continue;
         }
         AsyncBlock blk(st);
         const int64_t nb = scan_sums_len(n_rec + 1);
-        HIP_CHECK(hipMallocAsync(&blk.p, sizeof(uint32_t) * (n_rec + 1) + sizeof(int64_t) * nb + 16, st));
+        // (Utf8 layout: int64 offsets scanned into the block, narrowed to the column's int32 after)
+        const int64_t n64 = P->packed ? n_rec + 1 : 0;
+        HIP_CHECK(hipMallocAsync(&blk.p, sizeof(int64_t) * (nb + n64) + sizeof(uint32_t) * (n_rec + 1) + 16, st));
         int64_t* sums = (int64_t*)blk.p;
-        uint32_t* len = (uint32_t*)(sums + nb);
+        int64_t* offs64 = P->packed ? sums + nb : (int64_t*)col.offsets;
+        uint32_t* len = (uint32_t*)(sums + nb + n64);
         SegIdArgs g{};
         g.state = sel->seg_state; g.n = n_rec; g.L = L; g.level = l; g.file_id = sel->file_id;
         g.prefix_len = P->opts.segments.prefix_len;
         g.m = (const CBX_CONST cbx_segment_map*)P->d_segmap;
         hipLaunchKernelGGL(segid_len_kernel, dim3(blocks_for(n_rec + 1, 256)), dim3(256), 0, st, g, len);
-        device_scan(len, n_rec + 1, col.offsets, sums, st);
-        hipLaunchKernelGGL(segid_write_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, g, (int64_t*)col.offsets,
+        device_scan(len, n_rec + 1, offs64, sums, st);
+        hipLaunchKernelGGL(segid_write_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, g, offs64,
                            col.data, col.data_capacity, col.validity, P->d_status);
+        if (P->packed)
+            hipLaunchKernelGGL(narrow_offsets_kernel, dim3(blocks_for(n_rec + 1, 256)), dim3(256), 0, st,
+                               (const int64_t*)offs64, n_rec + 1, (int32_t*)col.offsets, P->d_status);
         if (col.data_sizes)
-            HIP_CHECK(hipMemcpyAsync(col.data_sizes, col.offsets + n_rec, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+            HIP_CHECK(hipMemcpyAsync(col.data_sizes, offs64 + n_rec, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
         HIP_CHECK(hipGetLastError());
     }
     return CBX_OK;

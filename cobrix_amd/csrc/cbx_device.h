@@ -724,11 +724,38 @@ __device__ __forceinline__ void str_view_pair(const KernelArgs& a, const StrOp& 
     (gp((u32x4*)cb.views) + t.tile * kWave)[lane] = sa ? z : v;
 }
 
+// n bytes from the 16-byte aligned LDS staging s to global d at any alignment: the bytes up to d's
+// next 16-byte boundary and the tail past the last whole chunk as byte stores (neighbouring tiles
+// own the bytes on either side, so no store may cover them), 16-byte stores in between, each
+// composed from five LDS dwords and a byte align.
+__device__ __forceinline__ void lds_to_global_any(const uint8_t* s, CBX_GLOBAL uint8_t* d, uint32_t n, int lane) {
+    const uint32_t mis = (uint32_t)((uint64_t)(size_t)d & 15u);
+    uint32_t head = (16u - mis) & 15u;
+    if (head > n) head = n;
+    const uint32_t body = (n - head) >> 4;
+    const uint32_t tail0 = head + 16u * body;
+    if ((uint32_t)lane < head) d[lane] = s[lane];
+    if (tail0 + (uint32_t)lane < n) d[tail0 + lane] = s[tail0 + lane];
+    const uint32_t sh = head & 3u;
+    for (uint32_t q = lane; q < body; q += kWave) {
+        const uint32_t o = head + 16u * q;
+        const uint32_t* w = (const uint32_t*)(s + (o & ~3u));
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+        *(CBX_GLOBAL u32x4*)(d + o) = u32x4{align_bytes(w1, w0, sh), align_bytes(w2, w1, sh), align_bytes(w3, w2, sh),
+                                           align_bytes(w4, w3, sh)};
+    }
+}
+
 // One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):
-// span + tile-local scan; the tile's payload is staged contiguously in LDS and copied with
-// dword stores to the tile's scratch region; the tile-local start of every value and the
-// tile's byte total are recorded for the compaction kernel, which places tiles after a
-// device-wide scan of the totals (two-pass string offsets, no cross-tile waiting).
+// span + tile-local scan.
+// * Arrow large-string layout (str_view 0): the tile's payload is staged contiguously in LDS and
+//   copied with dword stores to the tile's scratch region; the tile-local start of every value and
+//   the tile's byte total are recorded for the compaction kernel, which places tiles after a
+//   device-wide scan of the totals (two-pass string offsets, no cross-tile waiting).
+// * Arrow Utf8 layout (str_view 2): a count pass (this function in mode 1: the tile totals only) and
+//   a device scan of the totals ran before the decode, so the tile's place in the slot's region is
+//   known here: the int32 offsets and the payload are written once, at their final place -- staged
+//   in LDS at the tile-local starts and copied out with 16-byte stores (byte stores at the edges).
 template <bool kView, typename Sink = DirectSink>
 __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
                                             const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
@@ -758,10 +785,40 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
         return;
     }
     gp(c.validity)[t.tile] = __ballot(ok);
-    (gp(c.local) + t.tile * kWave)[lane] = ex;
-    if (lane == 0) gp(a.str_tot)[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
     auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
     const uint8_t* sp_src = src + rec_addr + (uint32_t)op.eo;
+    if (a.str_view == 2) {
+        const int64_t base = c.excl[t.tile] - c.excl[0];   // the tile's place in the slot's region
+        const int64_t end = base + tot;
+        CBX_GLOBAL int32_t* offs = gp((int32_t*)c.local);
+        (offs + t.tile * kWave)[lane] = (int32_t)(base + ex);
+        if (t.rec == a.n_rec - 1) {   // the closing offset and the slot's size
+            offs[a.n_rec] = (int32_t)(base + ex + sp.utf8_len);
+            if (c.size) *gp(c.size) = base + ex + sp.utf8_len;
+        }
+        if (end > c.tile_cap || end > 0x7fffffffll) {   // the region (or an int32 offset) overflows
+            if (lane == 0) atomicOr(a.status, 1);
+            return;
+        }
+        CBX_GLOBAL uint8_t* dst = gp(c.scratch + base);
+        if ((int)tot <= a.str_stage) {
+            if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + a.dump_stride * lane, op.size, op.pad);
+            else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
+            wave_sync_lds();
+            lds_to_global_any(s_str, dst, tot, lane);
+            wave_sync_lds();
+        } else if (ok) {
+            if (fast) {
+                uint8_t dump[4];
+                string_write32e(ev, sp, (uint8_t*)(dst + ex), dump, op.size, op.pad);
+            } else {
+                string_write(op.kind, sp_src, sp, (uint8_t*)(dst + ex), lutf);
+            }
+        }
+        return;
+    }
+    (gp(c.local) + t.tile * kWave)[lane] = ex;
+    if (lane == 0) gp(a.str_tot)[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
     uint32_t* dst32 = (uint32_t*)(c.scratch + t.tile * (int64_t)c.tile_cap);   // 16-byte aligned region
     if ((int)tot <= a.str_stage) {
         if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + a.dump_stride * lane, op.size, op.pad);

@@ -57,11 +57,16 @@ struct NumCall {
 struct StrCall {
     uint64_t* validity;       // validity words of (column, slot)
     uint32_t* local;          // tile-local start of every value of the slot (pitch entries)
+                              // (Utf8 layout: the slot's int32 Arrow offsets, pitch + 1 entries)
     uint8_t* scratch;         // tile regions of the slot: tile t at scratch + t * tile_cap
-                              // (string-view layout: the slot's region of the caller's data buffer)
+                              // (string-view and Utf8 layouts: the slot's region of the caller's data buffer)
     int64_t tile_cap;         // bytes per tile region (64 * size * widest UTF-8 expansion, 16-aligned)
+                              // (Utf8 layout: the region's capacity)
     uint8_t* views;           // string-view layout: the slot's 16-byte views (pitch entries)
     int64_t tiles_per_buf;    // string-view layout: tiles per Arrow data buffer
+    const int64_t* excl;      // Utf8 layout: exclusive scan of the (sequence, tile) payload totals, this
+                              // sequence's row (entry 0 = the sequence's start)
+    int64_t* size;            // Utf8 layout: the slot's payload bytes (data_sizes, may be null)
 };
 
 // One field of a list-layout OCCURS DEPENDING ON array (CBX_F_LIST): the list kernel decodes its
@@ -120,7 +125,8 @@ struct KernelArgs {
     const int32_t* rec_seg;    // per-record active segment (selected records), nullptr: from segmap
     int32_t file_id;
     int32_t mode;              // 0 decode, 1 string sizes only
-    int32_t str_view;          // string columns in the Arrow string-view layout
+    int32_t str_view;          // string columns: 0 Arrow large-string (scratch + placement), 1 string views,
+                               // 2 Arrow Utf8 (int32 offsets; payload written at its final place)
     // fixed-length contiguous staging: the tile's byte span is loaded with 16-byte loads and
     // scattered dword-wise into rows of `cpitch` bytes (odd dword count: conflict-free lanes)
     int32_t contig;

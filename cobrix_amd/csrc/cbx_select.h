@@ -418,14 +418,16 @@ __global__ __launch_bounds__(64) void idx_walk_kernel(IdxArgs a, const int64_t* 
             step *= 64;
         }
         if (hi > n_cand) hi = n_cand;
-        // 64-ary search in [lo, hi]
+        // 64-ary search in [lo, hi]: probes at lo + lane * st with st = ceil(span / 63), so lane 63
+        // probes at or past hi and the ballot is never empty (with ceil(span / 64) a match in the
+        // last stride left it empty, and ctz(0) sent the search backwards)
         while (lo < hi) {
             const int64_t span = hi - lo;
-            const int64_t st = (span + 63) / 64;
+            const int64_t st = (span + 62) / 63;
             const int64_t r = lo + (int64_t)lane * st;
             const bool good = r >= hi || ok(r);
             const uint64_t m = __ballot(good);
-            const int f = __builtin_ctzll(m);     // lane 63 probes >= hi only when span <= 63*st
+            const int f = __builtin_ctzll(m);
             const int64_t rf = lo + (int64_t)f * st;
             if (f == 0) { hi = lo; break; }
             lo = lo + (int64_t)(f - 1) * st + 1;

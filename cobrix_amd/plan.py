@@ -153,7 +153,7 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
                segment_redefine_map: Optional[Dict[str, str]] = None, generate_record_id: bool = False,
                file_id: int = 0, window_bytes: int = 0, jit_min_records: int = 0,
                segment_levels: Sequence[str] = (), segment_filter: Optional[List[str]] = None,
-               segment_prefix: str = "", string_views: bool = False, occurs_lists: bool = False,
+               segment_prefix: str = "", string_views: int = 0, occurs_lists: bool = False,
                root_keys: Sequence[str] = (), walk: bool = False, variable_size_occurs: bool = False) -> DecodePlan:
     """root_keys: segment ids of a hierarchical file's root segment (sparse-index cuts at level-0
     keys, IndexGenerator.scala:89-113, without Seg_IdN columns).  walk: the plan decodes through the
@@ -348,7 +348,8 @@ def build_plan(cb: cbk.Copybook, *, segment_field: Optional[str] = None,
     opts.window_bytes = window_bytes
     opts.segment_column = seg_col
     opts.jit_min_records = jit_min_records
-    opts.string_views = 1 if string_views else 0
+    # 0 Arrow large-string, 1 string views, 2 Arrow Utf8 (int32 offsets, count pass + one decode pass)
+    opts.string_views = int(string_views) if string_views in (0, 1, 2) else 1
     # the byte table: the code page (EBCDIC), the charset (ASCII wrapper), or for a US-ASCII copybook
     # decodeAsciiString's own mapping (bytes < 32 and >= 128 -> ' ') -- its strings decode through
     # ascii_lut on the device; the table serves the segment-id match (segment_key)

@@ -80,6 +80,11 @@ class ReaderParameters:
     # output layout of string columns: Arrow large-string (offsets, two-pass placement) or Arrow
     # string views (one pass: every value written once by the decode kernel; cobrix_hip.h)
     string_views: bool = False
+    # Arrow Utf8 layout (cbx_plan_options.string_views = 2): int32 offsets relative to each slot's
+    # region, a count pass + device scan, then every offset and payload byte written once at its final
+    # place by the decode kernel (no placement pass); takes precedence over string_views except on the
+    # record walk, which writes views
+    string_utf8: bool = False
     # OCCURS DEPENDING ON arrays of numeric elements in the list layout (child elements packed per
     # record, absent elements unwritten; cobrix_hip.h CBX_F_LIST) instead of one slot row per element
     occurs_lists: bool = False
@@ -151,6 +156,11 @@ class DecodedBatch:
             # slot s: offsets[s * (pitch + 1) .. + n_rec], absolute into data (slot regions)
             out["offsets"] = c["offsets"].cpu().numpy().reshape(info.n_slots, 64 * pitch + 1)[:, : self.n_rec + 1]
             out["data"] = c["data"].cpu().numpy().tobytes()
+        elif c.get("offsets32") is not None:
+            # Utf8: int32 offsets relative to slot s's region -> absolute, as above
+            o = c["offsets32"].cpu().numpy().reshape(info.n_slots, 64 * pitch + 1)[:, : self.n_rec + 1].astype(np.int64)
+            out["offsets"] = o + (np.arange(info.n_slots, dtype=np.int64) * c["capacity"])[:, None]
+            out["data"] = c["data"].cpu().numpy().tobytes()
         else:
             v = c["values"].cpu().numpy()
             if info.out_type == N.O_DEC128:
@@ -190,6 +200,10 @@ class DecodedBatch:
         elif "offsets" in c:
             offs = c["offsets"].cpu().numpy().reshape(info.n_slots, pitch + 1)
             data = c["data"].cpu().numpy()
+        elif "offsets32" in c:
+            offs = c["offsets32"].cpu().numpy().reshape(info.n_slots, pitch + 1)
+            data = c["data"].cpu().numpy()
+            cap = c["capacity"]
         else:
             vals = c["values"].cpu().numpy()
         for s in range(info.n_slots):
@@ -199,6 +213,10 @@ class DecodedBatch:
                 bufs = [pa.py_buffer(region[k:k + bb].tobytes()) for k in range(0, max(len(region), 1), bb)]
                 typ = pa.string_view() if ot == N.O_STRING else pa.binary_view()
                 arr = pa.Array.from_buffers(typ, n, [valid, pa.py_buffer(views[s, :n].tobytes())] + bufs)
+            elif "offsets32" in c:   # Arrow Utf8 / Binary: the slot's own region, int32 offsets into it
+                typ = pa.string() if ot == N.O_STRING else pa.binary()
+                arr = pa.Array.from_buffers(typ, n, [valid, pa.py_buffer(offs[s, :n + 1].tobytes()),
+                                                     pa.py_buffer(data[s * cap:(s + 1) * cap].tobytes())])
             elif "offsets" in c:
                 typ = pa.large_string() if ot == N.O_STRING else pa.large_binary()
                 arr = pa.Array.from_buffers(typ, n, [valid, pa.py_buffer(offs[s, :n + 1].tobytes()), pa.py_buffer(data.tobytes())])
@@ -448,7 +466,18 @@ def _alloc_columns(plan: DecodePlan, n_rec: int, slot_capacity: Sequence[int], d
     for ci, info in enumerate(plan.columns):
         n = pitch * info.n_slots
         c: Dict[str, Any] = {"validity": torch.zeros(max(1, info.n_slots * pitch_words), dtype=torch.int64, device=device)}
-        if info.out_type in (N.O_STRING, N.O_BINARY) and plan.options.string_views:
+        if info.out_type in (N.O_STRING, N.O_BINARY) and plan.options.string_views == 2:
+            # Arrow Utf8: int32 offsets per slot (pitch + 1, relative to the slot's region) + regions
+            cap = int(slot_capacity[ci])
+            c["offsets32"] = torch.zeros(info.n_slots * (pitch + 1), dtype=torch.int32, device=device)
+            c["data"] = torch.empty(max(1, cap * info.n_slots), dtype=torch.uint8, device=device)
+            c["sizes"] = torch.zeros(info.n_slots, dtype=torch.int64, device=device)
+            c["capacity"] = cap
+            cstructs[ci].offsets = c["offsets32"].data_ptr()
+            cstructs[ci].data = c["data"].data_ptr()
+            cstructs[ci].data_capacity = cap
+            cstructs[ci].data_sizes = c["sizes"].data_ptr()
+        elif info.out_type in (N.O_STRING, N.O_BINARY) and plan.options.string_views:
             # string views: 16 bytes per value + per-slot regions of whole tiles (cobrix_hip.h)
             cap = int(slot_capacity[ci])
             c["views"] = torch.zeros(max(1, n * 16), dtype=torch.uint8, device=device)
@@ -716,7 +745,9 @@ class _BaseReader:
                               jit_min_records=params.jit_min_records,
                               segment_levels=params.segment_id_levels if var else (),
                               segment_filter=params.segment_id_filter if var else None,
-                              segment_prefix=params.segment_id_prefix, string_views=params.string_views or walk,
+                              segment_prefix=params.segment_id_prefix,
+                              string_views=1 if (walk or (params.string_views and not params.string_utf8))
+                              else 2 if params.string_utf8 else 0,
                               occurs_lists=params.occurs_lists, root_keys=root_keys, walk=walk,
                               variable_size_occurs=params.variable_size_occurs)
 

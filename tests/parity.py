@@ -126,7 +126,13 @@ def compare_sample(batch, idx: np.ndarray, res: "O.OracleResult", max_report: in
         ot = info.out_type
         if ot in (N.O_STRING, N.O_BINARY):
             views = c["views"].view(info.n_slots, pitch, 16) if "views" in c else None
-            offs = c["offsets"].view(info.n_slots, pitch + 1) if views is None else None
+            if views is not None:
+                offs = None
+            elif "offsets32" in c:   # Utf8: relative to the slot's region
+                offs = (c["offsets32"].view(info.n_slots, pitch + 1).to(torch.int64) +
+                        c["capacity"] * torch.arange(info.n_slots, device=c["offsets32"].device).view(-1, 1))
+            else:
+                offs = c["offsets"].view(info.n_slots, pitch + 1)
             for k in range(len(rec)):
                 r, s = int(idx[rec[k]]), int(slot[k])
                 if views is not None:

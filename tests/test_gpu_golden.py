@@ -42,13 +42,16 @@ def gpu_rows(case, **extra):
 
 
 @pytest.mark.parametrize("name", sorted(GC.CASES))
-@pytest.mark.parametrize("jit,views,lists", [(-1, False, False), (1, False, False), (-1, True, True), (1, True, True)])
+@pytest.mark.parametrize("jit,views,lists", [(-1, False, False), (1, False, False), (-1, True, True), (1, True, True),
+                                             (-1, "utf8", True), (1, "utf8", False)])
 def test_gpu_golden_rows(name, jit, views, lists):
-    """Both decode kernels (table-driven: jit=-1; copybook-specialised: jit=1), in both string
-    layouts (Arrow offsets / Arrow string views) and both OCCURS DEPENDING ON layouts (slot rows /
-    lists), reproduce the reference's golden rows and the oracle's full row set."""
+    """Both decode kernels (table-driven: jit=-1; copybook-specialised: jit=1), in the three string
+    layouts (Arrow large-string offsets / Arrow string views / Arrow Utf8 written in place after a count
+    pass) and both OCCURS DEPENDING ON layouts (slot rows / lists), reproduce the reference's golden
+    rows and the oracle's full row set."""
     case = GC.CASES[name]
-    rd, rows = gpu_rows(case, jit_min_records=jit, string_views=views, occurs_lists=lists)
+    rd, rows = gpu_rows(case, jit_min_records=jit, string_views=views is True, string_utf8=views == "utf8",
+                        occurs_lists=lists)
     errs = GC.compare(case, rows)
     assert not errs, errs[:10]
     p, var_len = GC.params(case)
@@ -174,7 +177,7 @@ def _norm(v):
     return v
 
 
-@pytest.mark.parametrize("views", [False, True])
+@pytest.mark.parametrize("views", [False, True, "utf8"])
 @pytest.mark.parametrize("name", ["test1", "test5", "test6", "test9_cp037", "test19", "test17a", "test17c", "test17d", "test17e", "test17f"])
 def test_gpu_arrow_export_matches_rows(name, views):
     _arrow_vs_rows(name, views)
@@ -187,8 +190,9 @@ def _arrow_vs_rows(name, views):
     from cobrix_amd.reader import FixedLenNestedReader, VarLenNestedReader
     case = GC.CASES[name]
     p, var_len = GC.params(case)
-    p.string_views = views
-    p.occurs_lists = views
+    p.string_views = views is True
+    p.string_utf8 = views == "utf8"
+    p.occurs_lists = bool(views)
     data = GC.data_bytes(case)
     rd = (VarLenNestedReader if var_len else FixedLenNestedReader)(GC.copybook_text(case), p)
     batch = rd.read(data) if var_len else rd.decode(data)
@@ -212,3 +216,65 @@ def test_gpu_var_occurs_framing(name, lengths):
     assert ln.cpu().tolist() == lengths
     assert off.cpu().tolist() == [sum(lengths[:i]) for i in range(len(lengths))]
     assert vb == max(len(data), sum(lengths))
+
+
+@pytest.mark.parametrize("n,entry_bytes", [(600_000, 1_500_000), (600_000, 2_000_000)])
+def test_gpu_sparse_index_reset_long_gaps(n, entry_bytes):
+    """Size splits with the reset rule at root segments over gaps of thousands of candidates: the
+    one-wave walk's galloping reaches step 64 and its 64-ary search spans of 4,095 candidates, where a
+    match in the last stride once left the ballot empty."""
+    from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow
+    raw = rdw_narrow(n, seed=5)[0].numpy().tobytes()
+    rd, p = _var_reader(RDW_NARROW_COPYBOOK, {**_SYN_OPTS, "segment_id_root": "C"})
+    got = _gpu_index(rd, raw, prm_override={"bytes_per_entry": entry_bytes, "subtract_size": 0})
+    exp = [(e.offset_from, e.offset_to, e.record_index) for e in RO.sparse_index(rd.copybook, raw, p, 0, entry_bytes)]
+    assert len(exp) > 20
+    assert got == exp
+
+
+def test_gpu_sparse_index_reset_bench_scale():
+    """The bench's index at scale: 100 MB entries (the default, reset) cut at roots over a 5 M-record
+    file with 16 MB entries (gaps of ~90 k candidates: galloping at step 4,096); expected entries
+    from the rule itself (next root whose header offset is >= the last entry's + the entry size),
+    which the oracle restatement pins on the smaller cases above."""
+    import bisect
+    import numpy as np
+    from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow_large
+    t, hdr = rdw_narrow_large(5_000_000, seed=9, device="cuda")
+    n_bytes = int(t.numel())
+    rd, p = _var_reader(RDW_NARROW_COPYBOOK, {**_SYN_OPTS, "segment_id_root": "C"})
+    off, ln = rd.frame(t, n_bytes)
+    h = hdr.cpu().numpy()
+    assert off.numel() == h.size
+    S = 16 * 1024 * 1024
+    ents = rd.generate_index(t, n_bytes, off, ln)
+    raw = t.cpu().numpy()
+    lens = ln.cpu().numpy().astype(np.int64)
+    root = (raw[h + 4] == 0xC3) & (h + 4 + lens < n_bytes)
+    cand = h[root].tolist()
+    exp, pp = [0], 0
+    while True:
+        r = bisect.bisect_left(cand, pp + S)
+        if r >= len(cand):
+            break
+        pp = cand[r]
+        exp.append(pp)
+    assert len(exp) > 20
+    # the reader's index uses the 100 MB default: cut this file with 16 MB entries instead
+    prm = rd.index_params()
+    prm.bytes_per_entry, prm.subtract_size = S, 0
+    import ctypes
+    from cobrix_amd import native as N
+    arr = (N.CbxIndexEntry * 1000)()
+    ne = ctypes.c_int64(0)
+    N.check(N.load().cbx_sparse_index(rd.native.handle, t.data_ptr(), n_bytes, off.data_ptr(), ln.data_ptr(),
+                                      int(off.numel()), ctypes.byref(prm), arr, 1000, ctypes.byref(ne), None))
+    assert [arr[k].offset_from for k in range(ne.value)] == exp
+    exp100, pp = [0], 0
+    while True:
+        r = bisect.bisect_left(cand, pp + 100 * 1024 * 1024)
+        if r >= len(cand):
+            break
+        pp = cand[r]
+        exp100.append(pp)
+    assert [e.offset_from for e in ents] == exp100 and len(exp100) == 4

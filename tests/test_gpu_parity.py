@@ -26,6 +26,13 @@ def _gpu():
         pytest.skip("no GPU")
 
 
+LAYOUTS = ["large", "views", "utf8"]   # Arrow large-string offsets, string views, Arrow Utf8 (in place)
+
+
+def _layout(name):
+    return {"string_views": name == "views", "string_utf8": name == "utf8"}
+
+
 def _fixed(copybook_text, data: bytes, **kw):
     params = ReaderParameters(**kw)
     rd = FixedLenNestedReader(copybook_text, params)
@@ -206,18 +213,18 @@ def _jit_cases():
     return {"test1": t1, "test6": t6, "syn200": syn, "fuzz_cp037": fz}
 
 
-@pytest.mark.parametrize("views", [False, True])
+@pytest.mark.parametrize("views", LAYOUTS)
 @pytest.mark.parametrize("case", ["test1", "test6", "syn200", "fuzz_cp037"])
 def test_specialised_kernel_vs_oracle(case, views):
     """The copybook-specialised kernel (hipRTC, cbx_jit.h) gives the oracle's results bit for bit,
-    in both string layouts (Arrow offsets / Arrow string views)."""
+    in the three string layouts (Arrow large-string offsets / string views / Utf8)."""
     cb_text, data, kw, okw = _jit_cases()[case]
-    rd, batch = _fixed(cb_text, data, jit_min_records=1, string_views=views, **kw)
+    rd, batch = _fixed(cb_text, data, jit_min_records=1, **_layout(views), **kw)
     assert _kernel_kind(rd) == 1, "specialised kernel did not run"
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data, **okw))
     assert not errs, errs
     # the table-driven kernel on the same plan layout agrees as well
-    rd2, batch2 = _fixed(cb_text, data, jit_min_records=-1, string_views=views, **kw)
+    rd2, batch2 = _fixed(cb_text, data, jit_min_records=-1, **_layout(views), **kw)
     assert _kernel_kind(rd2) == 0
     assert not compare_batch(batch2, O.decode_fixed(rd2.copybook, data, **okw))
 
@@ -238,15 +245,15 @@ def test_specialised_kernel_segments_and_offsets():
     assert not compare_batch(batch, res)
 
 
-@pytest.mark.parametrize("views", [False, True])
+@pytest.mark.parametrize("views", LAYOUTS)
 @pytest.mark.parametrize("n,jit", [(1, 0), (4097, 0), (50_000, 0), (50_000, 1), (300_001, 0)])
 def test_synstr200_vs_oracle(n, jit, views):
-    """Config C3 (string-heavy cp037, trim both): UTF-8 payloads bit-exact in both string layouts
-    (Arrow offsets, Arrow string views), on both kernels (jit=1 forces the copybook-specialised
-    kernel the bench runs; 300,001 records pass the default specialisation threshold)."""
+    """Config C3 (string-heavy cp037, trim both): UTF-8 payloads bit-exact in the three string
+    layouts, on both kernels (jit=1 forces the copybook-specialised kernel the bench runs; 300,001
+    records pass the default specialisation threshold)."""
     from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
     data = synstr200(n, seed=3 + n).numpy().tobytes()
-    rd, batch = _fixed(SYNSTR200_COPYBOOK, data, ebcdic_code_page="cp037", jit_min_records=jit, string_views=views)
+    rd, batch = _fixed(SYNSTR200_COPYBOOK, data, ebcdic_code_page="cp037", jit_min_records=jit, **_layout(views))
     if n >= 262_144 or jit == 1:
         assert _kernel_kind(rd) == 1
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
@@ -320,7 +327,7 @@ def test_list_layout_fixed_vs_oracle(n, jit):
     assert not errs, errs
 
 
-@pytest.mark.parametrize("views", [False, True])
+@pytest.mark.parametrize("views", LAYOUTS)
 def test_syn200_full_size_sampled_parity(views):
     """The bench's own configuration (C2: 50 M SYN200 records = 10 GB resident in HBM, the
     copybook-specialised kernel): 6,000 records sampled across the whole batch (random, plus the
@@ -328,7 +335,7 @@ def test_syn200_full_size_sampled_parity(views):
     from parity import compare_sample
     n = 50_000_000
     rec = syn200(n, seed=20261015, device="cuda")
-    rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters(string_views=views))
+    rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters(**_layout(views)))
     batch = rd.decode_device(rec.view(-1), n * 200)
     assert _kernel_kind(rd) == 1
     rng = np.random.default_rng(2)
@@ -337,8 +344,8 @@ def test_syn200_full_size_sampled_parity(views):
     errs = compare_sample(batch, idx, O.decode_fixed(rd.copybook, sample))
     assert not errs, errs
     for ci, info in enumerate(rd.plan.columns):
-        if info.out_type == 7 and not views:   # O_STRING: offsets non-decreasing over all 50 M records
-            offs = batch.cols[ci]["offsets"][: n + 1]
+        if info.out_type == 7 and views != "views":   # O_STRING: offsets non-decreasing over all 50 M records
+            offs = batch.cols[ci]["offsets" if views == "large" else "offsets32"][: n + 1]
             assert bool((offs[1:] >= offs[:-1]).all())
     del batch, rec
     torch.cuda.empty_cache()
@@ -379,10 +386,10 @@ def test_synstr200_full_size_sampled_views():
     torch.cuda.empty_cache()
 
 
-def _var_decode_vs_oracle(raw: bytes, views: bool, **kw):
+def _var_decode_vs_oracle(raw: bytes, views: str, **kw):
     from cobrix_amd.synth import RDW_NARROW_COPYBOOK, RDW_NARROW_SEGMENTS
     params = ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
-                              segment_id_redefine_map=RDW_NARROW_SEGMENTS, string_views=views, **kw)
+                              segment_id_redefine_map=RDW_NARROW_SEGMENTS, **_layout(views), **kw)
     rd = VarLenNestedReader(RDW_NARROW_COPYBOOK, params)
     t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
     off, ln = rd.frame(t, len(raw))
@@ -395,7 +402,7 @@ def _var_decode_vs_oracle(raw: bytes, views: bool, **kw):
     return rd, compare_batch(batch, res)
 
 
-@pytest.mark.parametrize("views", [False, True])
+@pytest.mark.parametrize("views", LAYOUTS)
 def test_var_span_kernel_vs_oracle(views):
     """The specialised span kernel (variable-length tiles staged by byte span, span_loop) on the C4
     layout, and on records of 1-3,000 bytes where many tiles overflow the span staging and fall
@@ -417,3 +424,49 @@ def test_var_span_kernel_vs_oracle(views):
         body += bytes([0, 0, ln & 0xFF, ln >> 8]) + bytes(payload)
     rd, errs = _var_decode_vs_oracle(bytes(body), views, jit_min_records=1)
     assert _kernel_kind(rd) == 1 and not errs, errs
+
+
+def test_synstr200_full_size_sampled_utf8():
+    """Config C3 as the bench runs it (50 M SYNSTR200 records, Arrow Utf8 layout: count pass, device
+    scan, every offset and payload byte written once by the specialised decode kernel): a sample
+    across the batch is bit-exact; every slot's int32 offsets start at 0, never decrease, end at the
+    slot's size, and the payload bytes equal the sum of the view-layout lengths of the same input."""
+    from parity import compare_sample
+    from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
+    n = 50_000_000
+    rec = synstr200(n, seed=20261017, device="cuda")
+    rd = FixedLenNestedReader(SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_utf8=True))
+    batch = rd.decode_device(rec.view(-1), n * 200)
+    assert _kernel_kind(rd) == 1
+    rng = np.random.default_rng(6)
+    idx = np.unique(np.concatenate([np.arange(128), n - 128 + np.arange(128), rng.integers(0, n, 3744)]))
+    sample = rec[torch.as_tensor(idx, device="cuda")].cpu().numpy().tobytes()
+    errs = compare_sample(batch, idx, O.decode_fixed(rd.copybook, sample))
+    assert not errs, errs
+    for c in batch.cols:
+        o = c["offsets32"][: n + 1]
+        assert int(o[0]) == 0 and bool((o[1:] >= o[:-1]).all())
+        assert int(o[n]) == int(c["sizes"][0]) and 0 < int(o[n]) <= c["capacity"]
+    del batch, rec
+    torch.cuda.empty_cache()
+
+
+def test_utf8_layout_capacity_overflow_reported():
+    """A Utf8 region smaller than the batch's payload: nothing is written past it, and the plan's
+    check reports CBX_E_CAPACITY (as the large-string layout does)."""
+    import ctypes
+    from cobrix_amd import native as N
+    from cobrix_amd.reader import _alloc_columns
+    from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
+    n = 10_000
+    data = synstr200(n, seed=8, device="cuda").view(-1)
+    rd = FixedLenNestedReader(SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_utf8=True))
+    cols, cs = _alloc_columns(rd.plan, n, [1000] * rd.plan.n_columns, "cuda")
+    guard = [c["data"].clone() for c in cols]
+    L = N.load()
+    N.check(L.cbx_decode_fixed(rd.native.handle, data.data_ptr(), n, 200, 0, 0, cs, None))
+    with pytest.raises(N.CbxError) as e:
+        N.check(L.cbx_plan_check(rd.native.handle, None))
+    assert e.value.code == N.CBX_E_CAPACITY
+    assert all(c["data"].numel() == g.numel() for c, g in zip(cols, guard))
+    N.check(L.cbx_plan_check(rd.native.handle, None))   # the flag is cleared

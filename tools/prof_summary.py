@@ -1,8 +1,8 @@
 """Summary of one workload's round-3 GPU evidence (tools/gpu_r03.sh): the bench JSON line, the
 rocprofv3 kernel trace of the SAME process and the PMC passes of a 1-step run.
 
-* per kernel: calls, rocprof average over all calls, and the average over the timed steps only (the
-  last `steps` dispatches; the warm-up dispatches run first);
+* per kernel: calls, rocprof average over all calls, and the average over the timed steps only
+  (dispatches warmup .. warmup + steps - 1: warm-up first, the end-to-end pass's chunks after);
 * roofline recomputed from the trace: algorithmic bytes (from the bench line) / the traced average
   of the decode kernel over the timed steps, next to the bench's HIP-event figure;
 * HBM traffic per launch: FETCH_SIZE (KiB) x 2 for the kernels that read with 16-byte-per-lane
@@ -18,12 +18,13 @@ import os
 import sys
 
 D = sys.argv[1]
-STAGED16 = ("cbx_jit_decode", "cbx::decode_kernel", "cbx::list_kernel")   # 16-byte/lane staged reads
+STAGED16 = ("cbx_jit_decode", "cbx_jit_count", "cbx::decode_kernel", "cbx::list_kernel")   # 16-byte/lane staged reads
 
 
 def base(name: str) -> str:
-    n = name.split("(")[0].replace("void ", "", 1)
-    return n.split("<")[0] if n.startswith("cbx::") else n
+    """Kernel name without its parameter list (template arguments kept: list_kernel<false> and
+    list_kernel<true> are two launches of a step)."""
+    return name.split("(")[0].replace("void ", "", 1).strip()
 
 
 def rows(pattern):
@@ -43,7 +44,8 @@ kernels = {}
 for k, d in per.items():
     if not (k.startswith("cbx") or "cbx" in k):
         continue
-    timed = d[-steps:] if len(d) >= steps else d
+    w0 = bench.get("warmup", 0)     # one launch per step: warm-up launches, the timed steps, then end-to-end chunks
+    timed = d[w0:w0 + steps] if len(d) >= w0 + steps else d
     kernels[k] = {"calls": len(d), "avg_ms_all": round(sum(d) / len(d), 4), "avg_ms_timed_steps": round(sum(timed) / len(timed), 4),
                   "max_ms": round(max(d), 4)}
 
@@ -52,11 +54,14 @@ alg = bench["roofline"]["algorithmic_bytes_per_launch"]
 check = {}
 if dec:
     k = dec[0]
-    t = kernels[k]["avg_ms_timed_steps"]
-    if "cbx::list_kernel" in kernels:      # the bench's decode time covers the record and the list kernel
-        t += kernels["cbx::list_kernel"]["avg_ms_timed_steps"]
+    # the bench's decode time (HIP events) covers the record kernel, the list kernels after it and,
+    # in the Utf8 layout, the count pass and its scan before it
+    parts = [k] + [x for x in kernels if x.startswith("cbx::list_kernel")]
+    if "cbx_jit_count" in kernels or bench["config"].get("string_layout", "").startswith("Arrow Utf8"):
+        parts += [x for x in kernels if x.startswith(("cbx_jit_count", "cbx::scan_"))]
+    t = sum(kernels[x]["avg_ms_timed_steps"] for x in parts)
     frac = alg / (t * 1e-3) / 1e9 / bench["roofline"]["peak"]
-    check = {"kernel": k + (" + cbx::list_kernel" if "cbx::list_kernel" in kernels else ""), "rocprof_ms": round(t, 4),
+    check = {"kernel": " + ".join(parts), "rocprof_ms": round(t, 4),
              "hip_event_ms": bench["kernel_ms"]["decode_kernel"], "frac_rocprof": round(frac, 4),
              "frac_bench": bench["roofline"]["frac"],
              "agree_within": round(abs(frac - bench["roofline"]["frac"]) / bench["roofline"]["frac"], 4)}
