@@ -1887,6 +1887,41 @@ extern "C" int cbx_plan_set_walk(cbx_plan* P, const cbx_walk_node* nodes, int32_
     return CBX_OK;
 }
 
+extern "C" int cbx_frame_length_field(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, int32_t field,
+                                      int32_t start_offset, int32_t end_offset, int32_t adjustment, int64_t* d_rec_off,
+                                      int32_t* d_rec_len, int64_t capacity, int64_t* n_records, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!P || !n_records || n_bytes < 0 || start_offset < 0 || end_offset < 0 || capacity < 0 ||
+        (n_bytes > 0 && !d_data) || (capacity > 0 && (!d_rec_off || !d_rec_len)) || field < 0 ||
+        field >= (int)P->hfields.size())
+        return fail(CBX_E_ARGUMENT, "cbx_frame_length_field: invalid arguments");
+    const cbx_field& hf = P->hfields[field];
+    if (hf.n_dims != 0 || !(hf.flags & CBX_F_INTEGRAL) || is_string_out(hf.out_type) || hf.kind == CBX_K_RECORD_ID ||
+        hf.kind == CBX_K_FILE_ID)
+        return fail(CBX_E_ARGUMENT, "cbx_frame_length_field: the record length field must be a primitive integral field");
+    *n_records = 0;
+    LenFieldArgs a{};
+    a.data = d_data; a.n_bytes = n_bytes;
+    a.field = (const CBX_CONST Field*)P->d_fields + field;
+    a.start_off = start_offset; a.end_off = end_offset; a.adjustment = adjustment;
+    a.lfb = hf.offset + hf.size;
+    AsyncBlock blk(st);
+    HIP_CHECK(hipMallocAsync(&blk.p, 3 * sizeof(int64_t), st));
+    int64_t* d_out = (int64_t*)blk.p;
+    HIP_CHECK(hipMemsetAsync(d_out, 0, 3 * sizeof(int64_t), st));
+    hipLaunchKernelGGL(lenfield_frame_kernel, dim3(1), dim3(1), 0, st, a, capacity, d_rec_off, d_rec_len, d_out);
+    HIP_CHECK(hipGetLastError());
+    int64_t h[3] = {0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(h, d_out, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    *n_records = h[0];
+    if (h[1] == 1)
+        return fail(CBX_E_STATE, "Record length value of the field at byte " + std::to_string(h[2]) +
+                                     " must be an integral type.");
+    if (h[0] > capacity) return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(h[0]));
+    return CBX_OK;
+}
+
 extern "C" int cbx_frame_var_occurs(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, int64_t first_offset,
                                     int64_t* d_rec_off, int32_t* d_rec_len, int64_t capacity, int64_t* n_records,
                                     int64_t* virtual_bytes, void* stream) {

@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text",
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
                     "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs",
-                    "cbx_plan_set_record_base")
+                    "cbx_plan_set_record_base", "cbx_frame_length_field")
 ABI_VERSION = 10
 
 
@@ -191,7 +191,8 @@ def load():
                      ("cbx_hier_list_offsets", [P, i64, i64, i64, i64, P, P]),
                      ("cbx_plan_set_walk", [P, P, i32, i32, P, P, i32, i32]),
                      ("cbx_frame_var_occurs", [P, P, i64, i64, P, P, i64, P, P, P]),
-                     ("cbx_plan_set_record_base", [P, P])):
+                     ("cbx_plan_set_record_base", [P, P]),
+                     ("cbx_frame_length_field", [P, P, i64, i32, i32, i32, i32, P, P, i64, P, P])):
         if hasattr(L, name):   # (diagnostic builds of older revisions lack the newest entry points)
             getattr(L, name).argtypes = at
     if L.cbx_abi_version() != ABI_VERSION:

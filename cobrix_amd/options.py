@@ -39,7 +39,6 @@ KNOWN = {
 
 # options whose subsystem the GPU path does not cover (never silently ignored)
 UNSUPPORTED = {
-    "record_length_field": "record length fields (VRLRecordReader.fetchRecordUsingRecordLengthField)",
     "record_header_parser": "custom record header parsers",
     "record_extractor": "custom raw record extractors",
     "with_input_file_name_col": "input file name columns",
@@ -191,6 +190,7 @@ def parse_options(options: Mapping[str, object]) -> Tuple[ReaderParameters, bool
         ascii_charset=opts.get("ascii_charset", ""),
         variable_size_occurs=_bool(opts.get("variable_size_occurs", "false"), "variable_size_occurs") if var_len else False,
         record_length=int(opts["record_length"]) if "record_length" in opts else None,
+        record_length_field=opts.get("record_length_field") if var_len else None,
         is_record_sequence=_bool(opts.get("is_xcom", opts.get("is_record_sequence", "false")), "is_record_sequence") if var_len else False,
         is_text=_bool(opts.get("is_text", "false"), "is_text"),
         is_rdw_big_endian=_bool(opts.get("is_rdw_big_endian", "false"), "is_rdw_big_endian") if var_len else False,

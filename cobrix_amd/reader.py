@@ -85,6 +85,9 @@ class ReaderParameters:
     # place by the decode kernel (no placement pass); takes precedence over string_views except on the
     # record walk, which writes views
     string_utf8: bool = False
+    # record_length_field (VRLRecordReader.fetchRecordUsingRecordLengthField): records framed by a length
+    # field inside them instead of RDW headers (not with is_record_sequence)
+    record_length_field: Optional[str] = None
     # OCCURS DEPENDING ON arrays of numeric elements in the list layout (child elements packed per
     # record, absent elements unwritten; cobrix_hip.h CBX_F_LIST) instead of one slot row per element
     occurs_lists: bool = False
@@ -959,8 +962,46 @@ class VarLenNestedReader(_BaseReader):
         return [SparseIndexEntry(e.offset_from, e.offset_to, e.file_id, e.record_index) for e in ents[: n.value]]
 
     def index_generation_needed(self) -> bool:
-        """VarLenNestedReader.isIndexGenerationNeeded (:85): no record length field on this path."""
-        return self.params.enable_indexes
+        """VarLenNestedReader.isIndexGenerationNeeded (:85)."""
+        p = self.params
+        return (p.record_length_field is None or p.is_record_sequence) and p.enable_indexes
+
+    def length_field(self) -> Optional[int]:
+        """ReaderParametersValidator.getLengthField (CP/reader/validator/ReaderParametersValidator.scala:26-43):
+        the record length field's index in the plan's field table (None: no length field), after the
+        reference's checks (a primitive Integral field, not an array)."""
+        name = self.params.record_length_field
+        if name is None or self.params.is_record_sequence:
+            return None
+        node = self.copybook.get_field_by_name(name)
+        if not isinstance(node, cbk.Primitive):
+            raise ValueError(f"The record length field {name} must have an primitive integral type.")
+        if not isinstance(node.dtype, cbk.Integral):
+            raise ValueError(f"The record length field {name} must be an integral type.")
+        if node.occurs is not None and node.occurs > 1:
+            raise ValueError(f"The record length field '{name}' cannot be an array.")
+        fi = self.plan.field_of_node.get(id(node))
+        if fi is None:
+            raise ValueError(f"record length field {name} is not decoded by the plan (a FILLER)")
+        return fi
+
+    def frame_length_field(self, d_data, n_bytes: int, stream=None):
+        """VRLRecordReader.fetchRecordUsingRecordLengthField on the GPU (one device thread walks the
+        stream) -> (rec_off, rec_len) of the records: each starts where the previous ended, its length
+        from the field inside it (+ rdw_adjustment), record_start/end_offset included."""
+        torch = _torch()
+        st = stream if stream is not None else torch.cuda.current_stream()
+        p = self.params
+        fi = self.length_field()
+        lfb = self.plan.fields[fi].offset + self.plan.fields[fi].size
+        cap = max(1, n_bytes // max(1, p.start_offset + lfb) + 1)
+        off = torch.empty(cap, dtype=torch.int64, device=d_data.device)
+        ln = torch.empty(cap, dtype=torch.int32, device=d_data.device)
+        n = ctypes.c_int64(0)
+        N.check(N.load().cbx_frame_length_field(self.native.handle, d_data.data_ptr(), n_bytes, fi, p.start_offset,
+                                                p.end_offset, p.rdw_adjustment, off.data_ptr(), ln.data_ptr(), cap,
+                                                ctypes.byref(n), ctypes.c_void_p(st.cuda_stream)))
+        return off[: n.value], ln[: n.value]
 
     # ---- selection + decode
     def select(self, d_data, n_bytes: int, rec_off, rec_len, entries: Optional[Sequence[SparseIndexEntry]] = None,
@@ -1054,9 +1095,9 @@ class VarLenNestedReader(_BaseReader):
 
     def var_occurs_extractor(self) -> bool:
         """VarLenNestedReader.recordExtractor (:60-78): VarOccursRecordExtractor for variable-size
-        OCCURS without RDW headers (no custom extractor / header parser / length field here)."""
+        OCCURS without RDW headers or a record length field (no custom extractor / header parser here)."""
         p = self.params
-        return p.variable_size_occurs and not p.is_record_sequence and not p.is_text
+        return p.variable_size_occurs and not p.is_record_sequence and not p.is_text and p.record_length_field is None
 
     def frame_file(self, t, n_bytes: int):
         """(rec_off, rec_len, bytes the records are decoded against) of a whole file."""
@@ -1066,6 +1107,9 @@ class VarLenNestedReader(_BaseReader):
             return self.frame_var_occurs(t, n_bytes)
         if self.params.is_record_sequence:
             off, ln = self.frame(t, n_bytes)
+            return off, ln, n_bytes
+        if self.params.record_length_field is not None:
+            off, ln = self.frame_length_field(t, n_bytes)
             return off, ln, n_bytes
         off, ln = self.frame_fixed(t, n_bytes)
         return off, ln, n_bytes

@@ -427,6 +427,20 @@ int cbx_frame_var_occurs(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes,
                          int64_t* d_rec_off, int32_t* d_rec_len, int64_t capacity, int64_t* n_records,
                          int64_t* virtual_bytes, void* stream);
 
+/* Record length field framing (record_length_field, not is_record_sequence):
+ * VRLRecordReader.fetchRecordUsingRecordLengthField (CP/reader/iterator/VRLRecordReader.scala:114-149).
+ * From byte 0, each record is start_offset + lfb bytes (lfb = the field's offset + size; `field` indexes
+ * the plan's cbx_field table) plus max(0, value + adjustment - lfb + end_offset) more, fewer at the end
+ * of the data, which ends the walk; a stream holding fewer than start_offset + lfb bytes has no further
+ * record.  The field must be a primitive Integral one (ReaderParametersValidator.getLengthField); its
+ * value is decoded as extractPrimitiveField does (Int / Long -> toInt) and a null or BigDecimal value
+ * fails with CBX_E_STATE (the reference's IllegalStateException).  rec_off / rec_len receive
+ * the record starts and lengths (decode them with cbx_decode_var at start_offset).  Sequential in the
+ * stream: one device thread walks it. */
+int cbx_frame_length_field(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, int32_t field,
+                           int32_t start_offset, int32_t end_offset, int32_t adjustment, int64_t* d_rec_off,
+                           int32_t* d_rec_len, int64_t capacity, int64_t* n_records, void* stream);
+
 /* ---- hierarchical records (`segment-children`) ----
  *
  * Replaces VarLenHierarchicalIterator + the structure walk of RecordExtractors.extractHierarchicalRecord

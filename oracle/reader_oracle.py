@@ -316,8 +316,39 @@ def var_occurs_records(cb: cbk.Copybook, data: bytes) -> List[bytes]:
 
 
 def index_generation_needed(p) -> bool:
-    """VarLenNestedReader.isIndexGenerationNeeded (:85) -- no record length field on this path."""
-    return p.enable_indexes
+    """VarLenNestedReader.isIndexGenerationNeeded (:85)."""
+    return (getattr(p, "record_length_field", None) is None or p.is_record_sequence) and p.enable_indexes
+
+
+def _java_int(v: int) -> int:
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
+class LengthFieldReader:
+    """VRLRecordReader.fetchRecordUsingRecordLengthField (CP/reader/iterator/VRLRecordReader.scala:114-149)
+    with ReaderParametersValidator.getLengthField's checks (:26-43)."""
+
+    def __init__(self, cb: cbk.Copybook, p):
+        f = cb.get_field_by_name(p.record_length_field)
+        if not isinstance(f, cbk.Primitive) or not isinstance(f.dtype, cbk.Integral):
+            raise ValueError(f"The record length field {p.record_length_field} must be an integral type.")
+        if f.occurs is not None and f.occurs > 1:
+            raise ValueError(f"The record length field '{p.record_length_field}' cannot be an array.")
+        self.reader = FieldReader(cb, f)
+        self.lfb = f.offset + f.actual_size          # lengthFieldBlock
+        self.start, self.end, self.adj = p.start_offset, p.end_offset, p.rdw_adjustment
+        self.name = p.record_length_field
+
+    def fetch(self, s: "Stream") -> Optional[bytes]:
+        head = s.next(self.start + self.lfb)
+        if len(head) < self.start + self.lfb:
+            return None
+        v = self.reader.value(head, self.start)
+        if not isinstance(v, int) or isinstance(v, bool):   # Int / Long; null, BigDecimal: the catch-all case
+            raise RuntimeError(f"Record length value of the field {self.name} must be an integral type.")
+        rest = _java_int(_java_int(_java_int(v) + self.adj) - self.lfb + self.end)
+        return head + s.next(rest) if rest > 0 else head
 
 
 class SegmentIdAccumulator:
@@ -373,20 +404,26 @@ def var_len_records(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
         s = Stream(data, e.offset_from, n_bytes)
         acc = SegmentIdAccumulator(levels, p.segment_id_prefix, e.file_id) if p.segment_field else None
         record_index = e.record_index - 1
+        lf = LengthFieldReader(cb, p) if (getattr(p, "record_length_field", None) and not p.is_record_sequence) else None
         while True:
-            # VRLRecordReader.fetchRecordUsingRdwHeaders (:151-186)
-            valid = False
-            eof = False
-            rec = b""
-            while not valid and not eof:
-                hdr = s.next(rp.header_length)
-                n, valid = rp.metadata(hdr, s.offset, s.size)
-                if n > 0:
-                    rec = s.next(n)
-                else:
-                    eof = True
-            if eof:
-                break
+            if lf is not None:
+                rec = lf.fetch(s)
+                if rec is None:
+                    break
+            else:
+                # VRLRecordReader.fetchRecordUsingRdwHeaders (:151-186)
+                valid = False
+                eof = False
+                rec = b""
+                while not valid and not eof:
+                    hdr = s.next(rp.header_length)
+                    n, valid = rp.metadata(hdr, s.offset, s.size)
+                    if n > 0:
+                        rec = s.next(n)
+                    else:
+                        eof = True
+                if eof:
+                    break
             record_index += 1
             sid = _trim(seg_reader.segment_id(rec, p.start_offset)) if seg_reader else ""
             ids: List[Optional[str]] = []

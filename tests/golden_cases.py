@@ -94,6 +94,15 @@ CASES: Dict[str, Dict[str, Any]] = {
                             "segment_id_level1": "P", "segment_id_prefix": "A", **T5_SEG},
                    expected="test5_expected/test5b.txt", schema="test5_expected/test5b_schema.json",
                    sort=("File_Id", "Record_Id"), take=60),
+    # record_length_field instead of RDW headers: the BE RDW file read through a copybook whose first
+    # field is the RDW's length half (VRLRecordReader.fetchRecordUsingRecordLengthField)
+    "test5d": dict(spec="SCT/source/integration/Test5MultisegmentSpec.scala:273-310",
+                   copybook="test5d_copybook.cob", data="test5b_data/COMP.DETAILS.FEB02.DATA.RDW.BE.dat",
+                   options={"record_length_field": "RECORD-LENGTH", "rdw_adjustment": "4", "segment_field": "SEGMENT_ID",
+                            "segment_id_level0": "C", "segment_id_level1": "P", "generate_record_id": "true",
+                            "schema_retention_policy": "collapse_root", "segment_id_prefix": "A"},
+                   expected="test5_expected/test5d.txt", schema="test5_expected/test5d_schema.json",
+                   sort=("File_Id", "Record_Id"), take=60),
     "test6": dict(spec="SCT/source/integration/Test6TypeVarietySpec.scala:37-100",
                   copybook="test6_copybook.cob", data="test6_data/INTEGR.TYPES.NOV28.DATA.dat",
                   options={"schema_retention_policy": "collapse_root", "floating_point_format": "IEEE754"},

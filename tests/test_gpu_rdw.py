@@ -19,6 +19,7 @@ from cobrix_amd.native import CbxError  # noqa: E402
 from cobrix_amd.reader import ReaderParameters, VarLenNestedReader  # noqa: E402
 from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow  # noqa: E402
 from oracle import oracle as O  # noqa: E402
+from oracle import reader_oracle as RO  # noqa: E402
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -125,3 +126,78 @@ def test_zero_length_header_is_an_error_at_the_first_occurrence(monkeypatch, chu
         _frame(raw)
     want = int(re.search(r"offset (\d+)", str(oe.value)).group(1))
     assert f"at {want}." in str(ge.value), (str(ge.value), want)
+
+
+LENFIELD_COPYBOOK = """
+       01  REC.
+           05  HDR         PIC X(2).
+           05  REC-LEN     PIC 9(3).
+           05  KIND        PIC X(1).
+           05  BODY        PIC X(40).
+"""
+
+
+def _lenfield_file(rng, n, bad_at=None):
+    out = bytearray()
+    for i in range(n):
+        body_len = int(rng.integers(0, 40))
+        total = 6 + body_len
+        ln = f"{total:03d}" if i != bad_at else "x1y"
+        out += b"\x40\x40" + ln.encode("cp037") + ("C" if i % 3 else "P").encode("cp037")
+        out += bytes(rng.integers(0xC1, 0xCA, body_len, dtype=np.uint8))
+    return bytes(out)
+
+
+@pytest.mark.parametrize("start,end,adj", [(0, 0, 0), (3, 0, 3), (0, 2, -2), (2, 1, 1)])
+def test_record_length_field_framing_vs_oracle(start, end, adj):
+    """record_length_field (VRLRecordReader.fetchRecordUsingRecordLengthField) on the GPU: records
+    whose DISPLAY length field gives the record size (+ rdw_adjustment), record_start/end_offset
+    bytes around each record, a truncated last record -- framing and rows equal the oracle's."""
+    import dataclasses
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import VarLenNestedReader
+    rng = np.random.default_rng(start * 7 + end)
+    recs = []
+    for i in range(3000):
+        body_len = int(rng.integers(0, 40))
+        total = 6 + body_len
+        head = bytes(rng.integers(0, 256, start, dtype=np.uint8))
+        rec = b"\x40\x40" + f"{total - adj:03d}".encode("cp037") + ("C" if i % 3 else "P").encode("cp037")
+        rec += bytes(rng.integers(0xC1, 0xCA, body_len, dtype=np.uint8)) + bytes(rng.integers(0, 256, end, dtype=np.uint8))
+        recs.append(head + rec)
+    raw = b"".join(recs)[:-5]     # the last record is cut short
+    p, var_len = parse_options({"record_length_field": "REC-LEN", "rdw_adjustment": str(adj), "record_start_offset": str(start),
+                                "record_end_offset": str(end), "segment_field": "KIND", "generate_record_id": "true"})
+    assert var_len
+    rd = VarLenNestedReader(LENFIELD_COPYBOOK, p)
+    t = rd._device_file(raw)
+    off, ln, _ = rd.frame_file(t, len(raw))
+    lens = [len(r) for r in recs]
+    lens[-1] -= 5
+    assert ln.cpu().tolist() == lens
+    assert off.cpu().tolist() == [sum(lens[:i]) for i in range(len(lens))]
+    rows = rd.read(raw).to_rows()
+    exp = RO.var_len_rows(rd.copybook, raw, p)
+    assert len(rows) == len(exp) == 3000
+    assert rows == exp
+
+
+def test_record_length_field_errors():
+    """A length field that does not decode (non-digits) fails like the reference's
+    IllegalStateException; a non-integral length field is rejected when the reader frames."""
+    from cobrix_amd import native as N
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import VarLenNestedReader
+    rng = np.random.default_rng(3)
+    raw = _lenfield_file(rng, 50, bad_at=20)
+    p, _ = parse_options({"record_length_field": "REC-LEN"})
+    rd = VarLenNestedReader(LENFIELD_COPYBOOK, p)
+    with pytest.raises(N.CbxError) as e:
+        rd.read(raw)
+    assert e.value.code == N.CBX_E_STATE and "integral" in str(e.value)
+    with pytest.raises(RuntimeError):
+        RO.var_len_rows(rd.copybook, raw, p)
+    p2, _ = parse_options({"record_length_field": "KIND"})
+    rd2 = VarLenNestedReader(LENFIELD_COPYBOOK, p2)
+    with pytest.raises(ValueError):
+        rd2.read(_lenfield_file(rng, 5))
