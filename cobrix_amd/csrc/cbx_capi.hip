@@ -1191,7 +1191,7 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     if (!d_data || n_bytes < 0 || !params || !n_records || (n_seeds > 0 && !seeds))
         return fail(CBX_E_ARGUMENT, "cbx_frame_rdw: invalid arguments");
     *n_records = 0;
-    // seed ranges cut into chunks (rdw_spec_kernel / rdw_fix_kernel / rdw_place_kernel)
+    // seed ranges cut into chunks (rdw_wave_kernel: speculation + walk, fix rounds; rdw_place_kernel)
     // 64 KiB chunks: C4's 65-byte records ~1,000 per chunk; C5's 16 KB records still leave every
     // chunk a few headers (framing 13.9 ms at 16 KiB -> 3.4 ms; C4 4.6 -> 4.5 ms)
     int64_t chunk = 64 * 1024;
@@ -1213,8 +1213,11 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     // ranges | count (u32 x n)
     // staging: chunk bytes / 40 records per chunk (C4's ~65-byte records use ~60 % of it; chunks of
     // shorter records are walked again by the placement pass)
-    const int64_t stage_cap = (std::max<int64_t>(16, chunk / 40) + 7) & ~(int64_t)7;
-    const size_t bytes = sizeof(int64_t) * (5 * n + 4 + nb) + sizeof(RdwRange) * ranges.size() + sizeof(uint32_t) * n + 64;
+    // (a multiple of 64: the wave walk stores whole rows of 64 records)
+    const int64_t stage_cap = (std::max<int64_t>(64, chunk / 40) + 63) & ~(int64_t)63;
+    // + one changed flag per fix round (rounds <= n + 1)
+    const size_t bytes = sizeof(int64_t) * (5 * n + 4 + nb) + sizeof(RdwRange) * ranges.size() + sizeof(uint32_t) * n +
+                         sizeof(int32_t) * (n + 2) + 64;
     const size_t stage_bytes = (size_t)n * stage_cap * (sizeof(int64_t) + sizeof(int32_t));
     uint8_t* blk = nullptr;
     uint8_t* stage = nullptr;
@@ -1226,14 +1229,13 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     int64_t* d64 = (int64_t*)blk;
     RdwChunkArgs c{};
     c.entry = d64;
-    int64_t* exits[2] = {d64 + n, d64 + 2 * n};
     c.err = d64 + 3 * n;
     int64_t* d_base = d64 + 4 * n;
     unsigned long long* d_first_err = (unsigned long long*)(d64 + 5 * n);   // [0] first error, [1] total
-    c.changed = (int32_t*)(d64 + 5 * n + 2);
     int64_t* d_block_sums = d64 + 5 * n + 4;
     RdwRange* d_ranges = (RdwRange*)(d_block_sums + nb);
     c.count = (uint32_t*)(d_ranges + ranges.size());
+    c.changed = (int32_t*)(c.count + n);   // [round]
     c.ranges = d_ranges; c.n_ranges = (int32_t)ranges.size(); c.chunk = chunk; c.n = n;
     c.stage_off = (int64_t*)stage;
     c.stage_len = (int32_t*)(stage + (size_t)n * stage_cap * sizeof(int64_t));
@@ -1242,23 +1244,27 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     HIP_CHECK(hipMemsetAsync(d_first_err, 0xFF, sizeof(unsigned long long), st));
     RdwArgs a{};
     a.data = d_data; a.n_bytes = n_bytes; a.p = *params;
-    const unsigned threads = 64, blocks = (unsigned)((n + threads - 1) / threads);
-    c.exit_in = nullptr; c.exit_out = exits[0];
-    hipLaunchKernelGGL(rdw_spec_kernel, dim3(blocks), dim3(threads), 0, st, a, c);
+    c.exit_in = nullptr; c.exit_out = d64 + n;   // exits, updated in place by the fix rounds
+    HIP_CHECK(hipMemsetAsync(c.changed, 0, sizeof(int32_t) * (n + 2), st));
+    const unsigned wblocks = (unsigned)((n + kRdwWaves - 1) / kRdwWaves);
+    hipLaunchKernelGGL(rdw_wave_kernel<false>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, 0);
     HIP_CHECK(hipGetLastError());
-    // fix rounds until no entry changes (each round validates at least the next chunk of every
-    // range: bounded by the chunk count)
-    int cur = 0;
-    for (int64_t round = 0; round <= n; round++) {
-        HIP_CHECK(hipMemsetAsync(c.changed, 0, sizeof(int32_t), st));
-        c.exit_in = exits[cur]; c.exit_out = exits[cur ^ 1];
-        hipLaunchKernelGGL(rdw_fix_kernel, dim3(blocks), dim3(threads), 0, st, a, c);
+    // fix rounds until one changes no entry (each round validates at least the next chunk of every
+    // range: bounded by the chunk count).  The first kAsyncRounds go out without waiting: a round
+    // after one that changed nothing returns at once on the device.
+    constexpr int kAsyncRounds = 3;
+    int64_t round = 0;
+    for (; round < kAsyncRounds && round <= n; round++)
+        hipLaunchKernelGGL(rdw_wave_kernel<true>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, (int32_t)round);
+    HIP_CHECK(hipGetLastError());
+    int32_t last_changed = 0;
+    HIP_CHECK(hipMemcpyAsync(&last_changed, c.changed + round - 1, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    for (; last_changed && round <= n + 1; round++) {
+        hipLaunchKernelGGL(rdw_wave_kernel<true>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, (int32_t)round);
         HIP_CHECK(hipGetLastError());
-        cur ^= 1;
-        int32_t changed = 0;
-        HIP_CHECK(hipMemcpyAsync(&changed, c.changed, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(&last_changed, c.changed + round, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
-        if (!changed) break;
     }
     // record counts -> bases: device exclusive scan of the chunk counts
     hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)c.count, n,

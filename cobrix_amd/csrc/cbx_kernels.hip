@@ -808,101 +808,234 @@ __device__ __forceinline__ uint32_t zero_bytes4(uint32_t x) {   // bit j: byte j
     return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
 }
 
-__device__ int64_t rdw_strict_scan(const RdwArgs& a, int64_t s, int64_t e, int64_t re) {
-    const int64_t off = a.p.big_endian ? 2 : 0;
-    const int64_t p0 = s + off, p1 = e + off;          // pair start positions [p0, p1)
-    if (((uintptr_t)a.data & 15) == 0) {
-        // 16 bytes per step with the next 16 prefetched: a chunk of long records (C5: 16 KB) is
-        // scanned for kilobytes before its first header, and the scan is a chain of loads
-        int64_t w = p0 & ~(int64_t)15;
-        auto load = [&](int64_t q) -> uint4 {
-            if (q + 16 <= a.n_bytes) return *(const uint4*)(a.data + q);
-            uint32_t d[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int j = 0; j < 16; j++)   // past the end: 1, not a zero byte
-                d[j >> 2] |= (q + j < a.n_bytes ? (uint32_t)a.data[q + j] : 1u) << (8 * (j & 3));
-            return make_uint4(d[0], d[1], d[2], d[3]);
-        };
-        uint4 cur = w < a.n_bytes ? load(w) : make_uint4(1u, 1u, 1u, 1u);
-        uint32_t carry = 0;                             // byte w-1 is zero
-        for (; w < p1 && w < a.n_bytes; w += 16) {
-            const uint4 nxt = w + 16 < p1 && w + 16 < a.n_bytes ? load(w + 16) : make_uint4(1u, 1u, 1u, 1u);
-            const uint32_t zb = zero_bytes4(cur.x) | zero_bytes4(cur.y) << 4 | zero_bytes4(cur.z) << 8 | zero_bytes4(cur.w) << 12;
-            // pairs starting at w-1 .. w+14 (bit i <-> position w - 1 + i)
-            uint32_t pairs = (carry & zb) | ((zb & (zb >> 1)) << 1);
-            carry = zb >> 15;
-            while (pairs) {
-                const int i = __builtin_ctz(pairs);
-                pairs &= pairs - 1;
-                const int64_t p = w - 1 + i;
-                if (p < p0 || p >= p1) continue;
-                const int64_t q = p - off;
-                if (rdw_plausible(a, q, re, true)) return q;
-            }
-            cur = nxt;
-        }
-        return -1;
+// ---- the walk as one wave per chunk, headers read from an LDS ring (rdw_wave_kernel) ----
+// The lane-per-chunk walk above makes every header a dependent HBM load in a line no other lane
+// touches; with ~2,300 waves for 150 k chunks (C4) it is latency-bound (SQ_WAIT_ANY 83 % of its
+// wave cycles, profiles/r03_a).  Here a wave owns a chunk: the chunk's bytes stream through a
+// 4-window LDS ring (1 KiB windows, one 16-byte buffer load per lane, two windows in flight), the
+// header chain is walked wave-uniformly from LDS, and the wave's 64 lanes hold the last 64 records
+// found so the staging stores are whole 512 + 256-byte rows.  A walk whose next header lies past the
+// windows in flight (records longer than a window, C5) restarts the stream at that header.  The
+// speculated entry of a chunk (no seed) is the first strict candidate that starts a plausible chain:
+// the lanes test the zero-byte pairs of a window in parallel and the lowest plausible one wins.
+// Fix rounds walk in place: a chunk whose entry differs from its predecessor's exit re-walks; a
+// round that changed nothing ends the loop (device flag per round, checked by the next round's
+// kernel, so rounds are launched without waiting for the host).
+constexpr int kRdwWin = 1024;                  // window bytes: one 16-byte load per lane
+constexpr int kRdwRingWins = 4;                // windows resident in the wave's ring
+constexpr int kRdwRing = kRdwWin * kRdwRingWins;
+constexpr int kRdwWaveLds = kRdwRing + 16;     // + a copy of the ring's first 16 bytes (reads across its end)
+constexpr int kRdwWaves = 4;                   // waves per workgroup
+
+struct RdwStream {
+    const uint8_t* base;   // 16-byte aligned address at or before data
+    int64_t shift;         // data - base
+    int64_t limit;         // input bytes from base (shift + n_bytes)
+    uint8_t* ring;         // the wave's LDS ring
+    int64_t hi;            // next window (index from base) to enter the ring
+    uint4 nx0, nx1;        // windows hi, hi + 1 in flight
+};
+
+__device__ __forceinline__ uint4 rdw_win_load(const RdwStream& s, int64_t win, int lane) {
+    const int64_t a0 = win * kRdwWin;
+    int64_t left = s.limit - a0;
+    left = left < 0 ? 0 : (left > kRdwWin ? kRdwWin : left);
+    const uint64_t b = (uint64_t)(s.base + (a0 < s.limit ? a0 : 0));
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane((int)left);
+    void* bp = (void*)(((uint64_t)hi << 32) | lo);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bp, (short)0, nbytes, 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 0, 0);   // past the input: zeros
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ void rdw_win_put(RdwStream& s, int64_t win, uint4 v, int lane) {
+    const int slot = (int)(win & (kRdwRingWins - 1));
+    *(uint4*)(s.ring + slot * kRdwWin + 16 * lane) = v;
+    if (slot == 0 && lane == 0) *(uint4*)(s.ring + kRdwRing) = v;
+}
+
+__device__ __forceinline__ void rdw_stream_start(RdwStream& s, int64_t win, int lane) {
+    s.hi = win;
+    s.nx0 = rdw_win_load(s, win, lane);
+    s.nx1 = rdw_win_load(s, win + 1, lane);
+}
+
+// Bring the windows holding [pos, pos + 4) into the ring (pos: wave-uniform, relative to data).
+__device__ __forceinline__ void rdw_stream_need(RdwStream& s, int64_t pos, int lane) {
+    const int64_t w0 = (s.shift + pos) >> 10, w1 = (s.shift + pos + 3) >> 10;
+    if (w1 < s.hi) return;
+    if (w0 > s.hi + 1) rdw_stream_start(s, w0, lane);   // a jump past the windows in flight
+    while (w1 >= s.hi) {
+        rdw_win_put(s, s.hi, s.nx0, lane);
+        s.nx0 = s.nx1;
+        s.hi++;
+        s.nx1 = rdw_win_load(s, s.hi + 1, lane);
     }
-    uint32_t carry = 0;                                 // byte w-1 is zero
-    for (int64_t w = p0 & ~(int64_t)3; w < p1 && w < a.n_bytes; w += 4) {
-        uint32_t zb = 0;                                // bit j: byte w + j is zero
-        if (w + 4 <= a.n_bytes) {
-            const uint32_t x = *(const uint32_t*)(a.data + w);
-            const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-            zb = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-        } else {
-            for (int j = 0; j < 4 && w + j < a.n_bytes; j++) zb |= (a.data[w + j] == 0 ? 1u : 0u) << j;
+    wave_sync_lds();
+}
+
+// The 4 header bytes at pos (in the ring).
+__device__ __forceinline__ uint32_t rdw_ring_header(const RdwStream& s, int64_t pos) {
+    const uint32_t o = (uint32_t)((s.shift + pos) & (kRdwRing - 1));
+    const uint32_t* q = (const uint32_t*)(s.ring + (o & ~3u));
+    return __builtin_amdgcn_alignbyte(q[1], q[0], o & 3u);
+}
+
+// rdw_step with the header read from the ring (RecordHeaderParserRDW.getRecordMetadata + the
+// reader's next-record arithmetic)
+__device__ __forceinline__ RdwStep rdw_step_ring(const RdwArgs& a, RdwStream& s, int64_t pos, int lane) {
+    RdwStep r{0, 0, 0, false, false, 0};
+    const int64_t avail = a.n_bytes - pos;
+    const int64_t hl = avail < 4 ? avail : 4;
+    const int64_t fo = pos + hl;
+    int64_t rlen;
+    if (a.p.file_header_bytes > 4 && fo == 4) {
+        rlen = a.p.file_header_bytes - 4;
+    } else if (a.n_bytes > 0 && a.p.file_footer_bytes > 0 && a.n_bytes - fo <= a.p.file_footer_bytes) {
+        rlen = a.n_bytes - fo;
+    } else if (hl < 4) {
+        r.stop = true;
+        r.next = a.n_bytes;
+        return r;
+    } else {
+        rdw_stream_need(s, pos, lane);
+        rlen = rdw_len(a, rdw_ring_header(s, pos));
+        if (rlen <= 0) { r.err = -2; return r; }
+        if (rlen > 100ll * 1024 * 1024) { r.err = -3; return r; }
+        r.valid = true;
+    }
+    if (rlen <= 0) { r.stop = true; r.next = a.n_bytes; return r; }
+    const int64_t rem = a.n_bytes - fo;
+    const int64_t got = rlen < rem ? rlen : rem;
+    r.off = fo;
+    r.len = (int32_t)got;
+    r.next = fo + got;
+    return r;
+}
+
+// The chain from pos to the first header at or past end, staging (offset, length) of the valid
+// records at so / sl [0, cap) in rows of 64 (records past cap are counted, not kept).
+__device__ RdwWalk rdw_walk_wave(const RdwArgs& a, RdwStream& s, int64_t pos, int64_t end, int64_t* so, int32_t* sl,
+                                 int64_t cap, int lane) {
+    RdwWalk w{pos, 0, -1};
+    if (pos < 0) { w.exit = pos; return w; }
+    if (pos < end) rdw_stream_start(s, (s.shift + pos) >> 10, lane);
+    int64_t my_off = 0;
+    int32_t my_len = 0;
+    uint32_t count = 0;
+    while (pos < end) {
+        const RdwStep st = rdw_step_ring(a, s, pos, lane);
+        if (st.err) {
+            w.err = ((pos + 4) << 2) | (st.err == -2 ? 2 : 3);   // reported at the payload offset
+            w.exit = -2;
+            w.count = count;
+            return w;
         }
-        // pairs starting at w-1, w, w+1, w+2 (bit i <-> position w - 1 + i)
-        uint32_t pairs = (carry & zb) | ((zb & (zb >> 1)) << 1);
-        carry = zb >> 3;
+        if (st.stop) { pos = st.next; break; }
+        if (st.valid) {
+            if ((uint32_t)lane == (count & 63u)) { my_off = st.off; my_len = st.len; }
+            count++;
+            if ((count & 63u) == 0 && (int64_t)count <= cap) {
+                so[count - 64 + lane] = my_off;
+                sl[count - 64 + lane] = my_len;
+            }
+        }
+        pos = st.next;
+    }
+    const uint32_t done = count & ~63u;
+    if ((uint32_t)lane < (count & 63u) && (int64_t)(done + lane) < cap) {
+        so[done + lane] = my_off;
+        sl[done + lane] = my_len;
+    }
+    w.exit = pos;
+    w.count = count;
+    return w;
+}
+
+// Speculated entry of a chunk [s0, e) of a range ending at re: the first strict candidate (the two
+// non-length header bytes zero) starting a plausible chain, else the first position starting a
+// plausible chain at all (the chunk's start when none: the fix rounds correct it).
+__device__ int64_t rdw_entry_wave(const RdwArgs& a, RdwStream& s, int64_t s0, int64_t e, int64_t re, int lane) {
+    const int64_t off = a.p.big_endian ? 2 : 0;   // position of the zero pair inside a header
+    for (int64_t w = (s.shift + s0 + off) >> 10; ; w++) {
+        const int64_t wa = w * kRdwWin - s.shift;   // window start relative to data
+        if (wa >= e + off || wa >= a.n_bytes) break;
+        // the lane's 16 bytes + the next one (from the following lane's slice, or the next window)
+        const uint4 v = rdw_win_load(s, w, lane);
+        const uint32_t nb_in = __shfl_down(v.x, 1, kWave) & 0xFFu;
+        uint32_t next_byte = nb_in;
+        if (lane == kWave - 1) {
+            const int64_t q = wa + kRdwWin;
+            next_byte = q < a.n_bytes ? a.data[q] : 1u;
+        }
+        const uint32_t zb = zero_bytes4(v.x) | zero_bytes4(v.y) << 4 | zero_bytes4(v.z) << 8 | zero_bytes4(v.w) << 12 |
+                            (next_byte == 0 ? 1u << 16 : 0u);
+        uint32_t pairs = zb & (zb >> 1) & 0xFFFFu;   // bit i: bytes i, i + 1 of the slice are zero
+        int64_t found = -1;
         while (pairs) {
             const int i = __builtin_ctz(pairs);
             pairs &= pairs - 1;
-            const int64_t p = w - 1 + i;
-            if (p < p0 || p >= p1) continue;
-            const int64_t q = p - off;
-            if (rdw_plausible(a, q, re, true)) return q;
+            const int64_t p = wa + 16 * lane + i;   // pair position (relative to data)
+            const int64_t q = p - off;              // header position
+            if (p < s0 + off || q >= e || p < 0) continue;
+            if (rdw_plausible(a, q, re, true)) { found = q; break; }
         }
+        const uint64_t m = __ballot(found >= 0);
+        if (m) return __shfl(found, __builtin_ctzll(m), kWave);
     }
-    return -1;
+    // no strict candidate: any plausible chain (lanes over consecutive positions)
+    for (int64_t p0 = s0; p0 < e; p0 += kWave) {
+        const int64_t p = p0 + lane;
+        const bool ok = p < e && rdw_plausible(a, p, re, false);
+        const uint64_t m = __ballot(ok);
+        if (m) return p0 + __builtin_ctzll(m);
+    }
+    return s0;
 }
 
-__global__ void rdw_spec_kernel(RdwArgs a, RdwChunkArgs c) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= c.n) return;
-    const RdwChunk ch = rdw_chunk(c, k);
-    const int64_t s = ch.start, e = ch.end, re = ch.range_end;
-    int64_t entry = s;
-    if (!ch.known) {
-        const int64_t q = rdw_strict_scan(a, s, e, re);
-        if (q >= 0) {
-            entry = q;
+__device__ __forceinline__ RdwStream rdw_stream(const RdwArgs& a, uint8_t* ring) {
+    RdwStream s;
+    const uintptr_t d = (uintptr_t)a.data;
+    s.base = (const uint8_t*)(d & ~(uintptr_t)15);
+    s.shift = (int64_t)(d & 15);
+    s.limit = s.shift + a.n_bytes;
+    s.ring = ring;
+    s.hi = 0;
+    s.nx0 = s.nx1 = make_uint4(0, 0, 0, 0);
+    return s;
+}
+
+// kFix false: speculate every chunk's entry and walk it; true: one fix round (changed[round - 1] == 0
+// ends the loop: every thread returns).
+template <bool kFix>
+__global__ __launch_bounds__(kWave * kRdwWaves) void rdw_wave_kernel(RdwArgs a, RdwChunkArgs c, int32_t round) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kRdwWaves * kRdwWaveLds];
+    const int lane = threadIdx.x % kWave;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    if (kFix && round > 0 && c.changed[round - 1] == 0) return;
+    RdwStream s = rdw_stream(a, smem + wid * kRdwWaveLds);
+    for (int64_t k = (int64_t)blockIdx.x * kRdwWaves + wid; k < c.n; k += (int64_t)gridDim.x * kRdwWaves) {
+        const RdwChunk ch = rdw_chunk(c, k);
+        int64_t entry;
+        if (kFix) {
+            if (ch.known) continue;
+            entry = c.exit_out[k - 1];   // in place: the predecessor's exit of this round or the last
+            if (entry == c.entry[k]) continue;
+            if (lane == 0) { c.entry[k] = entry; c.changed[round] = 1; }
         } else {
-            for (int64_t p = s; p < e; p++)
-                if (rdw_plausible(a, p, re, false)) { entry = p; break; }
+            entry = ch.known ? ch.start : rdw_entry_wave(a, s, ch.start, ch.end, ch.range_end, lane);
+            if (lane == 0) c.entry[k] = entry;
+        }
+        const RdwWalk w = rdw_walk_wave(a, s, entry, ch.end, c.stage_off + k * c.stage_cap, c.stage_len + k * c.stage_cap,
+                                        c.stage_cap, lane);
+        if (lane == 0) {
+            c.exit_out[k] = w.exit;
+            c.count[k] = w.count;
+            c.err[k] = w.err;
         }
     }
-    c.entry[k] = entry;
-    const RdwWalk w = rdw_walk<1>(a, entry, e, c.stage_off + k * c.stage_cap, c.stage_len + k * c.stage_cap, 0, c.stage_cap);
-    c.exit_out[k] = w.exit;
-    c.count[k] = w.count;
-    c.err[k] = w.err;
-}
-
-__global__ void rdw_fix_kernel(RdwArgs a, RdwChunkArgs c) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= c.n) return;
-    const RdwChunk ch = rdw_chunk(c, k);
-    if (ch.known) { c.exit_out[k] = c.exit_in[k]; return; }
-    const int64_t e = c.exit_in[k - 1];
-    if (e == c.entry[k]) { c.exit_out[k] = c.exit_in[k]; return; }
-    c.entry[k] = e;
-    *c.changed = 1;
-    const RdwWalk w = rdw_walk<1>(a, e, ch.end, c.stage_off + k * c.stage_cap, c.stage_len + k * c.stage_cap, 0, c.stage_cap);
-    c.exit_out[k] = w.exit;
-    c.count[k] = w.count;
-    c.err[k] = w.err;
 }
 
 // One wave per chunk: its staged records -> rec_off / rec_len[base, base + count) (coalesced);
