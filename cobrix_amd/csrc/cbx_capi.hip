@@ -112,9 +112,9 @@ struct cbx_plan {
     // specialised kernels: [0] windowed op set, [kp] contiguous op set with kp chunks per lane,
     // [kPre + 1 + kp] the contiguous op set over variable-length spans (span_loop)
     // specialised kernels: [0, kPre] contiguous decode by prefetch depth, kPre + 1 + kp span decode,
-    // 2 (kPre + 1) + kp the Utf8 layout's contiguous count pass
-    bool jit_tried[3 * kPre + 3] = {};
-    hipFunction_t jit_fn[3 * kPre + 3] = {};
+    // 2 (kPre + 1) + kp / 3 (kPre + 1) + kp the Utf8 layout's contiguous / span count pass
+    bool jit_tried[4 * kPre + 4] = {};
+    hipFunction_t jit_fn[4 * kPre + 4] = {};
     int rec_extent = 0;          // bytes past the decode base that any field (any OCCURS element) reaches
     std::string jit_error;
     int last_kind = 0;
@@ -904,28 +904,29 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
         HIP_CHECK(hipEventRecord(ce.e[0], st));
     }
-    if (mode == 0 && P->packed && P->n_seq > 0 && !contig) {
-        // Arrow Utf8 layout, windowed / span-staged records: the table-driven count pass (a mode-1
-        // call: tile payload totals + their scan), timed with the decode
+    // Arrow Utf8 layout: the count pass (tile payload totals) and their scan, so the decode writes
+    // every offset and payload byte once, at its final place (timed with the decode).  Contiguous and
+    // span-staged batches count with a specialised kernel of the same staging; windowed ones (and a
+    // failed specialisation) with a mode-1 call of the table-driven kernel.
+    hipFunction_t cfn = nullptr;
+    if (mode == 0 && P->packed && P->n_seq > 0 && (contig || span) && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
+        const int kp = contig ? contig_kp(sdw) : span_kp;
+        const int k = (contig ? 2 : 3) * (kPre + 1) + kp;
+        if (!P->jit_tried[k]) {
+            P->jit_tried[k] = true;
+            std::string err;
+            P->jit_fn[k] = jit_get(jit_source(true, kp, jit_pro(P), false, S.win, S.nops, S.batches, S.sops, span, true),
+                                   &err, "cbx_jit_count");
+        }
+        cfn = P->jit_fn[k];
+    }
+    if (mode == 0 && P->packed && P->n_seq > 0 && !cfn && !contig) {
         const int kind = P->last_kind;
         if ((r = launch(P, c, columns, 1, st))) return r;
         P->last_kind = kind;
     } else if (mode == 0 && P->packed && P->n_seq > 0) {
-        // Arrow Utf8 layout: the count pass (tile payload totals) and their scan, so the decode writes
-        // every offset and payload byte once, at its final place (timed with the decode)
         KernelArgs ac = a;
         ac.mode = 1;
-        hipFunction_t cfn = nullptr;
-        if (contig && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
-            const int k = 2 * (kPre + 1) + contig_kp(sdw);
-            if (!P->jit_tried[k]) {
-                P->jit_tried[k] = true;
-                std::string err;
-                P->jit_fn[k] = jit_get(jit_source(true, contig_kp(sdw), jit_pro(P), false, S.win, S.nops, S.batches, S.sops, false, true),
-                                       &err, "cbx_jit_count");
-            }
-            cfn = P->jit_fn[k];
-        }
         int cocc = 0;
         const hipError_t ce2 = cfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, cfn, kWave * kWavesPerBlock, lds)
                                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, decode_kernel, kWave * kWavesPerBlock, lds);
