@@ -77,28 +77,44 @@ def _register(objs: List[Any]) -> int:
     return k
 
 
-@_SCHEMA_RELEASE
-def _release_schema(p):
-    s = p.contents
-    if s.private_data:
-        _LIVE.pop(int(s.private_data), None)
-    for i in range(s.n_children):
-        c = s.children[i].contents
-        if c.release:
-            c.release(s.children[i])
-    s.release = _SCHEMA_RELEASE()
+def _make_release_callbacks():
+    """The release callbacks, closing over what they use: a consumer may release while the
+    interpreter shuts down, when module globals already read as None."""
+    live, SR, AR = _LIVE, _SCHEMA_RELEASE, _ARRAY_RELEASE
+    null_schema_cb, null_array_cb = SR(), AR()
+
+    def drop(key):
+        if key:
+            live.pop(int(key), None)
+
+    @SR
+    def release_schema(p):
+        s = p.contents
+        try:
+            for i in range(s.n_children):
+                c = s.children[i].contents
+                if c.release:
+                    c.release(s.children[i])
+            drop(s.private_data)
+        finally:
+            s.release = null_schema_cb   # released: the callback slot is cleared
+
+    @AR
+    def release_array(p):
+        a = p.contents
+        try:
+            for i in range(a.n_children):
+                c = a.children[i].contents
+                if c.release:
+                    c.release(a.children[i])
+            drop(a.private_data)
+        finally:
+            a.release = null_array_cb
+
+    return release_schema, release_array
 
 
-@_ARRAY_RELEASE
-def _release_array(p):
-    a = p.contents
-    if a.private_data:
-        _LIVE.pop(int(a.private_data), None)
-    for i in range(a.n_children):
-        c = a.children[i].contents
-        if c.release:
-            c.release(a.children[i])
-    a.release = _ARRAY_RELEASE()
+_release_schema, _release_array = _make_release_callbacks()
 
 
 class _Node:

@@ -104,7 +104,7 @@ def _import_host(da, schema, kids):
     host.array = _host_copy(root, keep)
     host.device_type, host.device_id, host.sync_event = AD.ARROW_DEVICE_CPU, -1, None
     rb = pa.RecordBatch._import_from_c_device(ctypes.addressof(host), ctypes.addressof(schema))
-    return rb
+    return rb, keep   # the import is zero-copy: the host copies must outlive rb
 
 
 def _norm(v):
@@ -117,10 +117,11 @@ def _norm(v):
     return v
 
 
-def _check(batch):
+def _check(batch, device_type=None):
     from cobrix_amd import arrow_device as AD
     da, schema, kids = AD.export_device(batch)
-    assert da.device_type == AD.ARROW_DEVICE_ROCM and da.device_id == torch.cuda.current_device()
+    if device_type is None:
+        assert da.device_type == AD.ARROW_DEVICE_ROCM and da.device_id == torch.cuda.current_device()
     assert da.array.length == batch.n_rec and da.array.n_children == len(kids)
     # zero copy: every pointer lies inside one of the batch's own device tensors
     spans = [(t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for c in batch.cols for t in c.values()
@@ -137,7 +138,7 @@ def _check(batch):
             walk(c)
     for k in kids:
         walk(k)
-    rb = _import_host(da, schema, kids)
+    rb, keep = _import_host(da, schema, kids)
     assert rb.num_rows == batch.n_rec
     plan = batch.plan
     got = {f.name: rb.column(i) for i, f in enumerate(rb.schema)}
