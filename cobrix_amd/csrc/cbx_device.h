@@ -870,7 +870,7 @@ __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window&
     for (int i = w.sop_begin; i < w.sop_end; i++) {
         const StrOp op = ldc(a.sops + i);
         const StrCall c = sizes ? StrCall{} : ldc(a.scall + i);
-        if (a.str_view) str_element<true>(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
+        if (a.str_view == 1) str_element<true>(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
         else str_element<false>(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
     }
     if (sizes) return;
