@@ -459,7 +459,15 @@ int cbx_frame_length_field(cbx_plan* plan, const uint8_t* d_data, int64_t n_byte
  * the rows with cbx_decode_selected (segment = the record's own segment: its redefine decodes); the
  * list of segment-C children of every parent row is a contiguous run of table 1 + C
  * (cbx_hier_list_offsets).  table_rows (host, n_segments + 1 entries) receives the row count per
- * table.  Output arrays need capacity n_rec. */
+ * table.  Output arrays need capacity n_rec.
+ * Not covered (reported by the host, CBX_E_UNSUPPORTED, never decoded differently):
+ * record_start_offset != 0 -- extractHierarchicalRecord decodes the root at the start offset but
+ * each child segment at its group's own offset, without it (RecordExtractors.scala:310, :376);
+ * several segment ids mapped to one parent segment.  Parity-unpinned (no reference fixture; the
+ * oracle restatement and these kernels agree): a DEPENDING ON field inside a child segment whose
+ * value is null -- the reference's dependFields map is shared by all segments of a hierarchical
+ * record (:226), so such an array takes the count an earlier segment left there; here each
+ * record's arrays use the record's own dependees. */
 typedef struct {
     int32_t n_segments;               /* segment redefines (cbx_field.segment / key_segment indices) */
     int32_t root_segment;             /* the segment without a parent */
