@@ -574,6 +574,8 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
 // String-view layout: bytes of a slot region owned by one tile (the tile's payload bound, 16-aligned)
 // and tiles per Arrow data buffer (buffers of at most 1 GiB, a whole number of tiles each).
 // a tile's region: 64 payloads of the column's widest value, each at a 4-byte-aligned position
+// KernelArgs.str_view / CBX_STR_LAYOUT: 0 Arrow large-string, 1 string views, 2 Arrow Utf8
+static int str_layout_of(const cbx_plan* P) { return P->view ? 1 : P->packed ? 2 : 0; }
 static int64_t view_tile_bytes(const cbx_plan* P, int c) { return ((int64_t)kWave * ((P->col_max_bytes[c] + 3) & ~3) + 15) & ~(int64_t)15; }
 // whole tiles per data buffer: the largest power of two fitting 1 GiB (the kernels split a tile
 // index into buffer and position by a shift)
@@ -654,7 +656,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.rec_seg = c.rec_seg;
     a.file_id = c.file_id >= 0 ? c.file_id : P->opts.file_id;
     a.mode = mode;
-    a.str_view = P->view ? 1 : P->packed ? 2 : 0;
+    a.str_view = str_layout_of(P);
     // staging mode
     const int sdw = c.stride / 4;
     const bool contig = !c.rec_off && P->contig_ok && c.stride > 0 && c.stride % 4 == 0 && a.base_shift % 4 == 0 &&
@@ -671,7 +673,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         const int k = kPre + 1 + span_kp;
         if (!P->jit_tried[k]) {
             P->jit_tried[k] = true;
-            P->jit_fn[k] = jit_get(jit_source(true, span_kp, jit_pro(P), P->view, P->cset.win, P->cset.nops, P->cset.batches,
+            P->jit_fn[k] = jit_get(jit_source(true, span_kp, jit_pro(P), str_layout_of(P), P->cset.win, P->cset.nops, P->cset.batches,
                                               P->cset.sops, true), &P->jit_error);
         }
         span_fn = P->jit_fn[k];
@@ -881,7 +883,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                                " windows, above the specialised-kernel limits (" + std::to_string(kJitMaxOps) + ", " +
                                std::to_string(kJitMaxWindows) + ")";
             else
-                P->jit_fn[k] = jit_get(jit_source(contig, k, jit_pro(P), P->view, S.win, S.nops, S.batches, S.sops, false), &P->jit_error);
+                P->jit_fn[k] = jit_get(jit_source(contig, k, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false), &P->jit_error);
         }
         jfn = P->jit_fn[k];
     }
@@ -915,7 +917,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         if (!P->jit_tried[k]) {
             P->jit_tried[k] = true;
             std::string err;
-            P->jit_fn[k] = jit_get(jit_source(true, kp, jit_pro(P), false, S.win, S.nops, S.batches, S.sops, span, true),
+            P->jit_fn[k] = jit_get(jit_source(true, kp, jit_pro(P), 2, S.win, S.nops, S.batches, S.sops, span, true),
                                    &err, "cbx_jit_count");
         }
         cfn = P->jit_fn[k];
@@ -1109,7 +1111,7 @@ extern "C" int cbx_debug_stamps(cbx_plan* P, uint64_t* out) {
 extern "C" int cbx_plan_specialize(cbx_plan* P, char* source, int64_t source_cap, int64_t* source_len, int32_t compile) {
     if (!P) return fail(CBX_E_ARGUMENT, "cbx_plan_specialize: invalid arguments");
     const cbx_plan::OpSet& S = P->contig_ok ? P->cset : P->wset;
-    const std::string src = jit_source(P->contig_ok, P->contig_ok ? kPre : 0, jit_pro(P), P->view, S.win, S.nops, S.batches, S.sops, false);
+    const std::string src = jit_source(P->contig_ok, P->contig_ok ? kPre : 0, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false);
     if (source_len) *source_len = (int64_t)src.size();
     if (source && source_cap > 0) {
         const size_t n = std::min<size_t>(src.size(), (size_t)source_cap - 1);
@@ -1121,7 +1123,7 @@ extern "C" int cbx_plan_specialize(cbx_plan* P, char* source, int64_t source_cap
         std::string err;
         if (!jit_compile(src, &code, &err)) return fail(CBX_E_HIP, err);
         if (P->packed && P->contig_ok && P->n_seq > 0 &&   // the Utf8 layout's count pass too
-            !jit_compile(jit_source(true, kPre, jit_pro(P), false, S.win, S.nops, S.batches, S.sops, false, true), &code, &err))
+            !jit_compile(jit_source(true, kPre, jit_pro(P), 2, S.win, S.nops, S.batches, S.sops, false, true), &code, &err))
             return fail(CBX_E_HIP, err);
     }
     return CBX_OK;

@@ -746,6 +746,18 @@ __device__ __forceinline__ void lds_to_global_any(const uint8_t* s, CBX_GLOBAL u
     }
 }
 
+// The plan's string layout (KernelArgs.str_view): a compile-time constant in the specialised
+// kernels (cbx_jit.h defines CBX_STR_LAYOUT), so a kernel inlines only its own layout's string path
+// per element -- with all three, layouts of hundreds of string elements took minutes in hipRTC.
+__device__ __forceinline__ int str_layout(const KernelArgs& a) {
+#ifdef CBX_STR_LAYOUT
+    (void)a;
+    return CBX_STR_LAYOUT;
+#else
+    return a.str_view;
+#endif
+}
+
 // One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):
 // span + tile-local scan.
 // * Arrow large-string layout (str_view 0): the tile's payload is staged contiguously in LDS and
@@ -787,7 +799,11 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
     gp(c.validity)[t.tile] = __ballot(ok);
     auto lutf = [&](uint32_t b) { return str_lut(op.kind, s_lut, b); };
     const uint8_t* sp_src = src + rec_addr + (uint32_t)op.eo;
-    if (a.str_view == 2) {
+    // the destination region: Utf8 -- the tile's final place in the slot's region (offsets written
+    // here, once); large-string -- the tile's scratch region (tile-local starts for the placement pass)
+    const bool packed = str_layout(a) == 2;
+    CBX_GLOBAL uint8_t* dst;
+    if (packed) {
         const int64_t base = c.excl[t.tile] - c.excl[0];   // the tile's place in the slot's region
         const int64_t end = base + tot;
         CBX_GLOBAL int32_t* offs = gp((int32_t*)c.local);
@@ -800,42 +816,31 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
             if (lane == 0) atomicOr(a.status, 1);
             return;
         }
-        CBX_GLOBAL uint8_t* dst = gp(c.scratch + base);
-        if ((int)tot <= a.str_stage) {
-            if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + a.dump_stride * lane, op.size, op.pad);
-            else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
-            wave_sync_lds();
-            lds_to_global_any(s_str, dst, tot, lane);
-            wave_sync_lds();
-        } else if (ok) {
-            if (fast) {
-                uint8_t dump[4];
-                string_write32e(ev, sp, (uint8_t*)(dst + ex), dump, op.size, op.pad);
-            } else {
-                string_write(op.kind, sp_src, sp, (uint8_t*)(dst + ex), lutf);
-            }
-        }
-        return;
+        dst = gp(c.scratch + base);
+    } else {
+        (gp(c.local) + t.tile * kWave)[lane] = ex;
+        if (lane == 0) gp(a.str_tot)[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
+        dst = gp(c.scratch + t.tile * (int64_t)c.tile_cap);   // 16-byte aligned region
     }
-    (gp(c.local) + t.tile * kWave)[lane] = ex;
-    if (lane == 0) gp(a.str_tot)[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
-    uint32_t* dst32 = (uint32_t*)(c.scratch + t.tile * (int64_t)c.tile_cap);   // 16-byte aligned region
     if ((int)tot <= a.str_stage) {
         if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + a.dump_stride * lane, op.size, op.pad);
         else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
         wave_sync_lds();
-        // 16-byte pieces: the staging area and the scratch region are 16-byte aligned and the
-        // region (a multiple of 16 bytes >= the tile's bound) holds the rounded-up total
-        const u32x4* s128 = (const u32x4*)s_str;
-        for (int q = lane; 16 * q < (int)tot; q += kWave) gp((u32x4*)dst32)[q] = s128[q];
+        if (packed) {
+            lds_to_global_any(s_str, dst, tot, lane);
+        } else {
+            // 16-byte pieces: the staging area and the scratch region are 16-byte aligned and the
+            // region (a multiple of 16 bytes >= the tile's bound) holds the rounded-up total
+            const u32x4* s128 = (const u32x4*)s_str;
+            for (int q = lane; 16 * q < (int)tot; q += kWave) gp((u32x4*)dst)[q] = s128[q];
+        }
         wave_sync_lds();
     } else if (ok) {
-        uint8_t* dst = (uint8_t*)dst32 + ex;
         if (fast) {
             uint8_t dump[4];
-            string_write32e(ev, sp, dst, dump, op.size, op.pad);
+            string_write32e(ev, sp, (uint8_t*)(dst + ex), dump, op.size, op.pad);
         } else {
-            string_write(op.kind, sp_src, sp, dst, lutf);
+            string_write(op.kind, sp_src, sp, (uint8_t*)(dst + ex), lutf);
         }
     }
 }
@@ -870,7 +875,7 @@ __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window&
     for (int i = w.sop_begin; i < w.sop_end; i++) {
         const StrOp op = ldc(a.sops + i);
         const StrCall c = sizes ? StrCall{} : ldc(a.scall + i);
-        if (a.str_view == 1) str_element<true>(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
+        if (str_layout(a) == 1) str_element<true>(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
         else str_element<false>(a, op, a.sops + i, c, t, s_cnt, src, rec_addr, kGlobal, s_lut, s_str, lane);
     }
     if (sizes) return;

