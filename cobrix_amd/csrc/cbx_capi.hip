@@ -113,8 +113,9 @@ struct cbx_plan {
     // [kPre + 1 + kp] the contiguous op set over variable-length spans (span_loop)
     // specialised kernels: [0, kPre] contiguous decode by prefetch depth, kPre + 1 + kp span decode,
     // 2 (kPre + 1) + kp / 3 (kPre + 1) + kp the Utf8 layout's contiguous / span count pass
-    bool jit_tried[4 * kPre + 4] = {};
-    hipFunction_t jit_fn[4 * kPre + 4] = {};
+    // + [4 (kPre + 1)] the specialised list kernel
+    bool jit_tried[4 * kPre + 5] = {};
+    hipFunction_t jit_fn[4 * kPre + 5] = {};
     int rec_extent = 0;          // bytes past the decode base that any field (any OCCURS element) reaches
     std::string jit_error;
     int last_kind = 0;
@@ -477,7 +478,12 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     for (const Field& d : P->dfields_h) {
         if (d.variant != V_STRING) continue;
         const bool fast = d.size <= kStrFastBytes && (d.kind == CBX_K_STRING || d.kind == CBX_K_STRING_ASCII);
-        if (P->view && fast) {
+        if (P->packed && fast) {
+            // Arrow Utf8 register path (str_utf8_fast): the lane slots, then the tile's bytes at their
+            // final offsets (+ a chunk of alignment and the shifted dwords' overhang)
+            P->str_stage = std::max(P->str_stage, std::max(kWave * str_lane_slot(d.size, d.max_utf8),
+                                                           kWave * d.size * d.max_utf8 + 64));
+        } else if (P->view && fast) {
             // (env CBX_STR_NO_SHIFT: single-byte pages through the slots too -- A/B runs; the
             // specialised kernel then compiles the slot path for them, cbx_jit.h)
             if (d.max_utf8 > 1 || getenv("CBX_STR_NO_SHIFT")) slots = std::max(slots, kWave * str_lane_slot(d.size, d.max_utf8));
@@ -929,15 +935,22 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     } else if (mode == 0 && P->packed && P->n_seq > 0) {
         KernelArgs ac = a;
         ac.mode = 1;
+        // the specialised count kernel: no string staging per wave (it only scans lengths), two LUT
+        // copies in front (full + count_lut_entry)
+        size_t clds = lds;
+        if (cfn) {
+            ac.lds_wave = (a.lds_rows + a.lds_counts + 16 + 15) & ~15;
+            clds = 2048 + (size_t)kWavesPerBlock * ac.lds_wave;
+        }
         int cocc = 0;
-        const hipError_t ce2 = cfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, cfn, kWave * kWavesPerBlock, lds)
-                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, decode_kernel, kWave * kWavesPerBlock, lds);
-        int cbpc = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / lds));
+        const hipError_t ce2 = cfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, cfn, kWave * kWavesPerBlock, clds)
+                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, decode_kernel, kWave * kWavesPerBlock, clds);
+        int cbpc = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / clds));
         if (ce2 == hipSuccess && cocc > 0) cbpc = std::min(cbpc, cocc);
         const int64_t cgrid = std::min<int64_t>(blocks_needed, (int64_t)P->num_cus * cbpc);
         if (cfn) {
             void* kargs[] = {&ac};
-            HIP_CHECK(hipModuleLaunchKernel(cfn, (unsigned)cgrid, 1, 1, kWave * kWavesPerBlock, 1, 1, (unsigned)lds, st, kargs, nullptr));
+            HIP_CHECK(hipModuleLaunchKernel(cfn, (unsigned)cgrid, 1, 1, kWave * kWavesPerBlock, 1, 1, (unsigned)clds, st, kargs, nullptr));
         } else {
             hipLaunchKernelGGL(decode_kernel, dim3((unsigned)cgrid), dim3(kWave * kWavesPerBlock), lds, st, ac);
             HIP_CHECK(hipGetLastError());
@@ -953,9 +966,27 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     }
     if (lists) {   // child elements of list-layout arrays, from the lengths and starts the prologue wrote
         const int64_t lgrid = std::min<int64_t>((n_tiles + kListWaves - 1) / kListWaves, (int64_t)P->num_cus * 8);
-        const size_t llds = kListWaves * (2 * kGuard + kListStage);
-        hipLaunchKernelGGL(list_kernel<false>, dim3((unsigned)lgrid), dim3(kWave * kListWaves), llds, st, a,
-                           (const CBX_CONST ListOp*)P->d_lops, (int32_t)P->lops.size());
+        const size_t llds = kListWaves * 2 * (2 * kGuard + kListStage);   // two staging buffers per wave (cbx_list.h)
+        // the copybook-specialised list kernel for large batches (cbx_jit.h: jit_list_source)
+        hipFunction_t lfn = nullptr;
+        if (P->jit_min >= 0 && c.n_rec >= P->jit_min) {
+            const int k = 4 * (kPre + 1);
+            if (!P->jit_tried[k]) {
+                P->jit_tried[k] = true;
+                const std::string src = jit_list_source(P->lops);
+                std::string err;
+                if (!src.empty()) P->jit_fn[k] = jit_get(src, &err, "cbx_jit_list");
+            }
+            lfn = P->jit_fn[k];
+        }
+        const CBX_CONST ListOp* d_lops = (const CBX_CONST ListOp*)P->d_lops;
+        int32_t n_lops = (int32_t)P->lops.size();
+        if (lfn) {
+            void* kargs[] = {&a, &d_lops, &n_lops};
+            HIP_CHECK(hipModuleLaunchKernel(lfn, (unsigned)lgrid, 1, 1, kWave * kListWaves, 1, 1, (unsigned)llds, st, kargs, nullptr));
+        } else {
+            hipLaunchKernelGGL(list_kernel<false>, dim3((unsigned)lgrid), dim3(kWave * kListWaves), llds, st, a, d_lops, n_lops);
+        }
         // byte-loop pass over the tiles the first one flagged (deferred zoned forms, wide fields)
         hipLaunchKernelGGL(list_kernel<true>, dim3((unsigned)lgrid), dim3(kWave * kListWaves), llds, st, a,
                            (const CBX_CONST ListOp*)P->d_lops, (int32_t)P->lops.size());
@@ -1187,6 +1218,24 @@ extern "C" int cbx_string_sizes_var(cbx_plan* P, const uint8_t* d_data, int64_t 
     return decode_common(P, c, nullptr, out_sizes, (hipStream_t)stream);
 }
 
+// The stream-ordered pool of the current device keeps what it holds (release threshold: no limit):
+// cbx_frame_rdw's staging (gigabytes for a 10 GB file) is then reused from call to call instead of
+// being unmapped at every synchronisation and mapped again by the next call's hipMallocAsync.
+static void keep_pool_memory() {
+    static std::mutex mu;
+    static std::vector<int> done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(mu);
+    for (int d : done) if (d == dev) return;
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t thr = ~0ull;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    done.push_back(dev);
+}
+
 extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,
                              const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len,
                              int64_t capacity, int64_t* n_records, void* stream) {
@@ -1194,6 +1243,7 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     if (!d_data || n_bytes < 0 || !params || !n_records || (n_seeds > 0 && !seeds))
         return fail(CBX_E_ARGUMENT, "cbx_frame_rdw: invalid arguments");
     *n_records = 0;
+    keep_pool_memory();
     // seed ranges cut into chunks (rdw_wave_kernel: speculation + walk, fix rounds; rdw_place_kernel)
     // 64 KiB chunks: C4's 65-byte records ~1,000 per chunk; C5's 16 KB records still leave every
     // chunk a few headers (framing 13.9 ms at 16 KiB -> 3.4 ms; C4 4.6 -> 4.5 ms)
@@ -1221,7 +1271,7 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     // + one changed flag per fix round (rounds <= n + 1)
     const size_t bytes = sizeof(int64_t) * (5 * n + 4 + nb) + sizeof(RdwRange) * ranges.size() + sizeof(uint32_t) * n +
                          sizeof(int32_t) * (n + 2) + 64;
-    const size_t stage_bytes = (size_t)n * stage_cap * (sizeof(int64_t) + sizeof(int32_t));
+    const size_t stage_bytes = (size_t)n * stage_cap * (sizeof(uint32_t) + sizeof(int32_t));
     uint8_t* blk = nullptr;
     uint8_t* stage = nullptr;
     HIP_CHECK(hipMallocAsync((void**)&blk, bytes, st));
@@ -1240,8 +1290,8 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     c.count = (uint32_t*)(d_ranges + ranges.size());
     c.changed = (int32_t*)(c.count + n);   // [round]
     c.ranges = d_ranges; c.n_ranges = (int32_t)ranges.size(); c.chunk = chunk; c.n = n;
-    c.stage_off = (int64_t*)stage;
-    c.stage_len = (int32_t*)(stage + (size_t)n * stage_cap * sizeof(int64_t));
+    c.stage_off = (uint32_t*)stage;
+    c.stage_len = (int32_t*)(stage + (size_t)n * stage_cap * sizeof(uint32_t));
     c.stage_cap = stage_cap;
     HIP_CHECK(hipMemcpyAsync(d_ranges, ranges.data(), sizeof(RdwRange) * ranges.size(), hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemsetAsync(d_first_err, 0xFF, sizeof(unsigned long long), st));

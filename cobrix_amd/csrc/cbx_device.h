@@ -746,6 +746,18 @@ __device__ __forceinline__ void lds_to_global_any(const uint8_t* s, CBX_GLOBAL u
     }
 }
 
+// The launch's mode (KernelArgs.mode: 0 decode, 1 the string sizes / Utf8 count pass): a
+// compile-time constant in the specialised kernels (CBX_MODE), so a count kernel carries no decode
+// code (and its register allocation) and a decode kernel no count branches.
+__device__ __forceinline__ int kmode(const KernelArgs& a) {
+#ifdef CBX_MODE
+    (void)a;
+    return CBX_MODE;
+#else
+    return a.mode;
+#endif
+}
+
 // The plan's string layout (KernelArgs.str_view): a compile-time constant in the specialised
 // kernels (cbx_jit.h defines CBX_STR_LAYOUT), so a kernel inlines only its own layout's string path
 // per element -- with all three, layouts of hundreds of string elements took minutes in hipRTC.
@@ -756,6 +768,170 @@ __device__ __forceinline__ int str_layout(const KernelArgs& a) {
 #else
     return a.str_view;
 #endif
+}
+
+// ---- LDS-DMA (buffer_load_dwordx4 ... lds) ----
+// 16 bytes per lane from the buffer resource at voffset (out of range: no access) into LDS at
+// lds_base + 16 * lane (lds_base wave-uniform: the instruction's M0).  Issued as inline asm so the
+// compiler does not drain it at the next LDS read (it waits vmcnt(0) after any LDS-DMA it knows of):
+// the caller waits with a counted s_waitcnt vmcnt (lds_dma_wait) before it reads the bytes.
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voffset, const void* lds_base) {
+    const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(size_t)lds_base);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\t"
+                 "s_mov_b32 m0, %3\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voffset), "s"(rs), "s"(dst) : "memory");
+}
+
+// wait until at most n vector memory operations are outstanding (n: the ones issued after the
+// DMA the caller needs; memory operations complete in issue order).  The s_waitcnt builtin (not
+// asm): the compiler's own wait insertion sees it, so it does not wait again for older loads or
+// stores it tracks (a later wait of its own would also drain DMAs issued after this one).
+// Encoding (gfx9): vmcnt bits 3:0, expcnt 6:4 and lgkmcnt 11:8 left at their maxima.
+__device__ __forceinline__ void lds_dma_wait(int n) {
+    switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(0x0F70); break;
+    case 1: __builtin_amdgcn_s_waitcnt(0x0F71); break;
+    case 2: __builtin_amdgcn_s_waitcnt(0x0F72); break;
+    case 3: __builtin_amdgcn_s_waitcnt(0x0F73); break;
+    case 4: __builtin_amdgcn_s_waitcnt(0x0F74); break;
+    case 5: __builtin_amdgcn_s_waitcnt(0x0F75); break;
+    case 6: __builtin_amdgcn_s_waitcnt(0x0F76); break;
+    default: __builtin_amdgcn_s_waitcnt(0x0F77); break;
+    }
+    asm volatile("" ::: "memory");   // no LDS read hoisted above the wait
+}
+
+// ---- Utf8 decode of a register-path element (str_view 2, decode mode) ----
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+
+// The tile's 16-byte chunks of a slot region from the LDS staging to global: staging byte
+// mis + j holds output byte j and the destination's chunk boundaries are the staging's (dst_a =
+// the 16-byte aligned address at or before the tile's first byte), so whole chunks go as aligned
+// 16-byte copies; the first and last chunk are shared with the neighbouring tiles: only their own
+// bytes, as byte stores.
+__device__ __forceinline__ void lds_to_global_chunks(const uint8_t* s, CBX_GLOBAL uint8_t* dst_a, uint32_t mis, uint32_t n,
+                                                     int lane) {
+    if (n == 0) return;
+    const uint32_t end = mis + n;
+    const uint32_t last = (end - 1) >> 4;   // last chunk
+    const uint32_t full0 = mis ? 1u : 0u, full1 = (end & 15u) ? last : last + 1;   // [full0, full1) whole chunks
+    for (uint32_t c = full0 + (uint32_t)lane; c < full1; c += kWave)
+        *(CBX_GLOBAL u32x4*)(dst_a + 16 * c) = *(const u32x4*)(s + 16 * c);
+    // edge bytes: chunk 0 from mis (when partial), the last chunk up to end (when partial)
+    if (mis) {
+        const uint32_t j = mis + (uint32_t)lane;
+        if (lane < 16 && j < 16 && j < end) dst_a[j] = s[j];
+    }
+    if ((end & 15u) && (last > 0 || !mis)) {
+        const uint32_t j = 16 * last + (uint32_t)lane;
+        if (lane < 16 && j < end && j >= mis) dst_a[j] = s[j];
+    }
+}
+
+// One register-path string element of the tile in the Arrow Utf8 layout: the value composed in the
+// lane's registers (str_lane_compose: single-byte pages in registers, multi-byte ones through the
+// lane's conflict-free LDS slot), the tile's exclusive scan of the lengths, then the lanes' bytes
+// OR-ed as shifted dwords into the zeroed staging at their final offsets (ds_or: neighbouring lanes
+// share boundary dwords) and copied out in whole 16-byte chunks.  Per byte of a value two LDS byte
+// stores into the lane slot instead of two stores at shared tile positions with dump selects
+// (those cost a third of the SYNSTR200 decode: 4.2 of 15 ms, CBX_DIAG=8 A/B).
+__device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
+                                              const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
+                                              const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
+                                              uint8_t* s_str, int lane) {
+    bool el = t.active && (op.segment < 0 || op.segment == t.seg);
+    if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
+    const int o = a.start_off + op.eo;
+    const bool ok = el && o <= t.avail;
+    const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
+    u32x4 q[kStrNC];
+    int len = str_lane_compose(op.kind, op.trim, op.pad, op.size, op.eo, n, ok, src, rec_addr, s_lut, s_str, lane, q);
+    len = ok ? len : 0;
+    gp(c.validity)[t.tile] = __ballot(ok);
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32((uint32_t)len, lane, tot);
+    const int64_t base = c.excl[t.tile] - c.excl[0];   // the tile's place in the slot's region
+    CBX_GLOBAL int32_t* offs = gp((int32_t*)c.local);
+    (offs + t.tile * kWave)[lane] = (int32_t)(base + ex);
+    if (t.rec == a.n_rec - 1) {   // the closing offset and the slot's size
+        offs[a.n_rec] = (int32_t)(base + ex + len);
+        if (c.size) *gp(c.size) = base + ex + len;
+    }
+    if (base + tot > c.tile_cap || base + tot > 0x7fffffffll) {   // the region (or an int32 offset) overflows
+        if (lane == 0) atomicOr(a.status, 1);
+        return;
+    }
+    CBX_GLOBAL uint8_t* dst = gp(c.scratch + base);
+    const uint32_t mis = (uint32_t)((uint64_t)(size_t)dst & 15u);
+    const int nbytes = op.size * op.pad;                  // the value's bound (compile-time in the specialised kernel)
+    constexpr int kNW = (kStrFastBytes * 3 + 3) / 4 + 1;  // shifted dwords of the largest value
+    const int nw = (nbytes + 3) / 4 + 1;
+    wave_sync_lds();   // the lane slots are read back
+    for (uint32_t z = (uint32_t)lane; 16 * z < mis + tot + 16; z += kWave) *(u32x4*)(s_str + 16 * z) = u32x4{0u, 0u, 0u, 0u};
+    wave_sync_lds();
+    const uint32_t pos = mis + ex;
+    const uint32_t sh = pos & 3u;
+    lds_u32_t* d = (lds_u32_t*)(s_str + (pos & ~3u));
+    uint32_t prev = 0;
+#pragma unroll
+    for (int k = 0; k < kNW; k++) {
+        if (k < nw) {
+            uint32_t w = 0;
+            if (k < 4 * kStrNC && 4 * k < nbytes) {
+                const u32x4 qq = q[k >> 2];
+                w = (k & 3) == 0 ? qq.x : (k & 3) == 1 ? qq.y : (k & 3) == 2 ? qq.z : qq.w;
+                const int r = len - 4 * k;   // the value's bytes in this dword
+                w = r >= 4 ? w : r <= 0 ? 0u : w & ((1u << (8 * r)) - 1u);
+            }
+            const uint32_t v = sh ? __builtin_amdgcn_alignbyte(w, prev, 4u - sh) : w;
+            if (v) __atomic_fetch_or(d + k, v, __ATOMIC_RELAXED);
+            prev = w;
+        }
+    }
+    wave_sync_lds();
+    if (!(CBX_DIAG & 16)) lds_to_global_chunks(s_str, dst - mis, mis, tot, lane);
+    wave_sync_lds();   // the staging area is reused by the next element
+}
+
+// ---- Utf8 count pass (specialised kernels only: CBX_COUNT_LUT) ----
+// The count kernel's LDS copy of the code-page LUT keeps, per byte, only what a UTF-8 length needs:
+// the trim flag (bit 31) and the UTF-8 length (bits 24-25).  A trimmed character maps to <= U+0020,
+// one UTF-8 byte, so a value's length is the sum over all its bytes of the lengths, minus its
+// leading and trailing trimmable bytes: per byte one LDS read, a funnel shift collecting the trim
+// bits (byte j at bit size-1-j) and one add of the entry's top byte (trim * 128 + length: the sum of
+// the lengths of <= 32 bytes stays below 128).
+__device__ __forceinline__ uint32_t count_lut_entry(uint32_t e) {
+    return (e & 0x80000000u) | (e & 0x03000000u);   // trim flag | UTF-8 length (0..3)
+}
+
+// UTF-8 length of the lane's value of a register-path code-page element whose n bytes are all in
+// the record (n == op.size; the caller checks), from the count LUT.
+__device__ __forceinline__ int str_count_fast(const StrOp& op, const uint8_t* src, uint32_t rec_addr, bool ok,
+                                              const uint32_t* s_lut) {
+    uint32_t w[8];
+    img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
+    uint32_t tm = 0, acc = 0;
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++) {
+        if (j < op.size) {
+            const uint32_t e = *(const uint32_t*)((const uint8_t*)s_lut + byte_x4(w[j >> 2], j & 3));
+            tm = __builtin_amdgcn_alignbit(tm, e, 31);   // (tm << 1) | trim bit
+            acc += e >> 24;
+        }
+    }
+    const int size = op.size;
+    const uint32_t keep = ~tm & bits_below(size);
+    const int total = (int)(acc & 127u);
+    const bool tl = op.trim == CBX_TRIM_LEFT || op.trim == CBX_TRIM_BOTH;
+    const bool tr = op.trim == CBX_TRIM_RIGHT || op.trim == CBX_TRIM_BOTH;
+    if (!ok) return 0;
+    if (!keep) return (tl || tr) ? 0 : total;
+    const int lead = (int)clz32(keep) - (32 - size), trail = (int)ctz32(keep);
+    return total - (tl ? lead : 0) - (tr ? trail : 0);
 }
 
 // One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):
@@ -781,6 +957,31 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
         else str_view_fast(a, op, opp, i, c, t, s_cnt, src, rec_addr, s_lut, s_str, lane, ds);
         return;
     }
+    // (the plan sizes the staging for the lane slots and the tile's bytes up to the kStrStageBytes
+    // cap -- wider multi-byte fields keep the path below; compile-time in the specialised kernel)
+    if (!kView && fast && str_layout(a) == 2 && kmode(a) == 0 && kWave * op.size * op.pad + 64 <= kStrStageBytes &&
+        kWave * str_lane_slot(op.size, op.pad) <= kStrStageBytes) {
+        str_utf8_fast(a, op, opp, c, t, s_cnt, src, rec_addr, s_lut, s_str, lane);
+        return;
+    }
+#ifdef CBX_COUNT_LUT
+    // the count kernel of the Utf8 layout: code-page elements whose bytes are all in the record take
+    // the count LUT (str_count_fast); the others (short records, ASCII) sop_span with the full entries,
+    // which the count kernel keeps in its second LUT copy
+    if (!kView && fast && op.kind == CBX_K_STRING) {
+        bool el = t.active && (op.segment < 0 || op.segment == t.seg);
+        if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
+        const int o = a.start_off + op.eo;
+        const bool ok = el && o + op.size <= t.avail;
+        const bool part = el && o <= t.avail && !ok;   // a record ending inside the field
+        if (!__ballot(part)) {
+            uint32_t tot;
+            wave_excl_scan32((uint32_t)str_count_fast(op, src, rec_addr, ok, s_lut + 256), lane, tot);
+            if (lane == 0) gp(a.str_tot)[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
+            return;
+        }
+    }
+#endif
     bool ok;
     uint32_t ev[kStrFastBytes];
     const StrSpan sp = sop_span(a, op, opp, t, s_cnt, lane, src, rec_addr, s_lut, ok, fast, ev);
@@ -792,7 +993,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
     }
     uint32_t tot;
     const uint32_t ex = wave_excl_scan32((uint32_t)sp.utf8_len, lane, tot);
-    if (a.mode == 1) {
+    if (kmode(a) == 1) {
         if (lane == 0) gp(a.str_tot)[(int64_t)op.seq * a.n_tiles + t.tile] = tot;
         return;
     }
@@ -823,11 +1024,14 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
         dst = gp(c.scratch + t.tile * (int64_t)c.tile_cap);   // 16-byte aligned region
     }
     if ((int)tot <= a.str_stage) {
-        if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + a.dump_stride * lane, op.size, op.pad);
-        else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
+        // (diagnostic builds, CBX_JIT_DEFINES=CBX_DIAG=8 / 16: without the LDS byte writes / the copy-out)
+        if (!(CBX_DIAG & 8)) {
+            if (fast) string_write32e(ev, sp, s_str + ex, s_str + a.str_stage + a.dump_stride * lane, op.size, op.pad);
+            else if (ok) string_write(op.kind, sp_src, sp, s_str + ex, lutf);
+        }
         wave_sync_lds();
         if (packed) {
-            lds_to_global_any(s_str, dst, tot, lane);
+            if (!(CBX_DIAG & 16)) lds_to_global_any(s_str, dst, tot, lane);
         } else {
             // 16-byte pieces: the staging area and the scratch region are 16-byte aligned and the
             // region (a multiple of 16 bytes >= the tile's bound) holds the rounded-up total
@@ -850,7 +1054,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
 // must not issue that load (a load behind the prefetched tile makes its wait cover the prefetch).
 template <bool kSel = true>
 __device__ __forceinline__ void decode_generated(const KernelArgs& a, const Window& w, const TileCtx& t, int lane) {
-    if (a.mode == 1) return;
+    if (kmode(a) == 1) return;
     for (int i = w.gen_begin; i < w.gen_end; i++) {
         const GenOp g = ldc(a.gops + i);
         const DevColumn col = ldc(a.cols + g.column);
@@ -870,7 +1074,7 @@ template <bool kGlobal>
 __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window& w, const TileCtx& t, const uint8_t* src,
                                               uint32_t rec_addr, const int32_t* s_cnt, const uint32_t* s_lut,
                                               uint8_t* s_str, int lane) {
-    const bool sizes = a.mode == 1;
+    const bool sizes = kmode(a) == 1;
     // ---- strings (tile-local; placed by the compaction kernel)
     for (int i = w.sop_begin; i < w.sop_end; i++) {
         const StrOp op = ldc(a.sops + i);
@@ -1108,7 +1312,7 @@ __device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, c
     // ---- segment redefine selection
     if (kSel && a.rec_seg) t.seg = t.active ? a.rec_seg[t.rec] : -1;   // selected records: segment known
     else if (kSeg && a.segmap && t.active) t.seg = segment_of(a, s_lut, rp, t.avail);
-    if (kSeg && a.mode == 0 && a.seg_col >= 0) {
+    if (kSeg && kmode(a) == 0 && a.seg_col >= 0) {
         const DevColumn c = ldc(a.cols + a.seg_col);
         if (t.active) gp((int32_t*)c.values)[t.rec] = t.seg;
         const uint64_t m = __ballot(t.active);
@@ -1132,7 +1336,7 @@ __device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, c
             }
         }
         s_cnt[ai * kWave + lane] = cnt;
-        if (ar.offsets_column >= 0 && a.mode == 0) {
+        if (ar.offsets_column >= 0 && kmode(a) == 0) {
             // list layout: the record's present elements (none when the array's segment is not the
             // record's) get a run of the tile's child region starting at a multiple of 64; the
             // list kernel decodes them from these starts and lengths
@@ -1146,7 +1350,7 @@ __device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, c
             const uint64_t m = __ballot(t.active);
             if (lane == 0) gp(c.validity)[t.tile] = m;
         }
-        if (a.mode == 0 && ar.count_column >= 0) {
+        if (kmode(a) == 0 && ar.count_column >= 0) {
             const DevColumn c = ldc(a.cols + ar.count_column);
             const bool ok = t.active && (ar.segment < 0 || ar.segment == t.seg);
             if (t.active) gp((int32_t*)c.values)[t.rec] = cnt;

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include "cbx_device.h"
+#include "cbx_list.h"
 
 namespace cbx {
 
@@ -338,272 +339,10 @@ __global__ __launch_bounds__(256) void fixup_kernel(KernelArgs a, const CBX_CONS
 // extractArray's bounds check makes them).  Reference: the OCCURS loop of
 // RecordExtractors.extractRecord (RecordExtractors.scala:66-114) with the element decoders.
 // ------------------------------------------------------------------------------------------
-constexpr int kListWaves = 4;      // waves per workgroup
-constexpr int kListStage = 4096;   // LDS staging bytes per wave (staged: elements of up to 63 bytes)
-constexpr int kListKP = kListStage / (16 * kWave);   // 16-byte loads per lane per group
-
-// Dword at byte offset o of the record's descriptor; offsets before the record read as zero.
-__device__ __forceinline__ uint32_t list_dword(__amdgpu_buffer_rsrc_t rs, int o) {
-    return __builtin_amdgcn_raw_buffer_load_b32(rs, o < 0 ? 0x7ffffff0 : o, 0, 0);
-}
-
-// bytes [end - 8, end) of the descriptor as a little-endian u64 (cf. img_le64_ending)
-__device__ __forceinline__ uint64_t list_le64_ending(__amdgpu_buffer_rsrc_t rs, int end) {
-    const int s = end - 8;
-    const int a0 = s & ~3;
-    const uint32_t sh = (uint32_t)s & 3u;
-    const uint32_t d0 = list_dword(rs, a0), d1 = list_dword(rs, a0 + 4), d2 = list_dword(rs, a0 + 8);
-    return ((uint64_t)align_bytes(d2, d1, sh) << 32) | align_bytes(d1, d0, sh);
-}
-
-// Decode + store element k of a record (its step starts at element c0) for one field.
-// r1 / r0: the 8 (and 8 more) bytes ending at the element's end.
-// kFix = false: the fast decoders; lanes that need the byte loops (wide fields, zoned forms the
-// fast path defers, an element ending in the input's last partial dword) only raise `deferred`.
-// kFix = true (the second pass, over tiles that raised it): exactly those items again, byte loops
-// for the deferred lanes (the byte-loop decoders use scratch: they stay out of the first pass).
-// V >= 0: the fast decoder of variant V; V < 0: the variant read from the op (the byte-loop pass).
-// clean (wave-uniform): every present element of the step ends inside the record and before rsafe.
-// Every lane stores: lanes past the record's count write the padding of its 64-aligned run.
-template <int V, bool kFix>
-__device__ __forceinline__ void list_item(const KernelArgs& a, const ListOp& L, const DevColumn& col, int k, int c0,
-                                          int rlen, int ravail, int rsafe, bool clean, int64_t rbase, int64_t rstart,
-                                          uint64_t r1, uint64_t r0, bool& deferred) {
-    const NumOp& op = L.op;
-    const int v = V >= 0 ? V : op.variant;
-    const int eo = a.start_off + op.eo + k * L.stride;
-    const bool present = k < rlen;
-    const bool ok = present && (clean || eo + op.size <= ravail);
-    Val x = null_val();
-    bool slow = v == V_GENERIC;
-    if (v == V_BCD8) x = bcd8_raw<0>(op, r1);
-    else if (v == V_BCD16) x = bcd16_raw<0>(op, r1, r0);
-    else if (v == V_BIN8) x = bin8_raw<0>(op, r1);
-    else if (v == V_ZONED16) x = zoned16_raw<0>(op, r1, r0, slow);
-    else if (v == V_FP) x = fp_raw(op, r1);
-    if (kFix || !clean || v == V_ZONED16 || v == V_GENERIC) {
-        slow = (slow || eo + op.size > rsafe) && ok;   // (or ends in the input's last, partial dword)
-        const uint64_t sm = __ballot(slow);
-        if (!kFix) {
-            deferred |= sm != 0;
-            x.valid &= !slow;
-        } else {
-            if (sm == 0) return;
-            if (slow) x = decode_numeric(ldc(a.fields + L.field), a.data + rbase + eo);
-        }
-    }
-    x.valid &= ok;
-    store_value(col, op.out_type, rstart + k, x);
-    const uint64_t vm = __ballot(x.valid);
-    gp(col.validity)[(rstart + c0) >> 6] = vm;
-}
-
-constexpr int kListSteps = 4;   // element steps per round: reads first
-
-// One field over a group of element steps g0 .. g0+gn-1 of a record.  kStaged: the group's bytes are
-// in img (rel: the field's end in element 0 of the group, from img - kGuard); else read per lane
-// from the record's descriptor (rel: from the descriptor base).
-template <int V, bool kStaged, bool kFix = false>
-__device__ __forceinline__ void list_field(const KernelArgs& a, const ListOp& L, const DevColumn& col, const uint8_t* img,
-                                           __amdgpu_buffer_rsrc_t rs, int rel, int g0, int gn, int rlen, int ravail,
-                                           int rsafe, int64_t rbase, int64_t rstart, int lane, bool& deferred) {
-    const bool kWide = V >= 0 ? (V == V_BCD16 || V == V_ZONED16) : (L.op.variant == V_BCD16 || L.op.variant == V_ZONED16);
-    const int step_bytes = kWave * L.stride;
-    const int mine = rel + lane * L.stride;
-    // the group's last present element of this field ends inside the record, before rsafe
-    const int kmax = ((g0 + gn) * kWave < rlen ? (g0 + gn) * kWave : rlen) - 1;
-    const bool clean = a.start_off + L.op.eo + L.op.size + kmax * L.stride <= (ravail < rsafe ? ravail : rsafe);
-    if (kFix) {   // byte-loop pass: one step at a time (its decoders are large)
-        for (int st = 0; st < gn; st++) {
-            const int end = mine + st * step_bytes;
-            uint64_t r1, r0 = 0;
-            if (kStaged) {
-                r1 = img_le64_ending(img - kGuard, (uint32_t)end);
-                if (kWide) r0 = img_le64_ending(img - kGuard, (uint32_t)end - 8);
-            } else {
-                r1 = list_le64_ending(rs, end);
-                if (kWide) r0 = list_le64_ending(rs, end - 8);
-            }
-            const int c0 = (g0 + st) * kWave;
-            list_item<-1, true>(a, L, col, c0 + lane, c0, rlen, ravail, rsafe, clean, rbase, rstart, r1, r0, deferred);
-        }
-        return;
-    }
-    for (int st0 = 0; st0 < gn; st0 += kListSteps) {
-        uint64_t r1[kListSteps], r0[kListSteps];
-#pragma unroll
-        for (int u = 0; u < kListSteps; u++) {
-            const int st = st0 + u < gn ? st0 + u : gn - 1;   // (a repeat is not decoded)
-            const int end = mine + st * step_bytes;
-            r0[u] = 0;
-            if (V == V_GENERIC) { r1[u] = 0; continue; }
-            if (kStaged) {
-                r1[u] = img_le64_ending(img - kGuard, (uint32_t)end);
-                if (kWide) r0[u] = img_le64_ending(img - kGuard, (uint32_t)end - 8);
-            } else {
-                r1[u] = list_le64_ending(rs, end);
-                if (kWide) r0[u] = list_le64_ending(rs, end - 8);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kListSteps; u++) {
-            if (st0 + u >= gn) break;
-            const int c0 = (g0 + st0 + u) * kWave;
-            list_item<V, false>(a, L, col, c0 + lane, c0, rlen, ravail, rsafe, clean, rbase, rstart, r1[u], r0[u], deferred);
-        }
-    }
-}
-
-template <bool kStaged, bool kFix>
-__device__ __forceinline__ void list_field_v(const KernelArgs& a, const ListOp& L, const DevColumn& col, const uint8_t* img,
-                                             __amdgpu_buffer_rsrc_t rs, int rel, int g0, int gn, int rlen, int ravail,
-                                             int rsafe, int64_t rbase, int64_t rstart, int lane, bool& deferred) {
-#define CBX_LIST_V(VV) list_field<VV, kStaged>(a, L, col, img, rs, rel, g0, gn, rlen, ravail, rsafe, rbase, rstart, lane, deferred)
-    if (kFix) {
-        list_field<-1, kStaged, true>(a, L, col, img, rs, rel, g0, gn, rlen, ravail, rsafe, rbase, rstart, lane, deferred);
-        return;
-    }
-    switch (L.op.variant) {
-    case V_BCD8: CBX_LIST_V(V_BCD8); break;
-    case V_BCD16: CBX_LIST_V(V_BCD16); break;
-    case V_BIN8: CBX_LIST_V(V_BIN8); break;
-    case V_ZONED16: CBX_LIST_V(V_ZONED16); break;
-    case V_FP: CBX_LIST_V(V_FP); break;
-    default: CBX_LIST_V(V_GENERIC); break;
-    }
-#undef CBX_LIST_V
-}
-
-// A record with list elements (wave-uniform): its count, child start, byte offset and length, and
-// a buffer descriptor over its bytes from a 16-byte aligned base, rounded up to whole dwords (the
-// range check drops a dword that crosses it) within the input: elements ending past rsafe (only
-// in a last, partial dword of the input) take the byte-loop pass.
-struct ListRec {
-    int rlen, ravail, rsafe, bias;
-    int64_t rstart, rbase;
-    __amdgpu_buffer_rsrc_t rs;
-};
-
-__device__ __forceinline__ ListRec list_rec(const KernelArgs& a, int b, int len, int64_t start, int64_t base, int avail) {
-    ListRec r;
-    r.rlen = __builtin_amdgcn_readlane(len, b);
-    r.rstart = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(start >> 32), b) << 32) |
-               (uint32_t)__builtin_amdgcn_readlane((int)start, b);
-    r.rbase = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(base >> 32), b) << 32) |
-              (uint32_t)__builtin_amdgcn_readlane((int)base, b);
-    r.ravail = __builtin_amdgcn_readlane(avail, b);
-    const uint64_t addr = (uint64_t)(a.data + r.rbase);
-    r.bias = (int)(addr & 15);
-    const int64_t in_left = (a.data_len - r.rbase + r.bias) & ~(int64_t)3;
-    const int64_t want = ((int64_t)r.ravail + r.bias + 3) & ~(int64_t)3;
-    const int range = (int)(want < in_left ? want : in_left);
-    r.rsafe = range - r.bias;
-    r.rs = __builtin_amdgcn_make_buffer_rsrc((void*)(addr - r.bias), (short)0, range, 0x00020000);
-    return r;
-}
-
-// 16-byte chunks of group g0 of record r (its elements' bytes from the array's first field byte)
-__device__ __forceinline__ int list_n16(const ListRec& r, int s0, int s16, int g0, int gsteps, int stride) {
-    const int left = r.rlen - g0 * kWave;
-    const int ne = left < gsteps * kWave ? left : gsteps * kWave;
-    return (s0 - s16 + ne * stride + 15) >> 4;
-}
-
-// Issue the staging loads of group g0 of record r (chunks past the group: no access).
-__device__ __forceinline__ void list_issue(const KernelArgs& a, const ListRec& r, int elo, int stride, int g0, int gsteps,
-                                           int lane, uint4 (&v)[kListKP]) {
-    const int s0 = r.bias + a.start_off + elo + g0 * kWave * stride;
-    const int s16 = s0 & ~15;
-    const int n16 = list_n16(r, s0, s16, g0, gsteps, stride);
-#pragma unroll
-    for (int u = 0; u < kListKP; u++) {
-        const int c = u * kWave + lane;
-        const auto w = __builtin_amdgcn_raw_buffer_load_b128(r.rs, c < n16 ? s16 + 16 * c : 0x7ffffff0, 0, 0);
-        v[u] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-}
-
 template <bool kFix>
 __global__ __launch_bounds__(kWave * kListWaves) void list_kernel(KernelArgs a, const CBX_CONST ListOp* lops, int32_t n_lops) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x % kWave;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    uint8_t* img = smem + wid * (kGuard + kListStage + kGuard) + kGuard;
-    const int64_t nw = (int64_t)gridDim.x * kListWaves;
-    for (int64_t tile = (int64_t)blockIdx.x * kListWaves + wid; tile < a.n_tiles; tile += nw) {
-        if (kFix && a.list_flag[tile] == 0) continue;
-        bool deferred = false;
-        const int64_t rec = tile * kWave + lane;
-        const bool active = rec < a.n_rec;
-        int64_t base = a.base_shift;
-        int avail = 0;
-        if (active) {
-            if (a.rec_off) { base += a.rec_off[rec]; avail = a.rec_len[rec]; }
-            else { base += rec * (int64_t)a.stride; avail = a.stride; }
-        }
-        for (int i0 = 0; i0 < n_lops;) {
-            const int ai = lops[i0].array;
-            int i1 = i0 + 1;
-            while (i1 < n_lops && lops[i1].array == ai) i1++;
-            const int nops = i1 - i0;
-            const int stride = lops[i0].stride;
-            const int elo = lops[i0].elem_lo;             // the array's first byte in an element
-            // a staged group of element steps plus up to 15 bytes of alignment fits kListStage
-            const bool staged = kWave * stride <= kListStage - 16;
-            const int gsteps = staged ? (kListStage - 16) / (kWave * stride) : 1;
-            const DevColumn oc = ldc(a.cols + a.arrays[ai].offsets_column);
-            const int len = active ? a.list_len[(int64_t)ai * a.pitch + rec] : 0;
-            const int64_t start = active ? ((const int64_t*)oc.values)[rec] : 0;
-            uint64_t m = __ballot(len > 0);
-            if (m == 0) { i0 = i1; continue; }
-            // the tile's records with elements, a staged group at a time; the loads of the next
-            // group (of this record or the next one) are issued before the current group is decoded
-            ListRec cur = list_rec(a, __builtin_ctzll(m), len, start, base, avail);
-            m &= m - 1;
-            int g0 = 0;
-            uint4 v[kListKP];
-            if (staged) list_issue(a, cur, elo, stride, g0, gsteps, lane, v);
-            for (;;) {
-                const int nsteps = (cur.rlen + kWave - 1) / kWave;
-                const int gn = nsteps - g0 < gsteps ? nsteps - g0 : gsteps;
-                const int s0 = cur.bias + a.start_off + elo + g0 * kWave * stride;
-                const int s16 = s0 & ~15;
-                ListRec nxt = cur;
-                int ng0 = g0 + gsteps;
-                bool more = true;
-                if (ng0 >= nsteps) {
-                    if (m) { nxt = list_rec(a, __builtin_ctzll(m), len, start, base, avail); m &= m - 1; ng0 = 0; }
-                    else more = false;
-                }
-                if (staged) {
-                    const int n16 = list_n16(cur, s0, s16, g0, gsteps, stride);
-#pragma unroll
-                    for (int u = 0; u < kListKP; u++)
-                        if (u * kWave + lane < n16) *(uint4*)(img + 16 * (u * kWave + lane)) = v[u];
-                    wave_sync_lds();
-                    if (more) list_issue(a, nxt, elo, stride, ng0, gsteps, lane, v);
-                }
-                // field by field (its descriptor loaded once per group), the group's steps
-                for (int i = i0; i < i1; i++) {
-                    const ListOp L = ldc(lops + i);
-                    const DevColumn col = ldc(a.cols + L.op.column);
-                    const int rel = L.op.eo - elo + L.op.size;
-                    if (staged)
-                        list_field_v<true, kFix>(a, L, col, img, cur.rs, kGuard + s0 - s16 + rel, g0, gn, cur.rlen, cur.ravail,
-                                                 cur.rsafe, cur.rbase, cur.rstart, lane, deferred);
-                    else
-                        list_field_v<false, kFix>(a, L, col, img, cur.rs, s0 + rel, g0, gn, cur.rlen, cur.ravail, cur.rsafe,
-                                                  cur.rbase, cur.rstart, lane, deferred);
-                }
-                if (staged) wave_sync_lds();
-                if (!more) break;
-                cur = nxt;
-                g0 = ng0;
-            }
-            i0 = i1;
-        }
-        if (!kFix) gp(a.list_flag)[tile] = deferred ? 1 : 0;
-    }
+    ListFieldLoop body;
+    list_run<kFix>(a, lops, n_lops, body);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -705,7 +444,8 @@ struct RdwChunkArgs {
     int64_t* err;            // per chunk: (error position << 2 | code) or -1
     int32_t* changed;
     int64_t n;
-    int64_t* stage_off;      // chunk k's records: [k * stage_cap, k * stage_cap + min(count, stage_cap))
+    uint32_t* stage_off;     // chunk k's records: [k * stage_cap, k * stage_cap + min(count, stage_cap)), payload
+                             // offsets relative to the chunk's entry
     int32_t* stage_len;
     int64_t stage_cap;       // a multiple of 8
 };
@@ -822,20 +562,52 @@ __device__ __forceinline__ uint32_t zero_bytes4(uint32_t x) {   // bit j: byte j
 // round that changed nothing ends the loop (device flag per round, checked by the next round's
 // kernel, so rounds are launched without waiting for the host).
 constexpr int kRdwWin = 1024;                  // window bytes: one 16-byte load per lane
-constexpr int kRdwRingWins = 4;                // windows resident in the wave's ring
+constexpr int kRdwRingWins = 8;                // windows in the wave's ring (resident + loading ahead)
 constexpr int kRdwRing = kRdwWin * kRdwRingWins;
-constexpr int kRdwWaveLds = kRdwRing + 16;     // + a copy of the ring's first 16 bytes (reads across its end)
+constexpr int kRdwWaveLds = kRdwRing;
 constexpr int kRdwWaves = 4;                   // waves per workgroup
 
+// The ring is filled by LDS-DMA (buffer_load_dwordx4 ... lds: one instruction per window, 16 bytes
+// per lane straight into the window's slot, no registers).  The loads are issued as inline asm so
+// the compiler does not drain them (it waits vmcnt(0) before any LDS read after an LDS-DMA it
+// knows of); the walk waits for exactly the window it needs with a counted s_waitcnt vmcnt(N),
+// N = the windows issued after it: vector memory operations complete in issue order, and other
+// loads / stores issued after it only make the wait stricter.  (Register-held windows moved between
+// registers at each refill waited vmcnt(0) per window: C4 framing 10 ms.)
 struct RdwStream {
     const uint8_t* base;   // 16-byte aligned address at or before data
     int64_t shift;         // data - base
     int64_t limit;         // input bytes from base (shift + n_bytes)
     uint8_t* ring;         // the wave's LDS ring
-    int64_t hi;            // next window (index from base) to enter the ring
-    uint4 nx0, nx1;        // windows hi, hi + 1 in flight
+    uint32_t ring_lds;     // its LDS address (M0 of the DMA)
+    int64_t hi;            // next window (index from base) to issue
+    int64_t ready;         // windows <= ready are in the ring
 };
 
+__device__ __forceinline__ void rdw_vmwait(int n) { lds_dma_wait(n); }
+
+// Issue the DMA of window win into its slot (bytes past the input: zeros, range-checked).
+__device__ __forceinline__ void rdw_win_dma(const RdwStream& s, int64_t win, int lane) {
+    const int64_t a0 = win * kRdwWin;
+    int64_t left = s.limit - a0;
+    left = left < 0 ? 0 : (left > kRdwWin ? kRdwWin : left);
+    const uint64_t b = (uint64_t)(s.base + (a0 < s.limit ? a0 : 0));
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane((int)left);
+    void* bp = (void*)(((uint64_t)hi << 32) | lo);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bp, (short)0, nbytes, 0x00020000);
+    const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)(s.ring_lds + (uint32_t)(win & (kRdwRingWins - 1)) * kRdwWin));
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\t"
+                 "s_mov_b32 m0, %3\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(16 * lane), "s"(rs), "s"(dst) : "memory");
+}
+
+// Window win into registers (the speculation's scan): 16 bytes per lane, past the input zeros.
 __device__ __forceinline__ uint4 rdw_win_load(const RdwStream& s, int64_t win, int lane) {
     const int64_t a0 = win * kRdwWin;
     int64_t left = s.limit - a0;
@@ -846,41 +618,40 @@ __device__ __forceinline__ uint4 rdw_win_load(const RdwStream& s, int64_t win, i
     const int nbytes = __builtin_amdgcn_readfirstlane((int)left);
     void* bp = (void*)(((uint64_t)hi << 32) | lo);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bp, (short)0, nbytes, 0x00020000);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 0, 0);   // past the input: zeros
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 0, 0);
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
-__device__ __forceinline__ void rdw_win_put(RdwStream& s, int64_t win, uint4 v, int lane) {
-    const int slot = (int)(win & (kRdwRingWins - 1));
-    *(uint4*)(s.ring + slot * kRdwWin + 16 * lane) = v;
-    if (slot == 0 && lane == 0) *(uint4*)(s.ring + kRdwRing) = v;
-}
-
+// (re)start the stream at window win: 4 windows (a jump over a long record then costs 4 KiB, not
+// the ring); later calls top the ring up to 8 windows ahead of the position
 __device__ __forceinline__ void rdw_stream_start(RdwStream& s, int64_t win, int lane) {
-    s.hi = win;
-    s.nx0 = rdw_win_load(s, win, lane);
-    s.nx1 = rdw_win_load(s, win + 1, lane);
+    for (int j = 0; j < 4; j++) rdw_win_dma(s, win + j, lane);
+    s.hi = win + 4;
+    s.ready = win - 1;
 }
 
-// Bring the windows holding [pos, pos + 4) into the ring (pos: wave-uniform, relative to data).
-__device__ __forceinline__ void rdw_stream_need(RdwStream& s, int64_t pos, int lane) {
-    const int64_t w0 = (s.shift + pos) >> 10, w1 = (s.shift + pos + 3) >> 10;
-    if (w1 < s.hi) return;
-    if (w0 > s.hi + 1) rdw_stream_start(s, w0, lane);   // a jump past the windows in flight
-    while (w1 >= s.hi) {
-        rdw_win_put(s, s.hi, s.nx0, lane);
-        s.nx0 = s.nx1;
-        s.hi++;
-        s.nx1 = rdw_win_load(s, s.hi + 1, lane);
+// Bring the windows holding [pos, pos_hi) into the ring (wave-uniform positions relative to data,
+// pos_hi - pos <= 4 KiB), keeping the ring's other slots loading ahead.
+__device__ __forceinline__ void rdw_stream_range(RdwStream& s, int64_t pos, int64_t pos_hi, int lane) {
+    const int64_t w0 = (s.shift + pos) >> 10, w1 = (s.shift + pos_hi - 1) >> 10;
+    if (w1 <= s.ready && w0 >= s.hi - kRdwRingWins) return;
+    if (w0 >= s.hi || w0 < s.hi - kRdwRingWins) {   // a jump past the windows issued
+        rdw_stream_start(s, w0, lane);
+    } else {
+        while (s.hi <= w0 + kRdwRingWins - 1) rdw_win_dma(s, s.hi++, lane);   // slots of windows < w0 are free
     }
-    wave_sync_lds();
+    const int64_t n_after = s.hi - 1 - w1;   // the windows issued after w1 may stay in flight
+    rdw_vmwait((int)(n_after < 0 ? 0 : n_after));
+    s.ready = w1;
 }
 
-// The 4 header bytes at pos (in the ring).
+__device__ __forceinline__ void rdw_stream_need(RdwStream& s, int64_t pos, int lane) { rdw_stream_range(s, pos, pos + 4, lane); }
+
+// The 4 header bytes at pos (in the ring; the second dword wraps at the ring's end).
 __device__ __forceinline__ uint32_t rdw_ring_header(const RdwStream& s, int64_t pos) {
     const uint32_t o = (uint32_t)((s.shift + pos) & (kRdwRing - 1));
-    const uint32_t* q = (const uint32_t*)(s.ring + (o & ~3u));
-    return __builtin_amdgcn_alignbyte(q[1], q[0], o & 3u);
+    const uint32_t d0 = o & ~3u, d1 = (d0 + 4u) & (kRdwRing - 1);
+    return __builtin_amdgcn_alignbyte(*(const uint32_t*)(s.ring + d1), *(const uint32_t*)(s.ring + d0), o & 3u);
 }
 
 // rdw_step with the header read from the ring (RecordHeaderParserRDW.getRecordMetadata + the
@@ -915,17 +686,284 @@ __device__ __forceinline__ RdwStep rdw_step_ring(const RdwArgs& a, RdwStream& s,
     return r;
 }
 
-// The chain from pos to the first header at or past end, staging (offset, length) of the valid
-// records at so / sl [0, cap) in rows of 64 (records past cap are counted, not kept).
-__device__ RdwWalk rdw_walk_wave(const RdwArgs& a, RdwStream& s, int64_t pos, int64_t end, int64_t* so, int32_t* sl,
+// wave-uniform 64-bit value (SGPR pair): the walk's positions and lengths stay scalar
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)v));
+}
+
+// Staging of a walk: the lane that keeps record `count` of the current row of 64 (payload offset
+// relative to the walk's entry, 32 bits; length), stored as a row when it fills.
+struct RdwStage {
+    uint32_t* so;
+    int32_t* sl;
+    uint32_t cap;            // (uniform: row bases scalar, the row stores take the saddr form)
+    uint32_t count, my_off;
+    int32_t my_len;
+    __device__ __forceinline__ void push(uint32_t off, int32_t len, int lane) {
+        if ((uint32_t)lane == (count & 63u)) { my_off = off; my_len = len; }
+        count++;
+        if ((count & 63u) == 0 && count <= cap) {
+            (gp(so) + (count - 64))[lane] = my_off;
+            (gp(sl) + (count - 64))[lane] = my_len;
+        }
+    }
+    __device__ __forceinline__ void finish(int lane) {
+        const uint32_t done = count & ~63u;
+        if ((uint32_t)lane < (count & 63u) && done + (uint32_t)lane < cap) {
+            (gp(so) + done)[lane] = my_off;
+            (gp(sl) + done)[lane] = my_len;
+        }
+    }
+};
+
+// Ordinary headers from rp (relative to base) while rp < lim: the header from the ring made
+// wave-uniform (readfirstlane), so position and length arithmetic is 32-bit scalar and a record costs
+// a few vector instructions (the LDS read, the lane that keeps it).  With the generic step per header
+// (vector compares and branches on vector values) C4's 150 M headers took 11.4 G VALU instructions,
+// 24 ms (profiles/r03_a).  Returns false at a length the reference rejects (rp left at its header).
+template <bool kBE>
+__device__ __forceinline__ bool rdw_fast_run(const RdwArgs& a, RdwStream& s, int64_t base, int32_t& rp, int32_t lim,
+                                             int32_t in_left, uint32_t rel0, RdwStage& sg, int lane) {
+    const int32_t adj = a.p.adjustment;
+    while (rp < lim) {
+        rdw_stream_need(s, base + rp, lane);
+        const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)rdw_ring_header(s, base + rp));
+        const int32_t rlen = (kBE ? (int32_t)(((h & 0xFFu) << 8) | ((h >> 8) & 0xFFu)) : (int32_t)(h >> 16)) + adj;
+        if (rlen <= 0 || rlen > 100 * 1024 * 1024) return false;
+        const int32_t fo = rp + 4;
+        const int32_t rem = in_left - fo;
+        const int32_t got = rlen < rem ? rlen : rem;
+        sg.push(rel0 + (uint32_t)fo, got, lane);
+        rp = fo + got;
+    }
+    return true;
+}
+
+// The chain from pos to the first header at or past end, staging (offset relative to pos, length)
+// of the valid records at so / sl [0, cap) in rows of 64 (records past cap are counted, not kept).
+// Ordinary headers (not the file header record, not in the footer, 4 header bytes in the input)
+// take rdw_fast_run; the others the generic step.
+__device__ RdwWalk rdw_walk_wave(const RdwArgs& a, RdwStream& s, int64_t pos, int64_t end, uint32_t* so, int32_t* sl,
                                  int64_t cap, int lane) {
     RdwWalk w{pos, 0, -1};
+    pos = uni64(pos);
+    end = uni64(end);
     if (pos < 0) { w.exit = pos; return w; }
+    const int64_t entry = pos;
     if (pos < end) rdw_stream_start(s, (s.shift + pos) >> 10, lane);
-    int64_t my_off = 0;
-    int32_t my_len = 0;
+    RdwStage sg{so, sl, (uint32_t)(cap < 0x7fffffffll ? cap : 0x7fffffffll), 0u, 0u, 0};
+    // ordinary headers: pos >= fast_lo (past a file header record at 0) and pos < fast_hi (4 header
+    // bytes in the input, the payload start before the footer: n - (pos + 4) > footer)
+    const int64_t fast_lo = a.p.file_header_bytes > 4 ? 1 : 0;
+    const int64_t fast_hi = a.n_bytes - 4 - (a.p.file_footer_bytes > 0 ? (int64_t)a.p.file_footer_bytes : 0);
+    while (pos < end) {
+        if (pos >= fast_lo && pos < fast_hi) {
+            // 32-bit positions relative to the run's start: scalar compares (no 64-bit SALU compare)
+            const int64_t base = pos;
+            const int64_t lim64 = (end < fast_hi ? end : fast_hi) - base;
+            const int32_t lim = (int32_t)(lim64 < 0x40000000ll ? lim64 : 0x40000000ll);
+            const int64_t in64 = a.n_bytes - base;
+            const int32_t in_left = (int32_t)(in64 < 0x7fff0000ll ? in64 : 0x7fff0000ll);
+            int32_t rp = 0;
+            const uint32_t rel0 = (uint32_t)(base - entry);
+            const bool ok = a.p.big_endian ? rdw_fast_run<true>(a, s, base, rp, lim, in_left, rel0, sg, lane)
+                                           : rdw_fast_run<false>(a, s, base, rp, lim, in_left, rel0, sg, lane);
+            pos = base + rp;
+            if (ok) continue;
+        }
+        const RdwStep st = rdw_step_ring(a, s, pos, lane);
+        if (st.err) {
+            w.err = ((pos + 4) << 2) | (st.err == -2 ? 2 : 3);   // reported at the payload offset
+            w.exit = -2;
+            w.count = sg.count;
+            return w;
+        }
+        if (st.stop) { pos = st.next; break; }
+        if (st.valid) sg.push((uint32_t)(st.off - entry), st.len, lane);
+        pos = uni64(st.next);
+    }
+    sg.finish(lane);
+    w.exit = pos;
+    w.count = sg.count;
+    return w;
+}
+
+// ---- the walk over lane windows (dense records) ----
+// A wave walks its chunk in windows of 2 KiB from the chain position P (a header): lane i owns
+// [P + 32 i, P + 32 i + 32).  Every lane speculates the first header of its span (lane 0: P) -- the
+// first strict candidate (the two non-length RDW bytes zero) whose next two hops are plausible --
+// and walks from it to its span's end (headers read from the LDS ring): exit y_i and count c_i.  A
+// lane without a candidate assumes the chain jumps over its span.  Resolution: the true position
+// entering lane i is the exit of the last lane before it that holds a header (a ballot and a
+// shuffle); lanes whose assumption fails re-walk (or become jumps), until none fails.  Then the
+// counts are scanned over the wave and every lane walks its span once more, staging its records at
+// their indices.  Per 2 KiB about two hundred wave instructions instead of a serial wave-uniform
+// step per header (whose scalar instructions bound C4's framing: ~22 SALU per header, one SALU per
+// cycle per CU).
+constexpr int kLaneSpan = 32;
+constexpr int kLaneWin = kWave * kLaneSpan;   // 2 KiB
+
+// header at relative position rp (data position base + rp), from the ring
+__device__ __forceinline__ int32_t rdw_lane_len(const RdwArgs& a, const RdwStream& s, int64_t base, int32_t rp,
+                                                uint32_t& h) {
+    h = rdw_ring_header(s, base + rp);
+    return (a.p.big_endian ? (int32_t)(((h & 0xFFu) << 8) | ((h >> 8) & 0xFFu)) : (int32_t)(h >> 16)) + a.p.adjustment;
+}
+
+__device__ __forceinline__ bool rdw_lane_strict(const RdwArgs& a, uint32_t h, int32_t rl) {
+    return rl > 0 && rl <= 100 * 1024 * 1024 && (a.p.big_endian ? (h >> 16) : (h & 0xFFFFu)) == 0;
+}
+
+// Walk a lane's span from rp while rp < r1: records counted, exit position, first error (relative
+// position of the header, or -1).  kStore: stage record k at so / sl[idx + k] (idx < cap).
+template <bool kStore>
+__device__ __forceinline__ int32_t rdw_lane_walk(const RdwArgs& a, const RdwStream& s, int64_t base, int32_t rp, int32_t r1,
+                                                 int32_t in_left, uint32_t& cnt, int32_t& err, uint32_t rel0,
+                                                 uint32_t* so, int32_t* sl, uint32_t idx, uint32_t cap) {
+    cnt = 0;
+    err = -1;
+    while (rp < r1) {
+        uint32_t h;
+        const int32_t rl = rdw_lane_len(a, s, base, rp, h);
+        if (rl <= 0 || rl > 100 * 1024 * 1024) { err = rp; break; }
+        const int32_t fo = rp + 4;
+        const int32_t rem = in_left - fo;
+        const int32_t got = rl < rem ? rl : rem;
+        if (kStore && idx + cnt < cap) {
+            gp(so)[idx + cnt] = rel0 + (uint32_t)fo;
+            gp(sl)[idx + cnt] = got;
+        }
+        cnt++;
+        rp = fo + got;
+    }
+    return rp;
+}
+
+// The lanes' parallel walk of one window from P = base (relative positions, every header in
+// [base, base + kLaneWin) an ordinary one; lim = min(kLaneWin, end - base)).  Returns the exit
+// (relative), adds the records to `count` (staged from index count), err: the relative position of
+// a rejected header (-1 none) -- records before it are counted and staged.
+__device__ int32_t rdw_lane_window(const RdwArgs& a, const RdwStream& s, int64_t base, int32_t lim, int32_t in_left,
+                                   int32_t resident, uint32_t rel0, uint32_t* so, int32_t* sl, uint32_t cap,
+                                   uint32_t& count, int32_t& err, int lane) {
+    const int32_t r0 = lane * kLaneSpan;
+    const int32_t r1 = r0 + kLaneSpan < lim ? r0 + kLaneSpan : lim;
+    const bool live = r0 < lim;
+    // speculation: the first strict candidate of the span with two plausible hops
+    int32_t e = -1;
+    if (lane == 0) {
+        e = 0;
+    } else if (live) {
+        const int32_t off = a.p.big_endian ? 2 : 0;   // zero pair inside a header
+        const uint32_t o0 = (uint32_t)((s.shift + base + r0 + off) & (kRdwRing - 1));
+        const uint32_t a16 = o0 & ~15u, m = o0 & 15u;
+        uint32_t zb[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const u32x4 v = *(const u32x4*)(s.ring + ((a16 + 16u * j) & (kRdwRing - 1)));
+            zb[j] = zero_bytes4(v.x) | zero_bytes4(v.y) << 4 | zero_bytes4(v.z) << 8 | zero_bytes4(v.w) << 12;
+        }
+        const uint64_t z = (uint64_t)zb[0] | (uint64_t)zb[1] << 16 | (uint64_t)zb[2] << 32;
+        uint32_t pairs = (uint32_t)(((z & (z >> 1)) >> m) & ((1ull << (r1 - r0)) - 1));
+        while (pairs) {
+            const int32_t q = r0 + (int32_t)__builtin_ctz(pairs);
+            pairs &= pairs - 1;
+            uint32_t h;
+            int32_t rl = rdw_lane_len(a, s, base, q, h);
+            if (!rdw_lane_strict(a, h, rl)) continue;
+            bool ok = true;
+            int32_t p = q + 4 + rl;
+            for (int hop = 0; hop < 2 && ok; hop++) {   // hops past the resident bytes: not contradicted
+                if (p + 4 > resident || p + 4 > in_left) break;
+                rl = rdw_lane_len(a, s, base, p, h);
+                ok = rdw_lane_strict(a, h, rl);
+                p += 4 + rl;
+            }
+            if (ok) { e = q; break; }
+        }
+    }
+    // speculative walks
+    uint32_t c = 0;
+    int32_t er = -1;
+    int32_t y = e >= 0 ? rdw_lane_walk<false>(a, s, base, e, r1, in_left, c, er, 0u, nullptr, nullptr, 0u, 0u) : 0;
+    // resolution: the position entering lane i is the exit of the last holding lane before it
+    for (int round = 0; round <= kWave; round++) {
+        const uint64_t hold = __ballot(e >= 0 && live);
+        const uint64_t below = lane ? (hold & ((1ull << lane) - 1)) : 0ull;
+        const int src = below ? 63 - __builtin_clzll(below) : 0;
+        const int32_t x = __shfl(er >= 0 ? 0x7fffffff : y, src, kWave);   // (an error ends the chain)
+        bool bad = false;
+        if (lane > 0 && live) {
+            if (e >= 0 && x != e) {            // a false candidate (or a chain entering elsewhere)
+                bad = true;
+                e = x < r1 ? x : -1;
+            } else if (e < 0 && x < r1) {      // a header the speculation missed
+                bad = true;
+                e = x;
+            }
+            if (bad && e >= 0) y = rdw_lane_walk<false>(a, s, base, e, r1, in_left, c, er, 0u, nullptr, nullptr, 0u, 0u);
+            if (bad && e < 0) { c = 0; er = -1; }
+        }
+        if (!__ballot(bad)) break;
+    }
+    // the first error of the chain (holding lanes only) ends the window: lanes after it keep nothing
+    const uint64_t errs = __ballot(e >= 0 && live && er >= 0);
+    const int first_err = errs ? __builtin_ctzll(errs) : kWave;
+    const bool keep = e >= 0 && live && lane <= first_err;
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32(keep ? c : 0u, lane, tot);
+    if (keep) {
+        uint32_t c2;
+        int32_t er2;
+        rdw_lane_walk<true>(a, s, base, e, r1, in_left, c2, er2, rel0, so, sl, count + ex, cap);
+    }
+    count += tot;
+    const uint64_t hold = __ballot(keep);
+    const int last = 63 - __builtin_clzll(hold | 1ull);
+    err = first_err < kWave ? __shfl(er, first_err, kWave) : -1;
+    return __shfl(y, last, kWave);
+}
+
+// The chain from pos to the first header at or past end: windows of ordinary headers through the
+// lanes (rdw_lane_window), the file header record and footer records through the generic step.
+// Stages (offset relative to pos, length) of the valid records at so / sl [0, cap).
+__device__ RdwWalk rdw_walk_lanes(const RdwArgs& a, RdwStream& s, int64_t pos, int64_t end, uint32_t* so, int32_t* sl,
+                                  int64_t cap64, int lane) {
+    RdwWalk w{pos, 0, -1};
+    pos = uni64(pos);
+    end = uni64(end);
+    if (pos < 0) { w.exit = pos; return w; }
+    const int64_t entry = pos;
+    const uint32_t cap = (uint32_t)(cap64 < 0x7fffffffll ? cap64 : 0x7fffffffll);
+    const int64_t fast_lo = a.p.file_header_bytes > 4 ? 1 : 0;
+    const int64_t fast_hi = a.n_bytes - 4 - (a.p.file_footer_bytes > 0 ? (int64_t)a.p.file_footer_bytes : 0);
     uint32_t count = 0;
     while (pos < end) {
+        if (pos >= fast_lo && pos < fast_hi) {
+            // every header of [pos, pos + lim) is an ordinary one (lim clipped at fast_hi and the chunk end)
+            const int64_t lim64 = (end < fast_hi ? end : fast_hi) - pos;
+            const int32_t lim = (int32_t)(lim64 < kLaneWin ? lim64 : kLaneWin);
+            const int64_t in64 = a.n_bytes - pos;
+            const int32_t in_left = (int32_t)(in64 < 0x7fff0000ll ? in64 : 0x7fff0000ll);
+            const int64_t res64 = pos + 3 * 1024 < a.n_bytes ? pos + 3 * 1024 : a.n_bytes;
+            rdw_stream_range(s, pos, res64 > pos + 4 ? res64 : pos + 4, lane);
+            const int32_t resident = (int32_t)(res64 - pos);
+            int32_t err;
+            const int32_t x = rdw_lane_window(a, s, pos, lim, in_left, resident, (uint32_t)(pos - entry), so, sl, cap,
+                                              count, err, lane);
+            if (err >= 0) {
+                w.err = ((pos + err + 4) << 2) | 2;   // (the header's length: <= 0 or > 100 MiB; the code below)
+                const int64_t ep = uni64(pos + err);
+                const RdwStep st = rdw_step_ring(a, s, ep, lane);
+                w.err = ((ep + 4) << 2) | (st.err == -3 ? 3 : 2);
+                w.exit = -2;
+                w.count = count;
+                return w;
+            }
+            pos = uni64(pos + (int64_t)x);
+            continue;
+        }
         const RdwStep st = rdw_step_ring(a, s, pos, lane);
         if (st.err) {
             w.err = ((pos + 4) << 2) | (st.err == -2 ? 2 : 3);   // reported at the payload offset
@@ -935,19 +973,13 @@ __device__ RdwWalk rdw_walk_wave(const RdwArgs& a, RdwStream& s, int64_t pos, in
         }
         if (st.stop) { pos = st.next; break; }
         if (st.valid) {
-            if ((uint32_t)lane == (count & 63u)) { my_off = st.off; my_len = st.len; }
-            count++;
-            if ((count & 63u) == 0 && (int64_t)count <= cap) {
-                so[count - 64 + lane] = my_off;
-                sl[count - 64 + lane] = my_len;
+            if (lane == 0 && count < cap) {
+                gp(so)[count] = (uint32_t)(st.off - entry);
+                gp(sl)[count] = st.len;
             }
+            count++;
         }
-        pos = st.next;
-    }
-    const uint32_t done = count & ~63u;
-    if ((uint32_t)lane < (count & 63u) && (int64_t)(done + lane) < cap) {
-        so[done + lane] = my_off;
-        sl[done + lane] = my_len;
+        pos = uni64(st.next);
     }
     w.exit = pos;
     w.count = count;
@@ -1002,8 +1034,9 @@ __device__ __forceinline__ RdwStream rdw_stream(const RdwArgs& a, uint8_t* ring)
     s.shift = (int64_t)(d & 15);
     s.limit = s.shift + a.n_bytes;
     s.ring = ring;
+    s.ring_lds = (uint32_t)(uintptr_t)ring;   // a generic LDS address: the LDS offset in its low 32 bits
     s.hi = 0;
-    s.nx0 = s.nx1 = make_uint4(0, 0, 0, 0);
+    s.ready = -1;
     return s;
 }
 
@@ -1028,8 +1061,8 @@ __global__ __launch_bounds__(kWave * kRdwWaves) void rdw_wave_kernel(RdwArgs a, 
             entry = ch.known ? ch.start : rdw_entry_wave(a, s, ch.start, ch.end, ch.range_end, lane);
             if (lane == 0) c.entry[k] = entry;
         }
-        const RdwWalk w = rdw_walk_wave(a, s, entry, ch.end, c.stage_off + k * c.stage_cap, c.stage_len + k * c.stage_cap,
-                                        c.stage_cap, lane);
+        const RdwWalk w = rdw_walk_lanes(a, s, entry, ch.end, c.stage_off + k * c.stage_cap, c.stage_len + k * c.stage_cap,
+                                         c.stage_cap, lane);
         if (lane == 0) {
             c.exit_out[k] = w.exit;
             c.count[k] = w.count;
@@ -1059,10 +1092,11 @@ __global__ __launch_bounds__(kWave * kRdwPlaceWaves) void rdw_place_kernel(RdwAr
         if (lane == 0) rdw_walk<2>(a, c.entry[k], rdw_chunk(c, k).end, rec_off, rec_len, b, cap);
         return;
     }
-    const int64_t* so = c.stage_off + k * c.stage_cap;
+    const uint32_t* so = c.stage_off + k * c.stage_cap;
     const int32_t* sl = c.stage_len + k * c.stage_cap;
+    const int64_t e0 = c.entry[k];   // staged offsets are relative to the walk's entry
     for (int64_t j = lane; j < n && b + j < cap; j += kWave) {
-        rec_off[b + j] = so[j];
+        rec_off[b + j] = e0 + so[j];
         rec_len[b + j] = sl[j];
     }
 }

@@ -1,0 +1,118 @@
+"""The copybook-specialised kernels are compiled at run time by hipRTC (cobrix_amd/csrc/cbx_jit.h),
+whose headers differ from hipcc's (no <cstdint> extras such as uintptr_t, no hip_runtime.h): a device
+header that only hipcc accepts makes every specialised kernel fall back to the table-driven one on
+the GPU.  These CPU tests compile, through hipRTC (no device needed), sources of the shapes
+jit_source / jit_list_source generate -- the record kernel in the three string layouts and in the
+Utf8 count mode, and the list kernel -- against the headers the library bundles."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "cobrix_amd", "csrc")
+HEADERS = [("cobrix_hip.h", os.path.join(ROOT, "include", "cobrix_hip.h"))] + [
+    (n, os.path.join(CSRC, n)) for n in ("cbx_decode.h", "cbx_internal.h", "cbx_device.h", "cbx_list.h")]
+
+
+def _hiprtc():
+    for p in ("/opt/rocm/lib/libhiprtc.so", "libhiprtc.so"):
+        try:
+            return ctypes.CDLL(p)
+        except OSError:
+            continue
+    pytest.skip("libhiprtc not available")
+
+
+def _compile(src: str) -> str:
+    lib = _hiprtc()
+    texts = [open(p).read().encode() for _, p in HEADERS]
+    names = [n.encode() for n, _ in HEADERS]
+    prog = ctypes.c_void_p()
+    H = (ctypes.c_char_p * len(texts))(*texts)
+    N = (ctypes.c_char_p * len(names))(*names)
+    assert lib.hiprtcCreateProgram(ctypes.byref(prog), src.encode(), b"cbx_jit.hip", len(texts), H, N) == 0
+    opts = [b"--offload-arch=gfx950", b"-O3", b"-std=c++17"]
+    rc = lib.hiprtcCompileProgram(prog, len(opts), (ctypes.c_char_p * len(opts))(*opts))
+    n = ctypes.c_size_t()
+    lib.hiprtcGetProgramLogSize(prog, ctypes.byref(n))
+    log = ctypes.create_string_buffer(n.value + 1)
+    lib.hiprtcGetProgramLog(prog, log)
+    lib.hiprtcDestroyProgram(ctypes.byref(prog))
+    return "" if rc == 0 else (log.value.decode(errors="replace") or f"hiprtc error {rc}")
+
+
+def _record_kernel(layout: int, count: bool, loop: bool) -> str:
+    view = "true" if layout == 1 else "false"
+    ops = [f"{{{20 * i},20,1,4,0,2,{i},0,{i},-1,{{0,0,0,0}},{{0,0,0,0}},0}}" for i in range(3)]
+    if loop:
+        body = f"    for (int i = 0; i < 3; i++) str_element<{view}>(a, ldc(a.sops + i), a.sops + i, ldc(a.scall + i), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane);\n"
+    else:
+        body = "".join(f"    {{ constexpr StrOp op = {o}; str_element<{view}>(a, op, a.sops + {i}, ldc(a.scall + {i}), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane); }}\n"
+                       for i, o in enumerate(ops))
+    lut = ("  WaveLds l = wave_lds(a, smem + 1024, wid);\n  l.lut = (uint32_t*)smem;\n"
+           "  for (int i = threadIdx.x; i < 256; i += blockDim.x) { const uint32_t e = a.lut[i]; l.lut[i] = e; l.lut[256 + i] = count_lut_entry(e); }\n"
+           if count else
+           "  const WaveLds l = wave_lds(a, smem, wid);\n  for (int i = threadIdx.x; i < 256; i += blockDim.x) l.lut[i] = a.lut[i];\n")
+    sig = ("(const KernelArgs& a, const TileCtx& t, const uint8_t* img,\n"
+           "      uint32_t rec_addr, const WaveLds& l, int lane, Stamps& st) {\n")
+    return (f"#define CBX_STR_LAYOUT {layout}\n#define CBX_MODE {1 if count else 0}\n" + ("#define CBX_COUNT_LUT 1\n" if count else "") +
+            "#include \"cbx_device.h\"\nnamespace cbx {\nstruct JitBody {\n  static constexpr int kWords = 0;\n  DirectSink vw;\n"
+            "  __device__ __forceinline__ void begin(int64_t) {}\n"
+            "  __device__ __forceinline__ void flush(const KernelArgs&, int64_t, int) {}\n"
+            "  __device__ __forceinline__ void pre" + sig + body + "  }\n"
+            "  __device__ __forceinline__ void post" + sig + "  }\n};\n}  // namespace cbx\n"
+            "extern \"C\" __global__ __launch_bounds__(cbx::kWave * cbx::kWavesPerBlock) void k(cbx::KernelArgs a) {\n"
+            "  using namespace cbx;\n  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+            "  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);\n  const int lane = threadIdx.x % kWave;\n"
+            + lut + "  __syncthreads();\n  int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid;\n"
+            "  const int64_t tstep = (int64_t)gridDim.x * kWavesPerBlock;\n"
+            "  contig_loop<13, 0, false>(a, l, tile, tstep, lane, JitBody{});\n}\n")
+
+
+LIST_KERNEL = """#define CBX_STR_LAYOUT 0
+#define CBX_MODE 0
+#include "cbx_list.h"
+namespace cbx {
+struct JitListBody {
+  __device__ __forceinline__ bool group(const KernelArgs& a, int ai, const uint8_t* e0, const ListRec& r, int g0,
+                                        int gn, int lane, bool& deferred) {
+    const int kmax = ((g0 + gn) * kWave < r.rlen ? (g0 + gn) * kWave : r.rlen) - 1;
+    const int lim = r.ravail < r.rsafe ? r.ravail : r.rsafe;
+    switch (ai) {
+    case 0: {
+      constexpr NumOp op0 = {66,3,4,1,6,1,32,0,0,5,0,-1,0,0,0xffffffffull,0x0ull,0x1ull,0x1ull,0x0ull,0x1ull,{0,0,0,0},{0,0,0,0}};
+      if (a.start_off + op0.eo + op0.size + kmax * 8 > lim) return false;
+      const DevColumn c0 = ldc(a.cols + op0.column);
+      for (int st = 0; st < gn; st++) {
+        const int cb = (g0 + st) * kWave;
+        const uint8_t* el = e0 + (st * kWave + lane) * 8;
+        list_jit_field<3, 4>(op0, c0, el + 4, r.rstart + cb, cb + lane < r.rlen, lane, deferred);
+      }
+      return true;
+    }
+    }
+    return false;
+  }
+};
+}  // namespace cbx
+extern "C" __global__ __launch_bounds__(cbx::kWave * cbx::kListWaves) void cbx_jit_list(cbx::KernelArgs a,
+    const CBX_CONST cbx::ListOp* lops, int32_t n_lops) {
+  cbx::JitListBody body;
+  cbx::list_run<false>(a, lops, n_lops, body);
+}
+"""
+
+
+@pytest.mark.parametrize("layout,count,loop", [(0, False, False), (1, False, False), (2, False, False), (2, True, False),
+                                               (0, False, True)])
+def test_record_kernel_compiles_with_hiprtc(layout, count, loop):
+    err = _compile(_record_kernel(layout, count, loop))
+    assert not err, err[:3000]
+
+
+def test_list_kernel_compiles_with_hiprtc():
+    err = _compile(LIST_KERNEL)
+    assert not err, err[:3000]
