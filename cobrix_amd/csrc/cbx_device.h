@@ -838,22 +838,26 @@ __device__ __forceinline__ void lds_to_global_chunks(const uint8_t* s, CBX_GLOBA
 // OR-ed as shifted dwords into the zeroed staging at their final offsets (ds_or: neighbouring lanes
 // share boundary dwords) and copied out in whole 16-byte chunks.  Per byte of a value two LDS byte
 // stores into the lane slot instead of two stores at shared tile positions with dump selects
-// (those cost a third of the SYNSTR200 decode: 4.2 of 15 ms, CBX_DIAG=8 A/B).
-__device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
-                                              const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
-                                              const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
-                                              uint8_t* s_str, int lane) {
+// (those cost a third of the SYNSTR200 decode: 4.2 of 15 ms, CBX_DIAG=8 A/B).  str_utf8_two runs
+// the phases for two elements at once (one scan of 16-bit halves, one wait per phase).
+
+// The lane's value of element op (composed; length, 0 when the record lacks it).
+__device__ __forceinline__ int utf8_compose(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp, const TileCtx& t,
+                                            const int32_t* s_cnt, const uint8_t* src, uint32_t rec_addr,
+                                            const uint32_t* s_lut, uint8_t* s_str, int lane, bool& ok, u32x4 (&q)[kStrNC]) {
     bool el = t.active && (op.segment < 0 || op.segment == t.seg);
     if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
     const int o = a.start_off + op.eo;
-    const bool ok = el && o <= t.avail;
+    ok = el && o <= t.avail;
     const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
-    u32x4 q[kStrNC];
-    int len = str_lane_compose(op.kind, op.trim, op.pad, op.size, op.eo, n, ok, src, rec_addr, s_lut, s_str, lane, q);
-    len = ok ? len : 0;
-    gp(c.validity)[t.tile] = __ballot(ok);
-    uint32_t tot;
-    const uint32_t ex = wave_excl_scan32((uint32_t)len, lane, tot);
+    const int len = str_lane_compose(op.kind, op.trim, op.pad, op.size, op.eo, n, ok, src, rec_addr, s_lut, s_str, lane, q);
+    return ok ? len : 0;
+}
+
+// The element's int32 offsets (the tile's place from the count pass's scan) and the slot's size;
+// returns the tile's destination, or null when the region (or an int32 offset) overflows.
+__device__ __forceinline__ CBX_GLOBAL uint8_t* utf8_offsets(const KernelArgs& a, const StrCall& c, const TileCtx& t, uint32_t ex,
+                                                            int len, uint32_t tot, int lane) {
     const int64_t base = c.excl[t.tile] - c.excl[0];   // the tile's place in the slot's region
     CBX_GLOBAL int32_t* offs = gp((int32_t*)c.local);
     (offs + t.tile * kWave)[lane] = (int32_t)(base + ex);
@@ -861,21 +865,23 @@ __device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& 
         offs[a.n_rec] = (int32_t)(base + ex + len);
         if (c.size) *gp(c.size) = base + ex + len;
     }
-    if (base + tot > c.tile_cap || base + tot > 0x7fffffffll) {   // the region (or an int32 offset) overflows
+    if (base + tot > c.tile_cap || base + tot > 0x7fffffffll) {
         if (lane == 0) atomicOr(a.status, 1);
-        return;
+        return nullptr;
     }
-    CBX_GLOBAL uint8_t* dst = gp(c.scratch + base);
-    const uint32_t mis = (uint32_t)((uint64_t)(size_t)dst & 15u);
-    const int nbytes = op.size * op.pad;                  // the value's bound (compile-time in the specialised kernel)
+    return gp(c.scratch + base);
+}
+
+__device__ __forceinline__ void utf8_zero(uint8_t* s, uint32_t n, int lane) {
+    for (uint32_t z = (uint32_t)lane; 16 * z < n; z += kWave) *(u32x4*)(s + 16 * z) = u32x4{0u, 0u, 0u, 0u};
+}
+
+// The lane's len bytes (q) OR-ed into the zeroed staging s at byte pos.
+__device__ __forceinline__ void utf8_or(uint8_t* s, uint32_t pos, int len, int nbytes, const u32x4 (&q)[kStrNC]) {
     constexpr int kNW = (kStrFastBytes * 3 + 3) / 4 + 1;  // shifted dwords of the largest value
     const int nw = (nbytes + 3) / 4 + 1;
-    wave_sync_lds();   // the lane slots are read back
-    for (uint32_t z = (uint32_t)lane; 16 * z < mis + tot + 16; z += kWave) *(u32x4*)(s_str + 16 * z) = u32x4{0u, 0u, 0u, 0u};
-    wave_sync_lds();
-    const uint32_t pos = mis + ex;
     const uint32_t sh = pos & 3u;
-    lds_u32_t* d = (lds_u32_t*)(s_str + (pos & ~3u));
+    lds_u32_t* d = (lds_u32_t*)(s + (pos & ~3u));
     uint32_t prev = 0;
 #pragma unroll
     for (int k = 0; k < kNW; k++) {
@@ -892,9 +898,75 @@ __device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& 
             prev = w;
         }
     }
+}
+
+__device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
+                                              const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
+                                              const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
+                                              uint8_t* s_str, int lane) {
+    bool ok;
+    u32x4 q[kStrNC];
+    const int len = utf8_compose(a, op, opp, t, s_cnt, src, rec_addr, s_lut, s_str, lane, ok, q);
+    gp(c.validity)[t.tile] = __ballot(ok);
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32((uint32_t)len, lane, tot);
+    CBX_GLOBAL uint8_t* dst = utf8_offsets(a, c, t, ex, len, tot, lane);
+    if (!dst) return;
+    const uint32_t mis = (uint32_t)((uint64_t)(size_t)dst & 15u);
+    wave_sync_lds();   // the lane slots are read back
+    utf8_zero(s_str, mis + tot + 16, lane);
+    wave_sync_lds();
+    utf8_or(s_str, mis + ex, len, op.size * op.pad, q);
     wave_sync_lds();
     if (!(CBX_DIAG & 16)) lds_to_global_chunks(s_str, dst - mis, mis, tot, lane);
     wave_sync_lds();   // the staging area is reused by the next element
+}
+
+// Bytes of the staging the two-element form needs: the lane slots, or both tiles' regions (a
+// region: the tile's bytes + 16 of alignment + the last lane's shifted-dword overhang).
+__host__ __device__ constexpr int utf8_two_stage(int nbytes_a, int nbytes_b, int slot) {
+    return (kWave * nbytes_a + 48 + 15) / 16 * 16 + kWave * nbytes_b + 48 > slot
+               ? (kWave * nbytes_a + 48 + 15) / 16 * 16 + kWave * nbytes_b + 48 : slot;
+}
+// Whether two register-path Utf8 elements (size, widest UTF-8 byte count) can be decoded together
+// (the plan sizes the staging for any such pair, cbx_capi.hip).
+__host__ __device__ constexpr bool utf8_pair_fits(int size_a, int w_a, int size_b, int w_b) {
+    return utf8_two_stage(size_a * w_a, size_b * w_b,
+                          kWave * (str_lane_slot(size_a, w_a) > str_lane_slot(size_b, w_b) ? str_lane_slot(size_a, w_a)
+                                                                                            : str_lane_slot(size_b, w_b))) <=
+           kStrPairStageBytes;
+}
+
+// Two register-path elements of the tile (the specialised kernel pairs consecutive ones): composed
+// one after the other through the same lane slots, then one scan of 16-bit halves, one zeroing of
+// both regions, the ORs of both, the copy-outs of both -- three waits for the pair instead of six.
+__device__ __forceinline__ void str_utf8_two(const KernelArgs& a, const StrOp& A, const CBX_CONST StrOp* oppA, const StrCall& ca,
+                                             const StrOp& B, const CBX_CONST StrOp* oppB, const StrCall& cb,
+                                             const TileCtx& t, const int32_t* s_cnt, const uint8_t* src, uint32_t rec_addr,
+                                             const uint32_t* s_lut, uint8_t* s_str, int lane) {
+    bool oka, okb;
+    u32x4 qa[kStrNC], qb[kStrNC];
+    const int la = utf8_compose(a, A, oppA, t, s_cnt, src, rec_addr, s_lut, s_str, lane, oka, qa);
+    const int lb = utf8_compose(a, B, oppB, t, s_cnt, src, rec_addr, s_lut, s_str, lane, okb, qb);
+    gp(ca.validity)[t.tile] = __ballot(oka);
+    gp(cb.validity)[t.tile] = __ballot(okb);
+    uint32_t tot2;
+    const uint32_t ex2 = wave_excl_scan32((uint32_t)la | ((uint32_t)lb << 16), lane, tot2);   // a tile's total < 64 KiB
+    const uint32_t exa = ex2 & 0xFFFFu, exb = ex2 >> 16, tota = tot2 & 0xFFFFu, totb = tot2 >> 16;
+    CBX_GLOBAL uint8_t* da = utf8_offsets(a, ca, t, exa, la, tota, lane);
+    CBX_GLOBAL uint8_t* db = utf8_offsets(a, cb, t, exb, lb, totb, lane);
+    const uint32_t ma = da ? (uint32_t)((uint64_t)(size_t)da & 15u) : 0u, mb = db ? (uint32_t)((uint64_t)(size_t)db & 15u) : 0u;
+    const uint32_t rb = (uint32_t)((kWave * A.size * A.pad + 48 + 15) / 16 * 16);   // region B's start in the staging
+    wave_sync_lds();   // the lane slots are read back
+    utf8_zero(s_str, ma + tota + 16, lane);
+    utf8_zero(s_str + rb, mb + totb + 16, lane);
+    wave_sync_lds();
+    utf8_or(s_str, ma + exa, la, A.size * A.pad, qa);
+    utf8_or(s_str + rb, mb + exb, lb, B.size * B.pad, qb);
+    wave_sync_lds();
+    if (da) lds_to_global_chunks(s_str, da - ma, ma, tota, lane);
+    if (db) lds_to_global_chunks(s_str + rb, db - mb, mb, totb, lane);
+    wave_sync_lds();   // the staging area is reused by the next elements
 }
 
 // ---- Utf8 count pass (specialised kernels only: CBX_COUNT_LUT) ----

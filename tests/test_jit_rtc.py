@@ -44,10 +44,13 @@ def _compile(src: str) -> str:
     return "" if rc == 0 else (log.value.decode(errors="replace") or f"hiprtc error {rc}")
 
 
-def _record_kernel(layout: int, count: bool, loop: bool) -> str:
+def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False) -> str:
     view = "true" if layout == 1 else "false"
     ops = [f"{{{20 * i},20,1,4,0,2,{i},0,{i},-1,{{0,0,0,0}},{{0,0,0,0}},0}}" for i in range(3)]
-    if loop:
+    if pair:
+        body = (f"    {{ constexpr StrOp opa = {ops[0]}; constexpr StrOp opb = {ops[1]}; str_utf8_two(a, opa, a.sops + 0, "
+                f"ldc(a.scall + 0), opb, a.sops + 1, ldc(a.scall + 1), t, l.cnt, img, rec_addr, l.lut, l.str, lane); }}\n")
+    elif loop:
         body = f"    for (int i = 0; i < 3; i++) str_element<{view}>(a, ldc(a.sops + i), a.sops + i, ldc(a.scall + i), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane);\n"
     else:
         body = "".join(f"    {{ constexpr StrOp op = {o}; str_element<{view}>(a, op, a.sops + {i}, ldc(a.scall + {i}), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane); }}\n"
@@ -106,10 +109,11 @@ extern "C" __global__ __launch_bounds__(cbx::kWave * cbx::kListWaves) void cbx_j
 """
 
 
-@pytest.mark.parametrize("layout,count,loop", [(0, False, False), (1, False, False), (2, False, False), (2, True, False),
-                                               (0, False, True)])
-def test_record_kernel_compiles_with_hiprtc(layout, count, loop):
-    err = _compile(_record_kernel(layout, count, loop))
+@pytest.mark.parametrize("layout,count,loop,pair", [(0, False, False, False), (1, False, False, False),
+                                                    (2, False, False, False), (2, True, False, False),
+                                                    (0, False, True, False), (2, False, False, True)])
+def test_record_kernel_compiles_with_hiprtc(layout, count, loop, pair):
+    err = _compile(_record_kernel(layout, count, loop, pair))
     assert not err, err[:3000]
 
 
