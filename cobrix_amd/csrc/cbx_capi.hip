@@ -471,25 +471,15 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     build_contig(P);
     build_windowed(P, wmax);
     // string staging per wave: the byte-loop / large-string paths stage a tile's payload (kWave *
-    // size * max_utf8, capped); the view layout's register path composes multi-byte code pages in
-    // lane slots (str_view_fast) and single-byte ones in registers (no LDS at all)
-    int slots = 0, pair_stage = 0;
-    if (P->view) P->str_stage = 0;
+    // size * max_utf8, capped); the register path of the view and Utf8 layouts (str_view_fast,
+    // str_utf8_fast) composes multi-byte code pages in lane slots and single-byte ones in registers
+    // (no LDS at all), and stores the values from registers
+    int slots = 0;
+    if (P->view || P->packed) P->str_stage = 0;
     for (const Field& d : P->dfields_h) {
         if (d.variant != V_STRING) continue;
         const bool fast = d.size <= kStrFastBytes && (d.kind == CBX_K_STRING || d.kind == CBX_K_STRING_ASCII);
-        if (P->packed && fast) {
-            // Arrow Utf8 register path (str_utf8_fast): the lane slots, then the tile's bytes at their
-            // final offsets (+ a chunk of alignment and the shifted dwords' overhang); two such
-            // elements decoded together (str_utf8_two) hold both tiles' regions
-            P->str_stage = std::max(P->str_stage, std::max(kWave * str_lane_slot(d.size, d.max_utf8),
-                                                           kWave * d.size * d.max_utf8 + 64));
-            if (utf8_pair_fits(d.size, d.max_utf8, d.size, d.max_utf8))
-                pair_stage = std::max(pair_stage, utf8_two_stage(d.size * d.max_utf8, d.size * d.max_utf8,
-                                                                 kWave * str_lane_slot(d.size, d.max_utf8)));
-            else
-                pair_stage = kStrPairStageBytes;   // (pairs of smaller elements still fit the cap)
-        } else if (P->view && fast) {
+        if ((P->view || P->packed) && fast) {
             // (env CBX_STR_NO_SHIFT: single-byte pages through the slots too -- A/B runs; the
             // specialised kernel then compiles the slot path for them, cbx_jit.h)
             if (d.max_utf8 > 1 || getenv("CBX_STR_NO_SHIFT")) slots = std::max(slots, kWave * str_lane_slot(d.size, d.max_utf8));
@@ -498,7 +488,7 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
             P->view_staged |= P->view;
         }
     }
-    P->str_stage = std::max(std::min(P->str_stage, kStrStageBytes), pair_stage);
+    P->str_stage = std::min(P->str_stage, kStrStageBytes);
     for (const cbx_field& f : P->hfields) {
         if (f.flags & CBX_F_LIST) continue;   // the list kernel reads those
         int64_t e = (int64_t)f.offset + f.size;

@@ -806,40 +806,15 @@ __device__ __forceinline__ void lds_dma_wait(int n) {
 }
 
 // ---- Utf8 decode of a register-path element (str_view 2, decode mode) ----
-typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
-
-// The tile's 16-byte chunks of a slot region from the LDS staging to global: staging byte
-// mis + j holds output byte j and the destination's chunk boundaries are the staging's (dst_a =
-// the 16-byte aligned address at or before the tile's first byte), so whole chunks go as aligned
-// 16-byte copies; the first and last chunk are shared with the neighbouring tiles: only their own
-// bytes, as byte stores.
-__device__ __forceinline__ void lds_to_global_chunks(const uint8_t* s, CBX_GLOBAL uint8_t* dst_a, uint32_t mis, uint32_t n,
-                                                     int lane) {
-    if (n == 0) return;
-    const uint32_t end = mis + n;
-    const uint32_t last = (end - 1) >> 4;   // last chunk
-    const uint32_t full0 = mis ? 1u : 0u, full1 = (end & 15u) ? last : last + 1;   // [full0, full1) whole chunks
-    for (uint32_t c = full0 + (uint32_t)lane; c < full1; c += kWave)
-        *(CBX_GLOBAL u32x4*)(dst_a + 16 * c) = *(const u32x4*)(s + 16 * c);
-    // edge bytes: chunk 0 from mis (when partial), the last chunk up to end (when partial)
-    if (mis) {
-        const uint32_t j = mis + (uint32_t)lane;
-        if (lane < 16 && j < 16 && j < end) dst_a[j] = s[j];
-    }
-    if ((end & 15u) && (last > 0 || !mis)) {
-        const uint32_t j = 16 * last + (uint32_t)lane;
-        if (lane < 16 && j < end && j >= mis) dst_a[j] = s[j];
-    }
-}
-
-// One register-path string element of the tile in the Arrow Utf8 layout: the value composed in the
-// lane's registers (str_lane_compose: single-byte pages in registers, multi-byte ones through the
-// lane's conflict-free LDS slot), the tile's exclusive scan of the lengths, then the lanes' bytes
-// OR-ed as shifted dwords into the zeroed staging at their final offsets (ds_or: neighbouring lanes
-// share boundary dwords) and copied out in whole 16-byte chunks.  Per byte of a value two LDS byte
-// stores into the lane slot instead of two stores at shared tile positions with dump selects
-// (those cost a third of the SYNSTR200 decode: 4.2 of 15 ms, CBX_DIAG=8 A/B).  str_utf8_two runs
-// the phases for two elements at once (one scan of 16-bit halves, one wait per phase).
+// The value is composed in the lane's registers exactly as in the view layout (str_lane_compose:
+// single-byte pages in registers, multi-byte ones through the lane's conflict-free LDS slot), the
+// tile's lengths are scanned, and every lane stores its own bytes at their final byte offset
+// straight from registers: the bytes up to the next 4-byte boundary and the bytes past the last
+// whole dword as byte stores (the neighbouring values own the rest of those dwords), the whole
+// dwords in between as 16 / 8 / 4-byte stores.  No LDS staging, no wave barrier.  (The earlier form
+// OR-ed the lanes' shifted dwords into a zeroed LDS staging and copied whole 16-byte chunks out:
+// ~130 VALU, 13 LDS instructions and three waits per element -- SYNSTR200 decode 10.75 ms,
+// profiles/r03_b.)  str_utf8_two runs two elements with one scan of 16-bit halves.
 
 // The lane's value of element op (composed; length, 0 when the record lacks it).
 __device__ __forceinline__ int utf8_compose(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp, const TileCtx& t,
@@ -872,32 +847,59 @@ __device__ __forceinline__ CBX_GLOBAL uint8_t* utf8_offsets(const KernelArgs& a,
     return gp(c.scratch + base);
 }
 
-__device__ __forceinline__ void utf8_zero(uint8_t* s, uint32_t n, int lane) {
-    for (uint32_t z = (uint32_t)lane; 16 * z < n; z += kWave) *(u32x4*)(s + 16 * z) = u32x4{0u, 0u, 0u, 0u};
-}
-
-// The lane's len bytes (q) OR-ed into the zeroed staging s at byte pos.
-__device__ __forceinline__ void utf8_or(uint8_t* s, uint32_t pos, int len, int nbytes, const u32x4 (&q)[kStrNC]) {
-    constexpr int kNW = (kStrFastBytes * 3 + 3) / 4 + 1;  // shifted dwords of the largest value
-    const int nw = (nbytes + 3) / 4 + 1;
-    const uint32_t sh = pos & 3u;
-    lds_u32_t* d = (lds_u32_t*)(s + (pos & ~3u));
-    uint32_t prev = 0;
+// The lane's len bytes (q, packed from byte 0; nbytes: the compile-time bound of len) to d at any
+// byte alignment.
+__device__ __forceinline__ void utf8_store_direct(CBX_GLOBAL uint8_t* d, int len, int nbytes, const u32x4 (&q)[kStrNC]) {
+    typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+    constexpr int kNW = 4 * kStrNC;
+    uint32_t w[kNW + 1];
+#pragma unroll
+    for (int k = 0; k < kStrNC; k++) {
+        w[4 * k] = q[k].x;
+        w[4 * k + 1] = q[k].y;
+        w[4 * k + 2] = q[k].z;
+        w[4 * k + 3] = q[k].w;
+    }
+    w[kNW] = 0u;
+    const uint32_t mis = (uint32_t)((uint64_t)(size_t)d & 3u);
+    int head = (int)((4u - mis) & 3u);
+    head = head < len ? head : len;
+    if (head > 0) d[0] = (uint8_t)w[0];
+    if (head > 1) d[1] = (uint8_t)(w[0] >> 8);
+    if (head > 2) d[2] = (uint8_t)(w[0] >> 16);
+    const int nb = (len - head) >> 2;   // whole dwords from d + head (4-byte aligned)
+    const int nbmax = nbytes / 4 + 1;   // (compile-time bound of nb + 1: the tail's dword)
+    uint32_t s[kNW];
+    uint32_t tl = 0;
 #pragma unroll
     for (int k = 0; k < kNW; k++) {
-        if (k < nw) {
-            uint32_t w = 0;
-            if (k < 4 * kStrNC && 4 * k < nbytes) {
-                const u32x4 qq = q[k >> 2];
-                w = (k & 3) == 0 ? qq.x : (k & 3) == 1 ? qq.y : (k & 3) == 2 ? qq.z : qq.w;
-                const int r = len - 4 * k;   // the value's bytes in this dword
-                w = r >= 4 ? w : r <= 0 ? 0u : w & ((1u << (8 * r)) - 1u);
-            }
-            const uint32_t v = sh ? __builtin_amdgcn_alignbyte(w, prev, 4u - sh) : w;
-            if (v) __atomic_fetch_or(d + k, v, __ATOMIC_RELAXED);
-            prev = w;
+        if (k < nbmax) {
+            s[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)head);
+            if (k == nb) tl = s[k];
         }
     }
+    CBX_GLOBAL uint8_t* body = d + head;
+#pragma unroll
+    for (int k = 0; 4 * k < kNW; k++) {
+        if (16 * k < nbytes) {
+            const int r = nb - 4 * k;
+            CBX_GLOBAL uint8_t* p = body + 16 * k;
+            if (r >= 4) {
+                *(CBX_GLOBAL u32x4a*)p = u32x4a{s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]};
+            } else if (r >= 2) {
+                *(CBX_GLOBAL u32x2a*)p = u32x2a{s[4 * k], s[4 * k + 1]};
+                if (r == 3) ((CBX_GLOBAL uint32_t*)p)[2] = s[4 * k + 2];
+            } else if (r == 1) {
+                *(CBX_GLOBAL uint32_t*)p = s[4 * k];
+            }
+        }
+    }
+    const int rem = len - head - 4 * nb;   // 0..3 tail bytes
+    CBX_GLOBAL uint8_t* tp = body + 4 * nb;
+    if (rem > 0) tp[0] = (uint8_t)tl;
+    if (rem > 1) tp[1] = (uint8_t)(tl >> 8);
+    if (rem > 2) tp[2] = (uint8_t)(tl >> 16);
 }
 
 __device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
@@ -911,35 +913,17 @@ __device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& 
     uint32_t tot;
     const uint32_t ex = wave_excl_scan32((uint32_t)len, lane, tot);
     CBX_GLOBAL uint8_t* dst = utf8_offsets(a, c, t, ex, len, tot, lane);
-    if (!dst) return;
-    const uint32_t mis = (uint32_t)((uint64_t)(size_t)dst & 15u);
-    wave_sync_lds();   // the lane slots are read back
-    utf8_zero(s_str, mis + tot + 16, lane);
-    wave_sync_lds();
-    utf8_or(s_str, mis + ex, len, op.size * op.pad, q);
-    wave_sync_lds();
-    if (!(CBX_DIAG & 16)) lds_to_global_chunks(s_str, dst - mis, mis, tot, lane);
-    wave_sync_lds();   // the staging area is reused by the next element
+    if (dst && !(CBX_DIAG & 16)) utf8_store_direct(dst + ex, len, op.size * op.pad, q);
 }
 
-// Bytes of the staging the two-element form needs: the lane slots, or both tiles' regions (a
-// region: the tile's bytes + 16 of alignment + the last lane's shifted-dword overhang).
-__host__ __device__ constexpr int utf8_two_stage(int nbytes_a, int nbytes_b, int slot) {
-    return (kWave * nbytes_a + 48 + 15) / 16 * 16 + kWave * nbytes_b + 48 > slot
-               ? (kWave * nbytes_a + 48 + 15) / 16 * 16 + kWave * nbytes_b + 48 : slot;
-}
-// Whether two register-path Utf8 elements (size, widest UTF-8 byte count) can be decoded together
-// (the plan sizes the staging for any such pair, cbx_capi.hip).
+// Whether two register-path Utf8 elements (size, widest UTF-8 byte count) can be decoded together:
+// a tile's payload of each must fit the 16-bit halves of the pair's scan.
 __host__ __device__ constexpr bool utf8_pair_fits(int size_a, int w_a, int size_b, int w_b) {
-    return utf8_two_stage(size_a * w_a, size_b * w_b,
-                          kWave * (str_lane_slot(size_a, w_a) > str_lane_slot(size_b, w_b) ? str_lane_slot(size_a, w_a)
-                                                                                            : str_lane_slot(size_b, w_b))) <=
-           kStrPairStageBytes;
+    return kWave * size_a * w_a < 65536 && kWave * size_b * w_b < 65536;
 }
 
 // Two register-path elements of the tile (the specialised kernel pairs consecutive ones): composed
-// one after the other through the same lane slots, then one scan of 16-bit halves, one zeroing of
-// both regions, the ORs of both, the copy-outs of both -- three waits for the pair instead of six.
+// one after the other through the same lane slot, one scan of 16-bit halves, the stores of both.
 __device__ __forceinline__ void str_utf8_two(const KernelArgs& a, const StrOp& A, const CBX_CONST StrOp* oppA, const StrCall& ca,
                                              const StrOp& B, const CBX_CONST StrOp* oppB, const StrCall& cb,
                                              const TileCtx& t, const int32_t* s_cnt, const uint8_t* src, uint32_t rec_addr,
@@ -955,18 +939,9 @@ __device__ __forceinline__ void str_utf8_two(const KernelArgs& a, const StrOp& A
     const uint32_t exa = ex2 & 0xFFFFu, exb = ex2 >> 16, tota = tot2 & 0xFFFFu, totb = tot2 >> 16;
     CBX_GLOBAL uint8_t* da = utf8_offsets(a, ca, t, exa, la, tota, lane);
     CBX_GLOBAL uint8_t* db = utf8_offsets(a, cb, t, exb, lb, totb, lane);
-    const uint32_t ma = da ? (uint32_t)((uint64_t)(size_t)da & 15u) : 0u, mb = db ? (uint32_t)((uint64_t)(size_t)db & 15u) : 0u;
-    const uint32_t rb = (uint32_t)((kWave * A.size * A.pad + 48 + 15) / 16 * 16);   // region B's start in the staging
-    wave_sync_lds();   // the lane slots are read back
-    utf8_zero(s_str, ma + tota + 16, lane);
-    utf8_zero(s_str + rb, mb + totb + 16, lane);
-    wave_sync_lds();
-    utf8_or(s_str, ma + exa, la, A.size * A.pad, qa);
-    utf8_or(s_str + rb, mb + exb, lb, B.size * B.pad, qb);
-    wave_sync_lds();
-    if (da) lds_to_global_chunks(s_str, da - ma, ma, tota, lane);
-    if (db) lds_to_global_chunks(s_str + rb, db - mb, mb, totb, lane);
-    wave_sync_lds();   // the staging area is reused by the next elements
+    if (CBX_DIAG & 16) return;
+    if (da) utf8_store_direct(da + exa, la, A.size * A.pad, qa);
+    if (db) utf8_store_direct(db + exb, lb, B.size * B.pad, qb);
 }
 
 // ---- Utf8 count pass (specialised kernels only: CBX_COUNT_LUT) ----
@@ -1029,10 +1004,8 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
         else str_view_fast(a, op, opp, i, c, t, s_cnt, src, rec_addr, s_lut, s_str, lane, ds);
         return;
     }
-    // (the plan sizes the staging for the lane slots and the tile's bytes up to the kStrStageBytes
-    // cap -- wider multi-byte fields keep the path below; compile-time in the specialised kernel)
-    if (!kView && fast && str_layout(a) == 2 && kmode(a) == 0 && kWave * op.size * op.pad + 64 <= kStrStageBytes &&
-        kWave * str_lane_slot(op.size, op.pad) <= kStrStageBytes) {
+    // (the plan sizes the staging for the lane slots of every register-path element)
+    if (!kView && fast && str_layout(a) == 2 && kmode(a) == 0) {
         str_utf8_fast(a, op, opp, c, t, s_cnt, src, rec_addr, s_lut, s_str, lane);
         return;
     }

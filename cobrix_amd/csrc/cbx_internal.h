@@ -20,7 +20,6 @@ constexpr int kWavesPerBlock = 2;      // waves per workgroup (each works on its
 constexpr int kGuard = 16;             // LDS guard bytes in front of / behind a record image
 constexpr int kMaxWindowBytes = 1024;  // fields wider than this are read from HBM directly
 constexpr int kStrStageBytes = 4096;   // per-wave LDS staging of one string item's tile payload
-constexpr int kStrPairStageBytes = 6144;   // ... of two register-path Utf8 elements decoded together (str_utf8_two)
 constexpr int kMaxStrItems = 256;      // string (field, slot) items per window (plan splits windows)
 
 // One string element (field, slot), pre-resolved by the plan (cf. NumOp in cbx_decode.h).

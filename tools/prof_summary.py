@@ -38,8 +38,10 @@ bench = json.loads([ln for ln in open(os.path.join(D, "bench.json")) if ln.start
 steps = bench["steps"]
 trace = rows("trace/**/run_kernel_trace.csv")
 per = collections.defaultdict(list)
+spans = collections.defaultdict(list)   # kernel -> [(start, end)] in ns, launch order
 for r in sorted(trace, key=lambda r: int(r["Start_Timestamp"])):
     per[base(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    spans[base(r["Kernel_Name"])].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
 kernels = {}
 for k, d in per.items():
     if not (k.startswith("cbx") or "cbx" in k):
@@ -56,10 +58,22 @@ if dec:
     k = dec[0]
     # the bench's decode time (HIP events) covers the record kernel, the list kernels after it and,
     # in the Utf8 layout, the count pass and its scan before it
-    parts = [k] + [x for x in kernels if x.startswith("cbx::list_kernel")]
+    # the timed steps' window: after the record kernel's last warm-up launch, up to the end of its
+    # last timed launch; every part kernel launched inside it counts (per step), so list / count
+    # kernels that only run in the end-to-end pieces (smaller batches) are left out
+    w0 = bench.get("warmup", 0)
+    sp = spans[k]
+    lo = sp[w0 - 1][1] if w0 > 0 else 0
+    hi = sp[min(w0 + steps, len(sp)) - 1][1]
+    cand = [k] + [x for x in kernels if x.startswith(("cbx::list_kernel", "cbx_jit_list"))]
     if "cbx_jit_count" in kernels or bench["config"].get("string_layout", "").startswith("Arrow Utf8"):
-        parts += [x for x in kernels if x.startswith(("cbx_jit_count", "cbx::scan_"))]
-    t = sum(kernels[x]["avg_ms_timed_steps"] for x in parts)
+        cand += [x for x in kernels if x.startswith(("cbx_jit_count", "cbx::scan_"))]
+    parts, t = [], 0.0
+    for x in cand:
+        d_in = [(e - s0) / 1e6 for s0, e in spans[x] if lo < s0 and e <= hi]
+        if d_in:
+            parts.append(x)
+            t += sum(d_in) / steps
     frac = alg / (t * 1e-3) / 1e9 / bench["roofline"]["peak"]
     check = {"kernel": " + ".join(parts), "rocprof_ms": round(t, 4),
              "hip_event_ms": bench["kernel_ms"]["decode_kernel"], "frac_rocprof": round(frac, 4),
