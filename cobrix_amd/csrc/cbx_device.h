@@ -592,10 +592,13 @@ __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, i
 #else
     lut_entries32(w, smax, [&](uint32_t b) { return str_lut(kind, s_lut, b); }, ev);
 #endif
-    uint32_t tm = 0;   // bit j: byte j trimmable (entry bit 31)
+    // bit j: byte j trimmable (entry bit 31) -- collected reversed with one funnel shift per byte
+    // ((tr << 1) | bit 31), then bit-reversed: 1 VALU per byte instead of shift, mask and OR
+    uint32_t tr = 0;
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++)
-        if (j < smax) tm |= (ev[j] >> 31) << j;
+        if (j < smax) tr = __builtin_amdgcn_alignbit(tr, ev[j], 31);
+    const uint32_t tm = __builtin_bitreverse32(tr) >> (32 - smax);
     const uint32_t keep = ~tm & bits_below(n);
     int b = 0, e = n;
     if (trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;

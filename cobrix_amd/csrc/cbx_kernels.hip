@@ -844,28 +844,90 @@ __device__ __forceinline__ int32_t rdw_lane_walk(const RdwArgs& a, const RdwStre
 // [base, base + kLaneWin) an ordinary one; lim = min(kLaneWin, end - base)).  Returns the exit
 // (relative), adds the records to `count` (staged from index count), err: the relative position of
 // a rejected header (-1 none) -- records before it are counted and staged.
+// Strict candidates (the zero pair of a header: bytes 0-1 little-endian, 2-3 big-endian) of the
+// lane's span [r0, r1) of the window at base: bit j <-> a header at relative position r0 + j.
+__device__ __forceinline__ uint32_t rdw_lane_pairs(const RdwArgs& a, const RdwStream& s, int64_t base, int32_t r0, int32_t r1) {
+    const int32_t off = a.p.big_endian ? 2 : 0;   // zero pair inside a header
+    const uint32_t o0 = (uint32_t)((s.shift + base + r0 + off) & (kRdwRing - 1));
+    const uint32_t a16 = o0 & ~15u, m = o0 & 15u;
+    uint32_t zb[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const u32x4 v = *(const u32x4*)(s.ring + ((a16 + 16u * j) & (kRdwRing - 1)));
+        zb[j] = zero_bytes4(v.x) | zero_bytes4(v.y) << 4 | zero_bytes4(v.z) << 8 | zero_bytes4(v.w) << 12;
+    }
+    const uint64_t z = (uint64_t)zb[0] | (uint64_t)zb[1] << 16 | (uint64_t)zb[2] << 32;
+    return (uint32_t)(((z & (z >> 1)) >> m) & ((1ull << (r1 - r0)) - 1));
+}
+
+// The chained-candidate form of a window (dense text-like records, C4): when the window's strict
+// candidates are exactly a chain from P -- P is the first one, every candidate's next header is
+// the following candidate, the last one's lies at or past the window's end -- they are exactly the
+// headers the sequential walk visits (by induction from P: no header lies between a header and its
+// next), so the window needs no speculation, hops, resolution rounds or walks: one candidate scan,
+// one header read per candidate, a wave scan of the counts and the stores.  Any other window (a
+// zero pair inside a payload, a non-strict or rejected header) returns false and takes the general
+// form.  Returns the exit; adds the records to count (staged from index count).
+__device__ __forceinline__ bool rdw_chain_window(const RdwArgs& a, const RdwStream& s, int64_t base, int32_t lim, int32_t in_left,
+                                                 uint32_t rel0, uint32_t* so, int32_t* sl, uint32_t cap, uint32_t& count,
+                                                 int32_t& exit, int lane, uint32_t pairs, int32_t r0) {
+    int32_t first = 0x7fffffff, next = -1;
+    uint32_t nc = 0;
+    bool bad = false;
+    for (uint32_t pm = pairs; pm; pm &= pm - 1) {
+        const int32_t q = r0 + (int32_t)__builtin_ctz(pm);
+        uint32_t h;
+        const int32_t rl = rdw_lane_len(a, s, base, q, h);
+        if (rl <= 0 || rl > 100 * 1024 * 1024 || (next >= 0 && next != q)) { bad = true; break; }
+        if (nc == 0) first = q;
+        const int32_t fo = q + 4;
+        const int32_t rem = in_left - fo;
+        next = fo + (rl < rem ? rl : rem);
+        nc++;
+    }
+    const uint64_t hold = __ballot(nc > 0);
+    // the first candidate of the next lane holding one (or none): the chain must enter it there
+    const uint64_t above = lane < kWave - 1 ? hold & ~((2ull << lane) - 1) : 0ull;
+    const int src = above ? __builtin_ctzll(above) : lane;
+    const int32_t nf = __shfl(first, src, kWave);
+    if (nc > 0) bad |= above ? next != nf : next < lim;
+    if (lane == 0) bad |= first != 0;
+    if (__ballot(bad)) return false;
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32(nc, lane, tot);
+    uint32_t idx = count + ex;
+    for (uint32_t pm = pairs; pm; pm &= pm - 1, idx++) {
+        const int32_t q = r0 + (int32_t)__builtin_ctz(pm);
+        uint32_t h;
+        const int32_t rl = rdw_lane_len(a, s, base, q, h);
+        const int32_t fo = q + 4;
+        const int32_t rem = in_left - fo;
+        if (idx < cap) {
+            gp(so)[idx] = rel0 + (uint32_t)fo;
+            gp(sl)[idx] = rl < rem ? rl : rem;
+        }
+    }
+    count += tot;
+    exit = __shfl(next, hold ? 63 - __builtin_clzll(hold) : 0, kWave);
+    return true;
+}
+
 __device__ int32_t rdw_lane_window(const RdwArgs& a, const RdwStream& s, int64_t base, int32_t lim, int32_t in_left,
                                    int32_t resident, uint32_t rel0, uint32_t* so, int32_t* sl, uint32_t cap,
                                    uint32_t& count, int32_t& err, int lane) {
     const int32_t r0 = lane * kLaneSpan;
     const int32_t r1 = r0 + kLaneSpan < lim ? r0 + kLaneSpan : lim;
     const bool live = r0 < lim;
+    const uint32_t all_pairs = live ? rdw_lane_pairs(a, s, base, r0, r1) : 0u;
+    err = -1;
+    int32_t cx;
+    if (rdw_chain_window(a, s, base, lim, in_left, rel0, so, sl, cap, count, cx, lane, all_pairs, r0)) return cx;
     // speculation: the first strict candidate of the span with two plausible hops
     int32_t e = -1;
     if (lane == 0) {
         e = 0;
     } else if (live) {
-        const int32_t off = a.p.big_endian ? 2 : 0;   // zero pair inside a header
-        const uint32_t o0 = (uint32_t)((s.shift + base + r0 + off) & (kRdwRing - 1));
-        const uint32_t a16 = o0 & ~15u, m = o0 & 15u;
-        uint32_t zb[3];
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const u32x4 v = *(const u32x4*)(s.ring + ((a16 + 16u * j) & (kRdwRing - 1)));
-            zb[j] = zero_bytes4(v.x) | zero_bytes4(v.y) << 4 | zero_bytes4(v.z) << 8 | zero_bytes4(v.w) << 12;
-        }
-        const uint64_t z = (uint64_t)zb[0] | (uint64_t)zb[1] << 16 | (uint64_t)zb[2] << 32;
-        uint32_t pairs = (uint32_t)(((z & (z >> 1)) >> m) & ((1ull << (r1 - r0)) - 1));
+        uint32_t pairs = all_pairs;
         while (pairs) {
             const int32_t q = r0 + (int32_t)__builtin_ctz(pairs);
             pairs &= pairs - 1;

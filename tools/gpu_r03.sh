@@ -32,5 +32,7 @@ for SPEC in "$@"; do
     timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $D/pmc$i -o run -- python3 bench.py --workload $W $EXTRA --steps 1 --warmup 1 --no-cpu-baseline --no-end-to-end > $D/pmc$i.log 2>&1 || { echo "pmc pass $i ($NAME) failed"; tail -3 $D/pmc$i.log; exit 1; }
   done
   python3 tools/prof_summary.py $D > $D/summary.json && python3 -c "import json; d=json.load(open('$D/summary.json')); print('$NAME', json.dumps(d['check']))"
+  # the raw per-dispatch CSVs compressed (gpurun copies back at most 64 MiB of gpurun_out/)
+  find $D -name "run_kernel_trace.csv" -o -name "run_counter_collection.csv" | xargs -r gzip -f
 done
 echo ALL_OK

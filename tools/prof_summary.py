@@ -13,6 +13,7 @@ Usage: prof_summary.py <workload dir> -> JSON on stdout."""
 import collections
 import csv
 import glob
+import gzip
 import json
 import os
 import sys
@@ -28,9 +29,13 @@ def base(name: str) -> str:
 
 
 def rows(pattern):
+    """CSV rows of the files matching pattern (or their gzip-compressed copies, pattern + ".gz")."""
     out = []
     for f in glob.glob(os.path.join(D, pattern), recursive=True):
         out += list(csv.DictReader(open(f)))
+    for f in glob.glob(os.path.join(D, pattern + ".gz"), recursive=True):
+        with gzip.open(f, "rt") as g:
+            out += list(csv.DictReader(g))
     return out
 
 
