@@ -518,7 +518,11 @@ __device__ __forceinline__ uint32_t byte_x4(uint32_t w, int k) {
 // words -- lanes at the same position fall on different banks (2-way at most for the byte stores;
 // the 8-byte read-backs conflict-free), where a 16-byte multiple put lanes 8 apart on one bank.
 __host__ __device__ constexpr int str_lane_slot(int size, int width) {
-    return (((size * width + 3 + 7) >> 3) | 1) << 3;
+    // an odd dword count: the lanes' byte stores at similar positions land on distinct banks
+    // (ds_write_b8: bank (a / 4) mod 32), and the dword read-backs are conflict-free.  (Odd counts of
+    // 8-byte words, read back as 8-byte words, left every byte store 2-way conflicted: 14 dwords
+    // per lane.)
+    return (((size * width + 3 + 3) >> 2) | 1) << 2;
 }
 
 // The view layout's register-path string element (fields of <= kStrFastBytes EBCDIC / ASCII bytes,
@@ -625,10 +629,12 @@ __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, i
     slot[len] = 0; slot[len + 1] = 0; slot[len + 2] = 0;   // the partial dword's tail
 #pragma unroll
     for (int k = 0; k < kStrNC; k++) {
-        if (16 * k < smax * width) {   // 8-byte reads (the slot is 8-byte aligned)
-            const uint2 lo = ((const uint2*)slot)[2 * k];
-            const uint2 hi = 16 * k + 8 < smax * width ? ((const uint2*)slot)[2 * k + 1] : make_uint2(0u, 0u);
-            q[k] = u32x4{lo.x, lo.y, hi.x, hi.y};
+        if (16 * k < smax * width) {   // dword reads (the slot is 4-byte aligned)
+            const uint32_t* sd = (const uint32_t*)slot + 4 * k;
+            uint32_t d[4];
+#pragma unroll
+            for (int m = 0; m < 4; m++) d[m] = 16 * k + 4 * m < smax * width ? sd[m] : 0u;
+            q[k] = u32x4{d[0], d[1], d[2], d[3]};
         }
     }
     return len;

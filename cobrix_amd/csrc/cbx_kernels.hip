@@ -915,11 +915,28 @@ __device__ __forceinline__ bool rdw_chain_window(const RdwArgs& a, const RdwStre
 __device__ int32_t rdw_lane_window(const RdwArgs& a, const RdwStream& s, int64_t base, int32_t lim, int32_t in_left,
                                    int32_t resident, uint32_t rel0, uint32_t* so, int32_t* sl, uint32_t cap,
                                    uint32_t& count, int32_t& err, int lane) {
+    err = -1;
+    {
+        // a record spanning the window (C5's 16 KB roots): the chain goes from P straight past the
+        // window end, so P is the window's only header whatever the payload holds -- no candidate
+        // scan (binary payloads are full of zero pairs) and no lane walks
+        uint32_t h;
+        const int32_t rl = rdw_lane_len(a, s, base, 0, h);   // (the same LDS dwords for every lane)
+        const int32_t rem = in_left - 4;
+        const int32_t nx = 4 + (rl < rem ? rl : rem);
+        if (rl > 0 && rl <= 100 * 1024 * 1024 && nx >= lim) {
+            if (lane == 0 && count < cap) {
+                gp(so)[count] = rel0 + 4u;
+                gp(sl)[count] = nx - 4;
+            }
+            count += 1;
+            return nx;
+        }
+    }
     const int32_t r0 = lane * kLaneSpan;
     const int32_t r1 = r0 + kLaneSpan < lim ? r0 + kLaneSpan : lim;
     const bool live = r0 < lim;
     const uint32_t all_pairs = live ? rdw_lane_pairs(a, s, base, r0, r1) : 0u;
-    err = -1;
     int32_t cx;
     if (rdw_chain_window(a, s, base, lim, in_left, rel0, so, sl, cap, count, cx, lane, all_pairs, r0)) return cx;
     // speculation: the first strict candidate of the span with two plausible hops

@@ -1,6 +1,6 @@
 """Dump (and hipRTC-compile) the copybook-specialised kernel of a layout: SYN200 by default.
 
-Usage: python tools/jit_check.py [copybook file | syn200 | synstr200] [views] -> gpurun_out/jit_<name>[_views].hip;
+Usage: python tools/jit_check.py [copybook file | syn200 | synstr200] [views | utf8] -> gpurun_out/jit_<name>[_views].hip;
 prints the status.
 """
 import ctypes
@@ -22,10 +22,11 @@ def main():
     elif len(sys.argv) > 1 and sys.argv[1] != "syn200":
         name, text = os.path.splitext(os.path.basename(sys.argv[1]))[0], open(sys.argv[1]).read()
     views = len(sys.argv) > 2 and sys.argv[2] == "views"
-    if views:
-        name += "_views"
+    utf8 = len(sys.argv) > 2 and sys.argv[2] == "utf8"
+    if views or utf8:
+        name += "_" + sys.argv[2]
     L = N.load()
-    rd = FixedLenNestedReader(text, ReaderParameters(ebcdic_code_page=cp, string_views=views))
+    rd = FixedLenNestedReader(text, ReaderParameters(ebcdic_code_page=cp, string_views=views, string_utf8=utf8))
     buf = ctypes.create_string_buffer(4 << 20)
     n = ctypes.c_int64()
     rc = L.cbx_plan_specialize(rd.native.handle, buf, len(buf), ctypes.byref(n), 1)
