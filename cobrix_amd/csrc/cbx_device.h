@@ -838,11 +838,15 @@ __device__ __forceinline__ int utf8_compose(const KernelArgs& a, const StrOp& op
     return ok ? len : 0;
 }
 
-// The element's int32 offsets (the tile's place from the count pass's scan) and the slot's size;
-// returns the tile's destination, or null when the region (or an int32 offset) overflows.
-__device__ __forceinline__ CBX_GLOBAL uint8_t* utf8_offsets(const KernelArgs& a, const StrCall& c, const TileCtx& t, uint32_t ex,
-                                                            int len, uint32_t tot, int lane) {
-    const int64_t base = c.excl[t.tile] - c.excl[0];   // the tile's place in the slot's region
+// The tile's place in the element's slot region (the count pass's exclusive scan).  The
+// specialised kernel loads it for all of a tile's elements before the first is decoded (one wait
+// for the tile instead of a dependent scalar load in front of every element's stores).
+__device__ __forceinline__ int64_t utf8_tile_base(const StrCall& c, const TileCtx& t) { return c.excl[t.tile] - c.excl[0]; }
+
+// The element's int32 offsets (from the tile's place, base) and the slot's size; returns the tile's
+// destination, or null when the region (or an int32 offset) overflows.
+__device__ __forceinline__ CBX_GLOBAL uint8_t* utf8_offsets(const KernelArgs& a, const StrCall& c, const TileCtx& t, int64_t base,
+                                                            uint32_t ex, int len, uint32_t tot, int lane) {
     CBX_GLOBAL int32_t* offs = gp((int32_t*)c.local);
     (offs + t.tile * kWave)[lane] = (int32_t)(base + ex);
     if (t.rec == a.n_rec - 1) {   // the closing offset and the slot's size
@@ -857,7 +861,9 @@ __device__ __forceinline__ CBX_GLOBAL uint8_t* utf8_offsets(const KernelArgs& a,
 }
 
 // The lane's len bytes (q, packed from byte 0; nbytes: the compile-time bound of len) to d at any
-// byte alignment.
+// byte alignment, in few store instructions (a wave issues every variant any lane needs, so the
+// variants are kept to: head byte + head short, whole 16-byte chunks, a remainder of 8 + 4 bytes
+// at a per-lane address, tail short + tail byte -- at most 9 stores with the offsets, 14 before).
 __device__ __forceinline__ void utf8_store_direct(CBX_GLOBAL uint8_t* d, int len, int nbytes, const u32x4 (&q)[kStrNC]) {
     typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
     typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
@@ -874,41 +880,48 @@ __device__ __forceinline__ void utf8_store_direct(CBX_GLOBAL uint8_t* d, int len
     const uint32_t mis = (uint32_t)((uint64_t)(size_t)d & 3u);
     int head = (int)((4u - mis) & 3u);
     head = head < len ? head : len;
-    if (head > 0) d[0] = (uint8_t)w[0];
-    if (head > 1) d[1] = (uint8_t)(w[0] >> 8);
-    if (head > 2) d[2] = (uint8_t)(w[0] >> 16);
+    // head: a byte at an odd address, then 2 bytes at the (2-aligned) next one or a last byte (a
+    // value shorter than its first dword's remainder)
+    const int b1 = (head > 0 && (mis & 1u)) ? 1 : 0;
+    const int h2 = head - b1;
+    if (b1) d[0] = (uint8_t)w[0];
+    if (h2 >= 2) *(CBX_GLOBAL uint16_t*)(d + b1) = (uint16_t)(w[0] >> (8 * b1));
+    else if (h2 == 1) d[b1] = (uint8_t)(w[0] >> (8 * b1));
     const int nb = (len - head) >> 2;   // whole dwords from d + head (4-byte aligned)
     const int nbmax = nbytes / 4 + 1;   // (compile-time bound of nb + 1: the tail's dword)
     uint32_t s[kNW];
-    uint32_t tl = 0;
 #pragma unroll
-    for (int k = 0; k < kNW; k++) {
-        if (k < nbmax) {
-            s[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)head);
-            if (k == nb) tl = s[k];
-        }
-    }
+    for (int k = 0; k < kNW; k++)
+        if (k < nbmax) s[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)head);
     CBX_GLOBAL uint8_t* body = d + head;
 #pragma unroll
+    for (int k = 0; 4 * k < kNW; k++)
+        if (16 * k + 16 <= nbytes && 4 * k + 4 <= nb)
+            *(CBX_GLOBAL u32x4a*)(body + 16 * k) = u32x4a{s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]};
+    // the remainder (nb & 3 dwords of chunk nb / 4) and the tail dword (s[nb]), selected by chunk
+    const int kr = nb >> 2, r = nb & 3;
+    uint32_t r0 = 0, r1 = 0, r2 = 0, tl = 0;
+#pragma unroll
     for (int k = 0; 4 * k < kNW; k++) {
-        if (16 * k < nbytes) {
-            const int r = nb - 4 * k;
-            CBX_GLOBAL uint8_t* p = body + 16 * k;
-            if (r >= 4) {
-                *(CBX_GLOBAL u32x4a*)p = u32x4a{s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]};
-            } else if (r >= 2) {
-                *(CBX_GLOBAL u32x2a*)p = u32x2a{s[4 * k], s[4 * k + 1]};
-                if (r == 3) ((CBX_GLOBAL uint32_t*)p)[2] = s[4 * k + 2];
-            } else if (r == 1) {
-                *(CBX_GLOBAL uint32_t*)p = s[4 * k];
+        if (4 * k < nbmax) {
+            if (kr == k) {
+                r0 = s[4 * k];
+                if (4 * k + 1 < nbmax) r1 = s[4 * k + 1];
+                if (4 * k + 2 < nbmax) r2 = s[4 * k + 2];
             }
         }
     }
+#pragma unroll
+    for (int k = 0; k < kNW; k++)
+        if (k < nbmax && k == nb) tl = s[k];
+    CBX_GLOBAL uint8_t* rp = body + 16 * kr;
+    if (r & 2) *(CBX_GLOBAL u32x2a*)rp = u32x2a{r0, r1};
+    if (r & 1) *(CBX_GLOBAL uint32_t*)(rp + 4 * (r & 2)) = (r & 2) ? r2 : r0;
+    // tail: 2 bytes at the 4-aligned tail, then 1 byte
     const int rem = len - head - 4 * nb;   // 0..3 tail bytes
     CBX_GLOBAL uint8_t* tp = body + 4 * nb;
-    if (rem > 0) tp[0] = (uint8_t)tl;
-    if (rem > 1) tp[1] = (uint8_t)(tl >> 8);
-    if (rem > 2) tp[2] = (uint8_t)(tl >> 16);
+    if (rem >= 2) *(CBX_GLOBAL uint16_t*)tp = (uint16_t)tl;
+    if (rem & 1) tp[rem & 2] = (uint8_t)(tl >> (8 * (rem & 2)));
 }
 
 __device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
@@ -921,7 +934,7 @@ __device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& 
     gp(c.validity)[t.tile] = __ballot(ok);
     uint32_t tot;
     const uint32_t ex = wave_excl_scan32((uint32_t)len, lane, tot);
-    CBX_GLOBAL uint8_t* dst = utf8_offsets(a, c, t, ex, len, tot, lane);
+    CBX_GLOBAL uint8_t* dst = utf8_offsets(a, c, t, utf8_tile_base(c, t), ex, len, tot, lane);
     if (dst && !(CBX_DIAG & 16)) utf8_store_direct(dst + ex, len, op.size * op.pad, q);
 }
 
@@ -936,7 +949,7 @@ __host__ __device__ constexpr bool utf8_pair_fits(int size_a, int w_a, int size_
 __device__ __forceinline__ void str_utf8_two(const KernelArgs& a, const StrOp& A, const CBX_CONST StrOp* oppA, const StrCall& ca,
                                              const StrOp& B, const CBX_CONST StrOp* oppB, const StrCall& cb,
                                              const TileCtx& t, const int32_t* s_cnt, const uint8_t* src, uint32_t rec_addr,
-                                             const uint32_t* s_lut, uint8_t* s_str, int lane) {
+                                             const uint32_t* s_lut, uint8_t* s_str, int lane, int64_t base_a, int64_t base_b) {
     bool oka, okb;
     u32x4 qa[kStrNC], qb[kStrNC];
     const int la = utf8_compose(a, A, oppA, t, s_cnt, src, rec_addr, s_lut, s_str, lane, oka, qa);
@@ -946,11 +959,19 @@ __device__ __forceinline__ void str_utf8_two(const KernelArgs& a, const StrOp& A
     uint32_t tot2;
     const uint32_t ex2 = wave_excl_scan32((uint32_t)la | ((uint32_t)lb << 16), lane, tot2);   // a tile's total < 64 KiB
     const uint32_t exa = ex2 & 0xFFFFu, exb = ex2 >> 16, tota = tot2 & 0xFFFFu, totb = tot2 >> 16;
-    CBX_GLOBAL uint8_t* da = utf8_offsets(a, ca, t, exa, la, tota, lane);
-    CBX_GLOBAL uint8_t* db = utf8_offsets(a, cb, t, exb, lb, totb, lane);
+    CBX_GLOBAL uint8_t* da = utf8_offsets(a, ca, t, base_a, exa, la, tota, lane);
+    CBX_GLOBAL uint8_t* db = utf8_offsets(a, cb, t, base_b, exb, lb, totb, lane);
     if (CBX_DIAG & 16) return;
     if (da) utf8_store_direct(da + exa, la, A.size * A.pad, qa);
     if (db) utf8_store_direct(db + exb, lb, B.size * B.pad, qb);
+}
+
+__device__ __forceinline__ void str_utf8_two(const KernelArgs& a, const StrOp& A, const CBX_CONST StrOp* oppA, const StrCall& ca,
+                                             const StrOp& B, const CBX_CONST StrOp* oppB, const StrCall& cb,
+                                             const TileCtx& t, const int32_t* s_cnt, const uint8_t* src, uint32_t rec_addr,
+                                             const uint32_t* s_lut, uint8_t* s_str, int lane) {
+    str_utf8_two(a, A, oppA, ca, B, oppB, cb, t, s_cnt, src, rec_addr, s_lut, s_str, lane, utf8_tile_base(ca, t),
+                 utf8_tile_base(cb, t));
 }
 
 // ---- Utf8 count pass (specialised kernels only: CBX_COUNT_LUT) ----

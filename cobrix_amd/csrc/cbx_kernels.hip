@@ -850,14 +850,28 @@ __device__ __forceinline__ uint32_t rdw_lane_pairs(const RdwArgs& a, const RdwSt
     const int32_t off = a.p.big_endian ? 2 : 0;   // zero pair inside a header
     const uint32_t o0 = (uint32_t)((s.shift + base + r0 + off) & (kRdwRing - 1));
     const uint32_t a16 = o0 & ~15u, m = o0 & 15u;
-    uint32_t zb[3];
+    // zero bytes as 0x80 per byte (exact: no carry leaves a byte), a pair as a byte and the next
+    // one (a funnel shift brings the next dword's byte 0 in), each dword's 4 pair bits gathered
+    // into a nibble by one dot product of the 0/1 bytes with (1, 2, 4, 8)
+    uint32_t z[13];
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         const u32x4 v = *(const u32x4*)(s.ring + ((a16 + 16u * j) & (kRdwRing - 1)));
-        zb[j] = zero_bytes4(v.x) | zero_bytes4(v.y) << 4 | zero_bytes4(v.z) << 8 | zero_bytes4(v.w) << 12;
+        const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) z[4 * j + k] = ~(((x[k] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x[k]) & 0x80808080u;
     }
-    const uint64_t z = (uint64_t)zb[0] | (uint64_t)zb[1] << 16 | (uint64_t)zb[2] << 32;
-    return (uint32_t)(((z & (z >> 1)) >> m) & ((1ull << (r1 - r0)) - 1));
+    z[12] = 0u;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const uint32_t pz = z[k] & __builtin_amdgcn_alignbit(z[k + 1], z[k], 8);
+        const uint32_t nib = __builtin_amdgcn_udot4(pz >> 7, 0x08040201u, 0u, false);
+        if (k < 8) lo |= nib << (4 * k);
+        else hi |= nib << (4 * (k - 8));
+    }
+    const uint64_t zp = (uint64_t)lo | (uint64_t)hi << 32;
+    return (uint32_t)((zp >> m) & ((1ull << (r1 - r0)) - 1));
 }
 
 // The chained-candidate form of a window (dense text-like records, C4): when the window's strict
