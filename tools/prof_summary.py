@@ -19,7 +19,7 @@ import os
 import sys
 
 D = sys.argv[1]
-STAGED16 = ("cbx_jit_decode", "cbx_jit_count", "cbx::decode_kernel", "cbx::list_kernel")   # 16-byte/lane staged reads
+STAGED16 = ("cbx_jit_decode", "cbx_jit_count", "cbx_jit_list", "cbx::decode_kernel", "cbx::list_kernel")   # 16-byte/lane staged reads
 
 
 def base(name: str) -> str:
