@@ -132,6 +132,10 @@ struct cbx_plan {
     const int64_t* d_rec_base = nullptr;   // caller's device Record_Id base (cbx_plan_set_record_base)
     int64_t n_str_slots = 0;
     uint32_t* d_wcursor = nullptr; int64_t wcursor_cap = 0;
+    int64_t* d_wvbase = nullptr;        // per column: first validity-word index among all column slots
+    int32_t* d_wvcol = nullptr;         // per validity word: column, slot
+    int32_t* d_wvslot = nullptr;
+    int32_t n_vslots = 0;
     int32_t fid_col = -1, rid_col = -1;
     // profiling: HIP events around the decode kernel and the post passes of every call (no sync)
     bool profiling = false;
@@ -568,6 +572,7 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
     (void)hipFree(P->d_lops); (void)hipFree(P->d_list_len); (void)hipFree(P->d_list_flag);
     (void)hipFree(P->d_wnodes); (void)hipFree(P->d_warr); (void)hipFree(P->d_whand); (void)hipFree(P->d_wslot_base);
     (void)hipFree(P->d_wtile_bytes); (void)hipFree(P->d_wcursor);
+    (void)hipFree(P->d_wvbase); (void)hipFree(P->d_wvcol); (void)hipFree(P->d_wvslot);
     for (auto& e : P->ev_pool) (void)hipEventDestroy(e);
     for (auto& c : P->ev_calls) for (auto& e : c.e) if (e) (void)hipEventDestroy(e);
     delete P;
@@ -1047,9 +1052,27 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
     a.segmap = P->opts.has_segments ? (const CBX_CONST cbx_segment_map*)P->d_segmap : nullptr;
     a.lut = P->d_lut; a.seg_col = P->seg_col; a.fid_col = P->fid_col; a.rid_col = P->rid_col;
     a.str_slot_base = P->d_wslot_base; a.cursors = P->d_wcursor; a.tile_bytes = P->d_wtile_bytes; a.status = P->d_status;
-    const int64_t grid = std::min<int64_t>((c.n_rec + 255) / 256, (int64_t)P->num_cus * 8);
-    hipLaunchKernelGGL(walk_kernel, dim3((unsigned)grid), dim3(256), 0, st, a);
+    // per-wave LDS words (validity of every column slot, string cursors) when they fit 8 KiB a wave
+    a.n_vslots = P->n_vslots;
+    a.n_sslots = (int32_t)P->n_str_slots;
+    a.wave_lds = (int32_t)((8 * (int64_t)P->n_vslots + 4 * P->n_str_slots + 15) & ~15ll);
+    a.vlds = P->n_vslots > 0 && a.wave_lds <= 8192 && !getenv("CBX_WALK_GLOBAL_ATOMICS") ? 1 : 0;
+    a.vslot_base = P->d_wvbase; a.vslot_col = P->d_wvcol; a.vslot_slot = P->d_wvslot;
+    const size_t wlds = a.vlds ? 4 * (size_t)a.wave_lds : 0;
+    const int64_t grid = std::min<int64_t>((n_tiles + 3) / 4, (int64_t)P->num_cus * 8);
+    // kernel timing (cbx_plan_set_profiling): the walk is the decode; it has no post passes
+    cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};
+    if (P->profiling) {
+        for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
+        HIP_CHECK(hipEventRecord(ce.e[0], st));
+    }
+    hipLaunchKernelGGL(walk_kernel, dim3((unsigned)grid), dim3(256), wlds, st, a);
     HIP_CHECK(hipGetLastError());
+    if (P->profiling) {
+        HIP_CHECK(hipEventRecord(ce.e[1], st));
+        HIP_CHECK(hipEventRecord(ce.e[2], st));
+        P->ev_calls.push_back(ce);
+    }
     P->last_kind = 2;
     return CBX_OK;
 }
@@ -1925,7 +1948,29 @@ extern "C" int cbx_plan_set_walk(cbx_plan* P, const cbx_walk_node* nodes, int32_
         tile_bytes[2 * c] = view_tile_bytes(P, c);
         tile_bytes[2 * c + 1] = view_tiles_per_buf(tile_bytes[2 * c]);
     }
+    // every column slot's validity word of a tile (the walk accumulates them in LDS per tile); a
+    // count column has one slot per element of its array's enclosing arrays
+    std::vector<int64_t> cslots(P->n_columns);
+    for (int c = 0; c < P->n_columns; c++) cslots[c] = P->col_slots[c];
+    for (const cbx_array& ar : P->harrays) {
+        if (ar.count_column < 0 || ar.count_column >= P->n_columns) continue;
+        int64_t k = 1;
+        for (int p = ar.parent, guard = 0; p >= 0 && p < (int)P->harrays.size() && guard < 64; p = P->harrays[p].parent, guard++)
+            k *= std::max(1, P->harrays[p].max_count);
+        cslots[ar.count_column] = std::max(cslots[ar.count_column], k);
+    }
+    std::vector<int64_t> vbase(P->n_columns, 0);
+    std::vector<int32_t> vcol, vslot;
+    for (int c = 0; c < P->n_columns; c++) {
+        vbase[c] = (int64_t)vcol.size();
+        for (int64_t k = 0; k < cslots[c] && vcol.size() < (1u << 20); k++) { vcol.push_back(c); vslot.push_back((int32_t)k); }
+    }
+    if (vcol.empty()) { vcol.push_back(0); vslot.push_back(0); }
     int r;
+    if ((r = upload(&P->d_wvbase, vbase.data(), vbase.size())) || (r = upload(&P->d_wvcol, vcol.data(), vcol.size())) ||
+        (r = upload(&P->d_wvslot, vslot.data(), vslot.size())))
+        return r;
+    P->n_vslots = P->n_columns > 0 ? (int32_t)vcol.size() : 0;
     if ((r = upload(&P->d_wnodes, nodes, n_nodes)) || (r = upload(&P->d_warr, arrays, na)) ||
         (r = upload(&P->d_whand, handlers, n_handlers)) || (r = upload(&P->d_wslot_base, slot_base.data(), slot_base.size())) ||
         (r = upload(&P->d_wtile_bytes, tile_bytes.data(), tile_bytes.size())))

@@ -52,6 +52,19 @@ struct WalkArgs {
     uint32_t* cursors;                // [string column slots][n_tiles] payload bytes used in the tile region
     const int64_t* tile_bytes;        // per column: view region bytes per tile, tiles per data buffer
     int32_t* status;
+    // per-wave LDS accumulation (vlds != 0): the tile's validity words of every (column, slot) and the
+    // string slots' payload cursors, stored once per tile instead of one global atomic per value
+    int32_t vlds, wave_lds;           // flag; LDS bytes per wave
+    int32_t n_vslots, n_sslots;       // validity words (all column slots); string column slots
+    const int64_t* vslot_base;        // per column: index of its slot 0 among all column slots
+    const int32_t* vslot_col;         // per validity word: its column and slot
+    const int32_t* vslot_slot;
+};
+
+// The wave's LDS area of the tile being walked (vlds): validity words, then string cursors.
+struct WalkLds {
+    uint64_t* vw;     // [n_vslots]
+    uint32_t* cur;    // [n_sslots]
 };
 
 struct WalkFrame {
@@ -72,8 +85,12 @@ __device__ __forceinline__ uint32_t walk_lut(const WalkArgs& a, int kind, uint32
     return kind == CBX_K_STRING_ASCII ? ascii_lut(b) : a.lut[b];
 }
 
-__device__ __forceinline__ void walk_set_valid(uint64_t* validity, int64_t word, int lane) {
-    atomicOr((unsigned long long*)(validity + word), 1ull << lane);
+// Record (tile * 64 + lane)'s value of (column, slot) is valid: an LDS OR into the tile's word
+// (vlds), else a global atomic OR into the column's bitmap.
+__device__ __forceinline__ void walk_set_valid(const WalkArgs& a, const WalkLds& wl, uint64_t* validity, int column, int slot,
+                                               int64_t tile, int lane) {
+    if (wl.vw) atomicOr((unsigned long long*)(wl.vw + a.vslot_base[column] + slot), 1ull << lane);
+    else atomicOr((unsigned long long*)(validity + (int64_t)slot * a.n_tiles + tile), 1ull << lane);
 }
 
 // extractArray's element count (:66-81)
@@ -95,8 +112,8 @@ __device__ __forceinline__ int walk_count(const WalkArgs& a, int ai, const WalkD
 // One primitive element at record offset `off` (relative to the decode base).  `element`: an
 // element of a primitive OCCURS -- extractArray decodes those with decodeTypeValue, which never
 // touches dependFields (RecordExtractors.scala:96-107), so they update no dependee.
-__device__ void walk_prim(const WalkArgs& a, const cbx_walk_node& nd, int off, int slot, const uint8_t* rec, int avail,
-                          int64_t r, int lane, WalkDep* dep, bool element) {
+__device__ void walk_prim(const WalkArgs& a, const WalkLds& wl, const cbx_walk_node& nd, int off, int slot, const uint8_t* rec,
+                          int avail, int64_t r, int lane, WalkDep* dep, bool element) {
     const bool decoded = nd.field >= 0;
     Field f{};
     if (decoded) f = ldc(a.fields + nd.field);
@@ -126,7 +143,7 @@ __device__ void walk_prim(const WalkArgs& a, const cbx_walk_node& nd, int off, i
             const int64_t tb = a.tile_bytes[2 * f.column];
             const int64_t tpb = a.tile_bytes[2 * f.column + 1];   // a power of two (view_tiles_per_buf)
             const int64_t cs = a.str_slot_base[f.column] + slot;
-            const uint32_t at = atomicAdd(a.cursors + cs * a.n_tiles + tile, (uint32_t)len);
+            const uint32_t at = wl.cur ? atomicAdd(wl.cur + cs, (uint32_t)len) : atomicAdd(a.cursors + cs * a.n_tiles + tile, (uint32_t)len);
             if ((int64_t)at + len > tb) { atomicOr(a.status, 1); return; }
             uint8_t* dst = c.data + (int64_t)slot * c.capacity + tile * tb + at;
             string_write(f.kind, p, sp, dst, lutf);
@@ -135,7 +152,7 @@ __device__ void walk_prim(const WalkArgs& a, const cbx_walk_node& nd, int off, i
             view.w = (uint32_t)((tile & (tpb - 1)) * tb + at);
         }
         ((u32x4*)c.values)[(int64_t)slot * a.pitch + r] = view;
-        walk_set_valid(c.validity, (int64_t)slot * a.n_tiles + tile, lane);
+        walk_set_valid(a, wl, c.validity, f.column, slot, tile, lane);
         if (nd.dep_slot >= 0 && !element) {   // Right(s): the handler key it equals (occurs_mappings)
             int key = 0;
             uint8_t buf[64];
@@ -163,7 +180,7 @@ __device__ void walk_prim(const WalkArgs& a, const cbx_walk_node& nd, int off, i
     if (w == 4) ((uint32_t*)c.values)[at] = (uint32_t)x.lo;
     else if (w == 8) ((uint64_t*)c.values)[at] = x.lo;
     else ((u32x4*)c.values)[at] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
-    walk_set_valid(c.validity, (int64_t)slot * a.n_tiles + tile, lane);
+    walk_set_valid(a, wl, c.validity, f.column, slot, tile, lane);
     if (nd.dep_slot >= 0 && !element) {   // Left(Number.intValue)
         const Val dv = decode_count_int(f, p);
         if (dv.valid) dep[nd.dep_slot] = WalkDep{1, (int32_t)dv.lo};
@@ -172,7 +189,7 @@ __device__ void walk_prim(const WalkArgs& a, const cbx_walk_node& nd, int off, i
 
 // The walk of one record (extractRecord's getGroupValues / extractArray / extractValue).
 // seg: the active segment redefine (-1 none).
-__device__ void walk_record(const WalkArgs& a, const uint8_t* rec, int avail, int seg, int64_t r, int lane) {
+__device__ void walk_record(const WalkArgs& a, const WalkLds& wl, const uint8_t* rec, int avail, int seg, int64_t r, int lane) {
     WalkFrame st[kWalkDepth];
     WalkDep dep[kWalkDeps];
     for (int i = 0; i < kWalkDeps; i++) dep[i] = WalkDep{0, 0};
@@ -197,7 +214,7 @@ __device__ void walk_record(const WalkArgs& a, const uint8_t* rec, int avail, in
                     sp++;
                     continue;
                 }
-                walk_prim(a, nd, fr.off, slot, rec, avail, r, lane, dep, true);
+                walk_prim(a, wl, nd, fr.off, slot, rec, avail, r, lane, dep, true);
                 fr.off += nd.data_size;
                 fr.cur++;
                 continue;
@@ -229,7 +246,7 @@ __device__ void walk_record(const WalkArgs& a, const uint8_t* rec, int avail, in
             if (ccol >= 0) {
                 const DevColumn c = ldc(a.cols + ccol);
                 ((int32_t*)c.values)[(int64_t)fr.slot * a.pitch + r] = cnt;
-                walk_set_valid(c.validity, (int64_t)fr.slot * a.n_tiles + r / kWave, lane);
+                walk_set_valid(a, wl, c.validity, ccol, fr.slot, r / kWave, lane);
             }
             if (sp + 1 >= kWalkDepth) { atomicOr(a.status, 2); return; }
             st[sp + 1] = WalkFrame{ci, 1, 0, cnt, fr.off, fr.off, fr.slot};
@@ -247,43 +264,67 @@ __device__ void walk_record(const WalkArgs& a, const uint8_t* rec, int avail, in
             sp++;
             continue;
         }
-        walk_prim(a, ch, fr.off, fr.slot, rec, avail, r, lane, dep, false);
+        walk_prim(a, wl, ch, fr.off, fr.slot, rec, avail, r, lane, dep, false);
         if (!(ch.flags & CBX_W_REDEFINED)) fr.off += ch.actual_size;
         fr.cur = ch.next;
     }
 }
 
 __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
     const int lane = threadIdx.x & 63;
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n_rec; r += (int64_t)gridDim.x * blockDim.x) {
-        int64_t base;
-        int avail;
-        if (a.rec_off) { base = a.rec_off[r]; avail = a.rec_len[r]; }
-        else { base = r * (int64_t)a.stride; avail = a.stride; }
-        const uint8_t* rec = a.data + base;
-        int seg = -1;
-        if (a.rec_seg) seg = a.rec_seg[r];
-        else if (a.segmap) {
-            const int k = segment_key(a.segmap, a.lut, a.fields, rec, avail, a.start_off);
-            if (k >= 0) seg = a.segmap->key_segment[k];
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    WalkLds wl{nullptr, nullptr};
+    if (a.vlds) {
+        wl.vw = (uint64_t*)(wsm + wid * a.wave_lds);
+        wl.cur = (uint32_t*)(wsm + wid * a.wave_lds + 8 * a.n_vslots);
+        for (int i = lane; i < a.n_vslots; i += kWave) wl.vw[i] = 0;
+        for (int i = lane; i < a.n_sslots; i += kWave) wl.cur[i] = 0;
+        wave_sync_lds();
+    }
+    // one wave per tile of 64 records (lane = record): every lane of the wave takes part in the
+    // tile's flush of the LDS words, records past the batch included
+    for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid; tile < a.n_tiles; tile += (int64_t)gridDim.x * (blockDim.x >> 6)) {
+        const int64_t r = tile * kWave + lane;
+        if (r < a.n_rec) {
+            int64_t base;
+            int avail;
+            if (a.rec_off) { base = a.rec_off[r]; avail = a.rec_len[r]; }
+            else { base = r * (int64_t)a.stride; avail = a.stride; }
+            const uint8_t* rec = a.data + base;
+            int seg = -1;
+            if (a.rec_seg) seg = a.rec_seg[r];
+            else if (a.segmap) {
+                const int k = segment_key(a.segmap, a.lut, a.fields, rec, avail, a.start_off);
+                if (k >= 0) seg = a.segmap->key_segment[k];
+            }
+            if (a.seg_col >= 0) {
+                const DevColumn c = ldc(a.cols + a.seg_col);
+                ((int32_t*)c.values)[r] = seg;
+                walk_set_valid(a, wl, c.validity, a.seg_col, 0, tile, lane);
+            }
+            if (a.fid_col >= 0) {
+                const DevColumn c = ldc(a.cols + a.fid_col);
+                ((int32_t*)c.values)[r] = a.file_id;
+                walk_set_valid(a, wl, c.validity, a.fid_col, 0, tile, lane);
+            }
+            if (a.rid_col >= 0) {
+                const DevColumn c = ldc(a.cols + a.rid_col);
+                ((int64_t*)c.values)[r] = a.rec_id ? a.rec_id[r] : a.first_record_id + (a.rec_id_base ? *a.rec_id_base : 0) + r;
+                walk_set_valid(a, wl, c.validity, a.rid_col, 0, tile, lane);
+            }
+            walk_record(a, wl, rec, avail, seg, r, lane);
         }
-        const int64_t tile = r / kWave;
-        if (a.seg_col >= 0) {
-            const DevColumn c = ldc(a.cols + a.seg_col);
-            ((int32_t*)c.values)[r] = seg;
-            walk_set_valid(c.validity, tile, lane);
+        if (a.vlds) {   // the tile's words: one plain store each (this wave owns them), then cleared
+            wave_sync_lds();
+            for (int i = lane; i < a.n_vslots; i += kWave) {
+                const DevColumn c = ldc(a.cols + a.vslot_col[i]);
+                c.validity[(int64_t)a.vslot_slot[i] * a.n_tiles + tile] = wl.vw[i];
+                wl.vw[i] = 0;
+            }
+            for (int i = lane; i < a.n_sslots; i += kWave) wl.cur[i] = 0;
+            wave_sync_lds();
         }
-        if (a.fid_col >= 0) {
-            const DevColumn c = ldc(a.cols + a.fid_col);
-            ((int32_t*)c.values)[r] = a.file_id;
-            walk_set_valid(c.validity, tile, lane);
-        }
-        if (a.rid_col >= 0) {
-            const DevColumn c = ldc(a.cols + a.rid_col);
-            ((int64_t*)c.values)[r] = a.rec_id ? a.rec_id[r] : a.first_record_id + (a.rec_id_base ? *a.rec_id_base : 0) + r;
-            walk_set_valid(c.validity, tile, lane);
-        }
-        walk_record(a, rec, avail, seg, r, lane);
     }
 }
 

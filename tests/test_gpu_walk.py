@@ -13,20 +13,8 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from oracle import reader_oracle as RO  # noqa: E402
-
-NESTED = """
-       01  REC.
-           05  SEG         PIC X(1).
-           05  N-OUT       PIC 9(1).
-           05  OUTER       OCCURS 0 TO 3 TIMES DEPENDING ON N-OUT.
-               10  N-IN    PIC 9(1).
-               10  KIND    PIC X(2).
-               10  INNER   OCCURS 1 TO 4 TIMES DEPENDING ON N-IN.
-                   15  AMT   PIC S9(5) COMP-3.
-                   15  NAME  PIC X(3).
-           05  TAIL-NUM    PIC 9(4) COMP.
-           05  TAIL-TXT    PIC X(6).
-"""
+from cobrix_amd.synth import WALK_NESTED_COPYBOOK as NESTED, _ebcdic, rdw_file  # noqa: E402
+from cobrix_amd.synth import walk_nested_record as nested_record  # noqa: E402
 
 MAPPED = """
        01  REC.
@@ -42,41 +30,6 @@ MAPPED = """
 def _gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-
-
-def _ebcdic(s: str) -> bytes:
-    return s.encode("cp037")
-
-
-def nested_record(rnd: random.Random, var_size: bool) -> bytes:
-    """One NESTED record: counts sometimes out of range or non-numeric (the reference then takes the
-    maximum), the arrays' bytes as the layout variant lays them out."""
-    n_out = rnd.choice([0, 1, 2, 3, 3, 7])
-    b = bytearray(_ebcdic(rnd.choice("ABC")))
-    b += bytes([0xF0 + n_out]) if rnd.random() < 0.95 else b"\x40"
-    eff_out = n_out if 0 <= n_out <= 3 else 3
-    for i in range(3):
-        if var_size and i >= eff_out:
-            break
-        n_in = rnd.choice([1, 2, 3, 4, 0, 9])
-        b += bytes([0xF0 + n_in])
-        b += _ebcdic(rnd.choice(["AA", "BB", "  ", "ZZ"]))
-        eff_in = n_in if 1 <= n_in <= 4 else 4
-        for j in range(4):
-            if var_size and j >= eff_in:
-                break
-            dg = [int(c) for c in f"{rnd.randrange(100000):05d}"]
-            sign = rnd.choice([0x0C, 0x0D, 0x0F, 0x0A])   # 0x0A: a bad sign nibble -> null
-            b += bytes([dg[0] << 4 | dg[1], dg[2] << 4 | dg[3], dg[4] << 4 | sign])
-            b += _ebcdic(rnd.choice(["ABC", "X  ", "   ", "Q1 "]))
-    b += rnd.randrange(65536).to_bytes(2, "big")
-    b += _ebcdic(rnd.choice(["TAIL  ", "T", "      "]).ljust(6))
-    cut = len(b) if rnd.random() < 0.85 else rnd.randint(1, len(b))
-    return bytes(b[:cut])
-
-
-def rdw_file(recs) -> bytes:
-    return b"".join(bytes([0, 0, len(r) & 0xFF, len(r) >> 8]) + r for r in recs)
 
 
 def _reader(copybook: str, options: dict, **params):
