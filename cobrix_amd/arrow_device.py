@@ -18,7 +18,10 @@ copy, no repacking:
 * an OCCURS DEPENDING ON array in the list layout: a LargeListView "+vL" per field (offsets = the
   array's int64 offsets column, sizes = its element counts widened to int64 on the device, nulls
   where the array's segment is not the record's) over the packed child elements;
-* generated File_Id / Record_Id / Seg_IdN columns first, as the reference's schema has them.
+* generated File_Id / Record_Id / Seg_IdN columns first, as the reference's schema has them; the
+  with_input_file_name_col column as a dictionary-encoded Utf8 (one entry, zero indices);
+* a Utf8View's variadic buffer-sizes buffer is host memory (metadata the importer reads on the
+  CPU); every other buffer is the decode's device memory.
 device_type is ARROW_DEVICE_ROCM (10) with the tensors' device id; the export synchronises the
 decode stream, so sync_event is NULL (the data is ready).  The export owns references to the
 batch's tensors until both release callbacks ran.
@@ -121,9 +124,10 @@ class _Node:
     """One exported array: its format, buffers (device pointers), length and children."""
 
     def __init__(self, fmt: str, name: str, length: int, buffers: List[int], children: List["_Node"] = (),
-                 keep: List[Any] = (), nullable: bool = True):
+                 keep: List[Any] = (), nullable: bool = True, dictionary: Optional["_Node"] = None):
         self.fmt, self.name, self.length = fmt, name, length
         self.buffers, self.children, self.keep, self.nullable = list(buffers), list(children), list(keep), nullable
+        self.dictionary = dictionary   # dictionary-encoded: fmt is the index type, this the values
 
     def schema(self) -> ArrowSchema:
         s = ArrowSchema()
@@ -135,8 +139,11 @@ class _Node:
         s.flags = ARROW_FLAG_NULLABLE if self.nullable else 0
         s.n_children = len(kids)
         s.children = ctypes.cast(arr, ctypes.POINTER(ctypes.POINTER(ArrowSchema)))
+        dic = self.dictionary.schema() if self.dictionary is not None else None
+        if dic is not None:
+            s.dictionary = ctypes.pointer(dic)
         s.release = _release_schema
-        s.private_data = _register([fmt, name, kids, arr])
+        s.private_data = _register([fmt, name, kids, arr, dic])
         return s
 
     def array(self) -> ArrowArray:
@@ -151,8 +158,11 @@ class _Node:
         a.n_children = len(kids)
         a.buffers = ctypes.cast(bufs, ctypes.POINTER(ctypes.c_void_p))
         a.children = ctypes.cast(karr, ctypes.POINTER(ctypes.POINTER(ArrowArray)))
+        dic = self.dictionary.array() if self.dictionary is not None else None
+        if dic is not None:
+            a.dictionary = ctypes.pointer(dic)
         a.release = _release_array
-        a.private_data = _register([kids, karr, bufs, self.keep])
+        a.private_data = _register([kids, karr, bufs, self.keep, dic])
         return a
 
 
@@ -201,8 +211,9 @@ def _column_nodes(batch, ci: int, name: str) -> List[_Node]:
             cap, bb = c["capacity"], max(1, c["buffer_bytes"])
             region = c["data"].data_ptr() + s * cap
             n_buf = max(1, (cap + bb - 1) // bb)
-            sizes = torch.tensor([min(bb, cap - k * bb) for k in range(n_buf)], dtype=torch.int64,
-                                 device=c["data"].device)
+            # the variadic buffer sizes are metadata a consumer reads on the host while it imports the
+            # array (to size the data buffers): host memory, unlike every data buffer
+            sizes = torch.tensor([min(bb, cap - k * bb) for k in range(n_buf)], dtype=torch.int64)
             bufs = [vptr, c["views"].data_ptr() + 16 * s * pitch] + [region + k * bb for k in range(n_buf)] + \
                 [sizes.data_ptr()]
             out.append(_Node("vu" if ot == N.O_STRING else "vz", nm, n, bufs, keep=[c, sizes]))
@@ -217,6 +228,19 @@ def _column_nodes(batch, ci: int, name: str) -> List[_Node]:
             fmt, w = _prim_format(info)
             out.append(_Node(fmt, nm, n, [vptr, c["values"].data_ptr() + w * s * pitch], keep=[c]))
     return out
+
+
+def _file_name_node(input_file, n: int, dev) -> _Node:
+    """The input-file-name column: int32 indices (all 0) over a one-entry Utf8 dictionary, both on
+    the batch's device."""
+    import torch
+    name, value = input_file
+    raw = value.encode("utf-8")
+    idx = torch.zeros(max(1, n), dtype=torch.int32, device=dev)
+    offs = torch.tensor([0, len(raw)], dtype=torch.int32, device=dev)
+    data = torch.tensor(list(raw) or [0], dtype=torch.uint8, device=dev)
+    dic = _Node("u", "", 1, [0, offs.data_ptr(), data.data_ptr()], keep=[offs, data])
+    return _Node("i", name, n, [0, idx.data_ptr()], keep=[idx], dictionary=dic)
 
 
 def _column_name(plan, ci: int) -> str:
@@ -254,6 +278,12 @@ def export_device(batch, generated_first: bool = True) -> Tuple[ArrowDeviceArray
     kids: List[_Node] = []
     for ci in order:
         kids += _column_nodes(batch, ci, _column_name(plan, ci))
+    if getattr(batch, "input_file", None) is not None and generated_first:
+        # with_input_file_name_col: a dictionary-encoded Utf8 column (one entry, n zero indices), in
+        # the position the batch's generated fields give it (DecodedBatch.generated)
+        names = [nm for nm, _ in batch.generated(lambda ci: ci)]
+        pos = names.index(batch.input_file[0])
+        kids.insert(pos, _file_name_node(batch.input_file, batch.n_rec, dev))
     if dev is not None and dev.type == "cuda":
         torch.cuda.synchronize(dev)
     root = _Node("+s", "", batch.n_rec, [0], kids, nullable=False)

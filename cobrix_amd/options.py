@@ -10,8 +10,9 @@ a job switching to it keeps its `spark.read.format("cobol").option(...)` calls:
   * ReaderParameters mapping        SC/source/DefaultSource.scala:141-209
 
 (SC = spark-cobol/src/main/scala/za/co/absa/cobrix/spark/cobol/.)  Options of subsystems outside
-the accelerated path (custom record header parsers / extractors, record_length_field, input file
-name columns) raise UnsupportedOption instead of being dropped.
+the accelerated path (custom record header parsers / extractors, multiple copybooks) raise
+UnsupportedOption instead of being dropped; the reference's option-combination checks
+(validateSparkCobolOptions) raise ValueError as its IllegalArgumentException does.
 """
 from __future__ import annotations
 
@@ -41,7 +42,6 @@ KNOWN = {
 UNSUPPORTED = {
     "record_header_parser": "custom record header parsers",
     "record_extractor": "custom raw record extractors",
-    "with_input_file_name_col": "input file name columns",
     "copybooks": "multiple copybooks (Copybook.merge)",
 }
 
@@ -117,6 +117,54 @@ def segment_redefine_parents(opts: Mapping[str, str]) -> Dict[str, str]:
     return out
 
 
+def _flag(opts: Mapping[str, str], key: str) -> bool:
+    return _bool(opts.get(key, "false"), key)
+
+
+# options that cannot accompany `record_extractor` / `record_length` / `is_text`
+# (CobolParametersParser.validateSparkCobolOptions, :495-610), in the reference's order
+_NOT_WITH_EXTRACTOR = ("is_text", "record_length", "is_record_sequence", "is_xcom", "is_rdw_big_endian",
+                       "is_rdw_part_of_record_length", "rdw_adjustment", "record_length_field",
+                       "record_header_parser", "rhp_additional_info")
+_NOT_WITH_RECORD_LENGTH = ("is_text", "is_record_sequence", "is_xcom", "is_rdw_big_endian",
+                           "is_rdw_part_of_record_length", "rdw_adjustment", "record_length_field",
+                           "record_header_parser", "rhp_additional_info")
+_NOT_WITH_TEXT = ("is_rdw_big_endian", "is_rdw_part_of_record_length", "rdw_adjustment", "is_xcom",
+                  "record_length", "record_header_parser", "rhp_additional_info")
+
+
+def validate_options(opts: Mapping[str, str]) -> None:
+    """validateSparkCobolOptions (CobolParametersParser.scala:473-620): option combinations the
+    reference rejects with IllegalArgumentException (ValueError here), checked before any reader
+    is built.  `is_text` counts as set when it is "true" (the reference reads it as a boolean);
+    the other options count when present, whatever their value (`params.contains`)."""
+    is_text = _flag(opts, "is_text")
+    # a "record sequence" for the input-file-name column (:474-479)
+    is_seq = (_flag(opts, "is_xcom") or _flag(opts, "is_record_sequence") or _flag(opts, "variable_size_occurs")
+              or "file_start_offset" in opts or "file_end_offset" in opts or "record_length_field" in opts)
+
+    def clash(lead: str, keys) -> None:
+        bad = [k for k in keys if (is_text if k == "is_text" else k in opts)]
+        if bad:
+            raise ValueError(f"Option '{lead}' and {', '.join(bad)} cannot be used together.")
+
+    if "record_extractor" in opts:
+        clash("record_extractor", _NOT_WITH_EXTRACTOR)
+    if "record_length" in opts:
+        clash("record_length", _NOT_WITH_RECORD_LENGTH)
+    if segment_redefine_parents(opts) and segment_levels(opts):
+        raise ValueError("Options 'segment-children:*' cannot be used with 'segment_id_level*' or 'segment_id_root' "
+                         "since ID fields generation is not supported for hierarchical records reader.")
+    # (the message names a custom record extractor, the condition does not test for one: as in :581)
+    if not is_seq and "with_input_file_name_col" in opts:
+        raise ValueError("Option 'with_input_file_name_col' is supported only when one of this holds: "
+                         "'is_record_sequence' = true or 'variable_size_occurs' = true or one of these options is set: "
+                         "'record_length_field', 'file_start_offset', 'file_end_offset' or a custom record extractor "
+                         "is specified")
+    if is_text:
+        clash("is_text", _NOT_WITH_TEXT)
+
+
 def is_variable_length(opts: Mapping[str, str]) -> bool:
     """parseVariableLengthParameters (:242-290): which options select VarLenNestedReader."""
     if "record_length_field" in opts and ("is_record_sequence" in opts or "is_xcom" in opts):
@@ -133,6 +181,8 @@ def parse_options(options: Mapping[str, object]) -> Tuple[ReaderParameters, bool
     Returns (ReaderParameters, variable_length) where variable_length says whether the reference
     would build a VarLenNestedReader (DefaultSource.buildEitherReader, :72-81)."""
     opts = {str(k): str(v) for k, v in options.items()}
+    var_len = is_variable_length(opts)   # parseVariableLengthParameters runs before the validation
+    validate_options(opts)
     pedantic = _bool(opts.get("pedantic", "false"), "pedantic")
     if pedantic:
         unknown = [k for k in opts if k not in KNOWN and not k.lower().startswith(("segment_id_level", "redefine-segment-id-map", "redefine_segment_id_map", "segment-children"))]
@@ -170,15 +220,10 @@ def parse_options(options: Mapping[str, object]) -> Tuple[ReaderParameters, bool
             raise ValueError(f"Code page class '{cls}' is not registered (register_code_page_class)")
         code_page_table = _CODE_PAGE_CLASSES[cls]
 
-    var_len = is_variable_length(opts)
     seg_field = opts.get("segment_field")
     levels = segment_levels(opts) if seg_field is not None else []
     filt = opts["segment_filter"].split(",") if (seg_field is not None and "segment_filter" in opts) else None
     parents = segment_redefine_parents(opts)
-    if parents and segment_levels(opts):
-        # CobolParametersParser.validateSparkCobolOptions (:568-574)
-        raise ValueError("Options 'segment-children:*' cannot be used with 'segment_id_level*' or 'segment_id_root' "
-                         "since ID fields generation is not supported for hierarchical records reader.")
     occurs = json.loads(opts.get("occurs_mappings", "{}"))
     non_terminals = [s for s in opts.get("non_terminals", "").split(",") if s]
     p = ReaderParameters(
@@ -217,5 +262,8 @@ def parse_options(options: Mapping[str, object]) -> Tuple[ReaderParameters, bool
         non_terminals=non_terminals,
         occurs_mappings=occurs,
         debug_fields_policy=debug_policy,
+        # VariableLengthParameters.inputFileNameColumn: only the variable-length readers generate the
+        # column (the fixed-length defaults carry "", DefaultSource.scala:141-162)
+        input_file_name_column=opts.get("with_input_file_name_col", "") if var_len else "",
     )
     return p, var_len

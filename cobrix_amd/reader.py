@@ -91,6 +91,9 @@ class ReaderParameters:
     # OCCURS DEPENDING ON arrays of numeric elements in the list layout (child elements packed per
     # record, absent elements unwritten; cobrix_hip.h CBX_F_LIST) instead of one slot row per element
     occurs_lists: bool = False
+    # with_input_file_name_col (ReaderParameters.inputFileNameColumn): a string column holding the
+    # name of the file each record came from (RecordExtractors.applyRecordPostProcessing)
+    input_file_name_column: str = ""
 
 
 @dataclass
@@ -111,6 +114,28 @@ class DecodedBatch:
         self.first_record_id = first_record_id
         self.collapse_root = collapse_root
         self.generate_record_id = generate_record_id
+        # with_input_file_name_col: (column name, the file's name) -- a per-batch constant column
+        self.input_file: Optional[Tuple[str, str]] = None
+
+    def generated(self, column, r=None) -> List[Tuple[str, Any]]:
+        """The generated leading fields of the rows: (schema name, value) pairs, value = column(ci)
+        for a decoded column, the file name for the input-file-name column.  Names follow the Spark
+        schema (File_Id, Record_Id, the file column, Seg_Id0..; SC/schema/CobolSchema.scala:99-110),
+        values follow the Row (RecordExtractors.applyRecordPostProcessing, :409-451) -- which without
+        generate_record_id puts the segment ids BEFORE the file name, so with both present the
+        Row's values sit one position off the schema's names, as in the reference."""
+        plan = self.plan
+        gen = [("File_Id", column(plan.file_id_column)), ("Record_Id", column(plan.record_id_column))] \
+            if self.generate_record_id else []
+        segs = [(f"Seg_Id{lv}", column(ci)) for lv, ci in enumerate(plan.seg_id_columns)]
+        if self.input_file is None:
+            return gen + segs
+        fname = (self.input_file[0], ("file", self.input_file[1]))
+        if self.generate_record_id or not segs:
+            return gen + [fname] + segs
+        names = [fname[0]] + [n for n, _ in segs]
+        values = [v for _, v in segs] + [fname[1]]
+        return list(zip(names, values))
 
     # ---- host views
     def _list_dense(self, ci: int):
@@ -326,12 +351,9 @@ class DecodedBatch:
         R0 = np.arange(n, dtype=np.int64)
         S0 = np.zeros(n, dtype=np.int64)
         names, arrays = [], []
-        if self.generate_record_id:
-            names += ["File_Id", "Record_Id"]
-            arrays += [column(plan.file_id_column), column(plan.record_id_column)]
-        for lv, ci in enumerate(plan.seg_id_columns):
-            names.append(f"Seg_Id{lv}")
-            arrays.append(column(ci))
+        for nm, v in self.generated(column):
+            names.append(nm)
+            arrays.append(_file_name_array(v[1], n) if isinstance(v, tuple) else v)
         for g in plan.copybook.ast.children:
             if not isinstance(g, cbk.Group):
                 continue
@@ -444,11 +466,8 @@ class DecodedBatch:
         for r in range(self.n_rec):
             recs = [(g.name, walk(g, r, [])) for g in plan.copybook.ast.children if isinstance(g, cbk.Group)]
             row: Dict[str, Any] = {}
-            if self.generate_record_id:
-                row["File_Id"] = self.cell(plan.file_id_column, 0, r)
-                row["Record_Id"] = self.cell(plan.record_id_column, 0, r)
-            for lv, ci in enumerate(plan.seg_id_columns):
-                row[f"Seg_Id{lv}"] = self.cell(ci, 0, r)
+            for nm, v in self.generated(lambda ci: ci):
+                row[nm] = v[1] if isinstance(v, tuple) else self.cell(v, 0, r)
             if self.collapse_root:
                 for _, v in recs:
                     row.update(v)
@@ -456,6 +475,13 @@ class DecodedBatch:
                 row.update({k: v for k, v in recs})
             rows.append(row)
         return rows
+
+
+def _file_name_array(name: str, n: int):
+    """The input-file-name column of a batch as Arrow: one dictionary entry (the name) and n zero
+    indices -- the value is constant per file, so the batch holds it once."""
+    import pyarrow as pa
+    return pa.DictionaryArray.from_arrays(pa.array(np.zeros(n, dtype=np.int32)), pa.array([name], pa.string()))
 
 
 def _alloc_columns(plan: DecodePlan, n_rec: int, slot_capacity: Sequence[int], device) -> Tuple[List[Dict[str, Any]], ctypes.Array]:
@@ -592,7 +618,8 @@ def reader_schema(cb: cbk.Copybook, params: ReaderParameters, variable_length: b
     (CP/reader/VarLenNestedReader.scala:223-225); the fixed-length reader neither."""
     levels = len(params.segment_id_levels) if (variable_length and params.segment_field) else 0
     return spark_schema(cb, params.schema_policy == "collapse_root",
-                        params.generate_record_id and variable_length, seg_id_levels=levels)
+                        params.generate_record_id and variable_length, seg_id_levels=levels,
+                        input_file_name_field=params.input_file_name_column if variable_length else "")
 
 
 def hier_root_keys(cb: cbk.Copybook, params: ReaderParameters) -> List[str]:
@@ -638,6 +665,7 @@ class HierBatch:
         self.table_base = [int(x) for x in np.concatenate([[0], np.cumsum(table_rows)])]
         self.offsets = offsets
         self.collapse_root, self.generate_record_id = collapse_root, generate_record_id
+        self.input_file: Optional[Tuple[str, str]] = None
         self.n_rec = table_rows[0]
         self.children = {id(g): [c for c in self.plan.segment_groups if c.parent_segment is g]
                          for g in self.plan.segment_groups}
@@ -675,6 +703,8 @@ class HierBatch:
             if self.generate_record_id:
                 row["File_Id"] = flat.cell(plan.file_id_column, 0, r)
                 row["Record_Id"] = flat.cell(plan.record_id_column, 0, r)
+            if self.input_file is not None:   # extractHierarchicalRecord: no segment ids (:384)
+                row[self.input_file[0]] = self.input_file[1]
             if self.collapse_root:
                 for _, v in recs:
                     row.update(v)
@@ -714,6 +744,9 @@ class HierBatch:
         if self.generate_record_id:
             names += ["File_Id", "Record_Id"]
             arrays += [column(plan.file_id_column).slice(0, self.n_rec), column(plan.record_id_column).slice(0, self.n_rec)]
+        if self.input_file is not None:
+            names.append(self.input_file[0])
+            arrays.append(_file_name_array(self.input_file[1], self.n_rec))
         for g in plan.copybook.ast.children:
             if not isinstance(g, cbk.Group) or g.parent_segment is not None:
                 continue
@@ -998,9 +1031,14 @@ class VarLenNestedReader(_BaseReader):
         off = torch.empty(cap, dtype=torch.int64, device=d_data.device)
         ln = torch.empty(cap, dtype=torch.int32, device=d_data.device)
         n = ctypes.c_int64(0)
-        N.check(N.load().cbx_frame_length_field(self.native.handle, d_data.data_ptr(), n_bytes, fi, p.start_offset,
-                                                p.end_offset, p.rdw_adjustment, off.data_ptr(), ln.data_ptr(), cap,
-                                                ctypes.byref(n), ctypes.c_void_p(st.cuda_stream)))
+        rc = N.load().cbx_frame_length_field(self.native.handle, d_data.data_ptr(), n_bytes, fi, p.start_offset,
+                                             p.end_offset, p.rdw_adjustment, off.data_ptr(), ln.data_ptr(), cap,
+                                             ctypes.byref(n), ctypes.c_void_p(st.cuda_stream))
+        if rc == N.CBX_E_STATE:
+            # the reference's IllegalStateException names the field (VRLRecordReader.scala:131-134);
+            # the C ABI knows only its byte position
+            raise N.CbxError(rc, f"Record length value of the field {p.record_length_field} must be an integral type.")
+        N.check(rc)
         return off[: n.value], ln[: n.value]
 
     # ---- selection + decode
@@ -1162,23 +1200,33 @@ class VarLenNestedReader(_BaseReader):
             offsets[s] = o.cpu().numpy()
         return HierBatch(flat, table_rows, offsets, self.collapse_root, self.params.generate_record_id)
 
-    def read(self, data: bytes, file_id: int = 0) -> DecodedBatch:
+    def _file_column(self, batch, input_file_name: str):
+        """with_input_file_name_col: the batch's file-name column (SimpleStream.inputFileName)."""
+        if self.params.input_file_name_column:
+            batch.input_file = (self.params.input_file_name_column, input_file_name)
+        return batch
+
+    def read(self, data: bytes, file_id: int = 0, input_file_name: str = "") -> DecodedBatch:
         """A whole file, as the reference reads it: sparse-index entries (when index generation
-        applies) each read by its own VarLenNestedIterator, concatenated in file order."""
+        applies) each read by its own VarLenNestedIterator, concatenated in file order.
+        input_file_name: the file's name for the with_input_file_name_col column."""
         t = self._device_file(data)
         off, ln, vb = self.frame_file(t, len(data))
         if self.hierarchical:
-            return self.read_hierarchical(t, vb, off, ln, file_id)
+            return self._file_column(self.read_hierarchical(t, vb, off, ln, file_id), input_file_name)
         entries = None
         if self.index_generation_needed() and not self.params.is_text:
             entries = self.generate_index(t, len(data), off, ln, file_id)
         sel = self.select(t, vb, off, ln, entries, file_id)
-        return self.decode_selected(t, vb, sel)
+        return self._file_column(self.decode_selected(t, vb, sel), input_file_name)
 
     def decode(self, data: bytes, seeds: Optional[Sequence[int]] = None, first_record_id: int = 0) -> DecodedBatch:
         """Frame + decode as one entry (no selection stage)."""
         t = self._device_file(data)
-        if self.params.is_text or self.var_occurs_extractor():
+        if self.params.is_text or self.var_occurs_extractor() or (
+                self.params.record_length_field is not None and not self.params.is_record_sequence):
+            # framings that are not seeded by RDW headers: text lines, VarOccursRecordExtractor,
+            # record_length_field (VRLRecordReader.fetchRecordUsingRecordLengthField)
             off, ln, vb = self.frame_file(t, len(data))
             return self.decode_device(t, vb, off, ln, first_record_id)
         off, ln = self.frame(t, len(data), seeds) if self.params.is_record_sequence else self.frame_fixed(t, len(data))

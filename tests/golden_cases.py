@@ -250,6 +250,21 @@ CASES: Dict[str, Dict[str, Any]] = {
                    options={"encoding": "ascii", "variable_size_occurs": "true",
                             "occurs_mappings": '{"DETAIL1":{"A":0,"B":1},"DETAIL2":{"A":1,"B":2}}'},
                    expected="test25_expected/test25.txt", schema="test25_expected/test25_schema.json", take=60),
+    "test10": dict(spec="SCT/source/integration/Test10NonTerminalsSpec.scala:38-70",
+                   copybook="test10_copybook.cob", data="test10_data/data.dat",
+                   options={"non_terminals": "NAME,ACCOUNT-NO", "encoding": "ascii"},
+                   expected="test10_expected/test10.txt", schema="test10_expected/test10_schema.json", take=60),
+    "test1b": dict(spec="SCT/source/integration/Test1bGeneratedFieldsSpec.scala:38-68",
+                   copybook="test1_copybook.cob", data="test1_data/example.bin",
+                   options={"generate_record_id": "true", "schema_retention_policy": "collapse_root"},
+                   expected="test1b_expected/test1b.txt", schema="test1b_expected/test1b_schema.json", take=60),
+    **{name: dict(spec=f"SCT/source/integration/Test24DebugModeSpec.scala:{lines}",
+                  copybook="test24_copybook.cob", data="test24_data/INTEGR.TYPES.NOV28.DATA.dat",
+                  options={"schema_retention_policy": "collapse_root", "floating_point_format": "IEEE754",
+                           "pedantic": "true", "debug": debug},
+                  expected=f"test24_expected/{name}.txt", schema=f"test24_expected/{name}_schema.json",
+                  sort=("ID",), take=20, na_fill=True)
+       for name, debug, lines in (("test24", "true", "39-93"), ("test24b", "raw", "95-149"))},
     "test19": dict(spec="SCT/source/integration/Test19DisplayNumParsingSpec.scala:32-75",
                    copybook="test19_display_num.cob", data="test19_display_num/data.dat",
                    options={"pedantic": "true", "generate_record_id": "true", "schema_retention_policy": "collapse_root"},
@@ -269,6 +284,9 @@ LAYOUTS = {
     "test16": ("test16_fix_len_segments.cob", {}, "test16_expected/test16_layout.txt"),
     "test17a": ("test17_hierarchical.cob", {}, "test17_expected/test17a_layout.txt"),
     "test19": ("test19_display_num.cob", {}, "test19_display_num_expected/test19_layout.txt"),
+    # Test24DebugModeSpec.scala:53-62, 109-118: the layout with the debug fields of each policy
+    "test24": ("test24_copybook.cob", dict(debug_fields_policy="hex"), "test24_expected/test24_layout.txt"),
+    "test24b": ("test24_copybook.cob", dict(debug_fields_policy="raw"), "test24_expected/test24b_layout.txt"),
 }
 
 

@@ -5,6 +5,7 @@ are printed at the schema scale; float/double goldens are Java's shortest round-
 """
 from __future__ import annotations
 
+import base64
 import json
 import os
 from decimal import Decimal
@@ -70,6 +71,10 @@ def _eq(a, g, where: str, na_fill: bool) -> List[str]:
         if na_fill and isinstance(g, (int, Decimal)) and g == 0:
             return []
         return [f"{where}: expected {g!r}, got null"]
+    if isinstance(g, str) and isinstance(a, (bytes, bytearray)):
+        # Spark's JSON writer prints BinaryType values base64-encoded (debug=raw fields, test24b)
+        got = base64.b64encode(bytes(a)).decode("ascii")
+        return [] if got == g else [f"{where}: {a!r} ({got}) != {g!r}"]
     if isinstance(g, str):
         return [] if a == g else [f"{where}: {a!r} != {g!r}"]
     if isinstance(a, np.float32):

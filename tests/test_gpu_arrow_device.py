@@ -52,8 +52,8 @@ def _host_copy(node, keep):
         bufs.append(ctypes.addressof(b))
 
     v = node.buffers
-    if f == "+s":
-        bufs.append(0)
+    if f == "+s" or not v[0]:
+        bufs.append(0)   # no validity bitmap (struct root, dictionary indices of a constant column)
     else:
         take(v[0], 8 * ((n + 63) // 64))
     if f in ("i", "f"):
@@ -73,7 +73,8 @@ def _host_copy(node, keep):
     elif f in ("vu", "vz"):
         take(v[1], 16 * n)
         k = len(v) - 3
-        sizes = np.frombuffer(_d2h(v[-1], 8 * k), dtype=np.int64)
+        # the variadic buffer sizes are host memory: read in place, as an importer does
+        sizes = np.frombuffer(ctypes.string_at(v[-1], 8 * k), dtype=np.int64).copy()
         for j in range(k):
             take(v[2 + j], int(sizes[j]))
         b = ctypes.create_string_buffer(sizes.tobytes(), 8 * k)
@@ -84,6 +85,10 @@ def _host_copy(node, keep):
         take(v[2], 8 * n)
     kids = [_host_copy(c, keep) for c in node.children]
     a = AD.ArrowArray()
+    if node.dictionary is not None:
+        dic = _host_copy(node.dictionary, keep)
+        keep.append(dic)
+        a.dictionary = ctypes.pointer(dic)
     karr = (ctypes.POINTER(AD.ArrowArray) * max(1, len(kids)))(*[ctypes.pointer(k) for k in kids])
     barr = (ctypes.c_void_p * max(1, len(bufs)))(*[b or None for b in bufs])
     keep += [kids, karr, barr]
@@ -130,9 +135,15 @@ def _check(batch, device_type=None):
     def inside(p):
         return any(a <= p < b for a, b in spans)
 
+    host = [(t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for nd in kids for t in _tensors(nd)
+            if isinstance(t, torch.Tensor) and not t.is_cuda]
+
     def walk(nd):
         for j, b in enumerate(nd.buffers):
-            if b and not (nd.fmt in ("vu", "vz") and j == len(nd.buffers) - 1) and not (nd.fmt == "+vL" and j == 2):
+            if nd.fmt in ("vu", "vz") and j == len(nd.buffers) - 1:
+                # the variadic buffer sizes: host memory the importer can read (cpu tensor)
+                assert any(a <= b < e for a, e in host), (nd.name, "buffer sizes not in host memory")
+            elif b and not (nd.fmt == "+vL" and j == 2) and nd.dictionary is None:
                 assert inside(b), (nd.name, nd.fmt, j)
         for c in nd.children:
             walk(c)
@@ -146,6 +157,13 @@ def _check(batch, device_type=None):
         # assertion's traceback would otherwise keep it alive until shutdown)
         del rb
         keep.clear()
+
+
+def _tensors(nd):
+    out = [t for t in nd.keep if isinstance(t, torch.Tensor)]
+    for c in nd.children:
+        out += _tensors(c)
+    return out
 
 
 def _compare(batch, rb):
@@ -216,3 +234,32 @@ def test_device_export_lists():
     batch = rd.decode_device(t, int(t.numel()), off, ln)
     assert any(c.list_array >= 0 for c in rd.plan.columns)
     _check(batch)
+
+
+@pytest.mark.parametrize("gen_id", [False, True])
+def test_device_export_input_file_column(gen_id):
+    """with_input_file_name_col (Test20InputFileNameSpec.scala:94-165): the file name column is a
+    dictionary-encoded Utf8 on the device, in the schema position the reference gives it (first, or
+    after File_Id / Record_Id)."""
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import VarLenNestedReader
+    opts = {"is_record_sequence": "true", "encoding": "ascii", "with_input_file_name_col": "F"}
+    if gen_id:
+        opts["generate_record_id"] = "true"
+    p, var_len = parse_options(opts)
+    assert var_len
+    rd = VarLenNestedReader(GC.copybook_text({"copybook": "test4_copybook.cob"}), p)
+    data = GC.data_bytes({"data": "test4_data/COMP.DETAILS.SEP30.DATA.dat"})
+    batch = rd.read(data, input_file_name="COMP.DETAILS.SEP30.DATA.dat")
+    from cobrix_amd import arrow_device as AD
+    da, schema, kids = AD.export_device(batch)
+    rb, keep = _import_host(da, schema, kids)
+    try:
+        names = rb.schema.names
+        assert names.index("F") == (2 if gen_id else 0)
+        col = rb.column(names.index("F"))
+        assert col.to_pylist() == ["COMP.DETAILS.SEP30.DATA.dat"] * batch.n_rec
+        _compare(batch, rb)
+    finally:
+        del rb
+        keep.clear()

@@ -180,6 +180,9 @@ def test_record_length_field_framing_vs_oracle(start, end, adj):
     exp = RO.var_len_rows(rd.copybook, raw, p)
     assert len(rows) == len(exp) == 3000
     assert rows == exp
+    # decode() (frame + decode as one entry, no selection stage) frames by the length field too
+    rows_d = rd.decode(raw).to_rows()
+    assert rows_d == exp
 
 
 def test_record_length_field_errors():
@@ -194,7 +197,9 @@ def test_record_length_field_errors():
     rd = VarLenNestedReader(LENFIELD_COPYBOOK, p)
     with pytest.raises(N.CbxError) as e:
         rd.read(raw)
-    assert e.value.code == N.CBX_E_STATE and "integral" in str(e.value)
+    assert e.value.code == N.CBX_E_STATE
+    # the reference's message names the field (VRLRecordReader.scala:131-134)
+    assert "Record length value of the field REC-LEN must be an integral type." in str(e.value)
     with pytest.raises(RuntimeError):
         RO.var_len_rows(rd.copybook, raw, p)
     p2, _ = parse_options({"record_length_field": "KIND"})
