@@ -106,6 +106,28 @@ def present_elements(plan, cols, n_rec: int):
     return out
 
 
+def absent_element_bytes(plan, cols, n_rec: int) -> int:
+    """Input bytes of OCCURS DEPENDING ON elements past each record's count (records keep every
+    element's bytes at max size: variable_size_occurs = false): the list layout's kernels never read
+    them, so they are part of the 8(d) input term but not of the bytes the decode must move."""
+    import torch
+    total, seen = 0, set()
+    for f in plan.fields:
+        if f.n_dims != 1:
+            continue
+        ai = f.dim_array[0]
+        ar = plan.arrays[ai]
+        if ai in seen or ar.dependee < 0 or ar.count_column < 0:
+            continue
+        seen.add(ai)
+        cnt = cols[ar.count_column]["values"][:n_rec].to(dtype=torch.int64)
+        hold = torch.ones_like(cnt, dtype=torch.bool)
+        if ar.segment >= 0 and plan.segment_column >= 0:
+            hold = cols[plan.segment_column]["values"][:n_rec] == ar.segment
+        total += int(((f.dim_count[0] - cnt) * hold).sum().item()) * int(f.dim_stride[0])
+    return total
+
+
 def algorithmic_bytes(plan, n_rec: int, in_bytes: int, payload: dict, present: dict) -> int:
     """input + Arrow output bytes (see the module docstring), independent of the layout
     the library writes."""
@@ -181,9 +203,12 @@ WORKLOADS = {
                    desc="SYN200: fixed-length 200-byte EBCDIC records, numeric mix (COMP, COMP-3, zoned DISPLAY "
                         "overpunch, IBM COMP-2, cp037 X(18)) -- BASELINE config C2",
                    data="synthetic (cobrix_amd/synth.py SYN200, seed 20261015+rank, 0.5% malformed numerics)"),
-    "synstr200": dict(records=50_000_000, config="C3", strings="offsets",
+    # C3 is quoted on 64 GB strong-scaled: 320 M records over the job, decoded in
+    # batches whose int32 Utf8 offsets fit (an Arrow chunked array: one chunk per batch and column)
+    "synstr200": dict(records=320_000_000, config="C3", strings="offsets", strong=True,
+                      batch_records=50_000_000,
                       desc="SYNSTR200: fixed-length 200-byte records, 10 x PIC X(20) cp037 -> UTF-8, trim both "
-                           "-- BASELINE config C3",
+                           "-- BASELINE config C3 (64 GB strong-scaled over the job)",
                       data="synthetic (cobrix_amd/synth.py SYNSTR200: lengths 0-20, 25% accented, 10% leading "
                            "spaces, 1% control bytes)"),
     "rdw_narrow": dict(records=150_000_000, config="C4", strings="views",
@@ -210,11 +235,16 @@ def _layout_params(strings: str) -> dict:
 
 
 class _Fixed:
-    def __init__(self, name, n_rec, dev, rank, window, strings):
+    """A fixed-length shard resident in HBM, decoded as one call per batch of at most batch_records
+    records (every batch its own output columns: for the Utf8 layout one Arrow array per batch and
+    column -- a chunked array -- whose int32 offsets fit its slot region)."""
+
+    def __init__(self, name, n_rec, dev, rank, window, strings, batch_records=0, record_base=None):
         import torch
         from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters
         from cobrix_amd import synth
         lay = _layout_params(strings)
+        self.batch = batch_records if batch_records > 0 else n_rec
         if name == "syn200":
             cb, self.stride = synth.SYN200_COPYBOOK, synth.SYN200_RECORD_SIZE
             self.rec = synth.syn200(n_rec, seed=20261015 + rank, device=dev).view(-1)
@@ -226,21 +256,32 @@ class _Fixed:
         torch.cuda.synchronize()
         self.rd = FixedLenNestedReader(cb, params)
         self.n_rec, self.in_bytes, self.dev = n_rec, n_rec * self.stride, dev
-        self.record_base = rank * n_rec
-        self.shard_note = f"records [{rank} n, {rank + 1} n) of the job, Record_Id base static"
+        self.record_base = rank * n_rec if record_base is None else record_base
+        self.shard_note = f"records [{self.record_base}, {self.record_base + n_rec}) of the job, Record_Id base static"
+        if self.batch < n_rec:
+            self.shard_note += f"; {(n_rec + self.batch - 1) // self.batch} batches of <= {self.batch} records"
 
     def prepare(self, stream):
         from cobrix_amd import native as N
         from cobrix_amd.reader import _alloc_columns, string_capacity
         self.L, self.h, self.stream = N.load(), self.rd.native.handle, ctypes.c_void_p(stream.cuda_stream)
-        self.cols, self.cs = _alloc_columns(self.rd.plan, self.n_rec, string_capacity(self.rd.native, self.n_rec),
-                                            self.dev)
+        # parts: (first record, records, columns, cbx_column table) per batch
+        self.parts = []
+        for r0 in range(0, self.n_rec, self.batch):
+            m = min(self.batch, self.n_rec - r0)
+            cols, cs = _alloc_columns(self.rd.plan, m, string_capacity(self.rd.native, m), self.dev)
+            self.parts.append((r0, m, cols, cs))
+        self.cols, self.cs = self.parts[0][2], self.parts[0][3]
+
+    def calls_per_step(self) -> int:
+        return len(self.parts)
 
     def step(self, world=1):
         from cobrix_amd import native as N
         # fixed-length shards: rank r holds records [r n, (r + 1) n) -- the Record_Id base is static
-        N.check(self.L.cbx_decode_fixed(self.h, self.rec.data_ptr(), self.n_rec, self.stride, 0, self.record_base,
-                                        self.cs, self.stream))
+        for r0, m, _, cs in self.parts:
+            N.check(self.L.cbx_decode_fixed(self.h, self.rec.data_ptr() + r0 * self.stride, m, self.stride, 0,
+                                            self.record_base + r0, cs, self.stream))
         return None
 
     def verify(self, world):
@@ -606,11 +647,15 @@ def _cpu_baseline(workload: str, seconds: float = 10.0):
     data, fr, t_frame, _ = make(n, 100)
     dt1, nrec = timed(data, fr, t_frame, 1)
     nproc, quota = _cpu_counts()
-    T = int(os.environ.get("CBX_CPU_THREADS", str(min(64, nproc))))
+    # threads = the CPUs this process can actually use: nproc, capped by the cgroup quota (a quota of
+    # 16 CPUs runs 64 threads on at most 16 CPUs) and at 64
+    usable = min(64, nproc, max(1, int(quota)) if quota else nproc)
+    T = int(os.environ.get("CBX_CPU_THREADS", str(usable)))
     dtT, _ = timed(data, fr, t_frame, T)
     unit_n = {"syn200": "SYN200 records", "synstr200": "SYNSTR200 records", "rdw_narrow": "RDW records",
               "wide_odo": "root records (+ children)"}[workload]
-    return {"value": round(len(data) / dtT / 1e9, 6), "unit": "GB/s", "cores": T, "kind": "port",
+    return {"value": round(len(data) / dtT / 1e9, 6), "unit": "GB/s", "cores": min(T, usable), "threads": T,
+            "kind": "port",
             "value_1_core": round(len(data) / dt1 / 1e9, 6),
             "nproc": nproc, "cgroup_cpu_quota": quota,
             "sample": f"{n} {unit_n} ({len(data) / 1e6:.1f} MB, {nrec} records) through oracle/cobrix_oracle.c "
@@ -722,6 +767,13 @@ def main():
     W = WORKLOADS[args.workload]
     n_req = args.records or W["records"]
     strings = args.strings or W["strings"]
+    strong = bool(W.get("strong"))
+    rec_base = None
+    if strong:   # the job's records split over the ranks (strong scaling): rank r takes a contiguous range
+        rec_base = n_req * rank // world
+        n_req = n_req * (rank + 1) // world - rec_base
+    # a batch per call: Utf8 int32 offsets must fit each slot region (<= 40 UTF-8 bytes per X(20) value)
+    batch = W.get("batch_records", 0) if strings == "offsets" else 0
 
     def progress(msg):
         if rank == 0:
@@ -729,7 +781,7 @@ def main():
 
     progress(f"generating {n_req} records per GPU on {dev} (world {world})")
     if args.workload in ("syn200", "synstr200"):
-        job = _Fixed(args.workload, n_req, dev, rank, args.window, strings)
+        job = _Fixed(args.workload, n_req, dev, rank, args.window, strings, batch, rec_base)
     else:
         job = _VarLen(args.workload, n_req, dev, rank, world, args.window, strings, args.occurs == "lists",
                       args.seed_mb)
@@ -760,10 +812,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     N.check(L.cbx_plan_check(h, job.stream))
-    dec = (ctypes.c_float * args.steps)()
-    fix = (ctypes.c_float * args.steps)()
+    calls = args.steps * (job.calls_per_step() if hasattr(job, "calls_per_step") else 1)
+    dec = (ctypes.c_float * calls)()
+    fix = (ctypes.c_float * calls)()
     nc = ctypes.c_int32()
-    N.check(L.cbx_plan_kernel_times(h, dec, fix, args.steps, ctypes.byref(nc)))
+    N.check(L.cbx_plan_kernel_times(h, dec, fix, calls, ctypes.byref(nc)))
     N.check(L.cbx_plan_set_profiling(h, 0))
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -782,12 +835,21 @@ def main():
     ms_per_step = elapsed / steps * 1e3
     gbs = job_bytes / (elapsed / steps) / 1e9
     recs_per_s = job_recs / (elapsed / steps)
-    present = present_elements(plan, job.cols, n_rec)
-    payload = string_payload(plan, job.cols, n_rec)
-    alg = algorithmic_bytes(plan, n_rec, job.in_bytes, payload, present)
-    lay = layout_bytes(plan, job.cols, n_rec, job.in_bytes, payload, present)
-    dec_avg_ms = sum(dec[: nc.value]) / max(1, nc.value)
-    fix_avg_ms = sum(fix[: nc.value]) / max(1, nc.value)
+    # per batch (a fixed-length job decodes its shard in batches; the others in one call), summed
+    parts = getattr(job, "parts", None) or [(0, n_rec, job.cols, None)]
+    alg = lay = absent = 0
+    has_lists = any(c.list_array >= 0 for c in plan.columns)
+    for _, m, cols, _ in parts:
+        present = present_elements(plan, cols, m)
+        payload = string_payload(plan, cols, m)
+        in_b = m * job.stride if len(parts) > 1 else job.in_bytes
+        alg += algorithmic_bytes(plan, m, in_b, payload, present)
+        lay += layout_bytes(plan, cols, m, in_b, payload, present)
+        # OCCURS lists: the 8(d) input term counts every record byte, absent ODO elements included;
+        # the bytes the kernels must move leave those out (reported beside, never as `frac`)
+        absent += absent_element_bytes(plan, cols, m) if has_lists else 0
+    dec_avg_ms = sum(dec[: nc.value]) / max(1, args.steps)     # per step: every call of the step
+    fix_avg_ms = sum(fix[: nc.value]) / max(1, args.steps)
     achieved = alg / (dec_avg_ms * 1e-3) / 1e9
     kind = ctypes.c_int32(0)
     N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
@@ -825,12 +887,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": W["data"],
             "config": {"workload": W["desc"], "baseline_config": W["config"],
                        "records_per_gpu": n_rec, "input_bytes_per_gpu": job.in_bytes,
+                       **({"job_records": int(W["records"] if not args.records else args.records),
+                           "batches_per_gpu": len(parts), "batch_records": job.batch} if len(parts) > 1 or strong else {}),
                        "input_gb_per_gpu": round(job.in_bytes / 1e9, 3), "job_input_bytes": int(job_bytes),
                        "output_columns": plan.n_columns, "parallelism": f"dp{world}",
                        "shard": job.shard_note,
@@ -846,6 +910,11 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "frac_of_measured_peak": round(achieved / HBM_MEASURED_GBS, 4),
                          "algorithmic_bytes_per_launch": alg,
+                         **({"absent_element_bytes": absent, "moved_bytes_per_launch": alg - absent,
+                             "frac_moved_bytes": round((alg - absent) / (dec_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "note": "8(d) counts the input records whole (absent ODO elements included); "
+                                     "frac_moved_bytes counts what the kernels must read and write"}
+                            if absent else {}),
                          "layout_bytes_per_launch": lay, "layout_overhead": lay - alg,
                          "timing": "HIP events on the launch stream (cbx_plan_kernel_times), average of the timed steps",
                          "traffic": traffic, "traffic_source": traffic_src},

@@ -636,9 +636,6 @@ def check_hierarchical(cb: cbk.Copybook, params: ReaderParameters, plan: DecodeP
     segs = plan.segment_groups
     if len(segs) > 16:
         raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: more than 16 segment redefines")
-    if params.start_offset != 0:
-        # extractChildren decodes child segments without the record start offset (:310), the root with it
-        raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records with record_start_offset")
     ids: Dict[str, List[str]] = {}
     for sid, grp in params.segment_id_redefine_map.items():
         ids.setdefault(cbk._transform_identifier(grp), []).append(sid)
@@ -1187,6 +1184,19 @@ class VarLenNestedReader(_BaseReader):
                                   ctypes.byref(prm), ctypes.byref(cs), parent_row.data_ptr(), rows, ctypes.byref(n_rows), sp))
         table_rows = [int(x) for x in rows]
         sel["n"], sel["struct"] = n_rows.value, cs
+        s0 = self.params.start_offset
+        if s0 and n_rows.value > table_rows[0]:
+            # extractHierarchicalRecord decodes the root record from offsetBytes = record_start_offset
+            # (VarLenHierarchicalIterator.scala:139-144) but each child segment at its group's own offset
+            # in the child's data, without it (RecordExtractors.scala:308-310): the child rows are decoded
+            # as records starting s0 bytes earlier and s0 bytes longer, so the decode's start offset
+            # lands on the child's first byte and its bound on the child's own length
+            kid_off = sel["rec_off"][table_rows[0]:n_rows.value]
+            if int(kid_off.min().item()) < s0:
+                raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a child segment record starts within "
+                                                      "record_start_offset bytes of the data")
+            kid_off -= s0
+            sel["rec_len"][table_rows[0]:n_rows.value] += s0
         flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
         base = np.concatenate([[0], np.cumsum(table_rows)]).astype(np.int64)
         offsets: Dict[int, np.ndarray] = {}

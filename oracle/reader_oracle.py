@@ -521,13 +521,20 @@ def hier_rows(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
     out: List[dict] = []
     for e in entries:
         raw = raw_records(cb, data, p, e)
+        # the root record from offsetBytes = record_start_offset (:139-144 -> :379-381); a child segment
+        # at its group's offset in its own data, without the start offset (extractChildren, :308-310)
         res = O.decode_records(cb, [r for _, r in raw], start_offset=p.start_offset, active_segments="*")
-        pos = 0
-        decoded = []   # per record: {id(group): dict}
-        tops_of = []
+        res0 = res if not p.start_offset else O.decode_records(cb, [r for _, r in raw], start_offset=0,
+                                                               active_segments="*")
+        pos = pos0 = 0
+        decoded = []   # per record: {id(group): dict}, decoded as a child (no start offset)
+        tops_of = []   # per record: the top-level groups, decoded as a root
         for _ in raw:
             gm: Dict[int, Any] = {}
             pos, tops = _full_record(res, pos, gm)
+            if res0 is not res:
+                gm = {}
+                pos0, _ = _full_record(res0, pos0, gm)
             decoded.append(gm)
             tops_of.append(tops)
 

@@ -129,8 +129,29 @@ def test_hier_unsupported_layouts():
     from cobrix_amd import native as N
     with pytest.raises(N.CbxError):   # a parent segment with two ids
         _reader({"redefine-segment-id-map:2": "DEPT => 2,8"})
-    with pytest.raises(N.CbxError):
-        _reader({"record_start_offset": "2"})
+
+
+@pytest.mark.parametrize("start", [3, 8])
+def test_hier_record_start_offset_vs_oracle(start):
+    """record_start_offset on hierarchical records: the root record is decoded from the start offset
+    (VarLenHierarchicalIterator.scala:139-144 -> RecordExtractors.scala:379-381), each child segment at
+    its group's offset in its own data, without it (extractChildren, RecordExtractors.scala:308-310).
+    Every record carries `start` leading bytes; segment ids are read after them (VRLRecordReader)."""
+    rnd = np.random.default_rng(start)
+    raw = hier_stream(4000, 11 + start, 0.8)
+    out, pos = bytearray(), 0
+    while pos < len(raw):   # insert the leading bytes into every RDW record
+        ln = raw[pos + 2] | raw[pos + 3] << 8
+        body = bytes(rnd.integers(0, 256, start, dtype=np.uint8)) + raw[pos + 4:pos + 4 + ln]
+        out += bytes([0, 0, len(body) & 0xFF, len(body) >> 8]) + body
+        pos += 4 + ln
+    for jit in (-1, 1):
+        rd, p = _reader({"record_start_offset": str(start)}, jit_min_records=jit)
+        rows = rd.read(bytes(out), file_id=2).to_rows()
+        exp = RO.var_len_rows(rd.copybook, bytes(out), p, file_id=2)
+        assert len(rows) == len(exp) > 100
+        bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
+        assert not bad, (jit, bad[:5], rows[bad[0]], exp[bad[0]])
 
 
 def test_hier_record_id_is_next_root():

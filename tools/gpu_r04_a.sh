@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-4 probe: LUT microbenchmark, the string-compose parity tests, the new goldens, C3 bench lines.
+set -u
+mkdir -p gpurun_out
+timeout -k 10 120 ./tools/ubench_lut 2000 > gpurun_out/ubench_lut.json 2>&1 || { cat gpurun_out/ubench_lut.json; exit 1; }
+cat gpurun_out/ubench_lut.json
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_golden.py tests/test_gpu_rdw.py tests/test_gpu_arrow_device.py -x -q --timeout 300 --timeout-method thread \
+  -k "two_byte or synstr200 or var_span or fuzz or test10 or test1b or test24 or test9 or length_field or device_export" > gpurun_out/t_r04a.log 2>&1
+rc=$?; tail -3 gpurun_out/t_r04a.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" gpurun_out/t_r04a.log | head -20; exit $rc; }
+for S in offsets views; do
+  timeout -k 10 300 python -u bench.py --workload synstr200 --strings $S --steps 10 --warmup 3 --no-cpu-baseline --no-end-to-end > gpurun_out/c3_$S.json 2> gpurun_out/c3_$S.err || { tail -5 gpurun_out/c3_$S.err; exit 1; }
+  python3 -c "import json; d=json.load(open('gpurun_out/c3_$S.json')); print('$S', d['ms_per_step'], d['kernel_ms'], d['roofline']['frac'])"
+done

@@ -19,7 +19,10 @@ import os
 import sys
 
 D = sys.argv[1]
-STAGED16 = ("cbx_jit_decode", "cbx_jit_count", "cbx_jit_list", "cbx::decode_kernel", "cbx::list_kernel")   # 16-byte/lane staged reads
+# kernels whose reads are 16-byte-per-lane streaming loads (register staging or LDS-DMA `buffer_load_dwordx4
+# ... lds`): FETCH_SIZE counts half of those bytes on gfx950 (MI355X_MICROARCH.md, HBM)
+STAGED16 = ("cbx_jit_decode", "cbx_jit_count", "cbx_jit_list", "cbx::decode_kernel", "cbx::list_kernel",
+            "cbx::rdw_wave_kernel")
 
 
 def base(name: str) -> str:
@@ -63,19 +66,21 @@ if dec:
     k = dec[0]
     # the bench's decode time (HIP events) covers the record kernel, the list kernels after it and,
     # in the Utf8 layout, the count pass and its scan before it
-    # the timed steps' window: after the record kernel's last warm-up launch, up to the end of its
-    # last timed launch; every part kernel launched inside it counts (per step), so list / count
-    # kernels that only run in the end-to-end pieces (smaller batches) are left out
+    # the timed steps' window: after the record kernel's last warm-up launch, up to the START of the
+    # record kernel's first launch after the timed steps (the first end-to-end piece), or the end of
+    # the trace -- so a step's part kernels on either side of its record kernel count (the Utf8 count
+    # pass before it, the list kernels after it, the last timed step's included), and those of the
+    # end-to-end pieces (smaller batches) do not
     w0 = bench.get("warmup", 0)
     sp = spans[k]
     lo = sp[w0 - 1][1] if w0 > 0 else 0
-    hi = sp[min(w0 + steps, len(sp)) - 1][1]
+    hi = sp[w0 + steps][0] if len(sp) > w0 + steps else float("inf")
     cand = [k] + [x for x in kernels if x.startswith(("cbx::list_kernel", "cbx_jit_list"))]
     if "cbx_jit_count" in kernels or bench["config"].get("string_layout", "").startswith("Arrow Utf8"):
         cand += [x for x in kernels if x.startswith(("cbx_jit_count", "cbx::scan_"))]
     parts, t = [], 0.0
     for x in cand:
-        d_in = [(e - s0) / 1e6 for s0, e in spans[x] if lo < s0 and e <= hi]
+        d_in = [(e - s0) / 1e6 for s0, e in spans[x] if lo < s0 and s0 < hi]
         if d_in:
             parts.append(x)
             t += sum(d_in) / steps
