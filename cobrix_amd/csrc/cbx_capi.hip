@@ -130,6 +130,8 @@ struct cbx_plan {
     int64_t* d_wslot_base = nullptr;    // per column: first string-slot index
     int64_t* d_wtile_bytes = nullptr;   // per column: view tile bytes
     const int64_t* d_rec_base = nullptr;   // caller's device Record_Id base (cbx_plan_set_record_base)
+    const int32_t* d_odo = nullptr;        // caller's OCCURS DEPENDING ON counts (cbx_plan_set_odo_counts)
+    int64_t odo_pitch = 0;
     int64_t n_str_slots = 0;
     uint32_t* d_wcursor = nullptr; int64_t wcursor_cap = 0;
     int64_t* d_wvbase = nullptr;        // per column: first validity-word index among all column slots
@@ -661,6 +663,8 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.rec_id_base = P->d_rec_base;
     a.rec_id = c.rec_id;
     a.rec_seg = c.rec_seg;
+    a.odo_count = P->d_odo;
+    a.odo_pitch = P->odo_pitch;
     a.file_id = c.file_id >= 0 ? c.file_id : P->opts.file_id;
     a.mode = mode;
     a.str_view = str_layout_of(P);
@@ -720,7 +724,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // (wide windowed layouts sit close to the LDS limit; C5 decode 49.7 -> 62.1 ms with them)
     const int lds_base = a.lds_rows + a.lds_counts + a.str_stage;
     auto lds_blocks = [](int per_wave) {
-        return (160 * 1024) / (1024 + kWavesPerBlock * ((per_wave + 15) & ~15));
+        return (160 * 1024) / (kLutLds + kWavesPerBlock * ((per_wave + 15) & ~15));
     };
     const bool lane_dump = a.str_stage > 0 && lds_blocks(lds_base + 4 * kWave) >= lds_blocks(lds_base + 16);
     a.dump_stride = lane_dump ? 4 : 0;
@@ -870,7 +874,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.list_flag = P->d_list_flag;
     const int n_defer = n_defer_seq;
     a.defer_bits = P->d_defer_bits;
-    const size_t lds = 1024 + (size_t)kWavesPerBlock * a.lds_wave;
+    const size_t lds = kLutLds + (size_t)kWavesPerBlock * a.lds_wave;
     if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
     // resident blocks per CU: the LDS bound and the runtime's occupancy (registers); the grid
     // never exceeds what can be co-resident, so the static tile order of the look-back holds
@@ -937,11 +941,11 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         KernelArgs ac = a;
         ac.mode = 1;
         // the specialised count kernel: no string staging per wave (it only scans lengths), two LUT
-        // copies in front (full + count_lut_entry)
+        // copies in front (full + count_lut_byte)
         size_t clds = lds;
         if (cfn) {
             ac.lds_wave = (a.lds_rows + a.lds_counts + 16 + 15) & ~15;
-            clds = 2048 + (size_t)kWavesPerBlock * ac.lds_wave;
+            clds = 1024 + kLutLds + (size_t)kWavesPerBlock * ac.lds_wave;
         }
         int cocc = 0;
         const hipError_t ce2 = cfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, cfn, kWave * kWavesPerBlock, clds)
@@ -1136,6 +1140,14 @@ extern "C" int cbx_plan_check(cbx_plan* P, void* stream) {
 extern "C" int cbx_plan_set_record_base(cbx_plan* P, const int64_t* d_base) {
     if (!P) return fail(CBX_E_ARGUMENT, "cbx_plan_set_record_base: invalid plan");
     P->d_rec_base = d_base;
+    return CBX_OK;
+}
+
+extern "C" int cbx_plan_set_odo_counts(cbx_plan* P, const int32_t* d_counts, int64_t pitch) {
+    if (!P || pitch < 0 || (d_counts && pitch == 0)) return fail(CBX_E_ARGUMENT, "cbx_plan_set_odo_counts: invalid arguments");
+    if (d_counts && P->walk) return fail(CBX_E_UNSUPPORTED, "cbx_plan_set_odo_counts: the record walk reads its counts itself");
+    P->d_odo = d_counts;
+    P->odo_pitch = d_counts ? pitch : 0;
     return CBX_OK;
 }
 
@@ -1840,6 +1852,7 @@ extern "C" int cbx_hier_select(cbx_plan* P, const uint8_t* d_data, int64_t n_byt
         return fail(CBX_E_ARGUMENT, "cbx_hier_select: bad root segment");
     HierArgs a{};
     a.n_seg = S;
+    a.start_off = prm->start_offset;
     a.root = prm->root_segment;
     for (int s = 0; s < kHierMaxSeg; s++) { a.parent[s] = -1; a.anc[s] = 0; }
     for (int s = 0; s < S; s++) {

@@ -521,8 +521,31 @@ __host__ __device__ constexpr int str_lane_slot(int size, int width) {
     // an odd dword count: the lanes' byte stores at similar positions land on distinct banks
     // (ds_write_b8: bank (a / 4) mod 32), and the dword read-backs are conflict-free.  (Odd counts of
     // 8-byte words, read back as 8-byte words, left every byte store 2-way conflicted: 14 dwords
-    // per lane.)
-    return (((size * width + 3 + 3) >> 2) | 1) << 2;
+    // per lane.)  2-byte pages (str_lane_group2): the phase (<= 3 bytes), <= 8 bytes per group of 4
+    // characters and the carried dword written past them.
+    return width == 2 ? ((((3 + 8 * ((size + 3) / 4)) >> 2) + 1) | 1) << 2 : (((size * width + 3 + 3) >> 2) | 1) << 2;
+}
+
+// Pattern selectors of a group of 4 characters of a 2-byte code page (str_lane_group2): entry h (bit k
+// = character k takes 2 UTF-8 bytes) lists, for v_perm over (U23, U01) -- character k's first UTF-8
+// byte at source 2k, its second at 2k + 1 -- the first bytes in order with each wide character's
+// second byte after its first, then zero bytes (0x0C).  Two dwords per entry, 16 entries.
+__host__ __device__ constexpr uint32_t group_sel(int i) {
+    const int h = i >> 1;
+    uint32_t b[8] = {0x0C, 0x0C, 0x0C, 0x0C, 0x0C, 0x0C, 0x0C, 0x0C};
+    int n = 0;
+    for (int k = 0; k < 4; k++) {
+        b[n++] = (uint32_t)(2 * k);
+        if ((h >> k) & 1) b[n++] = (uint32_t)(2 * k + 1);
+    }
+    const int o = 4 * (i & 1);
+    return b[o] | b[o + 1] << 8 | b[o + 2] << 16 | b[o + 3] << 24;
+}
+
+// The code page LUT and the group selectors into the workgroup's LDS (kLutLds bytes at lut).
+__device__ __forceinline__ void lut_lds_fill(const KernelArgs& a, uint32_t* lut) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = a.lut[i];
+    if (threadIdx.x < 32) lut[256 + threadIdx.x] = group_sel((int)threadIdx.x);
 }
 
 // The view layout's register-path string element (fields of <= kStrFastBytes EBCDIC / ASCII bytes,
@@ -580,6 +603,77 @@ __device__ __forceinline__ int str_lane_shift(int smax, const uint32_t (&ev)[kSt
     return len;
 }
 
+// 2-byte code pages (every character 1 or 2 UTF-8 bytes: cp037, cp500, cp875, ...): the field's
+// UTF-8 bytes composed 4 characters at a time in registers and placed in the lane's LDS slot with
+// dword stores only.  A group's characters give two dwords of byte pairs (U01, U23: first byte, then
+// the second one or 0); one pattern selector (str_group_sel: which of the 4 are wide) and two v_perm
+// compact them to the group's 4..8 bytes; the group lands at its running byte position through a
+// 64-bit shift, OR-ed into the partial dword carried from the previous group, as one 2-dword store
+// at a dword boundary.  The untrimmed field is composed (a trimmed leading character is <= U+0020,
+// one UTF-8 byte), starting at phase (-b) & 3, so the kept bytes [b, e) begin on a dword and are
+// read back packed from byte 0.  Per character: the LUT read and ~4 VALU; per group: one 8-byte LDS
+// read and one 8-byte LDS store -- where the byte path (string_write32e) issued two byte stores per
+// character (SYNSTR200: 43 LDS stores per value).
+__device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kStrFastBytes], int b, int e,
+                                               const uint32_t* s_lut, uint8_t* slot, u32x4 (&q)[kStrNC]) {
+    const uint32_t* s_sel = s_lut + 256;
+    uint32_t wide = 0;   // bit j: character j is 2 UTF-8 bytes (entry length 2: bit 25)
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++)
+        if (j < smax) wide |= ((ev[j] >> 25) & 1u) << j;
+    const int len = (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b));
+    const uint32_t s0 = (uint32_t)(-b) & 3u;
+    uint32_t carry = 0, pos = s0;
+#pragma unroll
+    for (int g = 0; 4 * g < kStrFastBytes; g++) {
+        if (4 * g >= smax) break;
+        const uint32_t e0 = ev[4 * g], e1 = 4 * g + 1 < smax ? ev[4 * g + 1] : 0u;
+        const uint32_t e2 = 4 * g + 2 < smax ? ev[4 * g + 2] : 0u, e3 = 4 * g + 3 < smax ? ev[4 * g + 3] : 0u;
+        const uint32_t u01 = __builtin_amdgcn_perm(e1, e0, 0x05040100u);   // c0.b0 c0.b1 c1.b0 c1.b1
+        const uint32_t u23 = __builtin_amdgcn_perm(e3, e2, 0x05040100u);
+        const uint32_t h = (wide >> (4 * g)) & 15u;
+        const uint2 sel = *(const uint2*)(s_sel + 2 * h);
+        const uint32_t lo = __builtin_amdgcn_perm(u23, u01, sel.x), hi = __builtin_amdgcn_perm(u23, u01, sel.y);
+        const uint32_t k8 = 8u * (pos & 3u);
+        const uint64_t v = (((uint64_t)hi << 32) | lo) << k8;
+        const uint32_t w0 = (uint32_t)v | carry, w1 = (uint32_t)(v >> 32);
+        const uint32_t w2 = (uint32_t)(((uint64_t)hi << k8) >> 32);   // the group's bytes past w1 (k8 > 0)
+        uint32_t* d = (uint32_t*)(slot + (pos & ~3u));
+        d[0] = w0;
+        d[1] = w1;
+        const uint32_t np = pos + 4u + popc32(h);
+        carry = ((np >> 2) - (pos >> 2)) == 2u ? w2 : w1;
+        pos = np;
+    }
+    *(uint32_t*)(slot + (pos & ~3u)) = carry;
+    // the kept bytes, packed from byte 0 (dword reads clamped to the slot)
+    const uint32_t* sd = (const uint32_t*)slot;
+    const int last = (str_lane_slot(smax, 2) >> 2) - 1;
+    const int s_dw = (int)((s0 + (uint32_t)b) >> 2);
+#pragma unroll
+    for (int k = 0; k < kStrNC; k++) {
+        if (16 * k < 2 * smax) {
+            uint32_t d4[4];
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                const int i = s_dw + 4 * k + m;
+                d4[m] = 16 * k + 4 * m < 2 * smax ? sd[i < last ? i : last] : 0u;
+            }
+            if (k == 0) {
+                // a short string view inlines these dwords: zero the bytes past the value (the
+                // slot holds the untrimmed field there)
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    const int r = len - 4 * m;
+                    d4[m] = r >= 4 ? d4[m] : r <= 0 ? 0u : d4[m] & ((1u << (8 * r)) - 1u);
+                }
+            }
+            q[k] = u32x4{d4[0], d4[1], d4[2], d4[3]};
+        }
+    }
+    return len;
+}
+
 __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, int smax, int eo, int n, bool ok,
                                                 const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
                                                 uint8_t* s_str, int lane, u32x4 (&q)[kStrNC]) {
@@ -609,6 +703,9 @@ __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, i
     if (trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
 #ifndef CBX_STR_NO_SHIFT
     if (width == 1) return str_lane_shift(smax, ev, b, e, q);
+#endif
+#ifndef CBX_STR_W2_BYTES   // (A/B: the byte-store compose below for 2-byte pages too)
+    if (width == 2) return str_lane_group2(smax, ev, b, e, s_lut, s_str + lane * str_lane_slot(smax, 2), q);
 #endif
     const uint32_t range = bits_below(e) & ~bits_below(b);
     uint8_t* slot = s_str + lane * str_lane_slot(smax, width);
@@ -976,13 +1073,16 @@ __device__ __forceinline__ void str_utf8_two(const KernelArgs& a, const StrOp& A
 
 // ---- Utf8 count pass (specialised kernels only: CBX_COUNT_LUT) ----
 // The count kernel's LDS copy of the code-page LUT keeps, per byte, only what a UTF-8 length needs:
-// the trim flag (bit 31) and the UTF-8 length (bits 24-25).  A trimmed character maps to <= U+0020,
-// one UTF-8 byte, so a value's length is the sum over all its bytes of the lengths, minus its
-// leading and trailing trimmable bytes: per byte one LDS read, a funnel shift collecting the trim
-// bits (byte j at bit size-1-j) and one add of the entry's top byte (trim * 128 + length: the sum of
-// the lengths of <= 32 bytes stays below 128).
-__device__ __forceinline__ uint32_t count_lut_entry(uint32_t e) {
-    return (e & 0x80000000u) | (e & 0x03000000u);   // trim flag | UTF-8 length (0..3)
+// the trim flag and the UTF-8 length.  A trimmed character maps to <= U+0020, one UTF-8 byte, so a
+// value's length is the sum over all its bytes of the lengths, minus its leading and trailing
+// trimmable bytes: per byte one LDS read, a funnel shift collecting the trim bits (byte j at bit
+// size-1-j) and one add of the entry's low byte (trim * 128 + length: the sum of the lengths of <= 32
+// bytes stays below 128).  The count LUT is 256 bytes (trim flag at bit 7, UTF-8 length in bits 0-1), read with ds_read_i8:
+// the sign extension puts the trim flag at bit 31 for the funnel-shift collect, and a 256-byte table
+// spans 64 dwords -- at most 2 distinct dwords per bank for a wave's random bytes, where the 1 KiB
+// table of 4-byte entries put up to 8 on one bank (count kernel SQ_LDS_BANK_CONFLICT / active 2.2).
+__device__ __forceinline__ uint8_t count_lut_byte(uint32_t e) {
+    return (uint8_t)(((e >> 31) << 7) | ((e >> 24) & 3u));
 }
 
 // UTF-8 length of the lane's value of a register-path code-page element whose n bytes are all in
@@ -992,12 +1092,13 @@ __device__ __forceinline__ int str_count_fast(const StrOp& op, const uint8_t* sr
     uint32_t w[8];
     img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
     uint32_t tm = 0, acc = 0;
+    const int8_t* lut8 = (const int8_t*)s_lut;   // count_lut_byte entries
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++) {
         if (j < op.size) {
-            const uint32_t e = *(const uint32_t*)((const uint8_t*)s_lut + byte_x4(w[j >> 2], j & 3));
+            const uint32_t e = (uint32_t)(int32_t)lut8[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu];
             tm = __builtin_amdgcn_alignbit(tm, e, 31);   // (tm << 1) | trim bit
-            acc += e >> 24;
+            acc += e & 0xFFu;                            // trim * 128 + UTF-8 length
         }
     }
     const int size = op.size;
@@ -1410,6 +1511,12 @@ __device__ __forceinline__ void tile_prologue(const KernelArgs& a, TileCtx& t, c
                 }
             }
         }
+        if (a.odo_count && t.active && t.rec < a.odo_pitch) {
+            // the caller's count (hierarchical records: the dependee registered by an earlier segment
+            // of the record, extractHierarchicalRecord's shared dependFields)
+            const int32_t oc = a.odo_count[(int64_t)ai * a.odo_pitch + t.rec];
+            if (oc >= 0) cnt = oc;
+        }
         s_cnt[ai * kWave + lane] = cnt;
         if (ar.offsets_column >= 0 && kmode(a) == 0) {
             // list layout: the record's present elements (none when the array's segment is not the
@@ -1478,7 +1585,7 @@ struct WaveLds {
 __device__ __forceinline__ WaveLds wave_lds(const KernelArgs& a, uint8_t* smem, int wid) {
     WaveLds l;
     l.lut = (uint32_t*)smem;
-    uint8_t* wbase = smem + 1024 + wid * a.lds_wave;
+    uint8_t* wbase = smem + kLutLds + wid * a.lds_wave;
     l.img = wbase + kGuard;
     l.cnt = (int32_t*)(wbase + a.lds_rows);
     l.str = wbase + a.lds_rows + a.lds_counts;

@@ -38,6 +38,7 @@ struct HierArgs {
     const uint32_t* lut;
     const CBX_CONST Field* fields;
     int32_t n_seg;                    // segment types (<= kHierMaxSeg)
+    int32_t start_off;                // record_start_offset (segment ids are read past it)
     int32_t root;                     // the root segment
     int32_t parent[kHierMaxSeg];      // parent segment, -1 for the root / unused
     uint32_t anc[kHierMaxSeg];        // strict non-root ancestors of the parent of each segment (bits)
@@ -52,7 +53,7 @@ struct HierArgs {
 __global__ void hier_type_kernel(HierArgs a) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
-    const int k = segment_key(a.m, a.lut, a.fields, a.data + a.rec_off[i], a.rec_len[i], 0);
+    const int k = segment_key(a.m, a.lut, a.fields, a.data + a.rec_off[i], a.rec_len[i], a.start_off);
     int s = -1;
     if (k >= 0) s = a.m->key_segment[k];
     a.type[i] = (int8_t)(s >= 0 && s < a.n_seg ? s : -1);

@@ -18,6 +18,9 @@ namespace cbx {
 constexpr int kWave = 64;              // one wave = one tile of 64 consecutive records (lane = record)
 constexpr int kWavesPerBlock = 2;      // waves per workgroup (each works on its own tile)
 constexpr int kGuard = 16;             // LDS guard bytes in front of / behind a record image
+// LDS in front of the waves' regions: the code page LUT (256 x 4 bytes) + the 16 pattern selectors
+// of the 2-byte-page string compose (str_group_sel, 16 x 8 bytes)
+constexpr int kLutLds = 1024 + 128;
 constexpr int kMaxWindowBytes = 1024;  // fields wider than this are read from HBM directly
 constexpr int kStrStageBytes = 4096;   // per-wave LDS staging of one string item's tile payload
 constexpr int kMaxStrItems = 256;      // string (field, slot) items per window (plan splits windows)
@@ -123,6 +126,9 @@ struct KernelArgs {
     const int64_t* rec_id;     // per-record Record_Id (selected records), nullptr: first_record_id + r
     const int64_t* rec_id_base;// device int64 added to first_record_id (cbx_plan_set_record_base), nullptr: 0
     const int32_t* rec_seg;    // per-record active segment (selected records), nullptr: from segmap
+    const int32_t* odo_count;  // [n_arrays][odo_pitch] OCCURS DEPENDING ON counts given by the caller
+                               // (cbx_plan_set_odo_counts; < 0: from the record), nullptr: none
+    int64_t odo_pitch;
     int32_t file_id;
     int32_t mode;              // 0 decode, 1 string sizes only
     int32_t str_view;          // string columns: 0 Arrow large-string (scratch + placement), 1 string views,

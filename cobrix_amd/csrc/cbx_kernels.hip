@@ -64,7 +64,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void decode_kernel(KernelAr
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform to the compiler
     const int lane = threadIdx.x % kWave;
     const WaveLds l = wave_lds(a, smem, wid);
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) l.lut[i] = a.lut[i];
+    lut_lds_fill(a, l.lut);
     __syncthreads();
 
     // static grid-stride tile order (tiles are independent)

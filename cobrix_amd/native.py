@@ -41,8 +41,8 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text",
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
                     "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs",
-                    "cbx_plan_set_record_base", "cbx_frame_length_field")
-ABI_VERSION = 10
+                    "cbx_plan_set_record_base", "cbx_frame_length_field", "cbx_plan_set_odo_counts")
+ABI_VERSION = 11
 
 
 class NativeLibraryError(RuntimeError):
@@ -144,7 +144,8 @@ class CbxWalkHandler(ctypes.Structure):
 
 class CbxHierParams(ctypes.Structure):
     _fields_ = [("n_segments", ctypes.c_int32), ("root_segment", ctypes.c_int32),
-                ("parent", ctypes.c_int32 * CBX_MAX_SEG_KEYS), ("first_record_id", ctypes.c_int64)]
+                ("parent", ctypes.c_int32 * CBX_MAX_SEG_KEYS), ("first_record_id", ctypes.c_int64),
+                ("start_offset", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 _lib = None
@@ -192,7 +193,8 @@ def load():
                      ("cbx_plan_set_walk", [P, P, i32, i32, P, P, i32, i32]),
                      ("cbx_frame_var_occurs", [P, P, i64, i64, P, P, i64, P, P, P]),
                      ("cbx_plan_set_record_base", [P, P]),
-                     ("cbx_frame_length_field", [P, P, i64, i32, i32, i32, i32, P, P, i64, P, P])):
+                     ("cbx_frame_length_field", [P, P, i64, i32, i32, i32, i32, P, P, i64, P, P]),
+                     ("cbx_plan_set_odo_counts", [P, P, i64])):
         if hasattr(L, name):   # (diagnostic builds of older revisions lack the newest entry points)
             getattr(L, name).argtypes = at
     if L.cbx_abi_version() != ABI_VERSION:

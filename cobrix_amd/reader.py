@@ -1169,6 +1169,7 @@ class VarLenNestedReader(_BaseReader):
         for i, g in enumerate(segs):
             prm.parent[i] = segs.index(g.parent_segment) if g.parent_segment is not None else -1
         prm.first_record_id = first_record_id
+        prm.start_offset = self.params.start_offset
         sel = {"rec_off": torch.empty(max(1, n), dtype=torch.int64, device=dev),
                "rec_len": torch.empty(max(1, n), dtype=torch.int32, device=dev),
                "record_id": torch.empty(max(1, n), dtype=torch.int64, device=dev),
@@ -1184,6 +1185,7 @@ class VarLenNestedReader(_BaseReader):
                                   ctypes.byref(prm), ctypes.byref(cs), parent_row.data_ptr(), rows, ctypes.byref(n_rows), sp))
         table_rows = [int(x) for x in rows]
         sel["n"], sel["struct"] = n_rows.value, cs
+        rec_off0 = sel["rec_off"][: n_rows.value].clone()   # record order (before any start-offset shift)
         s0 = self.params.start_offset
         if s0 and n_rows.value > table_rows[0]:
             # extractHierarchicalRecord decodes the root record from offsetBytes = record_start_offset
@@ -1198,6 +1200,15 @@ class VarLenNestedReader(_BaseReader):
             kid_off -= s0
             sel["rec_len"][table_rows[0]:n_rows.value] += s0
         flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
+        odo = self._hier_dependee_counts(flat, table_rows, parent_row, rec_off0, prm.root_segment)
+        if odo is not None:
+            # arrays whose count comes from a dependee another segment of the hierarchical record
+            # registered: decode again with those counts
+            N.check(L.cbx_plan_set_odo_counts(self.native.handle, odo.data_ptr(), int(odo.shape[1])))
+            try:
+                flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
+            finally:
+                N.check(L.cbx_plan_set_odo_counts(self.native.handle, None, 0))
         base = np.concatenate([[0], np.cumsum(table_rows)]).astype(np.int64)
         offsets: Dict[int, np.ndarray] = {}
         for s, g in enumerate(segs):
@@ -1215,6 +1226,96 @@ class VarLenNestedReader(_BaseReader):
         if self.params.input_file_name_column:
             batch.input_file = (self.params.input_file_name_column, input_file_name)
         return batch
+
+    def _hier_dependee_counts(self, flat: DecodedBatch, table_rows: List[int], parent_row, rec_off, root_seg: int):
+        """extractHierarchicalRecord shares ONE dependFields map between the segments of a hierarchical
+        record (RecordExtractors.scala:224-245): a DEPENDING ON field registers its value when a record's
+        group holding it is decoded, and an array reads the value registered last -- in the walk's
+        order: the root record's groups, then each segment's children (extractChildren, :300-322).
+        The records' own bytes give the same count when the dependee sits in the array's own segment and
+        is not null there; otherwise (a dependee of the parent segment, of the common header, or a null
+        one) the count is the value of the last record BEFORE this one, in the same hierarchical record,
+        whose segment holds the dependee and gives it a value: same-type records are walked in record
+        order, and an ancestor of the array's segment is walked before its subtree.  Returns the counts
+        where they differ from the first decode (int32 [n_arrays, rows], -1 elsewhere), or None."""
+        torch = _torch()
+        plan = self.plan
+        arrays = [(ai, ar) for ai, ar in enumerate(plan.arrays) if ar.dependee >= 0 and ar.segment >= 0]
+        n = int(sum(table_rows))
+        if not arrays or n == 0:
+            return None
+        order: Dict[int, int] = {}
+
+        def dfs(st):
+            order[id(st)] = len(order)
+            for c in getattr(st, "children", []) or []:
+                dfs(c)
+        dfs(self.copybook.ast)
+        segs = plan.segment_groups
+        root_pos = order[id(segs[root_seg])]
+        seg_row = np.repeat(np.array([root_seg] + list(range(len(segs))), np.int64), table_rows)
+        par = parent_row[:n].cpu().numpy()
+        root_of = np.where(par < 0, np.arange(n), par)
+        for _ in range(len(segs) + 1):   # chase the parents up to the root rows (table 0)
+            nxt = np.where(root_of >= table_rows[0], par[np.minimum(root_of, n - 1)], root_of)
+            if np.array_equal(nxt, root_of):
+                break
+            root_of = nxt
+        off = rec_off.cpu().numpy()
+        out = np.full((len(plan.arrays), n), -1, np.int32)
+        changed = False
+        for ai, ar in arrays:
+            df = plan.fields[ar.dependee]
+            dcol = plan.columns[df.column]
+            anode = plan.columns[ar.count_column].node
+            if dcol.out_type in (N.O_STRING, N.O_BINARY):
+                if df.segment != ar.segment:
+                    raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a string DEPENDING ON field "
+                                                          "outside the array's segment")
+                continue
+            if any(order[id(g)] < root_pos for g in segs if g is not segs[root_seg]) and df.segment != ar.segment:
+                # the root record decodes a segment group placed before the root's from its own bytes,
+                # ahead of the children -- registrations this restatement does not model
+                raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a segment group before the root "
+                                                      "segment's with a cross-segment DEPENDING ON")
+            h = flat.host_column(df.column)
+            raw = np.asarray(h["values"])
+            if dcol.out_type == N.O_DEC128:
+                raw = raw.reshape(-1, 2)[:, 0]
+            dv = raw.reshape(dcol.n_slots, -1)[0, :n].astype(np.int64)
+            dok = np.asarray(h["validity"])[0, :n].astype(bool)
+            dv = ((dv + (1 << 31)) % (1 << 32) - (1 << 31)).astype(np.int64)   # Number.intValue
+            xs = np.nonzero(seg_row == ar.segment)[0]
+            if not len(xs):
+                continue
+            own = xs < table_rows[0]   # root rows: their own decode (the first record of the walk)
+            if df.segment < 0:
+                # the common header: only the root record decodes it, ahead of the children when it
+                # precedes the root's segment group
+                r = root_of[xs]
+                known = dok[r] & (order[id(dcol.node)] < root_pos)
+                val = dv[r]
+            else:
+                incl = df.segment == ar.segment and order[id(dcol.node)] < order[id(anode)]
+                ys = np.nonzero((seg_row == df.segment) & dok)[0]
+                key_y = root_of[ys].astype(np.int64) * (1 << 40) + off[ys]
+                srt = np.argsort(key_y, kind="stable")
+                ys, key_y = ys[srt], key_y[srt]
+                key_x = root_of[xs].astype(np.int64) * (1 << 40) + off[xs]
+                pos = np.searchsorted(key_y, key_x, side="right" if incl else "left") - 1
+                hit = (pos >= 0)
+                yy = ys[np.maximum(pos, 0)]
+                hit &= root_of[yy] == root_of[xs]
+                val = dv[yy]
+                known = hit
+            cnt = np.where(known & (val >= ar.min_count) & (val <= ar.max_count), val, ar.max_count)
+            cnt = np.where(own, -1, cnt)
+            got = np.asarray(flat.host_column(ar.count_column)["values"]).reshape(-1)[:n][xs]
+            diff = (cnt >= 0) & (cnt != got)
+            if diff.any():
+                out[ai, xs[diff]] = cnt[diff]
+                changed = True
+        return torch.as_tensor(out, device=parent_row.device) if changed else None
 
     def read(self, data: bytes, file_id: int = 0, input_file_name: str = "") -> DecodedBatch:
         """A whole file, as the reference reads it: sparse-index entries (when index generation

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 10
+#define CBX_ABI_VERSION 11
 
 /* status codes */
 #define CBX_OK 0
@@ -270,6 +270,17 @@ int cbx_string_sizes_var(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes,
  * (SC/reader/VarLenNestedReader.scala:52-81). */
 int cbx_plan_set_record_base(cbx_plan* plan, const int64_t* d_base);
 
+/* Hierarchical records (segment-children): OCCURS DEPENDING ON counts the caller resolved itself.
+ * d_counts: device int32[n_arrays][pitch] -- entry (a, r) the element count of the plan's array a in
+ * record r of the following decode calls (cbx_decode_selected / cbx_decode_var / cbx_decode_fixed),
+ * < 0: the count the record's own dependee gives.  Replaces the dependFields map that
+ * RecordExtractors.extractHierarchicalRecord shares between the segments of one hierarchical record
+ * (CP/reader/extractors/record/RecordExtractors.scala:224-245): a child segment's array depending on
+ * a field of its parent segment (or of a segment decoded earlier in the record) takes the value
+ * registered there.  NULL clears it; the pointer must stay valid while calls are in flight.
+ * CBX_E_UNSUPPORTED on a record-walk plan. */
+int cbx_plan_set_odo_counts(cbx_plan* plan, const int32_t* d_counts, int64_t pitch);
+
 /* Synchronise `stream` and report device-side errors of the plan's earlier decode calls
  * (CBX_E_CAPACITY: a string payload exceeded data_capacity). */
 int cbx_plan_check(cbx_plan* plan, void* stream);
@@ -460,19 +471,22 @@ int cbx_frame_length_field(cbx_plan* plan, const uint8_t* d_data, int64_t n_byte
  * list of segment-C children of every parent row is a contiguous run of table 1 + C
  * (cbx_hier_list_offsets).  table_rows (host, n_segments + 1 entries) receives the row count per
  * table.  Output arrays need capacity n_rec.
- * Not covered (reported by the host, CBX_E_UNSUPPORTED, never decoded differently):
- * record_start_offset != 0 -- extractHierarchicalRecord decodes the root at the start offset but
- * each child segment at its group's own offset, without it (RecordExtractors.scala:310, :376);
- * several segment ids mapped to one parent segment.  Parity-unpinned (no reference fixture; the
- * oracle restatement and these kernels agree): a DEPENDING ON field inside a child segment whose
- * value is null -- the reference's dependFields map is shared by all segments of a hierarchical
- * record (:226), so such an array takes the count an earlier segment left there; here each
- * record's arrays use the record's own dependees. */
+ * record_start_offset: extractHierarchicalRecord decodes the root at the start offset but each child
+ * segment at its group's own offset, without it (RecordExtractors.scala:308-310, :376) -- the host
+ * decodes the child rows as records starting start_offset bytes earlier.  The dependFields map the
+ * reference shares between the segments of a hierarchical record (:224-245: a child's array DEPENDING
+ * ON a field of its parent segment or of the common header, or on a null field of its own segment)
+ * is resolved by the host from the decoded rows and applied with cbx_plan_set_odo_counts.
+ * Not covered (reported by the host, CBX_E_UNSUPPORTED, never decoded differently): several segment
+ * ids mapped to one parent segment; a cross-segment DEPENDING ON when a segment group precedes the
+ * root segment's in the copybook; a string DEPENDING ON field outside the array's segment. */
 typedef struct {
     int32_t n_segments;               /* segment redefines (cbx_field.segment / key_segment indices) */
     int32_t root_segment;             /* the segment without a parent */
     int32_t parent[CBX_MAX_SEG_KEYS]; /* parent segment of each segment, -1 for the root */
     int64_t first_record_id;          /* startRecordId of the stream (entry.record_index) */
+    int32_t start_offset;             /* record_start_offset: the segment id is read past it (VRLRecordReader) */
+    int32_t reserved;
 } cbx_hier_params;
 
 int cbx_hier_select(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,

@@ -800,9 +800,14 @@ typedef struct {
     int dep_slen[MAX_DEPS];
     int depth;
     int idx_stack[16], max_stack[16];
+    /* extractHierarchicalRecord only: the walk's hierarchical state; mute = decode without events */
+    struct hier_ctx* hier;
+    int mute;
+    ora_event dummy;
 } walk_ctx;
 
 static ora_event* new_event(walk_ctx* c) {
+    if (c->mute) { memset(&c->dummy, 0, sizeof(c->dummy)); return &c->dummy; }
     if (c->n_ev >= c->ev_cap) { c->err = -1; return NULL; }
     ora_event* e = &c->ev[c->n_ev++];
     memset(e, 0, sizeof(*e));
@@ -846,6 +851,7 @@ static int cur_slot(const walk_ctx* c) {
 }
 
 static void emit_value(walk_ctx* c, int nid, const jvalue* v, int slot) {
+    if (c->mute) return;
     ora_event* e = new_event(c);
     if (!e) return;
     e->node = nid;
@@ -937,17 +943,43 @@ static int extract_value(walk_ctx* c, int nid, int use_offset) {
     return f->actual_size;
 }
 
-/* getGroupValues (:139-172) */
+static void hier_children(walk_ctx* c, int gid);
+
+/* getGroupValues (:139-172; the hierarchical form :324-369 also mutes child-segment fields and
+ * appends the group's children) */
+static void walk_group(walk_ctx* c, int gid, int offset, int* size_out);
+
+typedef struct hier_ctx {
+    int32_t n;
+    const uint8_t* const* datas;
+    const int32_t* lens;
+    const int32_t* seg_group;
+    const int32_t* seg_key;
+    const int32_t* child_begin;
+    const int32_t* child_end;
+    const int32_t* children;
+    const int32_t* node_offset;
+    const int32_t* is_child_seg;
+    uint32_t rec_base;
+    int cur;            /* currentIndex: the record whose group is being walked */
+    int path[64];       /* parentSegmentIds of that walk */
+    int path_len;
+} hier_ctx;
+
 static void walk_group(walk_ctx* c, int gid, int offset, int* size_out) {
     int bit_offset = offset;
     for (int ch = c->nodes[gid].first_child; ch >= 0; ch = c->nodes[ch].next_sibling) {
         const ora_node* f = &c->nodes[ch];
+        const int saved_mute = c->mute;
+        if (c->hier && c->hier->is_child_seg[ch]) c->mute = 1;
         if (f->is_array) {
             int sz = extract_array(c, ch, bit_offset);
+            c->mute = saved_mute;
             if (c->err) return;
             if (!f->is_redefined) bit_offset += sz;
         } else {
             int sz = extract_value(c, ch, bit_offset);
+            c->mute = saved_mute;
             if (c->err) return;
             if (!f->is_redefined) {
                 if (f->has_redefines) bit_offset += f->actual_size;
@@ -956,6 +988,90 @@ static void walk_group(walk_ctx* c, int gid, int offset, int* size_out) {
         }
     }
     *size_out = bit_offset - offset;
+    if (c->hier && c->nodes[gid].is_segment_redefine) hier_children(c, gid);
+}
+
+static int hier_in_path(const hier_ctx* h, int key) {
+    for (int i = 0; i < h->path_len; i++) if (h->path[i] == key) return 1;
+    return 0;
+}
+
+/* extractChildren (:300-322) for each child segment of gid, in parentChildMap order */
+static void hier_children(walk_ctx* c, int gid) {
+    hier_ctx* h = c->hier;
+    for (int k = h->child_begin[gid]; k < h->child_end[gid]; k++) {
+        const int field = h->children[k];
+        const int from = h->cur + 1;
+        int cnt = 0;
+        for (int i = from; i < h->n; i++) {
+            if (h->seg_group[i] == field) cnt++;
+            else if (hier_in_path(h, h->seg_key[i])) break;
+        }
+        ora_event* e = new_event(c);
+        if (!e) return;
+        e->node = field; e->kind = ORA_EV_CHILDREN; e->lo = cnt; e->slot = 0;
+        const uint8_t* sdata = c->data;
+        const int slen = c->data_len, scur = h->cur, sdepth = c->depth;
+        const uint32_t srec = c->rec;
+        for (int i = from; i < h->n; i++) {
+            if (h->seg_group[i] == field) {
+                if (h->path_len >= 64) { c->err = -5; return; }
+                c->data = h->datas[i]; c->data_len = h->lens[i]; c->rec = h->rec_base + (uint32_t)i;
+                h->cur = i;
+                memmove(h->path + 1, h->path, sizeof(int) * (size_t)h->path_len);   /* segmentId :: parentSegmentIds */
+                h->path[0] = h->seg_key[i];
+                h->path_len++;
+                c->depth = 0;
+                int sz;
+                walk_group(c, field, h->node_offset[field], &sz);
+                h->path_len--;
+                memmove(h->path, h->path + 1, sizeof(int) * (size_t)h->path_len);
+                c->depth = sdepth;
+                h->cur = scur;
+                if (c->err) return;
+            } else if (hier_in_path(h, h->seg_key[i])) {
+                break;
+            }
+        }
+        c->data = sdata; c->data_len = slen; c->rec = srec;
+    }
+}
+
+int ora_extract_hier(const ora_node* nodes, int32_t root, const ora_handler* handlers, const ora_options* opt,
+                     int32_t n_records, const uint8_t* const* datas, const int32_t* lens,
+                     const int32_t* seg_group, const int32_t* seg_key, const int32_t* child_begin,
+                     const int32_t* child_end, const int32_t* children, const int32_t* node_offset,
+                     const int32_t* is_child_seg, const int32_t* has_parent_seg, int32_t offset_bytes,
+                     uint32_t rec_base, ora_event* ev, int64_t ev_cap, int64_t* n_ev,
+                     uint8_t* heap, int64_t heap_cap, int64_t* heap_len) {
+    if (n_records <= 0) return 0;
+    walk_ctx* c = (walk_ctx*)calloc(1, sizeof(walk_ctx));
+    hier_ctx* h = (hier_ctx*)calloc(1, sizeof(hier_ctx));
+    if (!c || !h) { free(c); free(h); return -4; }
+    h->n = n_records; h->datas = datas; h->lens = lens; h->seg_group = seg_group; h->seg_key = seg_key;
+    h->child_begin = child_begin; h->child_end = child_end; h->children = children;
+    h->node_offset = node_offset; h->is_child_seg = is_child_seg; h->rec_base = rec_base;
+    h->cur = 0; h->path[0] = seg_key[0]; h->path_len = 1;   /* segmentsData(0)._1 :: Nil */
+    c->nodes = nodes; c->handlers = handlers; c->opt = opt; c->data = datas[0]; c->data_len = lens[0];
+    c->active_seg = ORA_ALL_SEGMENTS; c->rec = rec_base;
+    c->ev = ev; c->ev_cap = ev_cap; c->n_ev = *n_ev;
+    c->heap = heap; c->heap_cap = heap_cap; c->heap_len = *heap_len;
+    c->hier = h;
+    /* ast.children.collect { case grp: Group if grp.parentSegment.isEmpty => getGroupValues(nextOffset, ...) } */
+    int next_offset = offset_bytes;
+    for (int r = nodes[root].first_child; r >= 0; r = nodes[r].next_sibling) {
+        if (nodes[r].kind != ORA_GROUP || has_parent_seg[r]) continue;
+        int sz;
+        walk_group(c, r, next_offset, &sz);
+        if (c->err) break;
+        next_offset += sz;
+    }
+    int err = c->err;
+    *n_ev = c->n_ev;
+    *heap_len = c->heap_len;
+    free(h);
+    free(c);
+    return err;
 }
 
 int ora_extract_record(const ora_node* nodes, int32_t root, const ora_handler* handlers,

@@ -29,7 +29,7 @@ enum { ORA_ST_INT = 1, ORA_ST_LONG = 2, ORA_ST_DECIMAL = 3, ORA_ST_FLOAT = 4, OR
        ORA_ST_STRING = 6, ORA_ST_BINARY = 7 };
 
 /* events, emitted in extractRecord walk order */
-enum { ORA_EV_VALUE = 1, ORA_EV_ARRAY = 2, ORA_EV_SEGNULL = 3 };
+enum { ORA_EV_VALUE = 1, ORA_EV_ARRAY = 2, ORA_EV_SEGNULL = 3, ORA_EV_CHILDREN = 4 };
 
 typedef struct {
     int32_t kind;             /* ORA_GROUP / ORA_PRIMITIVE */
@@ -85,6 +85,25 @@ int ora_extract_record(const ora_node* nodes, int32_t root, const ora_handler* h
                        int32_t offset_bytes, int32_t active_segment_upper_id, uint32_t rec,
                        ora_event* ev, int64_t ev_cap, int64_t* n_ev,
                        uint8_t* heap, int64_t heap_cap, int64_t* heap_len);
+
+/* One hierarchical record (RecordExtractors.extractHierarchicalRecord, :211-385): records[0] is the root
+ * segment record, the others the records accumulated after it (VarLenHierarchicalIterator).  One
+ * dependFields map is shared by every segment of the record.  The root's top-level groups without a
+ * parent segment are walked from offset_bytes; at the end of a segment-redefine group the group's child
+ * segments (child_begin/child_end/children: parentChildMap, node ids) are extracted from the records after
+ * the current one (extractChildren) -- each child group at its own offset (node_offset) in its record's
+ * data -- preceded by one ORA_EV_CHILDREN event (node = the child group, lo = the count).  Fields that are
+ * child segments (is_child_seg) are decoded where they sit -- their dependees register -- but emit no
+ * events, as getGroupValues keeps no value for them.  seg_group: per record the node id of the
+ * segment-redefine group its segment id maps to (-1: none); seg_key: per record its segment id as an int
+ * key (equal ids, equal keys).  Events carry rec = rec_base + the record's index. */
+int ora_extract_hier(const ora_node* nodes, int32_t root, const ora_handler* handlers, const ora_options* opt,
+                     int32_t n_records, const uint8_t* const* datas, const int32_t* lens,
+                     const int32_t* seg_group, const int32_t* seg_key, const int32_t* child_begin,
+                     const int32_t* child_end, const int32_t* children, const int32_t* node_offset,
+                     const int32_t* is_child_seg, const int32_t* has_parent_seg, int32_t offset_bytes,
+                     uint32_t rec_base, ora_event* ev, int64_t ev_cap, int64_t* n_ev,
+                     uint8_t* heap, int64_t heap_cap, int64_t* heap_len);
 
 /* Batch of variable-length records: record i = data[rec_off[i], + rec_len[i]), active segment act[i]. */
 int ora_extract_var(const ora_node* nodes, int32_t root, const ora_handler* handlers,

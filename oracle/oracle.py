@@ -47,7 +47,7 @@ class OraOptions(ctypes.Structure):
 
 EVENT_DTYPE = np.dtype([("rec", "<u4"), ("node", "<i4"), ("kind", "<i4"), ("isnull", "<i4"),
                         ("slot", "<i4"), ("stype", "<i4"), ("lo", "<i8"), ("hi", "<i8")])
-EV_VALUE, EV_ARRAY, EV_SEGNULL = 1, 2, 3
+EV_VALUE, EV_ARRAY, EV_SEGNULL, EV_CHILDREN = 1, 2, 3, 4
 ORA_ALL_SEGMENTS = -3   # cobrix_oracle.h
 
 _TRIM = {"none": 1, "left": 2, "right": 3, "both": 4}
@@ -89,6 +89,8 @@ def lib():
                                        ctypes.c_int64]
         L.ora_sparse_index.restype = ctypes.c_int64
         L.ora_decode_field.argtypes = [P, P, P, ctypes.c_int32, P, P, ctypes.c_int64, P]
+        L.ora_extract_hier.argtypes = [P, ctypes.c_int32, P, P, ctypes.c_int32, P, P, P, P, P, P, P, P, P, P,
+                                       ctypes.c_int32, ctypes.c_uint32, P, ctypes.c_int64, P, P, ctypes.c_int64, P]
         _lib = L
     return _lib
 

@@ -459,13 +459,34 @@ def raw_records(cb: cbk.Copybook, data: bytes, p, e: Entry) -> List[Tuple[str, b
         out.append((_trim(seg_reader.segment_id(rec, p.start_offset)) if seg_reader else "", rec))
 
 
-def _full_record(res, r_events_pos: int, groups: Dict[int, Any]):
-    """Walk one record's event stream like O.rows, keeping every group's dict -- child segments
-    included -- keyed by id(group) (the values getGroupValues reads)."""
-    ast = res.ast
-    ev = res.events
-    heap = res.heap
-    pos = r_events_pos
+def _hier_tables(cb: cbk.Copybook, ast) -> Dict[str, Any]:
+    """Node-indexed tables ora_extract_hier walks by: parentChildMap (child segment group ids per
+    segment redefine, in the copybook's order), each node's binary offset, child-segment and
+    has-a-parent-segment flags."""
+    n = len(ast.stmts)
+    redefines = cb.all_segment_redefines()
+    begin = np.zeros(n, np.int32)
+    end = np.zeros(n, np.int32)
+    kids: List[int] = []
+    for i, st in enumerate(ast.stmts):
+        begin[i] = len(kids)
+        if isinstance(st, cbk.Group) and st.is_segment_redefine:
+            kids += [ast.node_of(c) for c in redefines if c.parent_segment is st]
+        end[i] = len(kids)
+    return {"begin": begin, "end": end, "children": np.array(kids or [0], np.int32),
+            "offset": np.array([getattr(st, "offset", 0) for st in ast.stmts], np.int32),
+            "child": np.array([int(isinstance(st, cbk.Group) and st.is_child_segment) for st in ast.stmts], np.int32),
+            "has_parent": np.array([int(isinstance(st, cbk.Group) and st.parent_segment is not None)
+                                    for st in ast.stmts], np.int32)}
+
+
+def _hier_row_values(ast, ev, heap) -> List[Tuple[Any, dict]]:
+    """The event stream of one ora_extract_hier call -> [(top-level group, values)]: getGroupValues'
+    shape -- no entry for a child-segment field, each segment redefine's child segments appended as
+    lists (one ORA_EV_CHILDREN count, then each child's group)."""
+    cb = ast.cb
+    redefines = cb.all_segment_redefines()
+    pos = 0
 
     def dec_value(st, e):
         v = O.event_value(e, heap)
@@ -477,6 +498,8 @@ def _full_record(res, r_events_pos: int, groups: Dict[int, Any]):
         nonlocal pos
         d = {}
         for c in g.children:
+            if isinstance(c, cbk.Group) and c.is_child_segment:
+                continue   # decoded, not kept (and no events)
             if c.is_array:
                 cnt = int(ev[pos]["lo"])
                 pos += 1
@@ -490,106 +513,83 @@ def _full_record(res, r_events_pos: int, groups: Dict[int, Any]):
                 val: Any = vals
             elif isinstance(c, cbk.Group):
                 val = walk(c)
-                groups[id(c)] = val
             else:
                 val = dec_value(c, ev[pos])
                 pos += 1
             if not c.is_filler:
                 d[c.name] = val
+        if g.is_segment_redefine:
+            for ch in (c for c in redefines if c.parent_segment is g):
+                e = ev[pos]
+                assert int(e["kind"]) == O.EV_CHILDREN and int(e["node"]) == ast.node_of(ch)
+                pos += 1
+                d[ch.name] = [walk(ch) for _ in range(int(e["lo"]))]
         return d
 
-    tops = []
-    for g in ast.cb.ast.children:
-        v = walk(g)
-        groups[id(g)] = v
-        tops.append((g, v))
-    return pos, tops
+    return [(g, walk(g)) for g in cb.ast.children if isinstance(g, cbk.Group) and g.parent_segment is None]
 
 
 def hier_rows(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
               entries: Optional[List[Entry]] = None) -> List[dict]:
-    """VarLenHierarchicalIterator (:83-160) per index entry + extractHierarchicalRecord (:211-385)
-    + applyRecordPostProcessing.  Every record is decoded whole (no segment-redefine nulls: the
-    hierarchical walk decodes each segment from its own record at the segment's offset)."""
+    """VarLenHierarchicalIterator (:83-160) per index entry -- records grouped from one root segment
+    record to the next -- + extractHierarchicalRecord (oracle/cobrix_oracle.c ora_extract_hier: one
+    dependFields map shared by the hierarchical record's segments, the root from record_start_offset,
+    children at their group's offset in their own data, the reference's DFS order) +
+    applyRecordPostProcessing."""
     if entries is None:
         entries = sparse_index(cb, data, p, file_id) if index_generation_needed(p) else [Entry(0, -1, file_id, 0)]
     red = p.segment_id_redefine_map
     roots = set(root_segment_ids(cb, p))
-    redefines = cb.all_segment_redefines()
-    children = {g.name: [c for c in redefines if c.parent_segment is not None and c.parent_segment.name == g.name]
-                for g in redefines}
+    ast = O.OracleAst(cb)
+    tb = _hier_tables(cb, ast)
+    group_node = {g.name: ast.node_of(g) for g in cb.all_segment_redefines()}
+    keys: Dict[str, int] = {}
+    L = O.lib()
     out: List[dict] = []
+
+    def emit(recs: List[Tuple[str, bytes]], record_id: int):
+        n = len(recs)
+        bufs = [np.frombuffer(r, dtype=np.uint8) if len(r) else np.zeros(1, np.uint8) for _, r in recs]
+        ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+        lens = np.array([len(r) for _, r in recs], np.int32)
+        seg_group = np.array([group_node.get(red.get(sid, ""), -1) for sid, _ in recs], np.int32)
+        seg_key = np.array([keys.setdefault(sid, len(keys)) for sid, _ in recs], np.int32)
+        ev_cap = max(1, n * ast.max_events_per_record() * 2 + 64)
+        ev = np.zeros(ev_cap, dtype=O.EVENT_DTYPE)
+        heap_cap = max(64, sum(len(r) for _, r in recs) * 3 * (1 + len(group_node)) + 64 * n + 64)
+        heap = np.zeros(heap_cap, dtype=np.uint8)
+        n_ev, hl = ctypes.c_int64(0), ctypes.c_int64(0)
+        rc = L.ora_extract_hier(ctypes.addressof(ast.nodes), 0, ctypes.addressof(ast.handlers),
+                                ctypes.addressof(ast.opts), n, ptrs, O._ptr(lens), O._ptr(seg_group), O._ptr(seg_key),
+                                O._ptr(tb["begin"]), O._ptr(tb["end"]), O._ptr(tb["children"]), O._ptr(tb["offset"]),
+                                O._ptr(tb["child"]), O._ptr(tb["has_parent"]), p.start_offset, 0, O._ptr(ev), ev_cap,
+                                ctypes.byref(n_ev), O._ptr(heap), heap_cap, ctypes.byref(hl))
+        if rc != 0:
+            raise RuntimeError(f"oracle hierarchical decode failed: {rc}")
+        recs_v = _hier_row_values(ast, ev[:n_ev.value], heap[:hl.value].tobytes())
+        row: Dict[str, Any] = {}
+        if p.generate_record_id:
+            row["File_Id"] = e.file_id
+            row["Record_Id"] = record_id
+        if p.schema_policy == "collapse_root":
+            for _, v in recs_v:
+                row.update(v)
+        else:
+            row.update({g.name: v for g, v in recs_v})
+        out.append(row)
+
     for e in entries:
         raw = raw_records(cb, data, p, e)
-        # the root record from offsetBytes = record_start_offset (:139-144 -> :379-381); a child segment
-        # at its group's offset in its own data, without the start offset (extractChildren, :308-310)
-        res = O.decode_records(cb, [r for _, r in raw], start_offset=p.start_offset, active_segments="*")
-        res0 = res if not p.start_offset else O.decode_records(cb, [r for _, r in raw], start_offset=0,
-                                                               active_segments="*")
-        pos = pos0 = 0
-        decoded = []   # per record: {id(group): dict}, decoded as a child (no start offset)
-        tops_of = []   # per record: the top-level groups, decoded as a root
-        for _ in raw:
-            gm: Dict[int, Any] = {}
-            pos, tops = _full_record(res, pos, gm)
-            if res0 is not res:
-                gm = {}
-                pos0, _ = _full_record(res0, pos0, gm)
-            decoded.append(gm)
-            tops_of.append(tops)
-
-        def group_values(group, vals: dict, seg_idx: List[int], cur: int, parent_ids: List[str]) -> dict:
-            d = {}
-            for c in group.children:
-                if c.is_filler or c.is_child_segment:
-                    continue
-                v = vals[c.name]
-                if isinstance(c, cbk.Group):
-                    v = [group_values(c, x, seg_idx, cur, parent_ids) for x in v] if c.is_array else \
-                        group_values(c, v, seg_idx, cur, parent_ids)
-                d[c.name] = v
-            if group.is_segment_redefine:
-                for ch in children[group.name]:
-                    d[ch.name] = extract_children(ch, seg_idx, cur + 1, parent_ids)
-            return d
-
-        def extract_children(field, seg_idx: List[int], cur: int, parent_ids: List[str]) -> list:
-            kids = []
-            i = cur
-            while i < len(seg_idx):
-                sid = raw[seg_idx[i]][0]
-                if red.get(sid, "") == field.name:
-                    kids.append(group_values(field, decoded[seg_idx[i]][id(field)], seg_idx, i, [sid] + parent_ids))
-                elif sid in parent_ids:
-                    break
-                i += 1
-            return kids
-
-        def emit(seg_idx: List[int], record_id: int):
-            r0 = seg_idx[0]
-            recs = [(g, group_values(g, v, seg_idx, 0, [raw[r0][0]])) for g, v in tops_of[r0]
-                    if isinstance(g, cbk.Group) and g.parent_segment is None]
-            row: Dict[str, Any] = {}
-            if p.generate_record_id:
-                row["File_Id"] = e.file_id
-                row["Record_Id"] = record_id
-            if p.schema_policy == "collapse_root":
-                for _, v in recs:
-                    row.update(v)
-            else:
-                row.update({g.name: v for g, v in recs})
-            out.append(row)
-
         record_index = e.record_index
-        fetched: List[int] = []
-        for i, (sid, _) in enumerate(raw):
+        fetched: List[Tuple[str, bytes]] = []
+        for sid, rec in raw:
             if sid in roots:
                 if fetched:
                     emit(fetched, record_index)
                     fetched = []
-                fetched.append(i)
+                fetched.append((sid, rec))
             elif fetched:
-                fetched.append(i)
+                fetched.append((sid, rec))
             record_index += 1
         if fetched:
             emit(fetched, record_index)

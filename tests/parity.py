@@ -105,7 +105,7 @@ def compare_sample(batch, idx: np.ndarray, res: "O.OracleResult", max_report: in
     words = pitch // 64
     dev_idx = torch.as_tensor(idx, dtype=torch.int64, device=batch.cols[0]["validity"].device)
     for ci, info in enumerate(plan.columns):
-        if info.kind != "value" or info.hidden:
+        if info.kind != "value" or info.hidden or info.list_array >= 0:   # lists: compare_sample_lists
             continue
         c = batch.cols[ci]
         o = ocols.get(res.ast.node_of(info.node))
@@ -169,6 +169,70 @@ def compare_sample(batch, idx: np.ndarray, res: "O.OracleResult", max_report: in
         if bad.any():
             k = int(np.nonzero(bad)[0][0])
             errs.append(f"{info.node.name}: {int(bad.sum())} values differ, first record {idx[rec[k]]}")
+        if len(errs) >= max_report:
+            break
+    return errs
+
+
+def compare_sample_lists(batch, idx: np.ndarray, res: "O.OracleResult", max_report: int = 10) -> List[str]:
+    """compare_sample for the list-layout columns (OCCURS DEPENDING ON elements packed per record):
+    for every sampled record its element count, list offset and the values + validity of its present
+    elements, gathered on the device, against the oracle's decode of those records."""
+    import torch
+    plan = batch.plan
+    ocols = O.columns(res)
+    errs: List[str] = []
+    dev = batch.cols[0]["validity"].device
+    di = torch.as_tensor(idx, dtype=torch.int64, device=dev)
+    for ci, info in enumerate(plan.columns):
+        if info.list_array < 0 or info.kind != "value" or info.hidden:
+            continue
+        ar = plan.arrays[info.list_array]
+        cnt = batch.cols[ar.count_column]["values"][di].to(torch.int64)
+        cv = batch.cols[ar.count_column]["validity"]
+        cbit = ((cv[di // 64] >> (di % 64)) & 1).bool()
+        cnt = torch.where(cbit, cnt, torch.zeros_like(cnt)).cpu().numpy()
+        off = batch.cols[ar.offsets_column]["values"][di].to(torch.int64).cpu().numpy()
+        o = ocols.get(res.ast.node_of(info.node))
+        orec = o["rec"].astype(np.int64) if o is not None else np.zeros(0, np.int64)
+        oslot = o["slot"].astype(np.int64) if o is not None else np.zeros(0, np.int64)
+        n_exp = np.zeros(len(idx), np.int64)
+        np.maximum.at(n_exp, orec, oslot + 1)
+        if not np.array_equal(cnt, n_exp):
+            k = int(np.nonzero(cnt != n_exp)[0][0])
+            errs.append(f"{info.node.name}: element count {cnt[k]} != {n_exp[k]} at record {idx[k]}")
+            continue
+        if not cnt.sum():
+            continue
+        pos = np.concatenate([off[k] + np.arange(cnt[k]) for k in range(len(idx))])
+        who = np.repeat(np.arange(len(idx)), cnt)
+        j = np.concatenate([np.arange(c) for c in cnt])
+        tp = torch.as_tensor(pos, dtype=torch.int64, device=dev)
+        vbits = ((batch.cols[ci]["validity"][tp // 64] >> (tp % 64)) & 1).bool().cpu().numpy()
+        vals = batch.cols[ci]["values"]
+        # the oracle's entries in (record, element) order, matched to the gathered elements
+        okey = orec * 65536 + oslot
+        srt = np.argsort(okey, kind="stable")
+        okey, ovalid = okey[srt], o["valid"][srt].astype(bool)
+        olo, ohi = o["lo"][srt].astype(np.int64), o["hi"][srt].astype(np.int64)
+        gk = who.astype(np.int64) * 65536 + j
+        at = np.searchsorted(okey, gk)
+        found = (at < len(okey)) & (okey[np.minimum(at, len(okey) - 1)] == gk)
+        at = np.minimum(at, len(okey) - 1)
+        bad = ~found | (ovalid[at] != vbits)
+        both = found & ovalid[at] & vbits
+        if info.out_type == N.O_DEC128:
+            got = vals.view(-1, 2)[tp].cpu().numpy()
+            bad |= both & ((got[:, 0] != olo[at]) | (got[:, 1] != ohi[at]))
+        elif N.OUT_WIDTH[info.out_type] == 4:
+            got = vals.view(-1)[tp].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+            bad |= both & (got != (olo[at] & 0xFFFFFFFF))
+        else:
+            got = vals.view(-1)[tp].cpu().numpy().astype(np.int64)
+            bad |= both & (got != olo[at])
+        bad = int(bad.sum())
+        if bad:
+            errs.append(f"{info.node.name}: {bad} of {len(pos)} sampled elements differ")
         if len(errs) >= max_report:
             break
     return errs

@@ -166,3 +166,51 @@ def test_hier_record_id_is_next_root():
     assert rows == RO.var_len_rows(rd.copybook, bytes(recs), p)
     assert [len(r["COMPANY"]["DEPT"]) for r in rows] == [1, 0, 0]
     assert len(rows[0]["COMPANY"]["DEPT"][0]["EMPLOYEE"]) == 1
+
+
+def _hier_odo_stream(n: int, seed: int, start: int = 0) -> bytes:
+    """Records of tests/test_hier_oracle.py's layout: parents, children and grandchildren in tree
+    order (with strays), count digits often invalid (null dependees), every length."""
+    rnd = random.Random(seed)
+    out = bytearray()
+    digits = "0123456789X "
+    while n > 0:
+        kind = rnd.choice("PPCCCGGGZ")
+        if kind == "P":
+            body = "P" + rnd.choice(digits) + "NAME" + rnd.choice(digits) + "AB" * 5
+        elif kind == "C":
+            body = "C" + rnd.choice(digits) + "ABC" + rnd.choice(digits) + "aa" * 5 + "bb" * 5 + "hhhhh"
+        elif kind == "G":
+            body = "G" + rnd.choice(digits) + rnd.choice(digits) + "xyzuv"
+        else:
+            body = rnd.choice("QZ") + "9" * 10
+        if rnd.random() < 0.15:
+            body = body[:rnd.randint(1, len(body))]
+        b = bytes(rnd.randrange(256) for _ in range(start)) + body.encode("cp037")
+        out += bytes([0, 0, len(b) & 0xFF, len(b) >> 8]) + b
+        n -= 1
+    return bytes(out)
+
+
+@pytest.mark.parametrize("start", [0, 3])
+@pytest.mark.parametrize("views", [False, True])
+def test_hier_shared_dependees_vs_oracle(start, views):
+    """Arrays of child segments DEPENDING ON a field of the parent segment, of the common header
+    (registered by the root only) and of their own segment when that field is null (the previous
+    registration stays): the GPU resolves the counts the shared dependFields map gives
+    (RecordExtractors.scala:224-245) and decodes the rows with them (cbx_plan_set_odo_counts); rows
+    equal the oracle's ora_extract_hier walk."""
+    import dataclasses
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import VarLenNestedReader
+    from test_hier_oracle import HIER_ODO_COPYBOOK, HIER_ODO_OPTS
+    raw = _hier_odo_stream(6000, 17 + start, start)
+    for jit in (-1, 1):
+        p, _ = parse_options({**HIER_ODO_OPTS, "generate_record_id": "true", "record_start_offset": str(start)})
+        p = dataclasses.replace(p, string_views=views, jit_min_records=jit)
+        rd = VarLenNestedReader(HIER_ODO_COPYBOOK, p)
+        rows = rd.read(raw).to_rows()
+        exp = RO.var_len_rows(rd.copybook, raw, p)
+        assert len(rows) == len(exp) > 100
+        bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
+        assert not bad, (jit, bad[:5], rows[bad[0]], exp[bad[0]])

@@ -470,3 +470,136 @@ def test_utf8_layout_capacity_overflow_reported():
     assert e.value.code == N.CBX_E_CAPACITY
     assert all(c["data"].numel() == g.numel() for c, g in zip(cols, guard))
     N.check(L.cbx_plan_check(rd.native.handle, None))   # the flag is cleared
+
+
+COMPOSE_COPYBOOK = """
+       01  REC.
+           05  S01   PIC X(1).
+           05  S03   PIC X(3).
+           05  S04   PIC X(4).
+           05  S05   PIC X(5).
+           05  S07   PIC X(7).
+           05  S08   PIC X(8).
+           05  S13   PIC X(13).
+           05  S20   PIC X(20).
+           05  S31   PIC X(31).
+           05  S32   PIC X(32).
+"""
+
+
+def _compose_records(n: int, size: int, seed: int) -> bytes:
+    """Record bytes that exercise the string compose: any byte value (cp037 maps half of them to
+    2-byte UTF-8, and 0x00-0x3F to C0/C1 controls, some trimmable), text with runs of EBCDIC
+    spaces at either end, all-space and all-wide values."""
+    rng = np.random.default_rng(seed)
+    out = np.empty((n, size), dtype=np.uint8)
+    kind = rng.integers(0, 5, n)
+    out[:] = rng.integers(0, 256, (n, size), dtype=np.uint8)
+    text = rng.integers(0x40, 0xFF, (n, size), dtype=np.uint8)
+    out[kind == 1] = text[kind == 1]
+    pad = rng.random((n, size)) < 0.3
+    out[(kind == 2)[:, None] & pad] = 0x40
+    out[kind == 3] = 0x40
+    out[kind == 4] = rng.integers(0x80, 0x100, (int((kind == 4).sum()), size), dtype=np.uint8)
+    return out.tobytes()
+
+
+@pytest.mark.parametrize("views", ["views", "utf8"])
+@pytest.mark.parametrize("trim", ["none", "left", "right", "both"])
+@pytest.mark.parametrize("jit", [-1, 1])
+def test_two_byte_page_compose_vs_oracle(views, trim, jit):
+    """Register-path strings of a 2-byte code page (cp037: str_lane_group2 composes 4 characters at a
+    time and places them with dword LDS stores) -- fields of 1-32 bytes at every dword phase, every
+    trimming policy, both kernels, the view and Utf8 layouts -- against the oracle's
+    StringDecoders.decodeEbcdicString + StringTools.trim* restatement."""
+    cb = cbk.parse_copybook(COMPOSE_COPYBOOK, code_page="cp037", string_trimming=trim)
+    data = _compose_records(4097, cb.record_size, seed=len(trim) + 7 * (jit + 2))
+    rd, batch = _fixed(COMPOSE_COPYBOOK, data, ebcdic_code_page="cp037", string_trimming_policy=trim,
+                       jit_min_records=jit, **_layout(views))
+    if jit == 1:
+        assert _kernel_kind(rd) == 1
+    errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
+    assert not errs, errs[:10]
+
+
+def _wide_odo_forced(n_roots: int, seed: int):
+    """C5 records (wide_odo) with the NUM-STRAT dependee forced, root by root, to 0, 1, 2000, out of
+    range (2001, 65535) or random, and a share of C records cut before NUM-STRAT (a null dependee:
+    decodeTypeValue past the record end, so the array takes its maximum) or inside the elements."""
+    from cobrix_amd.synth import wide_odo
+    raw_t, hdr = wide_odo(n_roots, seed=seed)
+    raw = raw_t.numpy()
+    hdr = hdr.numpy()
+    rng = np.random.default_rng(seed)
+    out = bytearray()
+    forced = [0, 1, 2000, 2001, 65535]
+    ci = 0
+    for i, h in enumerate(hdr):
+        ln = int(raw[h + 2]) | int(raw[h + 3]) << 8
+        payload = bytearray(raw[h + 4:h + 4 + ln].tobytes())
+        if payload[0] == 0xC3:
+            cnt = forced[ci % 6] if ci % 6 < 5 else int(rng.integers(0, 2001))
+            payload[64:66] = cnt.to_bytes(2, "big")
+            ci += 1
+            u = rng.random()
+            if u < 0.03:
+                payload = payload[:int(rng.integers(1, 66))]            # NUM-STRAT missing: null
+            elif u < 0.06:
+                payload = payload[:int(rng.integers(66, len(payload)))]  # elements cut short
+        out += bytes([0, 0, len(payload) & 0xFF, len(payload) >> 8]) + bytes(payload)
+    return bytes(out)
+
+
+@pytest.mark.parametrize("jit", [0, 1])
+def test_wide_odo_forced_counts_vs_oracle(jit):
+    """C5 at 2,000 roots (+ ~4,000 children): element counts 0, 1, 2000, out of range and null
+    (RecordExtractors.scala:66-114 extractArray: a dependee outside [min, max] or unset -> max), short
+    records, both kernels, the list layout -- every value bit-exact against the oracle."""
+    from cobrix_amd.synth import WIDE_ODO_COPYBOOK, WIDE_ODO_SEGMENTS
+    raw = _wide_odo_forced(2000, seed=31 + jit)
+    params = ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
+                              segment_id_redefine_map=WIDE_ODO_SEGMENTS, occurs_lists=True, jit_min_records=jit)
+    rd = VarLenNestedReader(WIDE_ODO_COPYBOOK, params)
+    t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+    off, ln = rd.frame(t, len(raw))
+    eo, el = O.frame_rdw(raw)
+    assert np.array_equal(off.cpu().numpy(), eo) and np.array_equal(ln.cpu().numpy(), el)
+    batch = rd.decode_device(t, len(raw), off, ln)
+    segs = [{"C": "STATIC_DETAILS", "P": "CONTACTS"}.get(G.java_trim(raw[o:o + min(5, l)].decode("cp037")))
+            for o, l in zip(eo, el)]
+    res = O.decode_records(rd.copybook, [raw[o:o + l] for o, l in zip(eo, el)], active_segments=segs)
+    errs = compare_batch(batch, res)
+    assert not errs, errs
+    # every forced count class is present
+    cnt_ci = rd.plan.arrays[0].count_column
+    cnts = batch.host_column(cnt_ci)["values"][:batch.n_rec]
+    for c in (0, 1, 2000):
+        assert (cnts == c).any()
+
+
+def test_wide_odo_full_size_sampled_parity():
+    """C5 as the bench runs it (770,000 roots + children = 2.31 M records, 12.5 GB, list layout, the
+    specialised kernels): 2,000 records sampled across the batch -- counts, list offsets and every
+    present element -- bit-exact against the oracle's decode of the same records."""
+    from parity import compare_sample_lists, compare_sample
+    from cobrix_amd.synth import WIDE_ODO_COPYBOOK, WIDE_ODO_SEGMENTS, wide_odo
+    raw_t, _ = wide_odo(770_000, seed=20261018, device="cuda")
+    params = ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
+                              segment_id_redefine_map=WIDE_ODO_SEGMENTS, occurs_lists=True, string_views=True)
+    rd = VarLenNestedReader(WIDE_ODO_COPYBOOK, params)
+    n_bytes = int(raw_t.numel())
+    off, ln = rd.frame(raw_t, n_bytes)
+    batch = rd.decode_device(raw_t, n_bytes, off, ln)
+    assert batch.n_rec > 2_000_000 and _kernel_kind(rd) == 1
+    rng = np.random.default_rng(12)
+    n = batch.n_rec
+    idx = np.unique(np.concatenate([np.arange(64), n - 64 + np.arange(64), rng.integers(0, n, 1872)]))
+    offs = off[torch.as_tensor(idx, device="cuda")].cpu().numpy()
+    lens = ln[torch.as_tensor(idx, device="cuda")].cpu().numpy()
+    recs = [raw_t[o:o + l].cpu().numpy().tobytes() for o, l in zip(offs, lens)]
+    segs = [{"C": "STATIC_DETAILS", "P": "CONTACTS"}.get(G.java_trim(r[:5].decode("cp037"))) for r in recs]
+    res = O.decode_records(rd.copybook, recs, active_segments=segs)
+    errs = compare_sample(batch, idx, res) + compare_sample_lists(batch, idx, res)
+    assert not errs, errs
+    del batch, raw_t
+    torch.cuda.empty_cache()

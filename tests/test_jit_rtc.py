@@ -56,9 +56,9 @@ def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False) -> 
         body = "".join(f"    {{ constexpr StrOp op = {o}; str_element<{view}>(a, op, a.sops + {i}, ldc(a.scall + {i}), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane); }}\n"
                        for i, o in enumerate(ops))
     lut = ("  WaveLds l = wave_lds(a, smem + 1024, wid);\n  l.lut = (uint32_t*)smem;\n"
-           "  for (int i = threadIdx.x; i < 256; i += blockDim.x) { const uint32_t e = a.lut[i]; l.lut[i] = e; l.lut[256 + i] = count_lut_entry(e); }\n"
+           "  for (int i = threadIdx.x; i < 256; i += blockDim.x) { const uint32_t e = a.lut[i]; l.lut[i] = e; ((uint8_t*)(l.lut + 256))[i] = count_lut_byte(e); }\n"
            if count else
-           "  const WaveLds l = wave_lds(a, smem, wid);\n  for (int i = threadIdx.x; i < 256; i += blockDim.x) l.lut[i] = a.lut[i];\n")
+           "  const WaveLds l = wave_lds(a, smem, wid);\n  lut_lds_fill(a, l.lut);\n")
     sig = ("(const KernelArgs& a, const TileCtx& t, const uint8_t* img,\n"
            "      uint32_t rec_addr, const WaveLds& l, int lane, Stamps& st) {\n")
     return (f"#define CBX_STR_LAYOUT {layout}\n#define CBX_MODE {1 if count else 0}\n" + ("#define CBX_COUNT_LUT 1\n" if count else "") +
