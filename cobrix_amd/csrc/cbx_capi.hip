@@ -874,8 +874,8 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.list_flag = P->d_list_flag;
     const int n_defer = n_defer_seq;
     a.defer_bits = P->d_defer_bits;
-    const size_t lds = kLutLds + (size_t)kWavesPerBlock * a.lds_wave;
-    if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
+    const size_t lds_own = kLutLds + (size_t)kWavesPerBlock * a.lds_wave;
+    if (lds_own > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
     // resident blocks per CU: the LDS bound and the runtime's occupancy (registers); the grid
     // never exceeds what can be co-resident, so the static tile order of the look-back holds
     // copybook-specialised kernel for large contiguous batches (cbx_jit.h)
@@ -899,6 +899,12 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         jfn = P->jit_fn[k];
     }
     P->last_kind = jfn ? 1 : 0;
+    // cooperative tiles (cbx_jit.h jit_coop, cbx_device.h coop_loop): one image per workgroup,
+    // one tile per workgroup
+    int coop_mid = 0;
+    const bool coop = jfn && jit_coop(contig, span, jit_pro(P), S.win, S.nops, S.sops, &coop_mid);
+    const size_t lds = coop ? kLutLds + (size_t)a.lds_rows + (size_t)kWavesPerBlock * (a.lds_wave - a.lds_rows) : lds_own;
+    if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
     int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / lds));
     int occ = 0;
     const hipError_t oe = jfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, jfn, kWave * kWavesPerBlock, lds)
@@ -907,9 +913,9 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // string-dominated contiguous layouts run best at 4 workgroups (8 waves) per CU: SYNSTR200 (10 x
     // X(20)) decodes in 8.7 ms at 4, 13.4 ms at 5 and 11.6 ms at 3, while SYN200 (1 string, 27
     // numerics) and the windowed C4/C5 layouts gain from every extra resident workgroup
-    if (contig && S.sops.size() >= S.nops.size() && S.sops.size() > 0) blocks_per_cu = std::min(blocks_per_cu, 4);
+    if (!coop && contig && S.sops.size() >= S.nops.size() && S.sops.size() > 0) blocks_per_cu = std::min(blocks_per_cu, 4);
     if (const char* e = getenv("CBX_MAX_BLOCKS_PER_CU")) blocks_per_cu = std::max(1, std::min(blocks_per_cu, atoi(e)));   // tuning
-    const int64_t blocks_needed = (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t blocks_needed = coop ? n_tiles : (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t grid = std::min<int64_t>(blocks_needed, (int64_t)P->num_cus * blocks_per_cu);
     const bool prof = P->profiling && mode == 0;
     cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};
@@ -942,22 +948,26 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         ac.mode = 1;
         // the specialised count kernel: no string staging per wave (it only scans lengths), two LUT
         // copies in front (full + count_lut_byte)
-        size_t clds = lds;
+        size_t clds = lds_own;
+        int cmid = 0;
+        const bool ccoop = cfn && jit_coop(true, span, jit_pro(P), S.win, S.nops, S.sops, &cmid);
         if (cfn) {
             ac.lds_wave = (a.lds_rows + a.lds_counts + 16 + 15) & ~15;
-            clds = 1024 + kLutLds + (size_t)kWavesPerBlock * ac.lds_wave;
+            clds = 1024 + kLutLds + (ccoop ? (size_t)a.lds_rows + (size_t)kWavesPerBlock * (ac.lds_wave - a.lds_rows)
+                                           : (size_t)kWavesPerBlock * ac.lds_wave);
         }
         int cocc = 0;
         const hipError_t ce2 = cfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, cfn, kWave * kWavesPerBlock, clds)
                                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, decode_kernel, kWave * kWavesPerBlock, clds);
         int cbpc = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / clds));
         if (ce2 == hipSuccess && cocc > 0) cbpc = std::min(cbpc, cocc);
-        const int64_t cgrid = std::min<int64_t>(blocks_needed, (int64_t)P->num_cus * cbpc);
+        const int64_t cneeded = ccoop ? n_tiles : (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+        const int64_t cgrid = std::min<int64_t>(cneeded, (int64_t)P->num_cus * cbpc);
         if (cfn) {
             void* kargs[] = {&ac};
             HIP_CHECK(hipModuleLaunchKernel(cfn, (unsigned)cgrid, 1, 1, kWave * kWavesPerBlock, 1, 1, (unsigned)clds, st, kargs, nullptr));
         } else {
-            hipLaunchKernelGGL(decode_kernel, dim3((unsigned)cgrid), dim3(kWave * kWavesPerBlock), lds, st, ac);
+            hipLaunchKernelGGL(decode_kernel, dim3((unsigned)cgrid), dim3(kWave * kWavesPerBlock), clds, st, ac);
             HIP_CHECK(hipGetLastError());
         }
         if ((r = string_scan(P, n_tiles, st))) return r;
@@ -1132,6 +1142,8 @@ extern "C" int cbx_plan_check(cbx_plan* P, void* stream) {
     HIP_CHECK(hipStreamSynchronize(st));
     if (status != 0) {
         HIP_CHECK(hipMemset(P->d_status, 0, sizeof(int32_t)));
+        if (status & 4)   // (cbx_device.h: lds_base_ok)
+            return fail(CBX_E_HIP, "specialised kernel: dynamic LDS does not start at address 0 (its outputs are invalid)");
         return fail(CBX_E_CAPACITY, "a string column's payload exceeded its data_capacity (size it with cbx_string_bound or cbx_string_sizes_*)");
     }
     return CBX_OK;

@@ -532,14 +532,17 @@ __host__ __device__ constexpr int str_lane_slot(int size, int width) {
 // second byte after its first, then zero bytes (0x0C).  Two dwords per entry, 16 entries.
 __host__ __device__ constexpr uint32_t group_sel(int i) {
     const int h = i >> 1;
-    uint32_t b[8] = {0x0C, 0x0C, 0x0C, 0x0C, 0x0C, 0x0C, 0x0C, 0x0C};
+    uint64_t v = 0x0C0C0C0C0C0C0C0Cull;   // the 8 selector bytes (no array: a run-time i indexed one in scratch)
     int n = 0;
     for (int k = 0; k < 4; k++) {
-        b[n++] = (uint32_t)(2 * k);
-        if ((h >> k) & 1) b[n++] = (uint32_t)(2 * k + 1);
+        v = (v & ~(0xFFull << (8 * n))) | ((uint64_t)(2 * k) << (8 * n));
+        n++;
+        if ((h >> k) & 1) {
+            v = (v & ~(0xFFull << (8 * n))) | ((uint64_t)(2 * k + 1) << (8 * n));
+            n++;
+        }
     }
-    const int o = 4 * (i & 1);
-    return b[o] | b[o + 1] << 8 | b[o + 2] << 16 | b[o + 3] << 24;
+    return (uint32_t)(v >> (32 * (i & 1)));
 }
 
 // The code page LUT and the group selectors into the workgroup's LDS (kLutLds bytes at lut).
@@ -562,7 +565,7 @@ constexpr int kStrNC = (kStrFastBytes * 3 + 15) / 16;   // 16-byte words of a la
 // Returns the UTF-8 length.
 __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, int smax, int eo, int n, bool ok,
                                                 const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
-                                                uint8_t* s_str, int lane, u32x4 (&q)[kStrNC]);
+                                                uint8_t* s_str, int lane, u32x4 (&q)[kStrNC], bool zero_tail = true);
 
 // Single-byte code pages: the kept bytes [b, e) are the mapped bytes shifted down by b -- packed
 // into dwords, a 3-stage dword shift by b / 4 and one byte align, in registers (no LDS).
@@ -606,34 +609,45 @@ __device__ __forceinline__ int str_lane_shift(int smax, const uint32_t (&ev)[kSt
 // 2-byte code pages (every character 1 or 2 UTF-8 bytes: cp037, cp500, cp875, ...): the field's
 // UTF-8 bytes composed 4 characters at a time in registers and placed in the lane's LDS slot with
 // dword stores only.  A group's characters give two dwords of byte pairs (U01, U23: first byte, then
-// the second one or 0); one pattern selector (str_group_sel: which of the 4 are wide) and two v_perm
+// the second one or 0); one pattern selector (group_sel: which of the 4 are wide) and two v_perm
 // compact them to the group's 4..8 bytes; the group lands at its running byte position through a
 // 64-bit shift, OR-ed into the partial dword carried from the previous group, as one 2-dword store
 // at a dword boundary.  The untrimmed field is composed (a trimmed leading character is <= U+0020,
 // one UTF-8 byte), starting at phase (-b) & 3, so the kept bytes [b, e) begin on a dword and are
-// read back packed from byte 0.  Per character: the LUT read and ~4 VALU; per group: one 8-byte LDS
-// read and one 8-byte LDS store -- where the byte path (string_write32e) issued two byte stores per
-// character (SYNSTR200: 43 LDS stores per value).
+// read back packed from byte 0.  Per group, from the 4 entries' byte 3 gathered into one dword (two
+// v_perm: trim flag bit 7, UTF-8 length bits 0-1 per byte): the selector's byte offset and the
+// group's byte count as one v_dot4 each.  Every group's selector is read before the first slot
+// store (the reads do not wait behind the stores).  zero_tail: the bytes of q[0] past the value
+// zeroed (a short string view inlines them; the Utf8 store writes exactly len bytes and skips it).
+// Read-backs past the lane's slot (dwords beyond the value) land in the next lane's slot or read 0
+// past the workgroup's LDS -- never part of a value.
 __device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kStrFastBytes], int b, int e,
-                                               const uint32_t* s_lut, uint8_t* slot, u32x4 (&q)[kStrNC]) {
-    const uint32_t* s_sel = s_lut + 256;
-    uint32_t wide = 0;   // bit j: character j is 2 UTF-8 bytes (entry length 2: bit 25)
+                                               const uint32_t* s_lut, uint8_t* slot, u32x4 (&q)[kStrNC],
+                                               bool zero_tail = true) {
+    constexpr int kNG = (kStrFastBytes + 3) / 4;
+    uint32_t u01[kNG], u23[kNG], nb[kNG];
+    uint2 sel[kNG];
+    uint32_t wide = 0;   // bit j: character j is 2 UTF-8 bytes
 #pragma unroll
-    for (int j = 0; j < kStrFastBytes; j++)
-        if (j < smax) wide |= ((ev[j] >> 25) & 1u) << j;
+    for (int g = 0; g < kNG; g++) {
+        if (4 * g >= smax) break;
+        const uint32_t e0 = ev[4 * g], e1 = 4 * g + 1 < smax ? ev[4 * g + 1] : 0u;
+        const uint32_t e2 = 4 * g + 2 < smax ? ev[4 * g + 2] : 0u, e3 = 4 * g + 3 < smax ? ev[4 * g + 3] : 0u;
+        u01[g] = __builtin_amdgcn_perm(e1, e0, 0x05040100u);   // c0.b0 c0.b1 c1.b0 c1.b1
+        u23[g] = __builtin_amdgcn_perm(e3, e2, 0x05040100u);
+        const uint32_t lb = __builtin_amdgcn_perm(e1, e0, 0x0C0C0703u) | __builtin_amdgcn_perm(e3, e2, 0x07030C0Cu);
+        const uint32_t so = __builtin_amdgcn_udot4(lb & 0x02020202u, 0x20100804u, 0u, false);   // 8 * (wide bits h)
+        nb[g] = __builtin_amdgcn_udot4(lb & 0x03030303u, 0x01010101u, 0u, false);            // 4 + popc(h)
+        wide |= g == 0 ? so >> 3 : so << (4 * g - 3);
+        sel[g] = *(const uint2*)((const uint8_t*)(s_lut + 256) + so);
+    }
     const int len = (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b));
     const uint32_t s0 = (uint32_t)(-b) & 3u;
     uint32_t carry = 0, pos = s0;
 #pragma unroll
-    for (int g = 0; 4 * g < kStrFastBytes; g++) {
+    for (int g = 0; g < kNG; g++) {
         if (4 * g >= smax) break;
-        const uint32_t e0 = ev[4 * g], e1 = 4 * g + 1 < smax ? ev[4 * g + 1] : 0u;
-        const uint32_t e2 = 4 * g + 2 < smax ? ev[4 * g + 2] : 0u, e3 = 4 * g + 3 < smax ? ev[4 * g + 3] : 0u;
-        const uint32_t u01 = __builtin_amdgcn_perm(e1, e0, 0x05040100u);   // c0.b0 c0.b1 c1.b0 c1.b1
-        const uint32_t u23 = __builtin_amdgcn_perm(e3, e2, 0x05040100u);
-        const uint32_t h = (wide >> (4 * g)) & 15u;
-        const uint2 sel = *(const uint2*)(s_sel + 2 * h);
-        const uint32_t lo = __builtin_amdgcn_perm(u23, u01, sel.x), hi = __builtin_amdgcn_perm(u23, u01, sel.y);
+        const uint32_t lo = __builtin_amdgcn_perm(u23[g], u01[g], sel[g].x), hi = __builtin_amdgcn_perm(u23[g], u01[g], sel[g].y);
         const uint32_t k8 = 8u * (pos & 3u);
         const uint64_t v = (((uint64_t)hi << 32) | lo) << k8;
         const uint32_t w0 = (uint32_t)v | carry, w1 = (uint32_t)(v >> 32);
@@ -641,25 +655,20 @@ __device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kS
         uint32_t* d = (uint32_t*)(slot + (pos & ~3u));
         d[0] = w0;
         d[1] = w1;
-        const uint32_t np = pos + 4u + popc32(h);
+        const uint32_t np = pos + nb[g];
         carry = ((np >> 2) - (pos >> 2)) == 2u ? w2 : w1;
         pos = np;
     }
     *(uint32_t*)(slot + (pos & ~3u)) = carry;
-    // the kept bytes, packed from byte 0 (dword reads clamped to the slot)
-    const uint32_t* sd = (const uint32_t*)slot;
-    const int last = (str_lane_slot(smax, 2) >> 2) - 1;
-    const int s_dw = (int)((s0 + (uint32_t)b) >> 2);
+    // the kept bytes, packed from byte 0
+    const uint32_t* sd = (const uint32_t*)slot + ((s0 + (uint32_t)b) >> 2);
 #pragma unroll
     for (int k = 0; k < kStrNC; k++) {
         if (16 * k < 2 * smax) {
             uint32_t d4[4];
 #pragma unroll
-            for (int m = 0; m < 4; m++) {
-                const int i = s_dw + 4 * k + m;
-                d4[m] = 16 * k + 4 * m < 2 * smax ? sd[i < last ? i : last] : 0u;
-            }
-            if (k == 0) {
+            for (int m = 0; m < 4; m++) d4[m] = 16 * k + 4 * m < 2 * smax ? sd[4 * k + m] : 0u;
+            if (k == 0 && zero_tail) {
                 // a short string view inlines these dwords: zero the bytes past the value (the
                 // slot holds the untrimmed field there)
 #pragma unroll
@@ -676,7 +685,7 @@ __device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kS
 
 __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, int smax, int eo, int n, bool ok,
                                                 const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
-                                                uint8_t* s_str, int lane, u32x4 (&q)[kStrNC]) {
+                                                uint8_t* s_str, int lane, u32x4 (&q)[kStrNC], bool zero_tail) {
     uint32_t w[8], ev[kStrFastBytes];
     img_bytes32(src, rec_addr + (ok ? (uint32_t)eo : 0u), smax, w);
 #ifndef CBX_STR_NO_SDWA
@@ -705,7 +714,7 @@ __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, i
     if (width == 1) return str_lane_shift(smax, ev, b, e, q);
 #endif
 #ifndef CBX_STR_W2_BYTES   // (A/B: the byte-store compose below for 2-byte pages too)
-    if (width == 2) return str_lane_group2(smax, ev, b, e, s_lut, s_str + lane * str_lane_slot(smax, 2), q);
+    if (width == 2) return str_lane_group2(smax, ev, b, e, s_lut, s_str + lane * str_lane_slot(smax, 2), q, zero_tail);
 #endif
     const uint32_t range = bits_below(e) & ~bits_below(b);
     uint8_t* slot = s_str + lane * str_lane_slot(smax, width);
@@ -931,7 +940,7 @@ __device__ __forceinline__ int utf8_compose(const KernelArgs& a, const StrOp& op
     const int o = a.start_off + op.eo;
     ok = el && o <= t.avail;
     const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
-    const int len = str_lane_compose(op.kind, op.trim, op.pad, op.size, op.eo, n, ok, src, rec_addr, s_lut, s_str, lane, q);
+    const int len = str_lane_compose(op.kind, op.trim, op.pad, op.size, op.eo, n, ok, src, rec_addr, s_lut, s_str, lane, q, false);
     return ok ? len : 0;
 }
 
@@ -1580,15 +1589,46 @@ struct WaveLds {
     uint8_t* img;       // record image (after the front guard)
     int32_t* cnt;       // OCCURS element counts
     uint8_t* str;       // string payload staging
+    int wid;            // the wave in its workgroup (coop_loop: which part of the tile's ops it runs)
 };
+
+// LDS byte address off as a pointer the compiler knows as a constant.  The kernels' only LDS is the
+// dynamic area (extern smem, no static __shared__), which starts at LDS address 0, so the LUT at its
+// front is at constant address 0: a LUT read's address is the byte * 4 itself, where the relocated
+// smem symbol cost a v_add of 0 per read (resolved after instruction selection).  lds_base_ok checks
+// the assumption on the device.
+__device__ __forceinline__ uint8_t* lds_abs(uint32_t off) {
+    return (uint8_t*)(__attribute__((address_space(3))) uint8_t*)(size_t)off;
+}
+__device__ __forceinline__ bool lds_base_ok(const uint8_t* smem) {
+    return (uint32_t)(size_t)(__attribute__((address_space(3))) const uint8_t*)smem == 0u;
+}
 
 __device__ __forceinline__ WaveLds wave_lds(const KernelArgs& a, uint8_t* smem, int wid) {
     WaveLds l;
-    l.lut = (uint32_t*)smem;
+    l.lut = (uint32_t*)lds_abs(0);
     uint8_t* wbase = smem + kLutLds + wid * a.lds_wave;
     l.img = wbase + kGuard;
     l.cnt = (int32_t*)(wbase + a.lds_rows);
     l.str = wbase + a.lds_rows + a.lds_counts;
+    l.wid = wid;
+    return l;
+}
+
+// LDS carve-up of a cooperative workgroup (coop_loop): the LUT, ONE record image for the
+// workgroup's tile, then each wave's counts / string staging / dump area (lds_wave - lds_rows).
+__device__ __forceinline__ WaveLds coop_lds(const KernelArgs& a, uint8_t* smem, int wid) {
+    WaveLds l;
+    l.lut = (uint32_t*)lds_abs(0);
+    // the image offset opaque (an SGPR): with the constant address torch's bundled hipRTC (the one a
+    // product process resolves libhiprtc.so.7 to) crashed compiling the kernel (tests/test_jit_rtc.py)
+    int img_off = kLutLds + kGuard;
+    asm volatile("" : "+s"(img_off));
+    l.img = smem + img_off;
+    uint8_t* wbase = smem + kLutLds + a.lds_rows + wid * (a.lds_wave - a.lds_rows);
+    l.cnt = (int32_t*)wbase;
+    l.str = wbase + a.lds_counts;
+    l.wid = wid;
     return l;
 }
 
@@ -1643,6 +1683,75 @@ __device__ __forceinline__ void contig_loop(const KernelArgs& a, const WaveLds& 
         run_end(a, body, tile, lane);
         wave_sync_lds();
         st.mark(5);   // end of tile
+        tile = next;
+    }
+    st.flush(a, lane);
+}
+
+// Cooperative tiles: the kWavesPerBlock waves of a workgroup decode ONE tile together -- each
+// stages its share of the span's chunks into the workgroup's image and runs its part of the
+// tile's ops (the specialised kernel splits them by cost, body.pre / body.post dispatch on
+// l.wid).  The image (64 records) is shared, so a wave's LDS is its string staging only: on
+// SYNSTR200 (12.8 KB of records per tile) twice the resident waves of contig_loop, whose waves
+// each hold their own tile's image -- string-heavy layouts, whose decode waits on LDS round
+// trips (LUT reads, slot writes and read-backs), want the waves.  Two workgroup barriers per tile
+// (image complete; image read before it is overwritten).  Plans without segment selection,
+// OCCURS arrays and run-gathered words only (the prologue writes nothing, every op's output is
+// its own).  Chunk row u (chunks u * 64 + lane) is staged by wave u % kWavesPerBlock.
+template <int KP>
+__device__ __forceinline__ void coop_issue(const KernelArgs& a, const ContigSpan& sp, int wid, int lane,
+                                           uint4 (&buf)[(KP + kWavesPerBlock - 1) / kWavesPerBlock]) {
+    constexpr int KH = (KP + kWavesPerBlock - 1) / kWavesPerBlock;
+    int64_t left = a.data_len - sp.a0;
+    left = left < 0 ? 0 : (left > (1 << 20) ? (1 << 20) : left);
+    const uint64_t base = (uint64_t)(a.data + sp.a0);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane((int)left);
+    const int nch = __builtin_amdgcn_readfirstlane(sp.nch);
+    void* bp = (void*)(((uint64_t)hi << 32) | lo);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(bp, (short)0, nbytes, 0x00020000);
+#pragma unroll
+    for (int v = 0; v < KH; v++) {
+        const int c = (v * kWavesPerBlock + wid) * kWave + lane;
+        const int off = c < nch ? 16 * c : 0x7ffffff0;   // past the descriptor's range: no access
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        buf[v] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+}
+
+template <int KP, typename Body>
+__device__ __forceinline__ void coop_loop(const KernelArgs& a, const WaveLds& l, int64_t tile, int64_t tstep,
+                                          int lane, Body body) {
+    constexpr int KH = (KP + kWavesPerBlock - 1) / kWavesPerBlock;
+    uint4 buf[KH];
+    const int wid = l.wid;
+    if (tile < a.n_tiles) coop_issue<KP>(a, contig_span(a, tile), wid, lane, buf);
+    Stamps st;
+    st.init();
+    while (tile < a.n_tiles) {
+        const ContigSpan sp = contig_span(a, tile);
+        {
+            int ln = lane;
+            asm volatile("" : "+v"(ln));   // (contig_store: no LDS addresses held across the decode)
+#pragma unroll
+            for (int v = 0; v < KH; v++) {
+                const int c = (v * kWavesPerBlock + wid) * kWave + ln;
+                if (c < sp.nch) contig_put(a, sp, c, buf[v], l.img);
+            }
+        }
+        __syncthreads();   // the tile's image complete
+        st.mark(0);
+        const int64_t next = tile + tstep;
+        coop_issue<KP>(a, contig_span(a, next), wid, lane, buf);
+        st.mark(1);
+        TileCtx t = tile_ctx<false>(a, tile, lane);
+        const uint32_t rec0 = (uint32_t)(lane * a.cpitch + 4 * sp.mis_dw);
+        st.mark(2);
+        body.pre(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
+        body.post(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
+        __syncthreads();   // every wave done with the image
+        st.mark(5);
         tile = next;
     }
     st.flush(a, lane);

@@ -3,11 +3,20 @@ whose headers differ from hipcc's (no <cstdint> extras such as uintptr_t, no hip
 header that only hipcc accepts makes every specialised kernel fall back to the table-driven one on
 the GPU.  These CPU tests compile, through hipRTC (no device needed), sources of the shapes
 jit_source / jit_list_source generate -- the record kernel in the three string layouts and in the
-Utf8 count mode, and the list kernel -- against the headers the library bundles."""
+Utf8 count mode, and the list kernel -- against the headers the library bundles.
+
+Two compilers: the image's (/opt/rocm) and the one bundled with torch.  Both have the soname
+libhiprtc.so.7, so in a process that imported torch first (every product process) the library's
+hipRTC calls resolve to torch's -- an older LLVM, which crashed (SIGSEGV) on the cooperative kernel's
+constant image address before coop_lds made it opaque.  Each compile runs in a child process, so a
+compiler crash fails its test instead of the test run."""
 from __future__ import annotations
 
 import ctypes
+import glob
 import os
+import subprocess
+import sys
 
 import pytest
 
@@ -17,17 +26,20 @@ HEADERS = [("cobrix_hip.h", os.path.join(ROOT, "include", "cobrix_hip.h"))] + [
     (n, os.path.join(CSRC, n)) for n in ("cbx_decode.h", "cbx_internal.h", "cbx_device.h", "cbx_list.h")]
 
 
-def _hiprtc():
-    for p in ("/opt/rocm/lib/libhiprtc.so", "libhiprtc.so"):
-        try:
-            return ctypes.CDLL(p)
-        except OSError:
-            continue
-    pytest.skip("libhiprtc not available")
+def _torch_hiprtc() -> str | None:
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    hits = glob.glob(os.path.join(list(spec.submodule_search_locations)[0], "lib", "libhiprtc.so*"))
+    return hits[0] if hits else None
 
 
-def _compile(src: str) -> str:
-    lib = _hiprtc()
+COMPILERS = [p for p in ("/opt/rocm/lib/libhiprtc.so", _torch_hiprtc()) if p and os.path.exists(p)]
+
+
+def _compile_here(lib_path: str, src: str) -> str:
+    lib = ctypes.CDLL(lib_path)
     texts = [open(p).read().encode() for _, p in HEADERS]
     names = [n.encode() for n, _ in HEADERS]
     prog = ctypes.c_void_p()
@@ -44,7 +56,24 @@ def _compile(src: str) -> str:
     return "" if rc == 0 else (log.value.decode(errors="replace") or f"hiprtc error {rc}")
 
 
-def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False) -> str:
+def _compile(src: str, lib_path: str | None = None) -> str:
+    """Compile src with the hipRTC at lib_path (default: the image's) in a child process; returns the
+    error log, "" on success."""
+    if not COMPILERS:
+        pytest.skip("libhiprtc not available")
+    lib_path = lib_path or COMPILERS[0]
+    code = ("import sys; sys.path.insert(0, %r); import test_jit_rtc as t; "
+            "err = t._compile_here(sys.argv[1], sys.stdin.read()); sys.stdout.write(err); sys.exit(3 if err else 0)"
+            % os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code, lib_path], input=src, capture_output=True, text=True, timeout=600)
+    if r.returncode == 0:
+        return ""
+    return r.stdout or f"hipRTC ({lib_path}) died: exit {r.returncode}\n{r.stderr[-2000:]}"
+
+
+def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coop: bool = False) -> str:
+    """The specialised record kernel's source as cbx_jit.h emits it (jit_source), for a 3-element
+    string layout; coop: the cooperative form (jit_coop: coop_lds / coop_loop, ops split on l.wid)."""
     view = "true" if layout == 1 else "false"
     ops = [f"{{{20 * i},20,1,4,0,2,{i},0,{i},-1,{{0,0,0,0}},{{0,0,0,0}},0}}" for i in range(3)]
     if pair:
@@ -54,11 +83,18 @@ def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False) -> 
         body = f"    for (int i = 0; i < 3; i++) str_element<{view}>(a, ldc(a.sops + i), a.sops + i, ldc(a.scall + i), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane);\n"
     else:
         body = "".join(f"    {{ constexpr StrOp op = {o}; str_element<{view}>(a, op, a.sops + {i}, ldc(a.scall + {i}), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane); }}\n"
-                       for i, o in enumerate(ops))
-    lut = ("  WaveLds l = wave_lds(a, smem + 1024, wid);\n  l.lut = (uint32_t*)smem;\n"
+                       + ("    } else {\n" if coop and i == 0 else "") for i, o in enumerate(ops))
+        if coop:
+            body = "    if (l.wid == 0) {\n" + body + "    }\n"
+    lds = "coop_lds" if coop else "wave_lds"
+    lut = (f"  WaveLds l = {lds}(a, smem + 1024, wid);\n  l.lut = (uint32_t*)lds_abs(0);\n"
            "  for (int i = threadIdx.x; i < 256; i += blockDim.x) { const uint32_t e = a.lut[i]; l.lut[i] = e; ((uint8_t*)(l.lut + 256))[i] = count_lut_byte(e); }\n"
            if count else
-           "  const WaveLds l = wave_lds(a, smem, wid);\n  lut_lds_fill(a, l.lut);\n")
+           f"  const WaveLds l = {lds}(a, smem, wid);\n  lut_lds_fill(a, l.lut);\n")
+    loop_call = ("  coop_loop<13>(a, l, (int64_t)blockIdx.x, (int64_t)gridDim.x, lane, JitBody{});\n}\n" if coop else
+                 "  int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid;\n"
+                 "  const int64_t tstep = (int64_t)gridDim.x * kWavesPerBlock;\n"
+                 "  contig_loop<13, 0, false>(a, l, tile, tstep, lane, JitBody{});\n}\n")
     sig = ("(const KernelArgs& a, const TileCtx& t, const uint8_t* img,\n"
            "      uint32_t rec_addr, const WaveLds& l, int lane, Stamps& st) {\n")
     return (f"#define CBX_STR_LAYOUT {layout}\n#define CBX_MODE {1 if count else 0}\n" + ("#define CBX_COUNT_LUT 1\n" if count else "") +
@@ -70,9 +106,8 @@ def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False) -> 
             "extern \"C\" __global__ __launch_bounds__(cbx::kWave * cbx::kWavesPerBlock) void k(cbx::KernelArgs a) {\n"
             "  using namespace cbx;\n  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
             "  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);\n  const int lane = threadIdx.x % kWave;\n"
-            + lut + "  __syncthreads();\n  int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid;\n"
-            "  const int64_t tstep = (int64_t)gridDim.x * kWavesPerBlock;\n"
-            "  contig_loop<13, 0, false>(a, l, tile, tstep, lane, JitBody{});\n}\n")
+            "  if (!lds_base_ok(smem)) { if (threadIdx.x == 0) atomicOr(a.status, 4); return; }\n"
+            + lut + "  __syncthreads();\n" + loop_call)
 
 
 LIST_KERNEL = """#define CBX_STR_LAYOUT 0
@@ -109,14 +144,22 @@ extern "C" __global__ __launch_bounds__(cbx::kWave * cbx::kListWaves) void cbx_j
 """
 
 
-@pytest.mark.parametrize("layout,count,loop,pair", [(0, False, False, False), (1, False, False, False),
-                                                    (2, False, False, False), (2, True, False, False),
-                                                    (0, False, True, False), (2, False, False, True)])
-def test_record_kernel_compiles_with_hiprtc(layout, count, loop, pair):
-    err = _compile(_record_kernel(layout, count, loop, pair))
+@pytest.mark.parametrize("layout,count,loop,pair,coop", [(0, False, False, False, False), (1, False, False, False, False),
+                                                         (2, False, False, False, False), (2, True, False, False, False),
+                                                         (0, False, True, False, False), (2, False, False, True, False),
+                                                         (1, False, False, False, True), (2, False, False, False, True),
+                                                         (2, True, False, False, True)])
+@pytest.mark.parametrize("compiler", range(2), ids=["rocm", "torch"])
+def test_record_kernel_compiles_with_hiprtc(layout, count, loop, pair, coop, compiler):
+    if compiler >= len(COMPILERS):
+        pytest.skip("no second hipRTC")
+    err = _compile(_record_kernel(layout, count, loop, pair, coop), COMPILERS[compiler])
     assert not err, err[:3000]
 
 
-def test_list_kernel_compiles_with_hiprtc():
-    err = _compile(LIST_KERNEL)
+@pytest.mark.parametrize("compiler", range(2), ids=["rocm", "torch"])
+def test_list_kernel_compiles_with_hiprtc(compiler):
+    if compiler >= len(COMPILERS):
+        pytest.skip("no second hipRTC")
+    err = _compile(LIST_KERNEL, COMPILERS[compiler])
     assert not err, err[:3000]

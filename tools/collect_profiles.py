@@ -1,7 +1,7 @@
-"""Copy one gpu_r03.sh run's evidence from gpurun_out/r03_<TAG>/ into profiles/r03_<TAG>/ (tracked):
+"""Copy one gpu_r0N.sh run's evidence from gpurun_out/r0N_<TAG>/ into profiles/r0N_<TAG>/ (tracked):
 per workload the bench JSON line, the rocprofv3 kernel stats (cbx kernels + the totals of the rest),
 the PMC summary (tools/prof_summary.py) and traffic_<tag>.json, the per-launch HBM bytes of the
-decode kernels that bench.py's measured_traffic() reads.  Usage: collect_profiles.py TAG"""
+decode kernels that bench.py's measured_traffic() reads.  Usage: collect_profiles.py TAG [ROUND, default r04]"""
 import csv
 import json
 import os
@@ -10,8 +10,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
-src = os.path.join(ROOT, "gpurun_out", f"r03_{tag}")
-dst = os.path.join(ROOT, "profiles", f"r03_{tag}")
+rnd = sys.argv[2] if len(sys.argv) > 2 else "r04"
+src = os.path.join(ROOT, "gpurun_out", f"{rnd}_{tag}")
+dst = os.path.join(ROOT, "profiles", f"{rnd}_{tag}")
 os.makedirs(dst, exist_ok=True)
 for w in sorted(os.listdir(src)):
     d = os.path.join(src, w)
