@@ -501,6 +501,27 @@ __device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrO
     wave_sync_lds();   // the staging area is reused by the next element
 }
 
+// LDS reads at an LDS byte address (a 32-bit integer): typed address-space-3 loads, so the
+// compiler emits no generic-to-LDS pointer conversion per read (torch's bundled compiler, the one the
+// specialised kernels are built with, null-checks each such conversion: v_cmp + v_cndmask per read).
+// lds_addr: the LDS address of a generic pointer into the workgroup's LDS (one conversion, hoisted).
+typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
+template <typename T>
+__device__ __forceinline__ T lds_ld(uint32_t addr) {
+    return *(const __attribute__((address_space(3))) T*)(lds_cu8*)addr;
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(size_t)(lds_cu8*)p;
+}
+
+// Diagnostic (CBX_DIAG & 32, timing only, wrong values): a LUT read's address replaced by the lane's
+// own bank (conflict-free), still issued after the address it replaces (one extra VALU) -- prices the
+// LUT's bank conflicts.
+__device__ __forceinline__ uint32_t diag_bank(uint32_t x) {
+    asm volatile("v_and_b32 %0, 0, %0" : "+v"(x));
+    return x | ((__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 31u) << 2);
+}
+
 // (byte k of w) * 4: the byte offset of its 4-byte LUT entry, one SDWA shift
 __device__ __forceinline__ uint32_t byte_x4(uint32_t w, int k) {
     uint32_t r;
@@ -625,6 +646,8 @@ __device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kS
                                                const uint32_t* s_lut, uint8_t* slot, u32x4 (&q)[kStrNC],
                                                bool zero_tail = true) {
     constexpr int kNG = (kStrFastBytes + 3) / 4;
+    const uint32_t sel_a = 1024u;   // the selectors after the LUT (lut_lds_fill; the LUT at LDS 0)
+    (void)s_lut;
     uint32_t u01[kNG], u23[kNG], nb[kNG];
     uint2 sel[kNG];
     uint32_t wide = 0;   // bit j: character j is 2 UTF-8 bytes
@@ -639,7 +662,8 @@ __device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kS
         const uint32_t so = __builtin_amdgcn_udot4(lb & 0x02020202u, 0x20100804u, 0u, false);   // 8 * (wide bits h)
         nb[g] = __builtin_amdgcn_udot4(lb & 0x03030303u, 0x01010101u, 0u, false);            // 4 + popc(h)
         wide |= g == 0 ? so >> 3 : so << (4 * g - 3);
-        sel[g] = *(const uint2*)((const uint8_t*)(s_lut + 256) + so);
+        const uint64_t sv = lds_ld<uint64_t>(sel_a + so);
+        sel[g] = make_uint2((uint32_t)sv, (uint32_t)(sv >> 32));
     }
     const int len = (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b));
     const uint32_t s0 = (uint32_t)(-b) & 3u;
@@ -656,7 +680,8 @@ __device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kS
         d[0] = w0;
         d[1] = w1;
         const uint32_t np = pos + nb[g];
-        carry = ((np >> 2) - (pos >> 2)) == 2u ? w2 : w1;
+        const uint32_t dd = (np >> 2) - (pos >> 2);   // 1 or 2 for 4 characters (>= 4 bytes); 0 too for a last partial group
+        carry = dd == 2u ? w2 : (4 * g + 4 <= smax || dd == 1u) ? w1 : w0;
         pos = np;
     }
     *(uint32_t*)(slot + (pos & ~3u)) = carry;
@@ -688,11 +713,15 @@ __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, i
                                                 uint8_t* s_str, int lane, u32x4 (&q)[kStrNC], bool zero_tail) {
     uint32_t w[8], ev[kStrFastBytes];
     img_bytes32(src, rec_addr + (ok ? (uint32_t)eo : 0u), smax, w);
+    // the LUT's LDS address: 0 in every kernel (wave_lds / coop_lds put it at smem, lds_base_ok);
+    // the constant lets each read's address be the SDWA shift's result itself
+    const uint32_t lut_a = 0;
+    (void)s_lut;
 #ifndef CBX_STR_NO_SDWA
     if (kind == CBX_K_STRING) {   // code page: LDS entries, byte offsets straight from the image dwords
 #pragma unroll
         for (int j = 0; j < kStrFastBytes; j++)
-            ev[j] = j < smax ? *(const uint32_t*)((const uint8_t*)s_lut + byte_x4(w[j >> 2], j & 3)) : 0u;
+            ev[j] = j < smax ? lds_ld<uint32_t>(lut_a + ((CBX_DIAG & 32) ? diag_bank(byte_x4(w[j >> 2], j & 3)) : byte_x4(w[j >> 2], j & 3))) : 0u;
     } else {
         lut_entries32(w, smax, [&](uint32_t b) { return ascii_lut(b); }, ev);
     }
@@ -1101,11 +1130,12 @@ __device__ __forceinline__ int str_count_fast(const StrOp& op, const uint8_t* sr
     uint32_t w[8];
     img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
     uint32_t tm = 0, acc = 0;
-    const int8_t* lut8 = (const int8_t*)s_lut;   // count_lut_byte entries
+    const uint32_t lut8 = lds_addr(s_lut);   // count_lut_byte entries
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++) {
         if (j < op.size) {
-            const uint32_t e = (uint32_t)(int32_t)lut8[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+            const uint32_t idx = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            const uint32_t e = (uint32_t)(int32_t)lds_ld<int8_t>(lut8 + ((CBX_DIAG & 32) ? diag_bank(idx) : idx));
             tm = __builtin_amdgcn_alignbit(tm, e, 31);   // (tm << 1) | trim bit
             acc += e & 0xFFu;                            // trim * 128 + UTF-8 length
         }
@@ -1592,21 +1622,18 @@ struct WaveLds {
     int wid;            // the wave in its workgroup (coop_loop: which part of the tile's ops it runs)
 };
 
-// LDS byte address off as a pointer the compiler knows as a constant.  The kernels' only LDS is the
-// dynamic area (extern smem, no static __shared__), which starts at LDS address 0, so the LUT at its
-// front is at constant address 0: a LUT read's address is the byte * 4 itself, where the relocated
-// smem symbol cost a v_add of 0 per read (resolved after instruction selection).  lds_base_ok checks
-// the assumption on the device.
-__device__ __forceinline__ uint8_t* lds_abs(uint32_t off) {
-    return (uint8_t*)(__attribute__((address_space(3))) uint8_t*)(size_t)off;
-}
+// The kernels' only LDS is the dynamic area (extern smem, no static __shared__), which starts at LDS
+// address 0: the LUT at its front is at LDS address 0, where the string paths read it through integer
+// LDS addresses (lds_ld: the byte * 4 itself, no add, no pointer conversion).  lds_base_ok checks
+// the assumption on the device.  (A pointer built from the constant address 0 is the LDS null pointer
+// to the compiler: torch's hipRTC dropped the fill's store to entry 0 through one.)
 __device__ __forceinline__ bool lds_base_ok(const uint8_t* smem) {
     return (uint32_t)(size_t)(__attribute__((address_space(3))) const uint8_t*)smem == 0u;
 }
 
 __device__ __forceinline__ WaveLds wave_lds(const KernelArgs& a, uint8_t* smem, int wid) {
     WaveLds l;
-    l.lut = (uint32_t*)lds_abs(0);
+    l.lut = (uint32_t*)smem;
     uint8_t* wbase = smem + kLutLds + wid * a.lds_wave;
     l.img = wbase + kGuard;
     l.cnt = (int32_t*)(wbase + a.lds_rows);
@@ -1619,7 +1646,7 @@ __device__ __forceinline__ WaveLds wave_lds(const KernelArgs& a, uint8_t* smem, 
 // workgroup's tile, then each wave's counts / string staging / dump area (lds_wave - lds_rows).
 __device__ __forceinline__ WaveLds coop_lds(const KernelArgs& a, uint8_t* smem, int wid) {
     WaveLds l;
-    l.lut = (uint32_t*)lds_abs(0);
+    l.lut = (uint32_t*)smem;
     // the image offset opaque (an SGPR): with the constant address torch's bundled hipRTC (the one a
     // product process resolves libhiprtc.so.7 to) crashed compiling the kernel (tests/test_jit_rtc.py)
     int img_off = kLutLds + kGuard;

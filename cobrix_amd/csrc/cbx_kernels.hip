@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void decode_kernel(KernelAr
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform to the compiler
     const int lane = threadIdx.x % kWave;
-    if (!lds_base_ok(smem)) { if (threadIdx.x == 0) atomicOr(a.status, 4); return; }   // (lds_abs)
+    if (!lds_base_ok(smem)) { if (threadIdx.x == 0) atomicOr(a.status, 4); return; }   // (lds_ld)
     const WaveLds l = wave_lds(a, smem, wid);
     lut_lds_fill(a, l.lut);
     __syncthreads();

@@ -87,7 +87,7 @@ def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coo
         if coop:
             body = "    if (l.wid == 0) {\n" + body + "    }\n"
     lds = "coop_lds" if coop else "wave_lds"
-    lut = (f"  WaveLds l = {lds}(a, smem + 1024, wid);\n  l.lut = (uint32_t*)lds_abs(0);\n"
+    lut = (f"  WaveLds l = {lds}(a, smem + 1024, wid);\n  l.lut = (uint32_t*)smem;\n"
            "  for (int i = threadIdx.x; i < 256; i += blockDim.x) { const uint32_t e = a.lut[i]; l.lut[i] = e; ((uint8_t*)(l.lut + 256))[i] = count_lut_byte(e); }\n"
            if count else
            f"  const WaveLds l = {lds}(a, smem, wid);\n  lut_lds_fill(a, l.lut);\n")

@@ -27,7 +27,8 @@ for SPEC in "$@"; do
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" \
              "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
-             "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"; do
+             "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
+             "SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_BUSY_CU_CYCLES GRBM_COUNT"; do
     i=$((i+1))
     timeout -s KILL 200 rocprofv3 --pmc $grp --output-format csv -d $D/pmc$i -o run -- python3 bench.py --workload $W $EXTRA --steps 1 --warmup 1 --no-cpu-baseline --no-end-to-end > $D/pmc$i.log 2>&1 || { echo "pmc pass $i ($NAME) failed"; tail -3 $D/pmc$i.log; exit 1; }
   done

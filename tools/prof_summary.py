@@ -110,6 +110,10 @@ for k, cs in pmc.items():
                       "traffic_bytes": int(f * scale + w), "fetch_scale": scale}
     if "SQ_LDS_BANK_CONFLICT" in last and last.get("SQ_ACTIVE_INST_LDS"):
         counters[k]["lds_conflict_per_active_lds"] = round(last["SQ_LDS_BANK_CONFLICT"] / last["SQ_ACTIVE_INST_LDS"], 3)
+    if last.get("SQ_LDS_IDX_ACTIVE") and last.get("GRBM_GUI_ACTIVE"):
+        # LDS-array cycles per CU over the kernel's cycles (GRBM_GUI_ACTIVE sums the 8 XCDs); raw
+        # counter units as rocprofv3 reports them
+        counters[k]["lds_idx_active_per_cu_cycle"] = round(last["SQ_LDS_IDX_ACTIVE"] / (last["GRBM_GUI_ACTIVE"] / 8.0 * 256.0), 3)
     if last.get("SQ_WAVE_CYCLES"):
         counters[k]["wait_any_frac"] = round(last.get("SQ_WAIT_ANY", 0) / last["SQ_WAVE_CYCLES"], 3)
 dec_traffic = sum(v["traffic_bytes"] for k, v in traffic.items() if k.startswith(STAGED16))
