@@ -522,6 +522,18 @@ __device__ __forceinline__ uint32_t diag_bank(uint32_t x) {
     return x | ((__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 31u) << 2);
 }
 
+// bits (byte k of w) & mask, one SDWA op (mask in a VGPR: SDWA takes no literal)
+__device__ __forceinline__ uint32_t byte_and(uint32_t w, int k, uint32_t mask) {
+    uint32_t r;
+    switch (k) {
+    case 0: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(mask), "v"(w)); break;
+    case 1: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(mask), "v"(w)); break;
+    case 2: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(mask), "v"(w)); break;
+    default: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(mask), "v"(w)); break;
+    }
+    return r;
+}
+
 // (byte k of w) * 4: the byte offset of its 4-byte LUT entry, one SDWA shift
 __device__ __forceinline__ uint32_t byte_x4(uint32_t w, int k) {
     uint32_t r;
@@ -567,8 +579,16 @@ __host__ __device__ constexpr uint32_t group_sel(int i) {
 }
 
 // The code page LUT and the group selectors into the workgroup's LDS (kLutLds bytes at lut).
+// With CBX_LATIN1, also the 256-byte table of the code points (kLat1Lds; entries of 1 or 2 UTF-8 bytes).
 __device__ __forceinline__ void lut_lds_fill(const KernelArgs& a, uint32_t* lut) {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = a.lut[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        const uint32_t e = a.lut[i];
+        lut[i] = e;
+#ifdef CBX_LATIN1
+        const uint32_t cp = ((e >> 24) & 3u) == 1u ? (e & 0xFFu) : (((e & 0x1Fu) << 6) | ((e >> 8) & 0x3Fu));
+        ((uint8_t*)lut)[1152 + i] = (uint8_t)cp;
+#endif
+    }
     if (threadIdx.x < 32) lut[256 + threadIdx.x] = group_sel((int)threadIdx.x);
 }
 
@@ -642,34 +662,17 @@ __device__ __forceinline__ int str_lane_shift(int smax, const uint32_t (&ev)[kSt
 // zeroed (a short string view inlines them; the Utf8 store writes exactly len bytes and skips it).
 // Read-backs past the lane's slot (dwords beyond the value) land in the next lane's slot or read 0
 // past the workgroup's LDS -- never part of a value.
-__device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kStrFastBytes], int b, int e,
-                                               const uint32_t* s_lut, uint8_t* slot, u32x4 (&q)[kStrNC],
-                                               bool zero_tail = true) {
-    constexpr int kNG = (kStrFastBytes + 3) / 4;
-    const uint32_t sel_a = 1024u;   // the selectors after the LUT (lut_lds_fill; the LUT at LDS 0)
-    (void)s_lut;
-    uint32_t u01[kNG], u23[kNG], nb[kNG];
-    uint2 sel[kNG];
-    uint32_t wide = 0;   // bit j: character j is 2 UTF-8 bytes
-#pragma unroll
-    for (int g = 0; g < kNG; g++) {
-        if (4 * g >= smax) break;
-        const uint32_t e0 = ev[4 * g], e1 = 4 * g + 1 < smax ? ev[4 * g + 1] : 0u;
-        const uint32_t e2 = 4 * g + 2 < smax ? ev[4 * g + 2] : 0u, e3 = 4 * g + 3 < smax ? ev[4 * g + 3] : 0u;
-        u01[g] = __builtin_amdgcn_perm(e1, e0, 0x05040100u);   // c0.b0 c0.b1 c1.b0 c1.b1
-        u23[g] = __builtin_amdgcn_perm(e3, e2, 0x05040100u);
-        const uint32_t lb = __builtin_amdgcn_perm(e1, e0, 0x0C0C0703u) | __builtin_amdgcn_perm(e3, e2, 0x07030C0Cu);
-        const uint32_t so = __builtin_amdgcn_udot4(lb & 0x02020202u, 0x20100804u, 0u, false);   // 8 * (wide bits h)
-        nb[g] = __builtin_amdgcn_udot4(lb & 0x03030303u, 0x01010101u, 0u, false);            // 4 + popc(h)
-        wide |= g == 0 ? so >> 3 : so << (4 * g - 3);
-        const uint64_t sv = lds_ld<uint64_t>(sel_a + so);
-        sel[g] = make_uint2((uint32_t)sv, (uint32_t)(sv >> 32));
-    }
-    const int len = (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b));
+constexpr int kStrNG = (kStrFastBytes + 3) / 4;   // groups of 4 characters of a register-path field
+
+// The placement half of the 2-byte compose: groups g < ceil(smax / 4) (byte pairs u01 / u23, byte
+// count nb, selector sel) into the lane's slot from phase (-b) & 3, the kept bytes read back into q.
+__device__ __forceinline__ void group2_place(int smax, const uint32_t (&u01)[kStrNG], const uint32_t (&u23)[kStrNG],
+                                             const uint32_t (&nb)[kStrNG], const uint2 (&sel)[kStrNG], int b, int len,
+                                             uint8_t* slot, u32x4 (&q)[kStrNC], bool zero_tail) {
     const uint32_t s0 = (uint32_t)(-b) & 3u;
     uint32_t carry = 0, pos = s0;
 #pragma unroll
-    for (int g = 0; g < kNG; g++) {
+    for (int g = 0; g < kStrNG; g++) {
         if (4 * g >= smax) break;
         const uint32_t lo = __builtin_amdgcn_perm(u23[g], u01[g], sel[g].x), hi = __builtin_amdgcn_perm(u23[g], u01[g], sel[g].y);
         const uint32_t k8 = 8u * (pos & 3u);
@@ -705,14 +708,109 @@ __device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kS
             q[k] = u32x4{d4[0], d4[1], d4[2], d4[3]};
         }
     }
+}
+
+__device__ __forceinline__ uint2 group2_sel(uint32_t so) {
+    const uint64_t sv = lds_ld<uint64_t>(1024u + so);   // the selectors after the LUT (lut_lds_fill; the LUT at LDS 0)
+    return make_uint2((uint32_t)sv, (uint32_t)(sv >> 32));
+}
+
+__device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kStrFastBytes], int b, int e,
+                                               uint8_t* slot, u32x4 (&q)[kStrNC], bool zero_tail = true) {
+    uint32_t u01[kStrNG], u23[kStrNG], nb[kStrNG];
+    uint2 sel[kStrNG];
+    uint32_t wide = 0;   // bit j: character j is 2 UTF-8 bytes
+#pragma unroll
+    for (int g = 0; g < kStrNG; g++) {
+        if (4 * g >= smax) break;
+        const uint32_t e0 = ev[4 * g], e1 = 4 * g + 1 < smax ? ev[4 * g + 1] : 0u;
+        const uint32_t e2 = 4 * g + 2 < smax ? ev[4 * g + 2] : 0u, e3 = 4 * g + 3 < smax ? ev[4 * g + 3] : 0u;
+        u01[g] = __builtin_amdgcn_perm(e1, e0, 0x05040100u);   // c0.b0 c0.b1 c1.b0 c1.b1
+        u23[g] = __builtin_amdgcn_perm(e3, e2, 0x05040100u);
+        const uint32_t lb = __builtin_amdgcn_perm(e1, e0, 0x0C0C0703u) | __builtin_amdgcn_perm(e3, e2, 0x07030C0Cu);
+        const uint32_t so = __builtin_amdgcn_udot4(lb & 0x02020202u, 0x20100804u, 0u, false);   // 8 * (wide bits h)
+        nb[g] = __builtin_amdgcn_udot4(lb & 0x03030303u, 0x01010101u, 0u, false);            // 4 + popc(h)
+        wide |= g == 0 ? so >> 3 : so << (4 * g - 3);
+        sel[g] = group2_sel(so);
+    }
+    const int len = (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b));
+    group2_place(smax, u01, u23, nb, sel, b, len, slot, q, zero_tail);
     return len;
 }
+
+// Latin-1 code pages (every character a code point < 256: cp037, cp500, cp1047, ...; the plan
+// compiles CBX_LATIN1 in when its page is one): the LUT reads go to a 256-byte table of the code
+// points instead of the 1 KiB table of UTF-8 entries.  ds_read_b64 banks are (address / 4) mod 64, so
+// the 256-byte table is one row across the 64 banks: a wave's 64 random bytes never conflict, where the
+// 4-byte entries (8 rows per 32 banks for ds_read_b32) cost ~3 LDS cycles per 32 lanes -- the
+// largest part of the decode's LDS time (SYNSTR200: ~1100 of ~2100 LDS cycles per tile).  A byte's
+// read fetches its 8-byte row; one v_perm picks its code point.  The UTF-8 bytes, the wide and the
+// keep (code point > U+0020) flags come from the 4 code points of a group in SWAR: per group ~20
+// VALU where the entries' flags cost ~10, for ~2 instead of ~6 LDS cycles per byte.  Opt-in (env
+// CBX_LATIN1=1): measured slower on SYNSTR200 (views 5.81 -> 6.26 ms) -- the decode is bound by its
+// VALU issue more than by the LUT's bank conflicts.
+#ifdef CBX_LATIN1
+constexpr uint32_t kLat1Lds = 1152;   // after the LUT (1 KiB) and the group selectors (128 B): lut_lds_fill
+
+// The code points of the 4 bytes of w (byte k <-> byte k).
+__device__ __forceinline__ uint32_t lat1_cp4(uint32_t w, uint32_t m_row, uint32_t m_col) {
+    uint32_t p[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t row = lds_ld<uint64_t>(kLat1Lds + byte_and(w, k, m_row));   // 8-byte aligned row
+        p[k] = __builtin_amdgcn_perm((uint32_t)(row >> 32), (uint32_t)row, byte_and(w, k, m_col));   // code point in byte 0
+    }
+    return __builtin_amdgcn_perm(p[1], p[0], 0x0C0C0400u) | __builtin_amdgcn_perm(p[3], p[2], 0x04000C0Cu);
+}
+
+// The lane's field from its image dwords w (n <= smax bytes in the record): trim range, UTF-8 length
+// and the composed bytes in q, as str_lane_compose + str_lane_group2.
+__device__ __forceinline__ int str_lane_latin1(int trim, int smax, int n, const uint32_t (&w)[8], uint8_t* slot,
+                                               u32x4 (&q)[kStrNC], bool zero_tail) {
+    uint32_t u01[kStrNG], u23[kStrNG], nb[kStrNG];
+    uint2 sel[kStrNG];
+    uint32_t wide = 0, keep = 0;   // bit j: character j is 2 UTF-8 bytes / is not trimmable (> U+0020)
+    uint32_t m_row = 0xF8u, m_col = 7u;
+    asm volatile("" : "+v"(m_row), "+v"(m_col));   // (VGPR operands of the SDWA ands, set once)
+#pragma unroll
+    for (int g = 0; g < kStrNG; g++) {
+        if (4 * g >= smax) break;
+        uint32_t c = lat1_cp4(w[g], m_row, m_col);
+        if (4 * g + 4 > smax) c &= (1u << (8 * (smax - 4 * g))) - 1u;   // no characters past the field
+        const uint32_t x = c & 0x80808080u, xw = x >> 7;   // wide: code point >= 0x80
+        const uint32_t so = __builtin_amdgcn_udot4(xw, 0x40201008u, 0u, false);   // 8 * (wide bits h)
+        nb[g] = __builtin_amdgcn_udot4(xw, 0x01010101u, 4u, false);               // 4 + popc(h)
+        wide |= g == 0 ? so >> 3 : so << (4 * g - 3);
+        // keep: code point >= 0x21 -- bit 7 of (c & 0x7F) + 0x5F, or already set (wide)
+        const uint32_t kb = ((((c & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | x) >> 7) & 0x01010101u;
+        keep |= __builtin_amdgcn_udot4(kb, 0x08040201u, 0u, false) << (4 * g);
+        // UTF-8: a narrow code point is its own byte; a wide one is 0xC2 | bit 6, then 0x80 | low 6 bits.
+        // The lead bytes: one v_perm over (0xC2 | bit 6 : c) whose selector byte k is k + 4 * wide_k.
+        const uint32_t lw = ((c >> 6) & 0x01010101u) | 0xC2C2C2C2u;
+        const uint32_t lead = __builtin_amdgcn_perm(lw, c, (xw << 2) + 0x03020100u);
+        const uint32_t cont = (c & 0x3F3F3F3Fu) | 0x80808080u;
+        u01[g] = __builtin_amdgcn_perm(cont, lead, 0x05010400u);              // lead0 cont0 lead1 cont1
+        u23[g] = __builtin_amdgcn_perm(cont, lead, 0x07030602u);
+        sel[g] = group2_sel(so);
+    }
+    keep &= bits_below(n);
+    int b = 0, e = n;
+    if (trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;
+    if (trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
+    const int len = (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b));
+    group2_place(smax, u01, u23, nb, sel, b, len, slot, q, zero_tail);
+    return len;
+}
+#endif
 
 __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, int smax, int eo, int n, bool ok,
                                                 const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
                                                 uint8_t* s_str, int lane, u32x4 (&q)[kStrNC], bool zero_tail) {
     uint32_t w[8], ev[kStrFastBytes];
     img_bytes32(src, rec_addr + (ok ? (uint32_t)eo : 0u), smax, w);
+#ifdef CBX_LATIN1
+    if (kind == CBX_K_STRING && width == 2) return str_lane_latin1(trim, smax, n, w, s_str + lane * str_lane_slot(smax, 2), q, zero_tail);
+#endif
     // the LUT's LDS address: 0 in every kernel (wave_lds / coop_lds put it at smem, lds_base_ok);
     // the constant lets each read's address be the SDWA shift's result itself
     const uint32_t lut_a = 0;
@@ -743,7 +841,7 @@ __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, i
     if (width == 1) return str_lane_shift(smax, ev, b, e, q);
 #endif
 #ifndef CBX_STR_W2_BYTES   // (A/B: the byte-store compose below for 2-byte pages too)
-    if (width == 2) return str_lane_group2(smax, ev, b, e, s_lut, s_str + lane * str_lane_slot(smax, 2), q, zero_tail);
+    if (width == 2) return str_lane_group2(smax, ev, b, e, s_str + lane * str_lane_slot(smax, 2), q, zero_tail);
 #endif
     const uint32_t range = bits_below(e) & ~bits_below(b);
     uint8_t* slot = s_str + lane * str_lane_slot(smax, width);
@@ -1129,25 +1227,55 @@ __device__ __forceinline__ int str_count_fast(const StrOp& op, const uint8_t* sr
                                               const uint32_t* s_lut) {
     uint32_t w[8];
     img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), op.size, w);
-    uint32_t tm = 0, acc = 0;
+    uint32_t acc = 0;
     const uint32_t lut8 = lds_addr(s_lut);   // count_lut_byte entries
+    const int size = op.size;
+#ifndef CBX_COUNT_B64   // one ds_read_i8 per byte (the 256-byte table spans 2 rows of the 32 ds_read_b32 banks)
+    uint32_t tm = 0;
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++) {
-        if (j < op.size) {
+        if (j < size) {
             const uint32_t idx = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
             const uint32_t e = (uint32_t)(int32_t)lds_ld<int8_t>(lut8 + ((CBX_DIAG & 32) ? diag_bank(idx) : idx));
             tm = __builtin_amdgcn_alignbit(tm, e, 31);   // (tm << 1) | trim bit
             acc += e & 0xFFu;                            // trim * 128 + UTF-8 length
         }
     }
-    const int size = op.size;
-    const uint32_t keep = ~tm & bits_below(size);
+    const uint32_t keep = ~__builtin_bitreverse32(tm << (32 - size)) & bits_below(size);
+#else
+    // (A/B, CBX_JIT_DEFINES=CBX_COUNT_B64) per byte its 8-byte row of the 256-byte table (ds_read_b64:
+    // one row of the 64 banks, never a conflict) and a v_perm of its entry; per group of 4 the entries
+    // packed into a dword: one v_dot4 adds their (trim * 128 + length), one gathers the trim bits.
+    // Measured slower: SYNSTR200 Utf8 10.46 -> 11.03 ms -- the kernel is bound by its VALU issue
+    // (+2 VALU per byte) more than by the LDS conflicts it removes.
+    uint32_t trimm = 0;
+    uint32_t m_row = 0xF8u, m_col = 7u;
+    asm volatile("" : "+v"(m_row), "+v"(m_col));   // (VGPR operands of the SDWA ands)
+#pragma unroll
+    for (int g = 0; 4 * g < kStrFastBytes; g++) {
+        if (4 * g >= size) break;
+        uint32_t p[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (4 * g + k < size) {
+                const uint64_t row = lds_ld<uint64_t>(lut8 + byte_and(w[g], k, m_row));
+                p[k] = __builtin_amdgcn_perm((uint32_t)(row >> 32), (uint32_t)row, byte_and(w[g], k, m_col));   // entry in byte 0
+            } else {
+                p[k] = 0u;
+            }
+        }
+        const uint32_t e4 = __builtin_amdgcn_perm(p[1], p[0], 0x0C0C0400u) | __builtin_amdgcn_perm(p[3], p[2], 0x04000C0Cu);
+        acc = __builtin_amdgcn_udot4(e4, 0x01010101u, acc, false);
+        trimm |= __builtin_amdgcn_udot4((e4 >> 7) & 0x01010101u, 0x08040201u, 0u, false) << (4 * g);
+    }
+    const uint32_t keep = ~trimm & bits_below(size);   // bit j: byte j not trimmable
+#endif
     const int total = (int)(acc & 127u);
     const bool tl = op.trim == CBX_TRIM_LEFT || op.trim == CBX_TRIM_BOTH;
     const bool tr = op.trim == CBX_TRIM_RIGHT || op.trim == CBX_TRIM_BOTH;
     if (!ok) return 0;
     if (!keep) return (tl || tr) ? 0 : total;
-    const int lead = (int)clz32(keep) - (32 - size), trail = (int)ctz32(keep);
+    const int lead = (int)ctz32(keep), trail = size - (32 - (int)clz32(keep));
     return total - (tl ? lead : 0) - (tr ? trail : 0);
 }
 
