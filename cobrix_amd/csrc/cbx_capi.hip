@@ -74,7 +74,6 @@ struct cbx_plan {
     std::vector<int32_t> col_max_bytes;   // per column: max payload bytes per value
     bool view = false;                    // string columns in the string-view layout
     bool packed = false;                  // string columns in the Arrow Utf8 layout (count pass + one decode pass)
-    bool latin1 = false;                  // the code page's characters are code points < 256 (specialised decode: CBX_LATIN1)
     std::vector<int32_t> segid_cols;      // segment levels with a Seg_Id column
     std::vector<ListOp> lops;             // list-layout fields (list_kernel), grouped by array
     ListOp* d_lops = nullptr;
@@ -397,14 +396,6 @@ extern "C" int cbx_plan_create(const cbx_field* fields, int32_t n_fields, const 
     // widest UTF-8 expansion of the code page
     int lut_max = 1;
     for (int i = 0; i < 256; i++) lut_max = std::max(lut_max, (int)((opts->lut[i] >> 24) & 3));
-    // a Latin-1 page (every character a code point < 256): with env CBX_LATIN1=1 the specialised decode
-    // kernels read the 256-byte code point table (cbx_device.h str_lane_latin1, an A/B variant)
-    P->latin1 = getenv("CBX_LATIN1") != nullptr;
-    for (int i = 0; i < 256 && P->latin1; i++) {
-        const uint32_t e = opts->lut[i], n = (e >> 24) & 3u;
-        const uint32_t cp = n == 1 ? (e & 0xFFu) : n == 2 ? (((e & 0x1Fu) << 6) | ((e >> 8) & 0x3Fu)) : 0x800u;
-        P->latin1 = cp < 256 && (n == 1) == (cp < 0x80) && (cp <= 0x20) == ((e >> 31) != 0);
-    }
 
     // ---- fields
     for (int i = 0; i < n_fields; i++) {
@@ -694,7 +685,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         if (!P->jit_tried[k]) {
             P->jit_tried[k] = true;
             P->jit_fn[k] = jit_get(jit_source(true, span_kp, jit_pro(P), str_layout_of(P), P->cset.win, P->cset.nops, P->cset.batches,
-                                              P->cset.sops, true, false, P->latin1), &P->jit_error);
+                                              P->cset.sops, true), &P->jit_error);
         }
         span_fn = P->jit_fn[k];
     }
@@ -903,15 +894,15 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                                " windows, above the specialised-kernel limits (" + std::to_string(kJitMaxOps) + ", " +
                                std::to_string(kJitMaxWindows) + ")";
             else
-                P->jit_fn[k] = jit_get(jit_source(contig, k, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false, false, P->latin1), &P->jit_error);
+                P->jit_fn[k] = jit_get(jit_source(contig, k, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false), &P->jit_error);
         }
         jfn = P->jit_fn[k];
     }
     P->last_kind = jfn ? 1 : 0;
     // cooperative tiles (cbx_jit.h jit_coop, cbx_device.h coop_loop): one image per workgroup,
     // one tile per workgroup
-    int coop_mid = 0;
-    const bool coop = jfn && jit_coop(contig, span, jit_pro(P), S.win, S.nops, S.sops, &coop_mid);
+    CoopSplit coop_split;
+    const bool coop = jfn && jit_coop_of(contig, span, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false, &coop_split);
     const size_t lds = coop ? kLutLds + (size_t)a.lds_rows + (size_t)kWavesPerBlock * (a.lds_wave - a.lds_rows) : lds_own;
     if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
     int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / lds));
@@ -958,8 +949,8 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         // the specialised count kernel: no string staging per wave (it only scans lengths), two LUT
         // copies in front (full + count_lut_byte)
         size_t clds = lds_own;
-        int cmid = 0;
-        const bool ccoop = cfn && jit_coop(true, span, jit_pro(P), S.win, S.nops, S.sops, &cmid);
+        CoopSplit csplit;
+        const bool ccoop = cfn && jit_coop_of(true, span, jit_pro(P), 2, S.win, S.nops, S.batches, S.sops, true, &csplit);
         if (cfn) {
             ac.lds_wave = (a.lds_rows + a.lds_counts + 16 + 15) & ~15;
             clds = 1024 + kLutLds + (ccoop ? (size_t)a.lds_rows + (size_t)kWavesPerBlock * (ac.lds_wave - a.lds_rows)
@@ -1194,7 +1185,7 @@ extern "C" int cbx_debug_stamps(cbx_plan* P, uint64_t* out) {
 extern "C" int cbx_plan_specialize(cbx_plan* P, char* source, int64_t source_cap, int64_t* source_len, int32_t compile) {
     if (!P) return fail(CBX_E_ARGUMENT, "cbx_plan_specialize: invalid arguments");
     const cbx_plan::OpSet& S = P->contig_ok ? P->cset : P->wset;
-    const std::string src = jit_source(P->contig_ok, P->contig_ok ? kPre : 0, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false, false, P->latin1);
+    const std::string src = jit_source(P->contig_ok, P->contig_ok ? kPre : 0, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false);
     if (source_len) *source_len = (int64_t)src.size();
     if (source && source_cap > 0) {
         const size_t n = std::min<size_t>(src.size(), (size_t)source_cap - 1);

@@ -247,12 +247,13 @@ struct VWords {
     __device__ __forceinline__ void defer(const NumCall&, int d, int64_t, uint64_t m) { if (d >= 0) put(NNUM + d, m); }
     __device__ __forceinline__ void svalid(const StrCall&, int i, int64_t, uint64_t m) { put(NNUM + NDEF + i, m); }
     // the run starting at tile t0: lanes 8k..8k+7 of pair r store word 8r + k of its tiles (64 B)
-    __device__ __forceinline__ void flush(const KernelArgs& a, int n_words, int64_t t0, int lane) {
+    // own: the words this wave gathered (a cooperative tile's waves each flush their own ops' words)
+    __device__ __forceinline__ void flush(const KernelArgs& a, int n_words, int64_t t0, int lane, uint64_t own = ~0ull) {
         const int jj = lane & 7;
 #pragma unroll
         for (int r = 0; r < NV; r++) {
             const int w = 8 * r + (lane >> 3);
-            if (w < n_words && t0 + jj < a.n_tiles) {
+            if (w < n_words && ((own >> (w & 63)) & 1) && t0 + jj < a.n_tiles) {
                 uint64_t* p = w < NNUM ? a.ncall[w].validity
                             : w < NNUM + NDEF ? a.defer_bits + (int64_t)(w - NNUM) * a.n_tiles
                                               : a.scall[w - NNUM - NDEF].validity;
@@ -579,16 +580,8 @@ __host__ __device__ constexpr uint32_t group_sel(int i) {
 }
 
 // The code page LUT and the group selectors into the workgroup's LDS (kLutLds bytes at lut).
-// With CBX_LATIN1, also the 256-byte table of the code points (kLat1Lds; entries of 1 or 2 UTF-8 bytes).
 __device__ __forceinline__ void lut_lds_fill(const KernelArgs& a, uint32_t* lut) {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        const uint32_t e = a.lut[i];
-        lut[i] = e;
-#ifdef CBX_LATIN1
-        const uint32_t cp = ((e >> 24) & 3u) == 1u ? (e & 0xFFu) : (((e & 0x1Fu) << 6) | ((e >> 8) & 0x3Fu));
-        ((uint8_t*)lut)[1152 + i] = (uint8_t)cp;
-#endif
-    }
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = a.lut[i];
     if (threadIdx.x < 32) lut[256 + threadIdx.x] = group_sel((int)threadIdx.x);
 }
 
@@ -738,79 +731,12 @@ __device__ __forceinline__ int str_lane_group2(int smax, const uint32_t (&ev)[kS
     return len;
 }
 
-// Latin-1 code pages (every character a code point < 256: cp037, cp500, cp1047, ...; the plan
-// compiles CBX_LATIN1 in when its page is one): the LUT reads go to a 256-byte table of the code
-// points instead of the 1 KiB table of UTF-8 entries.  ds_read_b64 banks are (address / 4) mod 64, so
-// the 256-byte table is one row across the 64 banks: a wave's 64 random bytes never conflict, where the
-// 4-byte entries (8 rows per 32 banks for ds_read_b32) cost ~3 LDS cycles per 32 lanes -- the
-// largest part of the decode's LDS time (SYNSTR200: ~1100 of ~2100 LDS cycles per tile).  A byte's
-// read fetches its 8-byte row; one v_perm picks its code point.  The UTF-8 bytes, the wide and the
-// keep (code point > U+0020) flags come from the 4 code points of a group in SWAR: per group ~20
-// VALU where the entries' flags cost ~10, for ~2 instead of ~6 LDS cycles per byte.  Opt-in (env
-// CBX_LATIN1=1): measured slower on SYNSTR200 (views 5.81 -> 6.26 ms) -- the decode is bound by its
-// VALU issue more than by the LUT's bank conflicts.
-#ifdef CBX_LATIN1
-constexpr uint32_t kLat1Lds = 1152;   // after the LUT (1 KiB) and the group selectors (128 B): lut_lds_fill
-
-// The code points of the 4 bytes of w (byte k <-> byte k).
-__device__ __forceinline__ uint32_t lat1_cp4(uint32_t w, uint32_t m_row, uint32_t m_col) {
-    uint32_t p[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint64_t row = lds_ld<uint64_t>(kLat1Lds + byte_and(w, k, m_row));   // 8-byte aligned row
-        p[k] = __builtin_amdgcn_perm((uint32_t)(row >> 32), (uint32_t)row, byte_and(w, k, m_col));   // code point in byte 0
-    }
-    return __builtin_amdgcn_perm(p[1], p[0], 0x0C0C0400u) | __builtin_amdgcn_perm(p[3], p[2], 0x04000C0Cu);
-}
-
-// The lane's field from its image dwords w (n <= smax bytes in the record): trim range, UTF-8 length
-// and the composed bytes in q, as str_lane_compose + str_lane_group2.
-__device__ __forceinline__ int str_lane_latin1(int trim, int smax, int n, const uint32_t (&w)[8], uint8_t* slot,
-                                               u32x4 (&q)[kStrNC], bool zero_tail) {
-    uint32_t u01[kStrNG], u23[kStrNG], nb[kStrNG];
-    uint2 sel[kStrNG];
-    uint32_t wide = 0, keep = 0;   // bit j: character j is 2 UTF-8 bytes / is not trimmable (> U+0020)
-    uint32_t m_row = 0xF8u, m_col = 7u;
-    asm volatile("" : "+v"(m_row), "+v"(m_col));   // (VGPR operands of the SDWA ands, set once)
-#pragma unroll
-    for (int g = 0; g < kStrNG; g++) {
-        if (4 * g >= smax) break;
-        uint32_t c = lat1_cp4(w[g], m_row, m_col);
-        if (4 * g + 4 > smax) c &= (1u << (8 * (smax - 4 * g))) - 1u;   // no characters past the field
-        const uint32_t x = c & 0x80808080u, xw = x >> 7;   // wide: code point >= 0x80
-        const uint32_t so = __builtin_amdgcn_udot4(xw, 0x40201008u, 0u, false);   // 8 * (wide bits h)
-        nb[g] = __builtin_amdgcn_udot4(xw, 0x01010101u, 4u, false);               // 4 + popc(h)
-        wide |= g == 0 ? so >> 3 : so << (4 * g - 3);
-        // keep: code point >= 0x21 -- bit 7 of (c & 0x7F) + 0x5F, or already set (wide)
-        const uint32_t kb = ((((c & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | x) >> 7) & 0x01010101u;
-        keep |= __builtin_amdgcn_udot4(kb, 0x08040201u, 0u, false) << (4 * g);
-        // UTF-8: a narrow code point is its own byte; a wide one is 0xC2 | bit 6, then 0x80 | low 6 bits.
-        // The lead bytes: one v_perm over (0xC2 | bit 6 : c) whose selector byte k is k + 4 * wide_k.
-        const uint32_t lw = ((c >> 6) & 0x01010101u) | 0xC2C2C2C2u;
-        const uint32_t lead = __builtin_amdgcn_perm(lw, c, (xw << 2) + 0x03020100u);
-        const uint32_t cont = (c & 0x3F3F3F3Fu) | 0x80808080u;
-        u01[g] = __builtin_amdgcn_perm(cont, lead, 0x05010400u);              // lead0 cont0 lead1 cont1
-        u23[g] = __builtin_amdgcn_perm(cont, lead, 0x07030602u);
-        sel[g] = group2_sel(so);
-    }
-    keep &= bits_below(n);
-    int b = 0, e = n;
-    if (trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;
-    if (trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
-    const int len = (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b));
-    group2_place(smax, u01, u23, nb, sel, b, len, slot, q, zero_tail);
-    return len;
-}
-#endif
 
 __device__ __forceinline__ int str_lane_compose(int kind, int trim, int width, int smax, int eo, int n, bool ok,
                                                 const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
                                                 uint8_t* s_str, int lane, u32x4 (&q)[kStrNC], bool zero_tail) {
     uint32_t w[8], ev[kStrFastBytes];
     img_bytes32(src, rec_addr + (ok ? (uint32_t)eo : 0u), smax, w);
-#ifdef CBX_LATIN1
-    if (kind == CBX_K_STRING && width == 2) return str_lane_latin1(trim, smax, n, w, s_str + lane * str_lane_slot(smax, 2), q, zero_tail);
-#endif
     // the LUT's LDS address: 0 in every kernel (wave_lds / coop_lds put it at smem, lds_base_ok);
     // the constant lets each read's address be the SDWA shift's result itself
     const uint32_t lut_a = 0;
@@ -1881,6 +1807,8 @@ __device__ __forceinline__ void coop_loop(const KernelArgs& a, const WaveLds& l,
     constexpr int KH = (KP + kWavesPerBlock - 1) / kWavesPerBlock;
     uint4 buf[KH];
     const int wid = l.wid;
+    body.wid = wid;
+    tile = first_tile<Body>(tile);   // (the workgroup's tiles: runs of kVRun with run-gathered words)
     if (tile < a.n_tiles) coop_issue<KP>(a, contig_span(a, tile), wid, lane, buf);
     Stamps st;
     st.init();
@@ -1897,7 +1825,8 @@ __device__ __forceinline__ void coop_loop(const KernelArgs& a, const WaveLds& l,
         }
         __syncthreads();   // the tile's image complete
         st.mark(0);
-        const int64_t next = tile + tstep;
+        const int64_t next = next_tile<Body>(tile, tstep);
+        body.begin(tile);
         coop_issue<KP>(a, contig_span(a, next), wid, lane, buf);
         st.mark(1);
         TileCtx t = tile_ctx<false>(a, tile, lane);
@@ -1905,6 +1834,7 @@ __device__ __forceinline__ void coop_loop(const KernelArgs& a, const WaveLds& l,
         st.mark(2);
         body.pre(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
         body.post(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
+        run_end(a, body, tile, lane);
         __syncthreads();   // every wave done with the image
         st.mark(5);
         tile = next;

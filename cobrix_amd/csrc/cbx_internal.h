@@ -19,9 +19,9 @@ constexpr int kWave = 64;              // one wave = one tile of 64 consecutive 
 constexpr int kWavesPerBlock = 2;      // waves per workgroup (each works on its own tile)
 constexpr int kGuard = 16;             // LDS guard bytes in front of / behind a record image
 // LDS in front of the waves' regions: the code page LUT (256 x 4 bytes) + the 16 pattern selectors
-// of the 2-byte-page string compose (group_sel, 16 x 8 bytes) + the Latin-1 code points (256 bytes,
-// specialised kernels of Latin-1 pages: cbx_device.h kLat1Lds)
-constexpr int kLutLds = 1024 + 128 + 256;
+// of the 2-byte-page string compose (group_sel, 16 x 8 bytes).  (Every byte counts: SYN200's two
+// 12.8 KB record images per workgroup sit at 6 workgroups per CU by a margin of ~200 bytes.)
+constexpr int kLutLds = 1024 + 128;
 constexpr int kMaxWindowBytes = 1024;  // fields wider than this are read from HBM directly
 constexpr int kStrStageBytes = 4096;   // per-wave LDS staging of one string item's tile payload
 constexpr int kMaxStrItems = 256;      // string (field, slot) items per window (plan splits windows)

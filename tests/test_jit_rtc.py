@@ -71,8 +71,7 @@ def _compile(src: str, lib_path: str | None = None) -> str:
     return r.stdout or f"hipRTC ({lib_path}) died: exit {r.returncode}\n{r.stderr[-2000:]}"
 
 
-def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coop: bool = False,
-                   latin1: bool = False) -> str:
+def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coop: bool = False) -> str:
     """The specialised record kernel's source as cbx_jit.h emits it (jit_source), for a 3-element
     string layout; coop: the cooperative form (jit_coop: coop_lds / coop_loop, ops split on l.wid)."""
     view = "true" if layout == 1 else "false"
@@ -99,8 +98,7 @@ def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coo
     sig = ("(const KernelArgs& a, const TileCtx& t, const uint8_t* img,\n"
            "      uint32_t rec_addr, const WaveLds& l, int lane, Stamps& st) {\n")
     return (f"#define CBX_STR_LAYOUT {layout}\n#define CBX_MODE {1 if count else 0}\n" + ("#define CBX_COUNT_LUT 1\n" if count else "") +
-            ("#define CBX_LATIN1 1\n" if latin1 else "") +
-            "#include \"cbx_device.h\"\nnamespace cbx {\nstruct JitBody {\n  static constexpr int kWords = 0;\n  DirectSink vw;\n"
+            "#include \"cbx_device.h\"\nnamespace cbx {\nstruct JitBody {\n  static constexpr int kWords = 0;\n  int wid = 0;\n  DirectSink vw;\n"
             "  __device__ __forceinline__ void begin(int64_t) {}\n"
             "  __device__ __forceinline__ void flush(const KernelArgs&, int64_t, int) {}\n"
             "  __device__ __forceinline__ void pre" + sig + body + "  }\n"
@@ -150,14 +148,12 @@ extern "C" __global__ __launch_bounds__(cbx::kWave * cbx::kListWaves) void cbx_j
                                                          (2, False, False, False, False), (2, True, False, False, False),
                                                          (0, False, True, False, False), (2, False, False, True, False),
                                                          (1, False, False, False, True), (2, False, False, False, True),
-                                                         (2, True, False, False, True), (1, False, False, False, "latin1"),
-                                                         (2, False, False, False, "latin1")])
+                                                         (2, True, False, False, True)])
 @pytest.mark.parametrize("compiler", range(2), ids=["rocm", "torch"])
 def test_record_kernel_compiles_with_hiprtc(layout, count, loop, pair, coop, compiler):
-    """coop "latin1": the cooperative kernel of a Latin-1 page (CBX_LATIN1)."""
     if compiler >= len(COMPILERS):
         pytest.skip("no second hipRTC")
-    err = _compile(_record_kernel(layout, count, loop, pair, bool(coop), latin1=coop == "latin1"), COMPILERS[compiler])
+    err = _compile(_record_kernel(layout, count, loop, pair, coop), COMPILERS[compiler])
     assert not err, err[:3000]
 
 
