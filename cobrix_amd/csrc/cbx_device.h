@@ -659,10 +659,10 @@ constexpr int kStrNG = (kStrFastBytes + 3) / 4;   // groups of 4 characters of a
 
 // The placement half of the 2-byte compose: groups g < ceil(smax / 4) (byte pairs u01 / u23, byte
 // count nb, selector sel) into the lane's slot from phase (-b) & 3, the kept bytes read back into q.
-__device__ __forceinline__ void group2_place(int smax, const uint32_t (&u01)[kStrNG], const uint32_t (&u23)[kStrNG],
-                                             const uint32_t (&nb)[kStrNG], const uint2 (&sel)[kStrNG], int b, int len,
-                                             uint8_t* slot, u32x4 (&q)[kStrNC], bool zero_tail) {
-    const uint32_t s0 = (uint32_t)(-b) & 3u;
+// The groups alone, from slot byte s0 on.
+__device__ __forceinline__ void group2_put(int smax, const uint32_t (&u01)[kStrNG], const uint32_t (&u23)[kStrNG],
+                                           const uint32_t (&nb)[kStrNG], const uint2 (&sel)[kStrNG], uint32_t s0,
+                                           uint8_t* slot) {
     uint32_t carry = 0, pos = s0;
 #pragma unroll
     for (int g = 0; g < kStrNG; g++) {
@@ -681,6 +681,13 @@ __device__ __forceinline__ void group2_place(int smax, const uint32_t (&u01)[kSt
         pos = np;
     }
     *(uint32_t*)(slot + (pos & ~3u)) = carry;
+}
+
+__device__ __forceinline__ void group2_place(int smax, const uint32_t (&u01)[kStrNG], const uint32_t (&u23)[kStrNG],
+                                             const uint32_t (&nb)[kStrNG], const uint2 (&sel)[kStrNG], int b, int len,
+                                             uint8_t* slot, u32x4 (&q)[kStrNC], bool zero_tail) {
+    const uint32_t s0 = (uint32_t)(-b) & 3u;
+    group2_put(smax, u01, u23, nb, sel, s0, slot);
     // the kept bytes, packed from byte 0
     const uint32_t* sd = (const uint32_t*)slot + ((s0 + (uint32_t)b) >> 2);
 #pragma unroll
@@ -1083,10 +1090,120 @@ __device__ __forceinline__ void utf8_store_direct(CBX_GLOBAL uint8_t* d, int len
     if (rem & 1) tp[rem & 2] = (uint8_t)(tl >> (8 * (rem & 2)));
 }
 
+// The Utf8 store of a 2-byte-page element from the lane's slot, its bytes placed at the phase of
+// the destination: the value's byte i at slot byte 4 * d0 + ph + i, where ph = dst & 3, so slot dword
+// d0 + k is destination dword k of A = dst - ph.  Every dword then goes out as it lies in the slot --
+// the bytes of the first dword from ph (byte / short), the whole dwords in 16-byte pieces plus a
+// remainder of 8 + 4 bytes, the bytes of the last one (short / byte) -- each piece read from LDS at
+// its own place: no alignbyte per dword and no register select of the remainder or the tail dword
+// (utf8_store_direct's ~100 instructions per element, half of the Utf8 decode's per-element store work).
+__device__ __forceinline__ void utf8_store_slot(CBX_GLOBAL uint8_t* dst, int len, int nbytes, const uint32_t* sd) {
+    typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+    if (len <= 0) return;
+    const int ph = (int)((uint64_t)(size_t)dst & 3u);
+    CBX_GLOBAL uint8_t* A = dst - ph;
+    const int T = ph + len;   // bytes from A
+    // head: bytes [ph, min(4, T)) of dword 0
+    if (ph) {
+        const uint32_t d0 = sd[0];
+        const int he = T < 4 ? T : 4;
+        if (ph & 1) A[ph] = (uint8_t)(d0 >> (8 * ph));
+        const int p2 = ph + (ph & 1);   // 2 or 4
+        if (p2 == 2 && he == 4) *(CBX_GLOBAL uint16_t*)(A + 2) = (uint16_t)(d0 >> 16);
+        else if (p2 == 2 && he == 3) A[2] = (uint8_t)(d0 >> 16);
+    }
+    // whole dwords [k0, k1)
+    const int k0 = ph ? 1 : 0, k1 = T >> 2;
+    const int n = k1 - k0;   // whole dwords: <= (nbytes + 3) / 4, nbytes the compile-time bound of len
+    const uint32_t* m = sd + k0;
+    CBX_GLOBAL uint8_t* mp = A + 4 * k0;
+#pragma unroll
+    for (int c = 0; 16 * c + 16 <= nbytes + 3; c++)
+        if (n >= 4 * c + 4) *(CBX_GLOBAL u32x4a*)(mp + 16 * c) = u32x4a{m[4 * c], m[4 * c + 1], m[4 * c + 2], m[4 * c + 3]};
+    const int j0 = n > 0 ? (n & ~3) : 0, r = n > 0 ? (n & 3) : 0;
+    if (r) {
+        const uint32_t* rm = m + j0;
+        const uint32_t r0 = rm[0], r1 = rm[1], r2 = rm[2];
+        CBX_GLOBAL uint8_t* rp = mp + 4 * j0;
+        if (r & 2) *(CBX_GLOBAL u32x2a*)rp = u32x2a{r0, r1};
+        if (r & 1) *(CBX_GLOBAL uint32_t*)(rp + 4 * (r & 2)) = (r & 2) ? r2 : r0;
+    }
+    // tail: bytes [0, T & 3) of dword T >> 2 (unless that is dword 0, done above)
+    const int tb = T & 3;
+    if (tb && (k1 > 0 || !ph)) {
+        const uint32_t td = sd[k1];
+        CBX_GLOBAL uint8_t* tp = A + 4 * k1;
+        if (tb >= 2) *(CBX_GLOBAL uint16_t*)tp = (uint16_t)td;
+        if (tb & 1) tp[tb & 2] = (uint8_t)(td >> (8 * (tb & 2)));
+    }
+}
+
+// Utf8 decode of a register-path element of a 2-byte code page: the LUT entries, trim range and
+// length first (str_lane_compose's first half and str_lane_group2's group build), then the tile
+// scan, then the groups placed in the lane's slot at the destination's phase (utf8_store_slot).
+__device__ __forceinline__ void str_utf8_fast2(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
+                                               const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
+                                               const uint8_t* src, uint32_t rec_addr, uint8_t* s_str, int lane) {
+    bool el = t.active && (op.segment < 0 || op.segment == t.seg);
+    if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
+    const int o = a.start_off + op.eo;
+    const bool ok = el && o <= t.avail;
+    const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
+    const int smax = op.size;
+    uint32_t w[8], ev[kStrFastBytes];
+    img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), smax, w);
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++)
+        ev[j] = j < smax ? lds_ld<uint32_t>(byte_x4(w[j >> 2], j & 3)) : 0u;   // (the LUT at LDS 0)
+    uint32_t tr = 0;
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++)
+        if (j < smax) tr = __builtin_amdgcn_alignbit(tr, ev[j], 31);
+    const uint32_t keep = ~(__builtin_bitreverse32(tr) >> (32 - smax)) & bits_below(n);
+    int b = 0, e = n;
+    if (op.trim == CBX_TRIM_LEFT || op.trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;
+    if (op.trim == CBX_TRIM_RIGHT || op.trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
+    uint32_t u01[kStrNG], u23[kStrNG], nb[kStrNG];
+    uint2 sel[kStrNG];
+    uint32_t wide = 0;
+#pragma unroll
+    for (int g = 0; g < kStrNG; g++) {
+        if (4 * g >= smax) break;
+        const uint32_t e0 = ev[4 * g], e1 = 4 * g + 1 < smax ? ev[4 * g + 1] : 0u;
+        const uint32_t e2 = 4 * g + 2 < smax ? ev[4 * g + 2] : 0u, e3 = 4 * g + 3 < smax ? ev[4 * g + 3] : 0u;
+        u01[g] = __builtin_amdgcn_perm(e1, e0, 0x05040100u);
+        u23[g] = __builtin_amdgcn_perm(e3, e2, 0x05040100u);
+        const uint32_t lb = __builtin_amdgcn_perm(e1, e0, 0x0C0C0703u) | __builtin_amdgcn_perm(e3, e2, 0x07030C0Cu);
+        const uint32_t so = __builtin_amdgcn_udot4(lb & 0x02020202u, 0x20100804u, 0u, false);
+        nb[g] = __builtin_amdgcn_udot4(lb & 0x03030303u, 0x01010101u, 0u, false);
+        wide |= g == 0 ? so >> 3 : so << (4 * g - 3);
+        sel[g] = group2_sel(so);
+    }
+    const int len = ok ? (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b)) : 0;
+    gp(c.validity)[t.tile] = __ballot(ok);
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan32((uint32_t)len, lane, tot);
+    CBX_GLOBAL uint8_t* dst = utf8_offsets(a, c, t, utf8_tile_base(c, t), ex, len, tot, lane);
+    if (!dst || (CBX_DIAG & 16)) return;
+    CBX_GLOBAL uint8_t* d = dst + ex;
+    const uint32_t ph = (uint32_t)((uint64_t)(size_t)d & 3u);
+    const uint32_t s0 = (ph - (uint32_t)b) & 3u;   // character b lands at slot byte s0 + b = ph (mod 4)
+    uint8_t* slot = s_str + lane * str_lane_slot(smax, 2);
+    group2_put(smax, u01, u23, nb, sel, s0, slot);
+    utf8_store_slot(d, len, 2 * smax, (const uint32_t*)slot + ((s0 + (uint32_t)b) >> 2));
+}
+
 __device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
                                               const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
                                               const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut,
                                               uint8_t* s_str, int lane) {
+#ifndef CBX_UTF8_DIRECT   // (A/B: the register read-back + utf8_store_direct for 2-byte pages too)
+    if (op.kind == CBX_K_STRING && op.pad == 2) {
+        str_utf8_fast2(a, op, opp, c, t, s_cnt, src, rec_addr, s_str, lane);
+        return;
+    }
+#endif
     bool ok;
     u32x4 q[kStrNC];
     const int len = utf8_compose(a, op, opp, t, s_cnt, src, rec_addr, s_lut, s_str, lane, ok, q);
