@@ -44,6 +44,28 @@ template <typename T>
 __device__ __forceinline__ CBX_GLOBAL T* gp(T* p) { return (CBX_GLOBAL T*)p; }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Whole-line output stores (numeric values, string views, Utf8 offsets: 4-16 bytes per lane of 64
+// consecutive lanes, written once, never read back by the decode) are nontemporal: SYN200 (C2) 4.63
+// -> 4.38 ms, measured same-box (env A/B: CBX_JIT_DEFINES=CBX_NO_NT_STORES).  String payloads keep
+// plain stores (st_pay): their pieces cover parts of lines that the L2 merges with the neighbouring
+// values' pieces -- nontemporal there made SYNSTR200's views decode 10 % slower (5.32 -> 5.85 ms).
+template <typename T>
+__device__ __forceinline__ void st_out(CBX_GLOBAL T* p, T v) {
+#ifdef CBX_NO_NT_STORES
+    *p = v;
+#else
+    __builtin_nontemporal_store(v, p);
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void st_pay(CBX_GLOBAL T* p, T v) {
+#ifdef CBX_NT_PAYLOAD   // (A/B)
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -203,9 +225,9 @@ __device__ __forceinline__ bool sop_fast(const StrOp& op, bool global) {
 template <int W>
 __device__ __forceinline__ void store_w(void* values, int64_t tile, int lane, const Val& x, int out_type) {
     const int w = W ? W : (out_type == CBX_O_I32 || out_type == CBX_O_F32 ? 4 : out_type == CBX_O_DEC128 ? 16 : 8);
-    if (w == 4) (gp((uint32_t*)values) + tile * kWave)[lane] = (uint32_t)x.lo;
-    else if (w == 8) (gp((uint64_t*)values) + tile * kWave)[lane] = x.lo;
-    else (gp((u32x4*)values) + tile * kWave)[lane] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
+    if (w == 4) st_out(gp((uint32_t*)values) + tile * kWave + lane, (uint32_t)x.lo);
+    else if (w == 8) st_out(gp((uint64_t*)values) + tile * kWave + lane, x.lo);
+    else st_out(gp((u32x4*)values) + tile * kWave + lane, u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)});
 }
 
 // Where a numeric op's validity / deferral word of a tile goes.  DirectSink: a wave ballot stored
@@ -498,7 +520,7 @@ __device__ __forceinline__ void str_view_element(const KernelArgs& a, const StrO
         }
         v = u32x4{(uint32_t)len, pre, view_buf(t.tile, c), view_pos(t.tile, c, ex)};
     }
-    (gp((u32x4*)c.views) + t.tile * kWave)[lane] = v;
+    st_out(gp((u32x4*)c.views) + t.tile * kWave + lane, v);
     wave_sync_lds();   // the staging area is reused by the next element
 }
 
@@ -817,12 +839,12 @@ __device__ __forceinline__ void str_store_long(CBX_GLOBAL uint8_t* dst, int len,
             const int r = n4 - 4 * k;
             CBX_GLOBAL uint8_t* d = dst + 16 * k;
             if (r >= 4) {
-                *(CBX_GLOBAL u32x4a*)d = u32x4a{q[k].x, q[k].y, q[k].z, q[k].w};
+                st_pay((CBX_GLOBAL u32x4a*)(d), u32x4a{q[k].x, q[k].y, q[k].z, q[k].w});
             } else if (r >= 2) {
-                *(CBX_GLOBAL u32x2a*)d = u32x2a{q[k].x, q[k].y};
+                st_pay((CBX_GLOBAL u32x2a*)(d), u32x2a{q[k].x, q[k].y});
                 if (r == 3) ((CBX_GLOBAL uint32_t*)d)[2] = q[k].z;
             } else if (r == 1) {
-                *(CBX_GLOBAL uint32_t*)d = q[k].x;
+                st_pay((CBX_GLOBAL uint32_t*)(d), q[k].x);
             }
         }
     }
@@ -855,7 +877,7 @@ __device__ __forceinline__ void str_view_fast(const KernelArgs& a, const StrOp& 
         str_store_long(gp(c.scratch + t.tile * c.tile_cap + ex), len, op.size * op.pad, q);
         v = u32x4{(uint32_t)len, q[0].x, view_buf(t.tile, c), view_pos(t.tile, c, ex)};
     }
-    (gp((u32x4*)c.views) + t.tile * kWave)[lane] = v;
+    st_out(gp((u32x4*)c.views) + t.tile * kWave + lane, v);
 }
 
 // Two register-path view elements of mutually exclusive segment redefines (the same record bytes
@@ -1014,7 +1036,7 @@ __device__ __forceinline__ int64_t utf8_tile_base(const StrCall& c, const TileCt
 __device__ __forceinline__ CBX_GLOBAL uint8_t* utf8_offsets(const KernelArgs& a, const StrCall& c, const TileCtx& t, int64_t base,
                                                             uint32_t ex, int len, uint32_t tot, int lane) {
     CBX_GLOBAL int32_t* offs = gp((int32_t*)c.local);
-    (offs + t.tile * kWave)[lane] = (int32_t)(base + ex);
+    st_out(offs + t.tile * kWave + lane, (int32_t)(base + ex));
     if (t.rec == a.n_rec - 1) {   // the closing offset and the slot's size
         offs[a.n_rec] = (int32_t)(base + ex + len);
         if (c.size) *gp(c.size) = base + ex + len;
@@ -1051,7 +1073,7 @@ __device__ __forceinline__ void utf8_store_direct(CBX_GLOBAL uint8_t* d, int len
     const int b1 = (head > 0 && (mis & 1u)) ? 1 : 0;
     const int h2 = head - b1;
     if (b1) d[0] = (uint8_t)w[0];
-    if (h2 >= 2) *(CBX_GLOBAL uint16_t*)(d + b1) = (uint16_t)(w[0] >> (8 * b1));
+    if (h2 >= 2) st_pay((CBX_GLOBAL uint16_t*)(d + b1), (uint16_t)(w[0] >> (8 * b1)));
     else if (h2 == 1) d[b1] = (uint8_t)(w[0] >> (8 * b1));
     const int nb = (len - head) >> 2;   // whole dwords from d + head (4-byte aligned)
     const int nbmax = nbytes / 4 + 1;   // (compile-time bound of nb + 1: the tail's dword)
@@ -1063,7 +1085,7 @@ __device__ __forceinline__ void utf8_store_direct(CBX_GLOBAL uint8_t* d, int len
 #pragma unroll
     for (int k = 0; 4 * k < kNW; k++)
         if (16 * k + 16 <= nbytes && 4 * k + 4 <= nb)
-            *(CBX_GLOBAL u32x4a*)(body + 16 * k) = u32x4a{s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]};
+            st_pay((CBX_GLOBAL u32x4a*)(body + 16 * k), u32x4a{s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]});
     // the remainder (nb & 3 dwords of chunk nb / 4) and the tail dword (s[nb]), selected by chunk
     const int kr = nb >> 2, r = nb & 3;
     uint32_t r0 = 0, r1 = 0, r2 = 0, tl = 0;
@@ -1081,12 +1103,12 @@ __device__ __forceinline__ void utf8_store_direct(CBX_GLOBAL uint8_t* d, int len
     for (int k = 0; k < kNW; k++)
         if (k < nbmax && k == nb) tl = s[k];
     CBX_GLOBAL uint8_t* rp = body + 16 * kr;
-    if (r & 2) *(CBX_GLOBAL u32x2a*)rp = u32x2a{r0, r1};
-    if (r & 1) *(CBX_GLOBAL uint32_t*)(rp + 4 * (r & 2)) = (r & 2) ? r2 : r0;
+    if (r & 2) st_pay((CBX_GLOBAL u32x2a*)(rp), u32x2a{r0, r1});
+    if (r & 1) st_pay((CBX_GLOBAL uint32_t*)(rp + 4 * (r & 2)), (uint32_t)((r & 2) ? r2 : r0));
     // tail: 2 bytes at the 4-aligned tail, then 1 byte
     const int rem = len - head - 4 * nb;   // 0..3 tail bytes
     CBX_GLOBAL uint8_t* tp = body + 4 * nb;
-    if (rem >= 2) *(CBX_GLOBAL uint16_t*)tp = (uint16_t)tl;
+    if (rem >= 2) st_pay((CBX_GLOBAL uint16_t*)(tp), (uint16_t)tl);
     if (rem & 1) tp[rem & 2] = (uint8_t)(tl >> (8 * (rem & 2)));
 }
 
@@ -1110,7 +1132,7 @@ __device__ __forceinline__ void utf8_store_slot(CBX_GLOBAL uint8_t* dst, int len
         const int he = T < 4 ? T : 4;
         if (ph & 1) A[ph] = (uint8_t)(d0 >> (8 * ph));
         const int p2 = ph + (ph & 1);   // 2 or 4
-        if (p2 == 2 && he == 4) *(CBX_GLOBAL uint16_t*)(A + 2) = (uint16_t)(d0 >> 16);
+        if (p2 == 2 && he == 4) st_pay((CBX_GLOBAL uint16_t*)(A + 2), (uint16_t)(d0 >> 16));
         else if (p2 == 2 && he == 3) A[2] = (uint8_t)(d0 >> 16);
     }
     // whole dwords [k0, k1)
@@ -1120,21 +1142,21 @@ __device__ __forceinline__ void utf8_store_slot(CBX_GLOBAL uint8_t* dst, int len
     CBX_GLOBAL uint8_t* mp = A + 4 * k0;
 #pragma unroll
     for (int c = 0; 16 * c + 16 <= nbytes + 3; c++)
-        if (n >= 4 * c + 4) *(CBX_GLOBAL u32x4a*)(mp + 16 * c) = u32x4a{m[4 * c], m[4 * c + 1], m[4 * c + 2], m[4 * c + 3]};
+        if (n >= 4 * c + 4) st_pay((CBX_GLOBAL u32x4a*)(mp + 16 * c), u32x4a{m[4 * c], m[4 * c + 1], m[4 * c + 2], m[4 * c + 3]});
     const int j0 = n > 0 ? (n & ~3) : 0, r = n > 0 ? (n & 3) : 0;
     if (r) {
         const uint32_t* rm = m + j0;
         const uint32_t r0 = rm[0], r1 = rm[1], r2 = rm[2];
         CBX_GLOBAL uint8_t* rp = mp + 4 * j0;
-        if (r & 2) *(CBX_GLOBAL u32x2a*)rp = u32x2a{r0, r1};
-        if (r & 1) *(CBX_GLOBAL uint32_t*)(rp + 4 * (r & 2)) = (r & 2) ? r2 : r0;
+        if (r & 2) st_pay((CBX_GLOBAL u32x2a*)(rp), u32x2a{r0, r1});
+        if (r & 1) st_pay((CBX_GLOBAL uint32_t*)(rp + 4 * (r & 2)), (uint32_t)((r & 2) ? r2 : r0));
     }
     // tail: bytes [0, T & 3) of dword T >> 2 (unless that is dword 0, done above)
     const int tb = T & 3;
     if (tb && (k1 > 0 || !ph)) {
         const uint32_t td = sd[k1];
         CBX_GLOBAL uint8_t* tp = A + 4 * k1;
-        if (tb >= 2) *(CBX_GLOBAL uint16_t*)tp = (uint16_t)td;
+        if (tb >= 2) st_pay((CBX_GLOBAL uint16_t*)(tp), (uint16_t)td);
         if (tb & 1) tp[tb & 2] = (uint8_t)(td >> (8 * (tb & 2)));
     }
 }
@@ -1394,7 +1416,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
         const int64_t base = c.excl[t.tile] - c.excl[0];   // the tile's place in the slot's region
         const int64_t end = base + tot;
         CBX_GLOBAL int32_t* offs = gp((int32_t*)c.local);
-        (offs + t.tile * kWave)[lane] = (int32_t)(base + ex);
+        st_out(offs + t.tile * kWave + lane, (int32_t)(base + ex));
         if (t.rec == a.n_rec - 1) {   // the closing offset and the slot's size
             offs[a.n_rec] = (int32_t)(base + ex + sp.utf8_len);
             if (c.size) *gp(c.size) = base + ex + sp.utf8_len;
@@ -1537,6 +1559,13 @@ __device__ __forceinline__ void decode_window(const KernelArgs& a, const Window&
 // KP: chunks per lane -- exact for the specialised kernel (ceil(chunks per span / 64)), the plan
 // limit (kPre) for the table-driven one.
 constexpr int kPre = 16;   // 16-byte chunks per lane: a 16 KiB tile span (plan limit for contig)
+// cache policy of the staging loads (the input is read once): 0, or with CBX_NT_LOADS (A/B) the
+// gfx940+ nontemporal bit (CPol::NT)
+#ifdef CBX_NT_LOADS
+constexpr int kStageCpol = 2;
+#else
+constexpr int kStageCpol = 0;
+#endif
 
 // Chunks per lane that cover any tile span of records of stride_dw dwords (up to 3 dwords of
 // misalignment in front of the first record).
@@ -1580,7 +1609,7 @@ __device__ __forceinline__ void contig_issue(const KernelArgs& a, const ContigSp
     for (int u = 0; u < KP; u++) {
         const int c = u * kWave + lane;
         const int off = c < nch ? 16 * c : 0x7ffffff0;   // past the descriptor's range: no access
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kStageCpol);
         buf[u] = make_uint4(v[0], v[1], v[2], v[3]);
     }
 }
@@ -1913,7 +1942,7 @@ __device__ __forceinline__ void coop_issue(const KernelArgs& a, const ContigSpan
     for (int v = 0; v < KH; v++) {
         const int c = (v * kWavesPerBlock + wid) * kWave + lane;
         const int off = c < nch ? 16 * c : 0x7ffffff0;   // past the descriptor's range: no access
-        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kStageCpol);
         buf[v] = make_uint4(x[0], x[1], x[2], x[3]);
     }
 }
