@@ -65,25 +65,33 @@ check = {}
 if dec:
     k = dec[0]
     # the bench's decode time (HIP events) covers the record kernel, the list kernels after it and,
-    # in the Utf8 layout, the count pass and its scan before it
-    # the timed steps' window: after the record kernel's last warm-up launch, up to the START of the
-    # record kernel's first launch after the timed steps (the first end-to-end piece), or the end of
-    # the trace -- so a step's part kernels on either side of its record kernel count (the Utf8 count
-    # pass before it, the list kernels after it, the last timed step's included), and those of the
-    # end-to-end pieces (smaller batches) do not
+    # in the Utf8 layout, the count pass and its scan before it.  Each part kernel is attributed to
+    # the timed steps by its side of the record kernel: a list kernel from the START of the first
+    # timed record launch up to the first record-kernel launch of ANY kind after the last timed one
+    # (the end-to-end pieces may run the table-driven kernel), a count/scan kernel from the END of
+    # the last warm-up record launch up to the START of the last timed one -- so the warm-up step's
+    # list kernels and the end-to-end pieces' parts (smaller batches) do not count
     w0 = bench.get("warmup", 0)
     sp = spans[k]
+    n_t = min(steps, len(sp) - w0)
+    first, last = sp[w0][0], sp[w0 + n_t - 1][0]
     lo = sp[w0 - 1][1] if w0 > 0 else 0
-    hi = sp[w0 + steps][0] if len(sp) > w0 + steps else float("inf")
-    cand = [k] + [x for x in kernels if x.startswith(("cbx::list_kernel", "cbx_jit_list"))]
+    after = [s0 for x in dec for s0, _ in spans[x] if s0 > last]
+    hi = min(after) if after else float("inf")
+    window = {k: (first - 1, last + 1)}
+    for x in kernels:
+        if x.startswith(("cbx::list_kernel", "cbx_jit_list")):
+            window[x] = (first, hi)
     if "cbx_jit_count" in kernels or bench["config"].get("string_layout", "").startswith("Arrow Utf8"):
-        cand += [x for x in kernels if x.startswith(("cbx_jit_count", "cbx::scan_"))]
+        for x in kernels:
+            if x.startswith(("cbx_jit_count", "cbx::scan_")):
+                window[x] = (lo, last)
     parts, t = [], 0.0
-    for x in cand:
-        d_in = [(e - s0) / 1e6 for s0, e in spans[x] if lo < s0 and s0 < hi]
+    for x, (a_, b_) in window.items():
+        d_in = [(e - s0) / 1e6 for s0, e in spans[x] if a_ < s0 < b_]
         if d_in:
             parts.append(x)
-            t += sum(d_in) / steps
+            t += sum(d_in) / n_t
     frac = alg / (t * 1e-3) / 1e9 / bench["roofline"]["peak"]
     check = {"kernel": " + ".join(parts), "rocprof_ms": round(t, 4),
              "hip_event_ms": bench["kernel_ms"]["decode_kernel"], "frac_rocprof": round(frac, 4),
