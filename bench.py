@@ -361,40 +361,22 @@ class _VarLen:
 
     def __init__(self, name, n_rec, dev, rank, world, window, strings, lists=True, seed_mb=100):
         import torch
+        import torch.distributed as dist
         from cobrix_amd import native as N
         from cobrix_amd import synth
         from cobrix_amd.reader import ReaderParameters, VarLenNestedReader
-        from cobrix_amd.shard import entry_shards
+        from cobrix_amd.shard import entry_shards, index_chain
         if name == "rdw_narrow":
-            gen = lambda b: synth.rdw_narrow_large(n_rec, seed=20261016 + b, device=dev)  # noqa: E731
+            gen = lambda b, out=None: synth.rdw_narrow_large(n_rec, seed=20261016 + b, device=dev, out=out)  # noqa: E731
+            size = lambda b: synth.rdw_narrow_large_size(n_rec, seed=20261016 + b, device=dev)  # noqa: E731
             cb, segs = synth.RDW_NARROW_COPYBOOK, synth.RDW_NARROW_SEGMENTS
         else:
-            gen = lambda b: synth.wide_odo(n_rec, seed=20261018 + b, device=dev)  # noqa: E731
+            gen = lambda b, out=None: synth.wide_odo(n_rec, seed=20261018 + b, device=dev, out=out)  # noqa: E731
+            size = lambda b: synth.wide_odo_size(n_rec, seed=20261018 + b, device=dev)  # noqa: E731
             cb, segs = synth.WIDE_ODO_COPYBOOK, synth.WIDE_ODO_SEGMENTS
         self.dev, self.world, self.rank = dev, world, rank
         L = N.load()
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        # the file: blocks 0..world-1 back to back (sizes first, then generated in place: bounded memory)
-        if world == 1:
-            full, hdr = gen(0)
-            starts, n_total = [0], int(hdr.numel())
-            del hdr
-        else:
-            sizes, counts = [], []
-            for b in range(world):
-                o, h = gen(b)
-                sizes.append(int(o.numel()))
-                counts.append(int(h.numel()))
-                del o, h
-            starts = [sum(sizes[:b]) for b in range(world)]
-            full = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
-            for b in range(world):
-                o, _ = gen(b)
-                full[starts[b]:starts[b] + sizes[b]].copy_(o)
-                del o
-            n_total = sum(counts)
-        torch.cuda.synchronize()
-        total_bytes = int(full.numel())
         opts = dict(is_record_sequence=True, segment_field="SEGMENT-ID", segment_id_redefine_map=segs,
                     window_bytes=window, occurs_lists=lists, generate_record_id=True, **_layout_params(strings))
         self.rd = VarLenNestedReader(cb, ReaderParameters(**opts))
@@ -404,7 +386,66 @@ class _VarLen:
             ip["hdfs_default_block_size_mb"] = seed_mb     # a block size: subtracted (VarLenNestedReader.scala:237-243)
         idx_rd = VarLenNestedReader(cb, ReaderParameters(**ip))
         self.prm = self.rd.rdw_params()
+        self.seed_mb = seed_mb
         t0 = time.perf_counter()
+        if world > 1 and seed_mb == 100:
+            # O(shard) setup: rank r generates block r only (its size first, then in place behind a
+            # room for one index entry of tail), and the file's index is built as a chain over the
+            # ranks (shard.index_chain: the 100 MB default resets at every cut) -- each rank holds its
+            # block + the tail of the file before it that its run starts in
+            S = 100 * 1024 * 1024
+            room = (S + (16 << 20) + 255) & ~255
+            blen = size(rank)
+            buf = torch.empty(room + blen, dtype=torch.uint8, device=dev)
+            _, hdr = gen(rank, out=buf[room:])
+            n_block = int(hdr.numel())
+            del hdr
+
+            def index_fn(region):
+                n = int(region.numel())
+                off, ln, nf = _frame_rdw(L, region, n, [0], self.prm, n_block + (n - blen) // 8 + 2, dev, st)
+                ents = idx_rd.generate_index(region, n, off[:nf], ln[:nf])
+                del off, ln
+                return [(e.offset_from, e.record_index) for e in ents], nf
+
+            res = index_chain(buf, room, index_fn)
+            torch.cuda.synchronize()
+            self.index_ms = (time.perf_counter() - t0) * 1e3
+            self.raw = res["run"]
+            self.in_bytes = int(self.raw.numel())
+            self.seeds = res["seeds"] or [0]
+            self.expected_base, self.n_expected = res["record_base"], res["n_records"]
+            counts = [None] * world
+            dist.all_gather_object(counts, (len(res["entries"]), blen))
+            k0 = sum(c[0] for c in counts[:rank])
+            self.n_entries_file, self.entry_run = sum(c[0] for c in counts), (k0, k0 + len(res["entries"]))
+            total_bytes, lo = sum(c[1] for c in counts), res["run_start"]
+            self.setup_bytes_held = int(buf.numel())
+            torch.cuda.empty_cache()
+            self.shard_note = (f"entries [{k0}, {k0 + len(res['entries'])}) of the file's {self.n_entries_file} "
+                               f"(100 MB index built as a chain over the ranks, shard.index_chain), bytes "
+                               f"[{lo}, {lo + self.in_bytes}) of {total_bytes}; this rank generated and holds "
+                               f"only its block + {room} bytes of room for the tail before it "
+                               f"({self.setup_bytes_held / max(1, self.in_bytes):.3f} x its run); Record_Id base "
+                               f"from a device all-gather of record counts")
+            return
+        # one GPU (or the subtracting 32 MB split, whose cuts carry a residual and are not a chain):
+        # the whole file of `world` blocks, framed and indexed here
+        if world == 1:
+            full, hdr = gen(0)
+            starts, n_total = [0], int(hdr.numel())
+            del hdr
+        else:
+            sizes = [size(b) for b in range(world)]
+            starts = [sum(sizes[:b]) for b in range(world)]
+            full = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
+            n_total = 0
+            for b in range(world):
+                _, h = gen(b, out=full[starts[b]:starts[b] + sizes[b]])
+                n_total += int(h.numel())
+                del h
+        torch.cuda.synchronize()
+        total_bytes = int(full.numel())
         off, ln, nf = _frame_rdw(L, full, total_bytes, starts, self.prm, n_total + 1, dev, st)
         if nf != n_total:
             raise RuntimeError(f"setup framing found {nf} records, the generator wrote {n_total}")
@@ -421,7 +462,7 @@ class _VarLen:
         self.in_bytes = hi - lo
         self.seeds = [e.offset_from - lo for e in entries[k0:k1]] or [0]
         self.n_entries_file, self.entry_run = len(entries), (k0, k1)
-        self.seed_mb = seed_mb
+        self.setup_bytes_held = int(self.raw.numel())
         del full, off, ln, hdr_off, idx_rd
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
@@ -437,30 +478,29 @@ class _VarLen:
         self.off = torch.empty(self.cap, dtype=torch.int64, device=self.dev)
         self.ln = torch.empty(self.cap, dtype=torch.int32, device=self.dev)
         self.sd = (ctypes.c_int64 * len(self.seeds))(*self.seeds)
-        self.nfr = ctypes.c_int64(0)
+        self.state = torch.zeros(3, dtype=torch.int64, device=self.dev)   # cbx_frame_rdw_async outcome
         self.n_rec = self.n_expected
         self.cols, self.cs = _alloc_columns(self.rd.plan, self.n_rec, string_capacity(self.rd.native, self.n_rec),
                                             self.dev)
         self.fr0, self.fr1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # the run's Record_Id base lives on the device: the decode kernels read it (cbx_plan_set_record_base)
         self.base = torch.zeros(1, dtype=torch.int64, device=self.dev)
-        self.count = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.gathered = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
         N.check(self.L.cbx_plan_set_record_base(self.h, self.base.data_ptr()))
 
     def step(self, world=1):
         import torch.distributed as dist
         from cobrix_amd import native as N
+        # no host wait inside the step: the framing's count stays on the device (cbx_frame_rdw_async),
+        # is all-gathered there, and the decode runs over the count the index run predicts (checked
+        # against the framing's after the timed steps, cbx_frame_rdw_state)
         self.fr0.record()
-        N.check(self.L.cbx_frame_rdw(self.raw.data_ptr(), self.in_bytes, self.sd, len(self.seeds),
-                                     ctypes.byref(self.prm), self.off.data_ptr(), self.ln.data_ptr(), self.cap,
-                                     ctypes.byref(self.nfr), self.stream))
+        N.check(self.L.cbx_frame_rdw_async(self.raw.data_ptr(), self.in_bytes, self.sd, len(self.seeds),
+                                           ctypes.byref(self.prm), self.off.data_ptr(), self.ln.data_ptr(), self.cap,
+                                           self.state.data_ptr(), 0, self.stream))
         self.fr1.record()
-        if self.nfr.value != self.n_expected:
-            raise RuntimeError(f"framing found {self.nfr.value} records, the index run holds {self.n_expected}")
         if world > 1:   # Record_Id base = exclusive prefix of the ranks' counts, computed on the device
-            self.count.fill_(self.nfr.value)
-            dist.all_gather_into_tensor(self.gathered, self.count)
+            dist.all_gather_into_tensor(self.gathered, self.state[:1])
             self.base.copy_(self.gathered[: self.rank].sum().view(1))
         N.check(self.L.cbx_decode_var(self.h, self.raw.data_ptr(), self.in_bytes, self.off.data_ptr(),
                                       self.ln.data_ptr(), self.n_rec, 0, 0, self.cs, self.stream))
@@ -470,6 +510,11 @@ class _VarLen:
         """After timing: the device base equals the records before this run in the setup framing, and
         the Record_Id column starts there."""
         import torch
+        from cobrix_amd import native as N
+        nfr = ctypes.c_int64(0)
+        N.check(self.L.cbx_frame_rdw_state(self.state.data_ptr(), ctypes.byref(nfr), self.stream))
+        if nfr.value != self.n_expected:
+            raise RuntimeError(f"framing found {nfr.value} records, the index run holds {self.n_expected}")
         got = int(self.base.item()) if world > 1 else 0
         rid = self.cols[self.rd.plan.record_id_column]["values"][: max(1, self.n_rec)]
         first = int(rid[0].item()) if self.n_rec else got
@@ -866,9 +911,10 @@ def main():
     fms = None
     if frame_ev:
         fms = sum(a.elapsed_time(b) for a, b in frame_ev) / len(frame_ev)
-        kernel_ms["rdw_framing (cbx_frame_rdw incl. count readback)"] = round(fms, 4)
+        kernel_ms["rdw_framing (cbx_frame_rdw_async, count on the device)"] = round(fms, 4)
     if hasattr(job, "index_ms"):
-        kernel_ms["sparse_index_setup (untimed: frame + cbx_sparse_index of the whole file, once)"] = round(job.index_ms, 3)
+        kernel_ms["sparse_index_setup (untimed, once: frame + cbx_sparse_index of the whole file, or of this "
+                  "rank's block + tail in the N > 1 chain)"] = round(job.index_ms, 3)
     e2e = None
     if not args.no_end_to_end and world == 1:
         progress("end-to-end (pinned host -> HBM) pass")
@@ -898,6 +944,7 @@ def main():
                        "input_gb_per_gpu": round(job.in_bytes / 1e9, 3), "job_input_bytes": int(job_bytes),
                        "output_columns": plan.n_columns, "parallelism": f"dp{world}",
                        "shard": job.shard_note,
+                       **({"setup_bytes_held_per_rank": job.setup_bytes_held} if hasattr(job, "setup_bytes_held") else {}),
                        "string_layout": STRING_LAYOUTS[strings],
                        "occurs_layout": "Arrow lists (present elements only)" if args.occurs == "lists"
                        else "one slot row per element",

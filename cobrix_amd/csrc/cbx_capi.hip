@@ -1279,13 +1279,65 @@ static void keep_pool_memory() {
     done.push_back(dev);
 }
 
-extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,
-                             const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len,
-                             int64_t capacity, int64_t* n_records, void* stream) {
-    hipStream_t st = (hipStream_t)stream;
-    if (!d_data || n_bytes < 0 || !params || !n_records || (n_seeds > 0 && !seeds))
-        return fail(CBX_E_ARGUMENT, "cbx_frame_rdw: invalid arguments");
-    *n_records = 0;
+namespace cbx {
+// The async walk's outcome (cbx_frame_rdw_async): count, first header error, capacity flag.
+__global__ void rdw_state_kernel(const unsigned long long* res, int64_t capacity, int64_t* state) {
+    if (threadIdx.x == 0) {
+        const int64_t total = (int64_t)res[1];
+        state[0] = total;
+        state[1] = (int64_t)res[0];
+        state[2] = total > capacity ? 1 : 0;
+    }
+}
+}  // namespace cbx
+
+// Host -> device copy of a small host array with no host wait: a ring of pinned buffers, each
+// reused once the copy that last read it has completed (one event per slot; long done in practice).
+static int upload_no_wait(const void* src, size_t n, void* dst, hipStream_t st) {
+    struct Slot { void* p = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; int dev = -1; };
+    static thread_local Slot ring[4];
+    static thread_local int next = 0;
+    Slot& sl = ring[next];
+    next = (next + 1) % 4;
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    if (sl.ev && sl.dev == dev) HIP_CHECK(hipEventSynchronize(sl.ev));
+    if (sl.ev && sl.dev != dev) {   // a slot last used on another device: start it over
+        (void)hipEventDestroy(sl.ev);
+        sl.ev = nullptr;
+    }
+    if (sl.cap < n) {
+        if (sl.p) HIP_CHECK(hipHostFree(sl.p));
+        sl.p = nullptr;
+        sl.cap = 0;
+        HIP_CHECK(hipHostMalloc(&sl.p, n, hipHostMallocDefault));
+        sl.cap = n;
+    }
+    if (!sl.ev) {
+        HIP_CHECK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+        sl.dev = dev;
+    }
+    memcpy(sl.p, src, n);
+    HIP_CHECK(hipMemcpyAsync(dst, sl.p, n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipEventRecord(sl.ev, st));
+    return CBX_OK;
+}
+
+static int rdw_error(unsigned long long first_err) {
+    const long long off = (long long)(first_err >> 2);
+    char msg[200];
+    if ((first_err & 3) == 2) snprintf(msg, sizeof msg, "RDW headers should never be zero. Found zero size record at %lld.", off);
+    else snprintf(msg, sizeof msg, "RDW headers too big (length > %lld) at %lld.", 100ll * 1024 * 1024, off);
+    return fail(CBX_E_STATE, msg);
+}
+
+// The walk of cbx_frame_rdw (d_state == nullptr: host waits for the settle check and the count) and of
+// cbx_frame_rdw_async (d_state: max_rounds parallel fix rounds + the settle pass enqueued without waiting,
+// the outcome on the device).
+static int frame_rdw_impl(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,
+                          const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len, int64_t capacity,
+                          int64_t* n_records, int64_t* d_state, int32_t max_rounds, hipStream_t st) {
+    const bool async = d_state != nullptr;
     keep_pool_memory();
     // seed ranges cut into chunks (rdw_wave_kernel: speculation + walk, fix rounds; rdw_place_kernel)
     // 64 KiB chunks: C4's 65-byte records ~1,000 per chunk; C5's 16 KB records still leave every
@@ -1336,7 +1388,12 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     c.stage_off = (uint32_t*)stage;
     c.stage_len = (int32_t*)(stage + (size_t)n * stage_cap * sizeof(uint32_t));
     c.stage_cap = stage_cap;
-    HIP_CHECK(hipMemcpyAsync(d_ranges, ranges.data(), sizeof(RdwRange) * ranges.size(), hipMemcpyHostToDevice, st));
+    if (async) {
+        const int r = upload_no_wait(ranges.data(), sizeof(RdwRange) * ranges.size(), d_ranges, st);
+        if (r) return r;
+    } else {
+        HIP_CHECK(hipMemcpyAsync(d_ranges, ranges.data(), sizeof(RdwRange) * ranges.size(), hipMemcpyHostToDevice, st));
+    }
     HIP_CHECK(hipMemsetAsync(d_first_err, 0xFF, sizeof(unsigned long long), st));
     RdwArgs a{};
     a.data = d_data; a.n_bytes = n_bytes; a.p = *params;
@@ -1346,21 +1403,26 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     hipLaunchKernelGGL(rdw_wave_kernel<false>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, 0);
     HIP_CHECK(hipGetLastError());
     // fix rounds until one changes no entry (each round validates at least the next chunk of every
-    // range: bounded by the chunk count).  The first kAsyncRounds go out without waiting: a round
-    // after one that changed nothing returns at once on the device.
-    constexpr int kAsyncRounds = 3;
+    // range: bounded by the chunk count).  The first kAsyncRounds (async: max_rounds) go out without
+    // waiting: a round after one that changed nothing returns at once on the device.
+    const int64_t async_rounds = std::min<int64_t>(async && max_rounds > 0 ? max_rounds : 3, n + 1);
     int64_t round = 0;
-    for (; round < kAsyncRounds && round <= n; round++)
+    for (; round < async_rounds && round <= n; round++)
         hipLaunchKernelGGL(rdw_wave_kernel<true>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, (int32_t)round);
     HIP_CHECK(hipGetLastError());
-    int32_t last_changed = 0;
-    HIP_CHECK(hipMemcpyAsync(&last_changed, c.changed + round - 1, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    for (; last_changed && round <= n + 1; round++) {
-        hipLaunchKernelGGL(rdw_wave_kernel<true>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, (int32_t)round);
+    if (async) {   // whatever the parallel rounds left unsettled, settled on the device in one pass
+        hipLaunchKernelGGL(rdw_settle_kernel, dim3(1), dim3(kWave), 0, st, a, c, (int32_t)(round - 1));
         HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipMemcpyAsync(&last_changed, c.changed + round, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    } else {
+        int32_t last_changed = 0;
+        HIP_CHECK(hipMemcpyAsync(&last_changed, c.changed + round - 1, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
+        for (; last_changed && round <= n + 1; round++) {
+            hipLaunchKernelGGL(rdw_wave_kernel<true>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, (int32_t)round);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(&last_changed, c.changed + round, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+        }
     }
     // record counts -> bases: device exclusive scan of the chunk counts
     hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)c.count, n,
@@ -1371,6 +1433,14 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     hipLaunchKernelGGL(rdw_place_kernel, dim3((unsigned)((n + kRdwPlaceWaves - 1) / kRdwPlaceWaves)), dim3(kWave * kRdwPlaceWaves),
                        0, st, a, c, (const int64_t*)d_base, d_rec_off, d_rec_len, capacity, d_first_err);
     HIP_CHECK(hipGetLastError());
+    if (async) {
+        hipLaunchKernelGGL(rdw_state_kernel, dim3(1), dim3(kWave), 0, st, (const unsigned long long*)d_first_err,
+                           capacity, d_state);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipFreeAsync(stage, st));
+        HIP_CHECK(hipFreeAsync(blk, st));
+        return CBX_OK;
+    }
     unsigned long long res[2] = {0, 0};
     HIP_CHECK(hipMemcpyAsync(res, d_first_err, sizeof(res), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipFreeAsync(stage, st));
@@ -1378,15 +1448,40 @@ extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64
     HIP_CHECK(hipStreamSynchronize(st));
     const unsigned long long first_err = res[0];
     const int64_t total = (int64_t)res[1];
-    if (first_err != ~0ull) {
-        const long long off = (long long)(first_err >> 2);
-        char msg[200];
-        if ((first_err & 3) == 2) snprintf(msg, sizeof msg, "RDW headers should never be zero. Found zero size record at %lld.", off);
-        else snprintf(msg, sizeof msg, "RDW headers too big (length > %lld) at %lld.", 100ll * 1024 * 1024, off);
-        return fail(CBX_E_STATE, msg);
-    }
+    if (first_err != ~0ull) return rdw_error(first_err);
     *n_records = total;
     if (total > capacity) return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(total));
+    return CBX_OK;
+}
+
+extern "C" int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,
+                             const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len,
+                             int64_t capacity, int64_t* n_records, void* stream) {
+    if (!d_data || n_bytes < 0 || !params || !n_records || (n_seeds > 0 && !seeds))
+        return fail(CBX_E_ARGUMENT, "cbx_frame_rdw: invalid arguments");
+    *n_records = 0;
+    return frame_rdw_impl(d_data, n_bytes, seeds, n_seeds, params, d_rec_off, d_rec_len, capacity, n_records, nullptr, 0,
+                          (hipStream_t)stream);
+}
+
+extern "C" int cbx_frame_rdw_async(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,
+                                   const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len,
+                                   int64_t capacity, int64_t* d_state, int32_t max_rounds, void* stream) {
+    if (!d_data || n_bytes < 0 || !params || !d_state || (n_seeds > 0 && !seeds) || max_rounds < 0)
+        return fail(CBX_E_ARGUMENT, "cbx_frame_rdw_async: invalid arguments");
+    return frame_rdw_impl(d_data, n_bytes, seeds, n_seeds, params, d_rec_off, d_rec_len, capacity, nullptr, d_state,
+                          max_rounds, (hipStream_t)stream);
+}
+
+extern "C" int cbx_frame_rdw_state(const int64_t* d_state, int64_t* n_records, void* stream) {
+    if (!d_state || !n_records) return fail(CBX_E_ARGUMENT, "cbx_frame_rdw_state: invalid arguments");
+    hipStream_t st = (hipStream_t)stream;
+    int64_t s[3] = {0, 0, 0};
+    HIP_CHECK(hipMemcpyAsync(s, d_state, sizeof(s), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    *n_records = s[0];
+    if ((unsigned long long)s[1] != ~0ull) return rdw_error((unsigned long long)s[1]);
+    if (s[2] & 1) return fail(CBX_E_CAPACITY, "record capacity < " + std::to_string(s[0]));
     return CBX_OK;
 }
 

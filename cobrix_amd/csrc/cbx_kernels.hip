@@ -1165,6 +1165,42 @@ __global__ __launch_bounds__(kWave * kRdwWaves) void rdw_wave_kernel(RdwArgs a, 
     }
 }
 
+// Settles the walk on the device after the parallel fix rounds (cbx_frame_rdw_async, no host check
+// between rounds): returns at once when the last round changed nothing; otherwise one wave goes over
+// the chunks in file order -- 64 (predecessor exit, entry) pairs per ballot -- and walks again every
+// chunk whose entry differs from its predecessor's exit, so a chain of failed speculations of any
+// length resolves in one pass (sequential along that chain only; rare).
+__global__ __launch_bounds__(kWave) void rdw_settle_kernel(RdwArgs a, RdwChunkArgs c, int32_t last_round) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kRdwWaveLds];
+    const int lane = threadIdx.x;
+    if (c.changed[last_round] == 0) return;
+    RdwStream s = rdw_stream(a, smem);
+    for (int64_t k0 = 1; k0 < c.n;) {
+        const int64_t k = k0 + lane;
+        bool bad = false;
+        if (k < c.n) bad = !rdw_chunk(c, k).known && c.exit_out[k - 1] != c.entry[k];
+        const uint64_t m = __ballot(bad);
+        if (m == 0) {
+            k0 += kWave;
+            continue;
+        }
+        const int64_t kb = k0 + __builtin_ctzll(m);
+        const int64_t entry = uni64(c.exit_out[kb - 1]);
+        const RdwChunk ch = rdw_chunk(c, kb);
+        const RdwWalk w = rdw_walk_lanes(a, s, entry, ch.end, c.stage_off + kb * c.stage_cap,
+                                         c.stage_len + kb * c.stage_cap, c.stage_cap, lane);
+        if (lane == 0) {
+            c.entry[kb] = entry;
+            c.exit_out[kb] = w.exit;
+            c.count[kb] = w.count;
+            c.err[kb] = w.err;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        k0 = kb + 1;   // the next pair reads exit_out[kb]: lane 0 wrote it, lane 0 reads it
+    }
+}
+
 // One wave per chunk: its staged records -> rec_off / rec_len[base, base + count) (coalesced);
 // a chunk whose count passed the staging capacity is walked again by one lane, writing directly.
 constexpr int kRdwPlaceWaves = 4;

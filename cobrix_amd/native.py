@@ -37,12 +37,13 @@ OUT_WIDTH = {O_I32: 4, O_I64: 8, O_DEC64: 8, O_DEC128: 16, O_F32: 4, O_F64: 8}
 # every symbol include/cobrix_hip.h declares
 EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx_plan_destroy",
                     "cbx_string_bound", "cbx_string_view_geometry", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
-                    "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_plan_set_profiling",
+                    "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_frame_rdw_async", "cbx_frame_rdw_state",
+                    "cbx_plan_set_profiling",
                     "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text",
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
                     "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs",
                     "cbx_plan_set_record_base", "cbx_frame_length_field", "cbx_plan_set_odo_counts")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class NativeLibraryError(RuntimeError):
@@ -180,6 +181,8 @@ def load():
     L.cbx_decode_var.argtypes = [P, P, i64, P, P, i64, i32, i64, P, P]
     L.cbx_string_sizes_var.argtypes = [P, P, i64, P, P, i64, i32, P, P]
     L.cbx_frame_rdw.argtypes = [P, i64, P, i32, P, P, P, i64, P, P]
+    L.cbx_frame_rdw_async.argtypes = [P, i64, P, i32, P, P, P, i64, P, i32, P]
+    L.cbx_frame_rdw_state.argtypes = [P, P, P]
     L.cbx_frame_text.argtypes = [P, i64, i32, P, P, i64, P, P, P]
     L.cbx_plan_set_profiling.argtypes = [P, i32]
     L.cbx_plan_kernel_times.argtypes = [P, P, P, i32, P]

@@ -88,6 +88,75 @@ def entry_shards(entries, n_bytes: int, world: int) -> List[Tuple[int, int]]:
     return out
 
 
+def index_chain(buf, tail_room: int, index_fn, group=None) -> dict:
+    """Sparse index of ONE variable-length file whose blocks are spread over the ranks (rank r holds
+    block r, the blocks in rank order, each starting at a record header), with every rank holding
+    only its own block plus, in front of it, the tail of the file before it that belongs to its run.
+
+    IndexGenerator.sparseIndexGenerator (CP/reader/index/IndexGenerator.scala:33-127) with the
+    default entry size resets its byte count at every cut, so the cuts after an entry start depend
+    only on the records from that start on: the file's index is a chain.  Rank r receives from rank
+    r - 1 the start of the last entry found so far (file offset, record index) and the bytes from
+    there to the end of block r - 1 (at most one entry), indexes that tail + its block as a file of
+    its own -- index_fn(region) -> ([(offset_from, record_index)] region-relative, the first (0, 0);
+    record count) -- keeps every entry but the last, and sends the last one on.  The last rank keeps
+    all of its entries.  Rank r's run = its entries: a contiguous, balanced (one block, give or take
+    an entry) share of the file in file order; the union over the ranks is the whole file's index.
+    (The subtracting split-size rule carries a residual across cuts and is not a chain of this form:
+    callers index such files whole.)
+
+    buf: uint8 tensor [tail_room + block bytes], the block at buf[tail_room:]; the received tail
+    lands right in front of it.  Point-to-point send/recv of int64[3] + the tail bytes (device
+    tensors over RCCL, CPU tensors over gloo), N - 1 hops in sequence (setup, not the step).
+    Returns {"run": uint8 view of buf, "run_start": file offset of the run, "seeds": entry offsets
+    relative to the run, "entries": [(offset_from, record_index)] absolute, "record_base": record
+    index of the run's first record, "n_records": records in the run}."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    meta = torch.zeros(3, dtype=torch.int64, device=buf.device)   # file offset, record index, tail bytes
+    if rank > 0:
+        dist.recv(meta, src=rank - 1, group=group)
+    r_off, r_rec, tail = (int(x) for x in meta.tolist())
+    if tail < 0:
+        raise RuntimeError(f"index_chain: rank {rank - 1} had a tail larger than the {tail_room}-byte room")
+    if tail > 0:
+        dist.recv(buf[tail_room - tail:tail_room], src=rank - 1, group=group)
+    res, fwd = chain_step(buf[tail_room - tail:], index_fn, r_off, r_rec, rank == world - 1)
+    if fwd is not None:
+        f_off, f_rec, f_bytes = fwd
+        ok = f_bytes.numel() <= tail_room
+        out = torch.tensor([f_off, f_rec, f_bytes.numel() if ok else -1], dtype=torch.int64, device=buf.device)
+        dist.send(out, dst=rank + 1, group=group)
+        if not ok:
+            raise RuntimeError(f"index_chain: {f_bytes.numel()}-byte tail for rank {rank + 1} exceeds the "
+                               f"{tail_room}-byte room")
+        if f_bytes.numel() > 0:
+            dist.send(f_bytes.contiguous(), dst=rank + 1, group=group)
+    return res
+
+
+def chain_step(region, index_fn, r_off: int, r_rec: int, last: bool):
+    """One link of index_chain: `region` starts at the file offset r_off (record index r_rec) at an
+    entry start and runs to the end of this rank's block.  Returns (result, forward): the result dict
+    of index_chain, and (file offset, record index, bytes) of the entry handed to the next rank (None
+    for the last rank)."""
+    ents, n_rec = index_fn(region)
+    if not ents or ents[0][0] != 0:
+        raise RuntimeError("index_chain: index_fn must return the region's entries, the first at offset 0")
+    fwd = None
+    if not last:
+        last_off, last_rec = ents[-1]
+        fwd = (r_off + last_off, r_rec + last_rec, region[last_off:])
+        keep, run_end, n_run = ents[:-1], last_off, last_rec
+    else:
+        keep, run_end, n_run = ents, int(region.numel()), n_rec
+    return ({"run": region[:run_end], "run_start": r_off, "seeds": [o for o, _ in keep],
+             "entries": [(r_off + o, r_rec + k) for o, k in keep], "record_base": r_rec, "n_records": n_run}, fwd)
+
+
 def init_from_env(backend: Optional[str] = None):
     """torch.distributed init from torchrun's environment (RANK / WORLD_SIZE / MASTER_*);
     no-op for a single process.  Returns (world, rank, local_rank)."""

@@ -221,16 +221,35 @@ def synstr200(n: int, seed: int = 20261017, device="cpu", chunk: int = 4_000_000
     return _cat_chunks(make, n, chunk).contiguous()
 
 
-def rdw_narrow_large(n: int, seed: int = 20261016, device="cpu", chunk: int = 16_000_000):
-    """rdw_narrow in chunks (bounded temporaries): -> (bytes, header offsets)."""
+def rdw_narrow_large(n: int, seed: int = 20261016, device="cpu", chunk: int = 16_000_000, out=None):
+    """rdw_narrow in chunks (bounded temporaries): -> (bytes, header offsets).  out: a uint8 tensor of
+    rdw_narrow_large_size(...) bytes to generate into (no concatenated copy)."""
     outs, hdrs, base = [], [], 0
     for ci, s in enumerate(range(0, n, chunk)):
         m = min(chunk, n - s)
         o, h = rdw_narrow(m, seed=seed * 1000 + ci, device=device)
-        outs.append(o)
+        if out is not None:
+            out[base:base + o.numel()].copy_(o)
+        else:
+            outs.append(o)
         hdrs.append(h + base)
         base += int(o.numel())
+        del o
+    if out is not None:
+        return out[:base], torch.cat(hdrs)
     return torch.cat(outs), torch.cat(hdrs)
+
+
+def rdw_narrow_large_size(n: int, seed: int = 20261016, device="cpu", chunk: int = 16_000_000) -> int:
+    """Bytes rdw_narrow_large(n, seed, device, chunk) writes (its first draw fixes every record's size)."""
+    total = 0
+    for ci, s in enumerate(range(0, n, chunk)):
+        m = min(chunk, n - s)
+        g = torch.Generator(device=device)
+        g.manual_seed(seed * 1000 + ci)
+        is_c = torch.rand((m,), generator=g, device=device) < 0.35
+        total += int(torch.where(is_c, 68, 64).sum().item())
+    return total
 
 
 # --------------------------------------------------------------------------------------------
@@ -265,9 +284,18 @@ WIDE_ODO_SEGMENTS = RDW_NARROW_SEGMENTS
 WIDE_C_PAYLOAD, WIDE_P_PAYLOAD = 16066, 60
 
 
-def wide_odo(n_roots: int, seed: int = 20261018, device="cpu"):
+def wide_odo_size(n_roots: int, seed: int = 20261018, device="cpu") -> int:
+    """Bytes wide_odo(n_roots, seed, device) writes (its first draw fixes the children per root)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    kids = torch.randint(0, 5, (n_roots,), generator=g, device=device)
+    return n_roots * (WIDE_C_PAYLOAD + 4) + int(kids.sum().item()) * (WIDE_P_PAYLOAD + 4)
+
+
+def wide_odo(n_roots: int, seed: int = 20261018, device="cpu", out=None):
     """n_roots C records, each followed by 0-4 P records, with LE RDW headers ->
-    (bytes uint8 [total], header offsets int64 [n_records])."""
+    (bytes uint8 [total], header offsets int64 [n_records]).  out: a uint8 tensor of
+    wide_odo_size(...) bytes to generate into."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     kids = torch.randint(0, 5, (n_roots,), generator=g, device=device)
@@ -278,7 +306,11 @@ def wide_odo(n_roots: int, seed: int = 20261018, device="cpu"):
     plen = torch.where(is_c, WIDE_C_PAYLOAD, WIDE_P_PAYLOAD).to(torch.int64)
     hdr = torch.cumsum(plen + 4, 0) - (plen + 4)
     total = int((plen + 4).sum().item())
-    out = torch.randint(0, 256, (total,), generator=g, device=device, dtype=torch.uint8)
+    if out is None:
+        out = torch.randint(0, 256, (total,), generator=g, device=device, dtype=torch.uint8)
+    else:
+        out = out[:total]
+        out.random_(0, 256, generator=g)
     lo, hi = (plen & 0xFF).to(torch.uint8), (plen >> 8).to(torch.uint8)
     z = torch.zeros_like(lo)
     for j, col in enumerate((z, z, lo, hi)):

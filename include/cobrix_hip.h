@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 11
+#define CBX_ABI_VERSION 12
 
 /* status codes */
 #define CBX_OK 0
@@ -321,6 +321,21 @@ typedef struct {
 int cbx_frame_rdw(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,
                   const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len,
                   int64_t capacity, int64_t* n_records, void* stream);
+
+/* The same walk with no host wait: everything is enqueued on `stream` and the outcome stays on the
+ * device in d_state (int64[3]): [0] the record count, [1] the first header error (-1: none; else
+ * offset << 2 | kind, kind 2 = zero-length header, 3 = header above 100 MB), [2] flags (1: more
+ * records than capacity).  max_rounds parallel fix rounds (0 = 3) run before a one-wave pass on the
+ * device settles whatever they left (a no-op when the last round changed nothing).  A
+ * multi-GPU step all-gathers d_state[0] on the device (the Record_Id bases) and decodes with the
+ * count its index run predicts; cbx_frame_rdw_state reads d_state afterwards (one host wait) and
+ * returns the error cbx_frame_rdw would have returned, *n_records the count.
+ * (Replaces the host out-parameter of VRLRecordReader's sequential count, VarLenNestedIterator.scala:80-147,
+ * for the all-gather RCCL performs) */
+int cbx_frame_rdw_async(const uint8_t* d_data, int64_t n_bytes, const int64_t* seeds, int32_t n_seeds,
+                        const cbx_rdw_params* params, int64_t* d_rec_off, int32_t* d_rec_len,
+                        int64_t capacity, int64_t* d_state, int32_t max_rounds, void* stream);
+int cbx_frame_rdw_state(const int64_t* d_state, int64_t* n_records, void* stream);
 
 /* ---- variable-length record streams: sparse index, record selection, selected decode ----
  *

@@ -206,3 +206,112 @@ def test_record_length_field_errors():
     rd2 = VarLenNestedReader(LENFIELD_COPYBOOK, p2)
     with pytest.raises(ValueError):
         rd2.read(_lenfield_file(rng, 5))
+
+
+def _frame_async(raw: bytes, seeds=None, cap=None, max_rounds=0):
+    """cbx_frame_rdw_async + cbx_frame_rdw_state -> (offsets, lengths, state) or CbxError."""
+    import ctypes
+    from cobrix_amd import native as N
+    rd = VarLenNestedReader(RDW_NARROW_COPYBOOK, ReaderParameters(is_record_sequence=True))
+    t = torch.frombuffer(bytearray(raw) if raw else bytearray(16), dtype=torch.uint8).cuda()
+    cap = cap if cap is not None else len(raw) // 4 + 2
+    off = torch.empty(max(1, cap), dtype=torch.int64, device="cuda")
+    ln = torch.empty(max(1, cap), dtype=torch.int32, device="cuda")
+    state = torch.full((3,), -7, dtype=torch.int64, device="cuda")
+    sd = seeds or [0]
+    arr = (ctypes.c_int64 * len(sd))(*sd)
+    prm = rd.rdw_params()
+    st = torch.cuda.current_stream().cuda_stream
+    L = N.load()
+    N.check(L.cbx_frame_rdw_async(t.data_ptr(), len(raw), arr, len(sd), ctypes.byref(prm), off.data_ptr(),
+                                  ln.data_ptr(), cap, state.data_ptr(), max_rounds, ctypes.c_void_p(st)))
+    n = ctypes.c_int64(-1)
+    rc = L.cbx_frame_rdw_state(state.data_ptr(), ctypes.byref(n), ctypes.c_void_p(st))
+    s = state.cpu().tolist()
+    N.check(rc)
+    return off[: n.value].cpu().numpy(), ln[: n.value].cpu().numpy(), s
+
+
+@pytest.mark.parametrize("chunk", [37, 4096, None])
+def test_async_framing_equals_sync(monkeypatch, chunk):
+    """cbx_frame_rdw_async (no host wait; count and errors left on the device) frames exactly what
+    cbx_frame_rdw does, seeded or not; its state row is (count, -1, 0)."""
+    if chunk:
+        monkeypatch.setenv("CBX_RDW_CHUNK_BYTES", str(chunk))
+    d, _ = rdw_narrow(20_000, seed=11)
+    raw = d.numpy().tobytes()
+    eo, el = _oracle(raw)
+    seeds = [e[0] for e in O.sparse_index(raw, records_per_entry=997)]
+    for sd in (None, seeds):
+        off, ln, s = _frame_async(raw, seeds=sd)
+        assert np.array_equal(off, eo) and np.array_equal(ln, el)
+        assert s == [len(eo), -1, 0]
+    off, ln, s = _frame_async(_adversarial(600, seed=5))
+    eo2, el2 = _oracle(_adversarial(600, seed=5))
+    assert np.array_equal(off, eo2) and np.array_equal(ln, el2)
+
+
+def test_async_framing_reports_errors_on_the_device(monkeypatch):
+    """A zero-length header and a capacity below the record count surface from cbx_frame_rdw_state
+    with the codes cbx_frame_rdw returns; fix rounds cut short are settled on the device."""
+    from cobrix_amd import native as N
+    d, hdr = rdw_narrow(400, seed=9)
+    raw = bytearray(d.numpy().tobytes())
+    h = int(hdr[123])
+    raw[h:h + 4] = bytes(4)
+    with pytest.raises(CbxError) as e:
+        _frame_async(bytes(raw))
+    with pytest.raises(CbxError) as e_sync:
+        _frame(bytes(raw))
+    assert e.value.code == N.CBX_E_STATE and str(e.value) == str(e_sync.value)
+    with pytest.raises(CbxError) as e:
+        _frame_async(d.numpy().tobytes(), cap=100)
+    assert e.value.code == N.CBX_E_CAPACITY
+    # 8-byte chunks over adversarial payloads, one parallel fix round: the device settle pass finishes
+    # the chains of failed speculations it leaves
+    monkeypatch.setenv("CBX_RDW_CHUNK_BYTES", "8")
+    adv = _adversarial(300, seed=3)
+    eo, el = _oracle(adv)
+    for rounds in (1, 2, 0):
+        off, ln, s = _frame_async(adv, max_rounds=rounds)
+        assert np.array_equal(off, eo) and np.array_equal(ln, el) and s == [len(eo), -1, 0]
+
+
+def test_index_chain_on_the_device_equals_whole_file_index():
+    """shard.chain_step links run in sequence on the GPU (framing + cbx_sparse_index of each rank's
+    tail + block, 64 kB entries at roots): the union of the runs' entries is the GPU index of the
+    whole file, the runs tile it, and the record bases are the counts before each run."""
+    import ctypes
+    from cobrix_amd import native as N
+    from cobrix_amd.shard import chain_step
+    from cobrix_amd.synth import rdw_narrow_large
+    blocks = [rdw_narrow_large(9000 + 2000 * b, seed=70 + b, device="cuda")[0] for b in range(4)]
+    rd = VarLenNestedReader(RDW_NARROW_COPYBOOK, ReaderParameters(
+        is_record_sequence=True, segment_field="SEGMENT-ID", segment_id_levels=["C"]))
+    S = 64 * 1024
+
+    def index_fn(region):
+        n = int(region.numel())
+        off, ln = rd.frame(region, n)
+        prm = rd.index_params()
+        prm.bytes_per_entry, prm.subtract_size = S, 0
+        arr = (N.CbxIndexEntry * 4096)()
+        ne = ctypes.c_int64(0)
+        N.check(N.load().cbx_sparse_index(rd.native.handle, region.data_ptr(), n, off.data_ptr(), ln.data_ptr(),
+                                          int(off.numel()), ctypes.byref(prm), arr, 4096, ctypes.byref(ne), None))
+        return [(arr[k].offset_from, arr[k].record_index) for k in range(ne.value)], int(off.numel())
+
+    whole = torch.cat(blocks)
+    exp, n_all = index_fn(whole)
+    got, runs, r_off, r_rec, tail = [], [], 0, 0, None
+    for b, blk in enumerate(blocks):
+        region = blk if tail is None else torch.cat([tail, blk])
+        res, fwd = chain_step(region, index_fn, r_off, r_rec, b == len(blocks) - 1)
+        assert res["record_base"] == sum(r["n_records"] for r in runs)
+        got += res["entries"]
+        runs.append(res)
+        if fwd is not None:
+            r_off, r_rec, tail = fwd[0], fwd[1], fwd[2].clone()
+    assert len(exp) > 8 and got == exp
+    assert torch.equal(torch.cat([r["run"] for r in runs]), whole)
+    assert sum(r["n_records"] for r in runs) == n_all

@@ -155,3 +155,74 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=root)
     assert r.returncode == 2 and "WORLD_SIZE 1 != --gpus 2" in r.stderr
+
+
+def _chain_worker(rank, world, port, q, entry_bytes):
+    """One rank of a chained index (shard.index_chain): it holds only its own block of the file and
+    the tail the rank before it sends; index_fn = the oracle restatement of IndexGenerator."""
+    import torch.distributed as dist
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import parse_copybook_for
+    from cobrix_amd.shard import index_chain
+    from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow
+    from oracle import oracle as O
+    from oracle import reader_oracle as RO
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    block = rdw_narrow(2500 + 700 * rank, seed=40 + rank)[0]
+    room = entry_bytes + 4096
+    buf = torch.zeros(room + block.numel(), dtype=torch.uint8)
+    buf[room:] = block
+    p, _ = parse_options({**_CHAIN_OPTS})
+    cb = parse_copybook_for(RDW_NARROW_COPYBOOK, p)
+
+    def index_fn(region):
+        raw = region.numpy().tobytes()
+        ents = RO.sparse_index(cb, raw, p, 0, entry_bytes)
+        return [(e.offset_from, e.record_index) for e in ents], len(O.frame_rdw(raw)[0])
+
+    r = index_chain(buf, room, index_fn)
+    q.put((rank, r["entries"], r["record_base"], r["n_records"], r["run_start"], r["seeds"],
+           r["run"].numpy().tobytes()))
+    dist.destroy_process_group()
+
+
+_CHAIN_OPTS = {"is_record_sequence": "true", "segment_field": "SEGMENT_ID", "segment_id_root": "C"}
+
+
+@pytest.mark.parametrize("world,entry_bytes", [(2, 20_000), (3, 7_000), (3, 100_000)])
+def test_index_chain_equals_whole_file_index_gloo(world, entry_bytes):
+    """A file's index computed as a chain over ranks that each hold one block (+ one entry of tail)
+    equals the oracle's index of the whole file: same entries, the runs tile the file in order, the
+    record bases are the record counts before each run.  At 100 kB entries over ~200 kB blocks
+    some ranks get one entry or none."""
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import parse_copybook_for
+    from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow
+    from oracle import oracle as O
+    from oracle import reader_oracle as RO
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chain_worker, args=(r, world, port, q, entry_bytes)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    whole = b"".join(rdw_narrow(2500 + 700 * b, seed=40 + b)[0].numpy().tobytes() for b in range(world))
+    p, _ = parse_options({**_CHAIN_OPTS})
+    cb = parse_copybook_for(RDW_NARROW_COPYBOOK, p)
+    exp = [(e.offset_from, e.record_index) for e in RO.sparse_index(cb, whole, p, 0, entry_bytes)]
+    assert len(exp) > world
+    assert [e for r in res for e in r[1]] == exp
+    assert b"".join(r[6] for r in res) == whole
+    n_before = 0
+    for rank, ents, base, n_rec, start, seeds, run in res:
+        assert base == n_before and start == sum(len(x[6]) for x in res[:rank])
+        assert [start + s for s in seeds] == [o for o, _ in ents]
+        assert n_rec == len(O.frame_rdw(run)[0])
+        n_before += n_rec
+    assert n_before == len(O.frame_rdw(whole)[0])
