@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -123,7 +124,7 @@ struct cbx_plan {
     int num_cus = 256;
     // record walk (cbx_plan_set_walk, cbx_walk.h)
     bool walk = false;
-    int32_t walk_root = 0, walk_var = 0, walk_n_handlers = 0;
+    int32_t walk_root = 0, walk_var = 0, walk_n_handlers = 0, walk_depth = 1;
     cbx_walk_node* d_wnodes = nullptr;
     cbx_walk_array* d_warr = nullptr;
     cbx_walk_handler* d_whand = nullptr;
@@ -1069,10 +1070,15 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
     // per-wave LDS words (validity of every column slot, string cursors) when they fit 8 KiB a wave
     a.n_vslots = P->n_vslots;
     a.n_sslots = (int32_t)P->n_str_slots;
-    a.wave_lds = (int32_t)((8 * (int64_t)P->n_vslots + 4 * P->n_str_slots + 15) & ~15ll);
-    a.vlds = P->n_vslots > 0 && a.wave_lds <= 8192 && !getenv("CBX_WALK_GLOBAL_ATOMICS") ? 1 : 0;
+    // per wave: the frame stack (uniform part + three 64-lane rows per level), then the tile's
+    // validity words and string cursors when they fit 8 KiB
+    a.depth = P->walk_depth;
+    a.stack_lds = (int32_t)((a.depth * (sizeof(WalkU) + 3 * sizeof(int32_t) * kWave) + 15) & ~(size_t)15);
+    const int32_t words = (int32_t)((8 * (int64_t)P->n_vslots + 4 * P->n_str_slots + 15) & ~15ll);
+    a.vlds = P->n_vslots > 0 && words <= 8192 && !getenv("CBX_WALK_GLOBAL_ATOMICS") ? 1 : 0;
+    a.wave_lds = a.stack_lds + (a.vlds ? words : 0);
     a.vslot_base = P->d_wvbase; a.vslot_col = P->d_wvcol; a.vslot_slot = P->d_wvslot;
-    const size_t wlds = a.vlds ? 4 * (size_t)a.wave_lds : 0;
+    const size_t wlds = 4 * (size_t)a.wave_lds;
     const int64_t grid = std::min<int64_t>((n_tiles + 3) / 4, (int64_t)P->num_cus * 8);
     // kernel timing (cbx_plan_set_profiling): the walk is the decode; it has no post passes
     cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};
@@ -2099,6 +2105,25 @@ extern "C" int cbx_plan_set_walk(cbx_plan* P, const cbx_walk_node* nodes, int32_
         if (d.variant == V_FILE_ID) P->fid_col = d.column;
         if (d.variant == V_RECORD_ID) P->rid_col = d.column;
     }
+    // the frame stack's depth: the root's frame, one per group level, two per OCCURS group level
+    // (the elements' frame and the element's), one per OCCURS of primitives
+    std::vector<int> memo(n_nodes, -1);
+    std::function<int(int, int)> body = [&](int g, int guard) -> int {   // frames of group g's body
+        if (guard > 64) return 1 << 20;
+        if (memo[g] >= 0) return memo[g];
+        int m = 0;
+        for (int c = nodes[g].child, k = 0; c >= 0 && k < n_nodes; c = nodes[c].next, k++) {
+            const cbx_walk_node& n = nodes[c];
+            const int sub = n.kind == CBX_W_GROUP ? body(c, guard + 1) : 0;
+            m = std::max(m, n.array >= 0 ? 1 + sub : sub);
+        }
+        return memo[g] = 1 + m;
+    };
+    const int depth = body(root, 0);
+    if (depth > kWalkDepth)
+        return fail(CBX_E_UNSUPPORTED, "cbx_plan_set_walk: the copybook nests " + std::to_string(depth) + " levels, above " +
+                                           std::to_string(kWalkDepth));
+    P->walk_depth = depth;
     P->n_str_slots = ns;
     P->walk_root = root;
     P->walk_var = variable_size_occurs != 0;

@@ -55,6 +55,7 @@ struct WalkArgs {
     // per-wave LDS accumulation (vlds != 0): the tile's validity words of every (column, slot) and the
     // string slots' payload cursors, stored once per tile instead of one global atomic per value
     int32_t vlds, wave_lds;           // flag; LDS bytes per wave
+    int32_t depth, stack_lds;         // frame stack depth (the copybook's nesting), its LDS bytes per wave
     int32_t n_vslots, n_sslots;       // validity words (all column slots); string column slots
     const int64_t* vslot_base;        // per column: index of its slot 0 among all column slots
     const int32_t* vslot_col;         // per validity word: its column and slot
@@ -81,25 +82,51 @@ struct WalkFrame {
 // string no handler lists)
 struct WalkDep { int32_t kind, v; };
 
+// The lane's dependFields in registers: slots are addressed with wave-uniform indices (a node's
+// dep_slot), unrolled into selects so the table never goes to scratch.
+struct WalkDeps {
+    int32_t kind[kWalkDeps], v[kWalkDeps];
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int i = 0; i < kWalkDeps; i++) { kind[i] = 0; v[i] = 0; }
+    }
+    __device__ __forceinline__ WalkDep get(int s) const {
+        WalkDep d{0, 0};
+#pragma unroll
+        for (int i = 0; i < kWalkDeps; i++)
+            if (i == s) d = WalkDep{kind[i], v[i]};
+        return d;
+    }
+    __device__ __forceinline__ void set(int s, bool on, WalkDep d) {
+#pragma unroll
+        for (int i = 0; i < kWalkDeps; i++)
+            if (i == s && on) { kind[i] = d.kind; v[i] = d.v; }
+    }
+};
+
 __device__ __forceinline__ uint32_t walk_lut(const WalkArgs& a, int kind, uint32_t b) {
     return kind == CBX_K_STRING_ASCII ? ascii_lut(b) : a.lut[b];
 }
 
-// Record (tile * 64 + lane)'s value of (column, slot) is valid: an LDS OR into the tile's word
-// (vlds), else a global atomic OR into the column's bitmap.
-__device__ __forceinline__ void walk_set_valid(const WalkArgs& a, const WalkLds& wl, uint64_t* validity, int column, int slot,
-                                               int64_t tile, int lane) {
-    if (wl.vw) atomicOr((unsigned long long*)(wl.vw + a.vslot_base[column] + slot), 1ull << lane);
-    else atomicOr((unsigned long long*)(validity + (int64_t)slot * a.n_tiles + tile), 1ull << lane);
+// Validity of (column, slot) for the tile's lanes with v set (wave-uniform call): one OR of the
+// ballot into the tile's LDS word (vlds), else one global atomic per tile.
+__device__ __forceinline__ void walk_valid(const WalkArgs& a, const WalkLds& wl, uint64_t* validity, int column, int slot,
+                                           int64_t tile, int lane, bool v) {
+    const uint64_t m = __ballot(v);
+    if (m == 0) return;
+    if (lane == 0) {
+        if (wl.vw) wl.vw[a.vslot_base[column] + slot] |= m;
+        else atomicOr((unsigned long long*)(validity + (int64_t)slot * a.n_tiles + tile), m);
+    }
 }
 
 // extractArray's element count (:66-81)
-__device__ __forceinline__ int walk_count(const WalkArgs& a, int ai, const WalkDep* dep) {
+__device__ __forceinline__ int walk_count(const WalkArgs& a, int ai, const WalkDeps& dep) {
     const cbx_array ar = ldc(a.arrays + ai);
     const cbx_walk_array wa = ldc(a.warr + ai);
     int v = ar.max_count;
     if (wa.dep_slot >= 0) {
-        const WalkDep d = dep[wa.dep_slot];
+        const WalkDep d = dep.get(wa.dep_slot);
         if (d.kind == 1) v = d.v;
         else if (d.kind == 2) {   // dependingOnHandlers.getOrElse(s, arraySize)
             for (int h = wa.h_begin; h < wa.h_end; h++)
@@ -109,54 +136,72 @@ __device__ __forceinline__ int walk_count(const WalkArgs& a, int ai, const WalkD
     return (v >= ar.min_count && v <= ar.max_count) ? v : ar.max_count;
 }
 
-// One primitive element at record offset `off` (relative to the decode base).  `element`: an
-// element of a primitive OCCURS -- extractArray decodes those with decodeTypeValue, which never
-// touches dependFields (RecordExtractors.scala:96-107), so they update no dependee.
+// One primitive element at record offset `off` (relative to the decode base) for the lanes with
+// `la` (wave-uniform call: the node, its field and slot are the wave's).  `element`: an element of a
+// primitive OCCURS -- extractArray decodes those with decodeTypeValue, which never touches
+// dependFields (RecordExtractors.scala:96-107), so they update no dependee.
 __device__ void walk_prim(const WalkArgs& a, const WalkLds& wl, const cbx_walk_node& nd, int off, int slot, const uint8_t* rec,
-                          int avail, int64_t r, int lane, WalkDep* dep, bool element) {
-    const bool decoded = nd.field >= 0;
-    Field f{};
-    if (decoded) f = ldc(a.fields + nd.field);
+                          int avail, int64_t r, int64_t tile, int lane, bool la, WalkDeps& dep, bool element) {
+    if (nd.field < 0) return;   // a FILLER that nothing depends on
+    const Field f = ldc(a.fields + nd.field);
     const int size = nd.data_size;
     const int o = a.start_off + off;
-    const int64_t tile = r / kWave;
-    const bool is_str = decoded && (f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII || f.kind == CBX_K_HEX ||
-                                    f.kind == CBX_K_RAW || f.kind == CBX_K_UTF16_BE || f.kind == CBX_K_UTF16_LE);
+    const uint8_t* p = rec + o;
+    const bool is_str = f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII || f.kind == CBX_K_HEX ||
+                        f.kind == CBX_K_RAW || f.kind == CBX_K_UTF16_BE || f.kind == CBX_K_UTF16_LE;
+    const DevColumn c = ldc(a.cols + f.column);
     if (is_str) {
         // Primitive.decodeTypeValue (:102-128): offset past the end -> null, else truncated
-        if (o > avail) return;
-        const int n = o + size <= avail ? size : avail - o;
-        const uint8_t* p = rec + o;
+        bool ok = la && o <= avail;
+        const int n = ok ? (o + size <= avail ? size : avail - o) : 0;
         auto lutf = [&](uint32_t b) { return walk_lut(a, f.kind, b); };
-        const StrSpan sp = string_span(f.kind, f.trim, p, n, lutf);
-        const DevColumn c = ldc(a.cols + f.column);
-        const int len = sp.utf8_len;
-        uint8_t inl[16] = {0};
-        u32x4 view;
-        view.x = (uint32_t)len;
-        if (len <= 12) {
-            string_write(f.kind, p, sp, inl, lutf);
-            view.y = inl[0] | (uint32_t)inl[1] << 8 | (uint32_t)inl[2] << 16 | (uint32_t)inl[3] << 24;
-            view.z = inl[4] | (uint32_t)inl[5] << 8 | (uint32_t)inl[6] << 16 | (uint32_t)inl[7] << 24;
-            view.w = inl[8] | (uint32_t)inl[9] << 8 | (uint32_t)inl[10] << 16 | (uint32_t)inl[11] << 24;
-        } else {
-            const int64_t tb = a.tile_bytes[2 * f.column];
-            const int64_t tpb = a.tile_bytes[2 * f.column + 1];   // a power of two (view_tiles_per_buf)
-            const int64_t cs = a.str_slot_base[f.column] + slot;
-            const uint32_t at = wl.cur ? atomicAdd(wl.cur + cs, (uint32_t)len) : atomicAdd(a.cursors + cs * a.n_tiles + tile, (uint32_t)len);
-            if ((int64_t)at + len > tb) { atomicOr(a.status, 1); return; }
-            uint8_t* dst = c.data + (int64_t)slot * c.capacity + tile * tb + at;
-            string_write(f.kind, p, sp, dst, lutf);
-            view.y = dst[0] | (uint32_t)dst[1] << 8 | (uint32_t)dst[2] << 16 | (uint32_t)dst[3] << 24;
-            view.z = (uint32_t)(tile >> __builtin_ctzll((unsigned long long)tpb));
-            view.w = (uint32_t)((tile & (tpb - 1)) * tb + at);
+        StrSpan sp{};
+        if (ok) sp = string_span(f.kind, f.trim, p, n, lutf);
+        const int len = ok ? sp.utf8_len : 0;
+        const bool lng = ok && len > 12;
+        // a long value's place in its tile's region: a wave scan of the long lengths (vlds), else
+        // one atomic per lane on the (slot, tile) cursor
+        const int64_t tb = a.tile_bytes[2 * f.column];
+        const int64_t tpb = a.tile_bytes[2 * f.column + 1];   // a power of two (view_tiles_per_buf)
+        const int64_t cs = a.str_slot_base[f.column] + slot;
+        uint32_t at = 0;
+        if (wl.cur) {
+            uint32_t tot = 0;
+            const uint32_t ex = wave_excl_scan32(lng ? (uint32_t)len : 0u, lane, tot);
+            if (tot) {
+                const uint32_t base = wl.cur[cs];
+                at = base + ex;
+                wave_sync_lds();
+                if (lane == 0) wl.cur[cs] = base + tot;
+                wave_sync_lds();
+            }
+        } else if (lng) {
+            at = atomicAdd(a.cursors + cs * a.n_tiles + tile, (uint32_t)len);
         }
-        ((u32x4*)c.values)[(int64_t)slot * a.pitch + r] = view;
-        walk_set_valid(a, wl, c.validity, f.column, slot, tile, lane);
+        if (lng && (int64_t)at + len > tb) { atomicOr(a.status, 1); ok = false; }
+        if (ok) {
+            u32x4 view;
+            view.x = (uint32_t)len;
+            if (!lng) {
+                uint8_t inl[16] = {0};
+                string_write(f.kind, p, sp, inl, lutf);
+                view.y = inl[0] | (uint32_t)inl[1] << 8 | (uint32_t)inl[2] << 16 | (uint32_t)inl[3] << 24;
+                view.z = inl[4] | (uint32_t)inl[5] << 8 | (uint32_t)inl[6] << 16 | (uint32_t)inl[7] << 24;
+                view.w = inl[8] | (uint32_t)inl[9] << 8 | (uint32_t)inl[10] << 16 | (uint32_t)inl[11] << 24;
+            } else {
+                uint8_t* dst = c.data + (int64_t)slot * c.capacity + tile * tb + at;
+                string_write(f.kind, p, sp, dst, lutf);
+                view.y = dst[0] | (uint32_t)dst[1] << 8 | (uint32_t)dst[2] << 16 | (uint32_t)dst[3] << 24;
+                view.z = (uint32_t)(tile >> __builtin_ctzll((unsigned long long)tpb));
+                view.w = (uint32_t)((tile & (tpb - 1)) * tb + at);
+            }
+            ((u32x4*)c.values)[(int64_t)slot * a.pitch + r] = view;
+        }
+        walk_valid(a, wl, c.validity, f.column, slot, tile, lane, ok);
         if (nd.dep_slot >= 0 && !element) {   // Right(s): the handler key it equals (occurs_mappings)
             int key = 0;
-            uint8_t buf[64];
-            if (len <= 64) {
+            if (ok && len <= 64) {
+                uint8_t buf[64];
                 string_write(f.kind, p, sp, buf, lutf);
                 for (int h = 0; h < a.n_handlers && key == 0; h++) {
                     const cbx_walk_handler hd = ldc(a.handlers + h);
@@ -165,62 +210,101 @@ __device__ void walk_prim(const WalkArgs& a, const WalkLds& wl, const cbx_walk_n
                     if (eq) key = hd.key_id + 1;
                 }
             }
-            dep[nd.dep_slot] = WalkDep{2, key};
+            dep.set(nd.dep_slot, ok, WalkDep{2, key});
         }
         return;
     }
-    if (!decoded) return;   // a FILLER that nothing depends on
-    if (o + size > avail) return;   // numeric past the end -> null
-    const uint8_t* p = rec + o;
-    const Val x = decode_numeric(f, p);
-    if (!x.valid) return;   // null: dependFields keeps its previous entry (:126-134)
-    const DevColumn c = ldc(a.cols + f.column);
-    const int w = f.out_type == CBX_O_I32 || f.out_type == CBX_O_F32 ? 4 : f.out_type == CBX_O_DEC128 ? 16 : 8;
-    const int64_t at = (int64_t)slot * a.pitch + r;
-    if (w == 4) ((uint32_t*)c.values)[at] = (uint32_t)x.lo;
-    else if (w == 8) ((uint64_t*)c.values)[at] = x.lo;
-    else ((u32x4*)c.values)[at] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
-    walk_set_valid(a, wl, c.validity, f.column, slot, tile, lane);
+    bool ok = la && o + size <= avail;   // numeric past the end -> null
+    Val x{0, 0, false};
+    if (ok) x = decode_numeric(f, p);
+    ok = ok && x.valid;                  // null: dependFields keeps its previous entry (:126-134)
+    if (ok) {
+        const int w = f.out_type == CBX_O_I32 || f.out_type == CBX_O_F32 ? 4 : f.out_type == CBX_O_DEC128 ? 16 : 8;
+        const int64_t at = (int64_t)slot * a.pitch + r;
+        if (w == 4) ((uint32_t*)c.values)[at] = (uint32_t)x.lo;
+        else if (w == 8) ((uint64_t*)c.values)[at] = x.lo;
+        else ((u32x4*)c.values)[at] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
+    }
+    walk_valid(a, wl, c.validity, f.column, slot, tile, lane, ok);
     if (nd.dep_slot >= 0 && !element) {   // Left(Number.intValue)
-        const Val dv = decode_count_int(f, p);
-        if (dv.valid) dep[nd.dep_slot] = WalkDep{1, (int32_t)dv.lo};
+        Val dv{0, 0, false};
+        if (ok) dv = decode_count_int(f, p);
+        dep.set(nd.dep_slot, ok && dv.valid, WalkDep{1, (int32_t)dv.lo});
     }
 }
 
-// The walk of one record (extractRecord's getGroupValues / extractArray / extractValue).
-// seg: the active segment redefine (-1 none).
-__device__ void walk_record(const WalkArgs& a, const WalkLds& wl, const uint8_t* rec, int avail, int seg, int64_t r, int lane) {
-    WalkFrame st[kWalkDepth];
-    WalkDep dep[kWalkDeps];
-    for (int i = 0; i < kWalkDeps; i++) dep[i] = WalkDep{0, 0};
+// A frame's wave-uniform part (the node, the loop position, the slot and the lanes taking part);
+// its per-lane part -- start and running offset, the array's element count -- lives in LDS rows
+// of 64 lanes beside it.
+struct WalkU {
+    int32_t node, elems, cur, cmax, slot, pad;
+    uint64_t mask;
+};
+
+__device__ __forceinline__ int32_t ufl(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ WalkU walk_u(const WalkU* p) {
+    const WalkU w = *p;
+    WalkU u;
+    u.node = ufl(w.node); u.elems = ufl(w.elems); u.cur = ufl(w.cur); u.cmax = ufl(w.cmax); u.slot = ufl(w.slot); u.pad = 0;
+    u.mask = (uint64_t)(uint32_t)ufl((int32_t)(uint32_t)w.mask) | (uint64_t)(uint32_t)ufl((int32_t)(uint32_t)(w.mask >> 32)) << 32;
+    return u;
+}
+
+// The walk of the tile's 64 records at once (extractRecord's getGroupValues / extractArray /
+// extractValue): every record has the copybook's shape, only its counts, segment and offsets
+// differ, so the wave walks the node tree in step -- an OCCURS loop runs to the largest count among
+// the lanes, each lane taking part in the elements it has -- and the control flow, the node-table
+// loads and the decoder dispatch are the wave's (scalar), the offsets and values the lanes'.
+// act: the lane has a record; seg: its active segment redefine (-1 none).
+__device__ void walk_tile(const WalkArgs& a, const WalkLds& wl, uint8_t* stk, const uint8_t* rec, int avail, int seg,
+                          int64_t r, int64_t tile, int lane, bool act) {
+    WalkU* U = (WalkU*)stk;
+    int32_t* VS = (int32_t*)(U + a.depth);    // [depth][64] frame start
+    int32_t* VO = VS + a.depth * kWave;       // [depth][64] running offset
+    int32_t* VC = VO + a.depth * kWave;       // [depth][64] element count (array frames)
+    WalkDeps dep;
+    dep.clear();
     int sp = 0;
-    st[0] = WalkFrame{a.root, 0, ldc(a.nodes + a.root).child, 0, 0, 0, 0};
-    int last_size = 0;   // size consumed by the frame just popped
+    U[0] = WalkU{a.root, 0, ldc(a.nodes + a.root).child, 0, 0, 0, __ballot(act)};
+    VS[lane] = 0;
+    VO[lane] = 0;
+    int last = 0;   // per lane: size consumed by the frame just popped
     bool popped = false;
     while (sp >= 0) {
-        WalkFrame& fr = st[sp];
+        WalkU fr = walk_u(U + sp);
         const cbx_walk_node nd = ldc(a.nodes + fr.node);
+        const bool la = (fr.mask >> lane) & 1;
+        const int row = sp * kWave + lane;
+        int off = VO[row];
         if (fr.elems) {   // the elements of an OCCURS node
+            const int cnt = VC[row];
             if (popped) {   // a group element finished
-                fr.off += last_size;
+                if (la && fr.cur < cnt) off += last;
                 fr.cur++;
                 popped = false;
             }
-            if (fr.cur < fr.cnt) {
+            if (fr.cur < fr.cmax) {
                 const int slot = fr.slot * ldc(a.arrays + nd.array).max_count + fr.cur;
+                const bool le = la && fr.cur < cnt;
                 if (nd.kind == CBX_W_GROUP) {
-                    if (sp + 1 >= kWalkDepth) { atomicOr(a.status, 2); return; }
-                    st[sp + 1] = WalkFrame{fr.node, 0, nd.child, 0, fr.off, fr.off, slot};
+                    if (sp + 1 >= a.depth) { if (lane == 0) atomicOr(a.status, 2); return; }
+                    U[sp].cur = fr.cur;
+                    VO[row] = off;
+                    U[sp + 1] = WalkU{fr.node, 0, nd.child, 0, slot, 0, __ballot(le)};
+                    VS[row + kWave] = off;
+                    VO[row + kWave] = off;
                     sp++;
                     continue;
                 }
-                walk_prim(a, wl, nd, fr.off, slot, rec, avail, r, lane, dep, true);
-                fr.off += nd.data_size;
-                fr.cur++;
+                walk_prim(a, wl, nd, off, slot, rec, avail, r, tile, lane, le, dep, true);
+                if (le) off += nd.data_size;
+                U[sp].cur = fr.cur + 1;
+                VO[row] = off;
                 continue;
             }
-            // extractArray's consumed size: the elements walked, or the static size (:109-113)
-            last_size = a.var_occurs ? fr.off - fr.start : nd.actual_size;
+            // extractArray's consumed size: the lane's elements walked, or the static size (:109-113)
+            last = a.var_occurs ? off - VS[row] : nd.actual_size;
             sp--;
             popped = true;
             continue;
@@ -228,45 +312,58 @@ __device__ void walk_record(const WalkArgs& a, const WalkLds& wl, const uint8_t*
         // a group's children (the group node itself, or one element of an OCCURS group)
         if (popped) {   // a child group / array finished: advance by its size (getGroupValues, :144-160)
             const cbx_walk_node ch = ldc(a.nodes + fr.cur);
-            if (!(ch.flags & CBX_W_REDEFINED)) fr.off += (ch.array < 0 && (ch.flags & CBX_W_REDEFINES)) ? ch.actual_size : last_size;
+            if (la && !(ch.flags & CBX_W_REDEFINED)) off += (ch.array < 0 && (ch.flags & CBX_W_REDEFINES)) ? ch.actual_size : last;
             fr.cur = ch.next;
             popped = false;
+            U[sp].cur = fr.cur;
+            VO[row] = off;
         }
         if (fr.cur < 0) {   // the group is done
-            last_size = fr.off - fr.start;
+            last = off - VS[row];
             sp--;
             popped = true;
             continue;
         }
         const int ci = fr.cur;
         const cbx_walk_node ch = ldc(a.nodes + ci);
-        if (ch.array >= 0) {   // an OCCURS node: its element count, then its elements
-            const int cnt = walk_count(a, ch.array, dep);
+        if (ch.array >= 0) {   // an OCCURS node: the lanes' element counts, then the elements
+            const int cnt = la ? walk_count(a, ch.array, dep) : 0;
             const int ccol = ldc(a.arrays + ch.array).count_column;
             if (ccol >= 0) {
                 const DevColumn c = ldc(a.cols + ccol);
-                ((int32_t*)c.values)[(int64_t)fr.slot * a.pitch + r] = cnt;
-                walk_set_valid(a, wl, c.validity, ccol, fr.slot, r / kWave, lane);
+                if (la) ((int32_t*)c.values)[(int64_t)fr.slot * a.pitch + r] = cnt;
+                walk_valid(a, wl, c.validity, ccol, fr.slot, tile, lane, la);
             }
-            if (sp + 1 >= kWalkDepth) { atomicOr(a.status, 2); return; }
-            st[sp + 1] = WalkFrame{ci, 1, 0, cnt, fr.off, fr.off, fr.slot};
+            if (sp + 1 >= a.depth) { if (lane == 0) atomicOr(a.status, 2); return; }
+            const int cmax = (int)wave_max64(cnt);
+            U[sp + 1] = WalkU{ci, 1, 0, cmax, fr.slot, 0, fr.mask};
+            VS[row + kWave] = off;
+            VO[row + kWave] = off;
+            VC[row + kWave] = cnt;
             sp++;
             continue;
         }
         if (ch.kind == CBX_W_GROUP) {
-            if (ch.segment >= 0 && ch.segment != seg) {   // inactive segment redefine: null, full size (:119-121)
-                last_size = ch.actual_size;
+            // a segment redefine of another segment: null, full size (:119-121) -- its lanes skip the
+            // group, and its start is set one size back so that popping it consumes that size
+            const bool on = la && (ch.segment < 0 || ch.segment == seg);
+            const uint64_t m = __ballot(on);
+            if (m == 0) {
+                last = ch.actual_size;
                 popped = true;
                 continue;
             }
-            if (sp + 1 >= kWalkDepth) { atomicOr(a.status, 2); return; }
-            st[sp + 1] = WalkFrame{ci, 0, ch.child, 0, fr.off, fr.off, fr.slot};
+            if (sp + 1 >= a.depth) { if (lane == 0) atomicOr(a.status, 2); return; }
+            U[sp + 1] = WalkU{ci, 0, ch.child, 0, fr.slot, 0, m};
+            VS[row + kWave] = on ? off : off - ch.actual_size;
+            VO[row + kWave] = off;
             sp++;
             continue;
         }
-        walk_prim(a, wl, ch, fr.off, fr.slot, rec, avail, r, lane, dep, false);
-        if (!(ch.flags & CBX_W_REDEFINED)) fr.off += ch.actual_size;
-        fr.cur = ch.next;
+        walk_prim(a, wl, ch, off, fr.slot, rec, avail, r, tile, lane, la, dep, false);
+        if (la && !(ch.flags & CBX_W_REDEFINED)) off += ch.actual_size;
+        U[sp].cur = ch.next;
+        VO[row] = off;
     }
 }
 
@@ -274,49 +371,53 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint8_t* area = wsm + wid * a.wave_lds;   // the frame stack, then (vlds) the tile's words and cursors
     WalkLds wl{nullptr, nullptr};
     if (a.vlds) {
-        wl.vw = (uint64_t*)(wsm + wid * a.wave_lds);
-        wl.cur = (uint32_t*)(wsm + wid * a.wave_lds + 8 * a.n_vslots);
+        wl.vw = (uint64_t*)(area + a.stack_lds);
+        wl.cur = (uint32_t*)(area + a.stack_lds + 8 * a.n_vslots);
         for (int i = lane; i < a.n_vslots; i += kWave) wl.vw[i] = 0;
         for (int i = lane; i < a.n_sslots; i += kWave) wl.cur[i] = 0;
         wave_sync_lds();
     }
     // one wave per tile of 64 records (lane = record): every lane of the wave takes part in the
-    // tile's flush of the LDS words, records past the batch included
+    // walk and in the tile's flush of the LDS words, records past the batch included
     for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid; tile < a.n_tiles; tile += (int64_t)gridDim.x * (blockDim.x >> 6)) {
         const int64_t r = tile * kWave + lane;
-        if (r < a.n_rec) {
-            int64_t base;
-            int avail;
+        const bool act = r < a.n_rec;
+        int64_t base = 0;
+        int avail = 0;
+        if (act) {
             if (a.rec_off) { base = a.rec_off[r]; avail = a.rec_len[r]; }
             else { base = r * (int64_t)a.stride; avail = a.stride; }
-            const uint8_t* rec = a.data + base;
-            int seg = -1;
+        }
+        const uint8_t* rec = a.data + base;
+        int seg = -1;
+        if (act) {
             if (a.rec_seg) seg = a.rec_seg[r];
             else if (a.segmap) {
                 const int k = segment_key(a.segmap, a.lut, a.fields, rec, avail, a.start_off);
                 if (k >= 0) seg = a.segmap->key_segment[k];
             }
-            if (a.seg_col >= 0) {
-                const DevColumn c = ldc(a.cols + a.seg_col);
-                ((int32_t*)c.values)[r] = seg;
-                walk_set_valid(a, wl, c.validity, a.seg_col, 0, tile, lane);
-            }
-            if (a.fid_col >= 0) {
-                const DevColumn c = ldc(a.cols + a.fid_col);
-                ((int32_t*)c.values)[r] = a.file_id;
-                walk_set_valid(a, wl, c.validity, a.fid_col, 0, tile, lane);
-            }
-            if (a.rid_col >= 0) {
-                const DevColumn c = ldc(a.cols + a.rid_col);
-                ((int64_t*)c.values)[r] = a.rec_id ? a.rec_id[r] : a.first_record_id + (a.rec_id_base ? *a.rec_id_base : 0) + r;
-                walk_set_valid(a, wl, c.validity, a.rid_col, 0, tile, lane);
-            }
-            walk_record(a, wl, rec, avail, seg, r, lane);
         }
+        if (a.seg_col >= 0) {
+            const DevColumn c = ldc(a.cols + a.seg_col);
+            if (act) ((int32_t*)c.values)[r] = seg;
+            walk_valid(a, wl, c.validity, a.seg_col, 0, tile, lane, act);
+        }
+        if (a.fid_col >= 0) {
+            const DevColumn c = ldc(a.cols + a.fid_col);
+            if (act) ((int32_t*)c.values)[r] = a.file_id;
+            walk_valid(a, wl, c.validity, a.fid_col, 0, tile, lane, act);
+        }
+        if (a.rid_col >= 0) {
+            const DevColumn c = ldc(a.cols + a.rid_col);
+            if (act) ((int64_t*)c.values)[r] = a.rec_id ? a.rec_id[r] : a.first_record_id + (a.rec_id_base ? *a.rec_id_base : 0) + r;
+            walk_valid(a, wl, c.validity, a.rid_col, 0, tile, lane, act);
+        }
+        walk_tile(a, wl, area, rec, avail, seg, r, tile, lane, act);
+        wave_sync_lds();
         if (a.vlds) {   // the tile's words: one plain store each (this wave owns them), then cleared
-            wave_sync_lds();
             for (int i = lane; i < a.n_vslots; i += kWave) {
                 const DevColumn c = ldc(a.cols + a.vslot_col[i]);
                 c.validity[(int64_t)a.vslot_slot[i] * a.n_tiles + tile] = wl.vw[i];
@@ -335,8 +436,8 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
 // stream (a record starts where the previous one ends): one thread.
 __device__ int walk_length(const WalkArgs& a, const uint8_t* rec, int avail) {
     WalkFrame st[kWalkDepth];
-    WalkDep dep[kWalkDeps];
-    for (int i = 0; i < kWalkDeps; i++) dep[i] = WalkDep{0, 0};
+    WalkDeps dep;
+    dep.clear();
     int sp = 0;
     st[0] = WalkFrame{a.root, 0, ldc(a.nodes + a.root).child, 0, 0, 0, 0};
     int last_size = 0;
@@ -403,10 +504,10 @@ __device__ int walk_length(const WalkArgs& a, const uint8_t* rec, int avail) {
                         if (eq) key = hd.key_id + 1;
                     }
                 }
-                dep[ch.dep_slot] = WalkDep{2, key};
+                dep.set(ch.dep_slot, true, WalkDep{2, key});
             } else {
                 const Val dv = decode_count_int(f, zb);
-                if (dv.valid) dep[ch.dep_slot] = WalkDep{1, (int32_t)dv.lo};
+                dep.set(ch.dep_slot, dv.valid, WalkDep{1, (int32_t)dv.lo});
             }
         }
         if (!(ch.flags & CBX_W_REDEFINED)) fr.off += ch.actual_size;
