@@ -1076,7 +1076,9 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
     a.stack_lds = (int32_t)((a.depth * (sizeof(WalkU) + 3 * sizeof(int32_t) * kWave) + 15) & ~(size_t)15);
     const int32_t words = (int32_t)((8 * (int64_t)P->n_vslots + 4 * P->n_str_slots + 15) & ~15ll);
     a.vlds = P->n_vslots > 0 && words <= 8192 && !getenv("CBX_WALK_GLOBAL_ATOMICS") ? 1 : 0;
-    a.wave_lds = a.stack_lds + (a.vlds ? words : 0);
+    // the tile's record bytes: 8 KiB covers 64 records of up to 128 bytes (wider tiles read HBM)
+    a.stage_cap = getenv("CBX_WALK_NO_STAGE") ? 0 : 8192;
+    a.wave_lds = a.stack_lds + a.stage_cap + (a.vlds ? words : 0);
     a.vslot_base = P->d_wvbase; a.vslot_col = P->d_wvcol; a.vslot_slot = P->d_wvslot;
     const size_t wlds = 4 * (size_t)a.wave_lds;
     const int64_t grid = std::min<int64_t>((n_tiles + 3) / 4, (int64_t)P->num_cus * 8);

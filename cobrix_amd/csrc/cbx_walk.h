@@ -56,6 +56,7 @@ struct WalkArgs {
     // string slots' payload cursors, stored once per tile instead of one global atomic per value
     int32_t vlds, wave_lds;           // flag; LDS bytes per wave
     int32_t depth, stack_lds;         // frame stack depth (the copybook's nesting), its LDS bytes per wave
+    int32_t stage_cap;                // LDS bytes per wave for the tile's record span (a multiple of 16)
     int32_t n_vslots, n_sslots;       // validity words (all column slots); string column slots
     const int64_t* vslot_base;        // per column: index of its slot 0 among all column slots
     const int32_t* vslot_col;         // per validity word: its column and slot
@@ -371,11 +372,13 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint8_t* area = wsm + wid * a.wave_lds;   // the frame stack, then (vlds) the tile's words and cursors
+    // per wave: the frame stack, the tile's record bytes, then (vlds) the tile's words and cursors
+    uint8_t* area = wsm + wid * a.wave_lds;
+    uint8_t* stage = area + a.stack_lds;
     WalkLds wl{nullptr, nullptr};
     if (a.vlds) {
-        wl.vw = (uint64_t*)(area + a.stack_lds);
-        wl.cur = (uint32_t*)(area + a.stack_lds + 8 * a.n_vslots);
+        wl.vw = (uint64_t*)(stage + a.stage_cap);
+        wl.cur = (uint32_t*)(stage + a.stage_cap + 8 * a.n_vslots);
         for (int i = lane; i < a.n_vslots; i += kWave) wl.vw[i] = 0;
         for (int i = lane; i < a.n_sslots; i += kWave) wl.cur[i] = 0;
         wave_sync_lds();
@@ -392,6 +395,23 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
             else { base = r * (int64_t)a.stride; avail = a.stride; }
         }
         const uint8_t* rec = a.data + base;
+        // the tile's records are one byte span of the file: staged in LDS with 16-byte loads (the
+        // decoders' byte reads then hit LDS, not HBM), unless it is wider than the stage
+        {
+            const int64_t lo = wave_min64(act ? base : INT64_MAX);
+            const int64_t hi = wave_max64(act ? base + avail : 0);
+            if (hi > lo) {
+                const uintptr_t g0 = (uintptr_t)(a.data + lo);
+                const int mis = (int)(g0 & 15);
+                const int64_t span = hi - lo + mis;
+                if (span <= a.stage_cap) {
+                    const u32x4* src = (const u32x4*)(g0 - mis);
+                    for (int q = lane; 16 * q < span; q += kWave) ((u32x4*)stage)[q] = src[q];
+                    wave_sync_lds();
+                    rec = stage + mis + (base - lo);
+                }
+            }
+        }
         int seg = -1;
         if (act) {
             if (a.rec_seg) seg = a.rec_seg[r];
