@@ -126,6 +126,10 @@ struct cbx_plan {
     bool walk = false;
     int32_t walk_root = 0, walk_var = 0, walk_n_handlers = 0, walk_depth = 1;
     cbx_walk_node* d_wnodes = nullptr;
+    std::vector<cbx_walk_node> h_wnodes;   // host copies: the copybook-specialised walk's source
+    std::vector<cbx_walk_array> h_warr;
+    bool walk_jit_tried = false;
+    hipFunction_t walk_jit_fn = nullptr;
     cbx_walk_array* d_warr = nullptr;
     cbx_walk_handler* d_whand = nullptr;
     int64_t* d_wslot_base = nullptr;    // per column: first string-slot index
@@ -1032,6 +1036,118 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     return CBX_OK;
 }
 
+// ---- the copybook-specialised record walk (cbx_jit_walk) ----
+// The node tree unrolled into code: a group's children in sequence, an OCCURS as a loop to the
+// largest count among the tile's lanes (each lane in the elements it has), every primitive a call of
+// walk_prim_f with its Field as a constant (the decoder dispatch folds away), offsets and masks as
+// per-lane registers -- the frame stack, the node-table loads and the generic decoders of the
+// table-driven walk (walk_tile) are gone.  Same semantics, statement for statement:
+// extractRecord's getGroupValues / extractArray / extractValue (RecordExtractors.scala:49-183).
+static std::string field_literal(const Field& f) {
+    std::ostringstream o;
+    auto arr = [&](const int32_t* v) { o << "{" << v[0] << "," << v[1] << "," << v[2] << "," << v[3] << "}"; };
+    o << "{" << f.kind << "," << f.out_type << "," << f.offset << "," << f.size << "," << f.precision << "," << f.scale << ","
+      << f.sf << "," << f.out_p << "," << f.out_s << "," << f.flags << "," << f.trim << "," << f.n_dims << ",";
+    arr(f.dim_count); o << ","; arr(f.dim_stride); o << ","; arr(f.dim_array);
+    o << "," << f.segment << "," << f.column << "," << f.n_slots << "," << f.variant << "," << f.seq << "," << f.max_utf8 << ","
+      << f.defer << "," << f.fin << "," << f.plus_null << "," << f.e_mul << "," << f.e_lim << "," << f.lim_lo << "ull," << f.lim_hi
+      << "ull}";
+    return o.str();
+}
+
+struct WalkGen {
+    const cbx_plan* P;
+    std::ostringstream o;
+    int uid = 0, prims = 0;
+    bool ok = true;
+
+    void line(int ind, const std::string& t) { o << std::string(2 * ind, ' ') << t << "\n"; }
+
+    void prim(const cbx_walk_node& n, const std::string& off, const std::string& slot, const std::string& m, bool element, int ind) {
+        if (n.field < 0) return;   // a FILLER that nothing depends on
+        if (++prims > 4096) { ok = false; return; }
+        line(ind, "{ constexpr Field f = " + field_literal(P->dfields_h[n.field]) + ";");
+        line(ind + 1, "walk_prim_f(a, wl, f, " + std::to_string(n.data_size) + ", " + std::to_string(n.dep_slot) + ", " + off + ", " +
+                          slot + ", rec, avail, r, tile, lane, " + m + ", dep, " + (element ? "true" : "false") + "); }");
+    }
+
+    // the children of group g: running offset variable `off`, slot expression, lane-mask variable m
+    void body(int g, const std::string& off, const std::string& slot, const std::string& m, int ind, int depth) {
+        if (depth > 64) { ok = false; return; }
+        const std::vector<cbx_walk_node>& N = P->h_wnodes;
+        for (int c = N[g].child, guard = 0; c >= 0 && ok && guard < (int)N.size(); c = N[c].next, guard++) {
+            const cbx_walk_node& n = N[c];
+            const std::string K = std::to_string(uid++);
+            const bool adv = !(n.flags & CBX_W_REDEFINED);
+            if (n.array >= 0) {   // extractArray (:66-114)
+                const cbx_array& ar = P->harrays[n.array];
+                line(ind, "{   // OCCURS (node " + std::to_string(c) + ")");
+                line(ind + 1, "const int cnt" + K + " = " + m + " ? walk_count(a, " + std::to_string(n.array) + ", dep) : 0;");
+                if (ar.count_column >= 0) {
+                    const std::string cc = std::to_string(ar.count_column);
+                    line(ind + 1, "{ const DevColumn cc = ldc(a.cols + " + cc + "); if (" + m + ") ((int32_t*)cc.values)[(int64_t)(" + slot +
+                                      ") * a.pitch + r] = cnt" + K + "; walk_valid(a, wl, cc.validity, " + cc + ", " + slot +
+                                      ", tile, lane, " + m + "); }");
+                }
+                line(ind + 1, "const int cmax" + K + " = (int)wave_max64(cnt" + K + ");");
+                line(ind + 1, "int eo" + K + " = " + off + ";");
+                line(ind + 1, "for (int e" + K + " = 0; e" + K + " < cmax" + K + "; e" + K + "++) {");
+                line(ind + 2, "const bool le" + K + " = " + m + " && e" + K + " < cnt" + K + ";");
+                line(ind + 2, "const int s" + K + " = (" + slot + ") * " + std::to_string(std::max(1, ar.max_count)) + " + e" + K + ";");
+                if (n.kind == CBX_W_GROUP) {
+                    line(ind + 2, "int go" + K + " = eo" + K + ";");
+                    body(c, "go" + K, "s" + K, "le" + K, ind + 2, depth + 1);
+                    line(ind + 2, "if (le" + K + ") eo" + K + " = go" + K + ";");
+                } else {
+                    prim(n, "eo" + K, "s" + K, "le" + K, true, ind + 2);
+                    line(ind + 2, "if (le" + K + ") eo" + K + " += " + std::to_string(n.data_size) + ";");
+                }
+                line(ind + 1, "}");
+                // the consumed size: the lane's elements walked, or the static size (:109-113)
+                if (adv)
+                    line(ind + 1, "if (" + m + ") " + off + " += " + (P->walk_var ? "eo" + K + " - " + off : std::to_string(n.actual_size)) + ";");
+                line(ind, "}");
+                continue;
+            }
+            if (n.kind == CBX_W_GROUP) {   // getGroupValues (:144-160); a segment redefine of another segment: null, full size (:119-121)
+                const std::string on = n.segment >= 0 ? m + " && seg == " + std::to_string(n.segment) : m;
+                line(ind, "{   // group (node " + std::to_string(c) + ")");
+                line(ind + 1, "const bool on" + K + " = " + on + ";");
+                line(ind + 1, "int last" + K + " = " + std::to_string(n.actual_size) + ";");
+                line(ind + 1, "if (__ballot(on" + K + ")) {");
+                line(ind + 2, "int go" + K + " = " + off + ";");
+                body(c, "go" + K, slot, "on" + K, ind + 2, depth + 1);
+                line(ind + 2, "if (on" + K + ") last" + K + " = go" + K + " - " + off + ";");
+                line(ind + 1, "}");
+                if (adv) {
+                    if (n.flags & CBX_W_REDEFINES) line(ind + 1, "if (" + m + ") " + off + " += " + std::to_string(n.actual_size) + ";");
+                    else line(ind + 1, "if (" + m + ") " + off + " += last" + K + ";");
+                }
+                line(ind, "}");
+                continue;
+            }
+            prim(n, off, slot, m, false, ind);
+            if (adv) line(ind, "if (" + m + ") " + off + " += " + std::to_string(n.actual_size) + ";");
+        }
+    }
+};
+
+// The specialised walk's source, or "" when the copybook is beyond the unrolled form's limits.
+static std::string jit_walk_source(const cbx_plan* P) {
+    WalkGen g{P};
+    g.o << "#define CBX_STR_LAYOUT 1\n#define CBX_MODE 0\n#define CBX_JIT_WALK 1\n#include \"cbx_device.h\"\n#include \"cbx_walk.h\"\n"
+           "namespace cbx {\nstruct JitWalk {\n"
+           "  __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, const uint8_t* rec,\n"
+           "      int avail, int seg, int64_t r, int64_t tile, int lane, bool act) const {\n"
+           "    WalkDeps dep;\n    dep.clear();\n    int off0 = 0;\n";
+    g.body(P->walk_root, "off0", "0", "act", 2, 0);
+    g.o << "  }\n};\n}  // namespace cbx\n"
+           "extern \"C\" __global__ __launch_bounds__(256) void cbx_jit_walk(cbx::WalkArgs a) {\n"
+           "  extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];\n"
+           "  cbx::walk_tiles(a, wsm, cbx::JitWalk{});\n}\n";
+    return g.ok ? g.o.str() : std::string();
+}
+
 // The record walk (cbx_walk.h): one lane per record, data-dependent offsets.
 static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hipStream_t st) {
     const int64_t n_tiles = (c.n_rec + kWave - 1) / kWave;
@@ -1080,7 +1196,7 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
     a.stage_cap = getenv("CBX_WALK_NO_STAGE") ? 0 : 8192;
     a.wave_lds = a.stack_lds + a.stage_cap + (a.vlds ? words : 0);
     a.vslot_base = P->d_wvbase; a.vslot_col = P->d_wvcol; a.vslot_slot = P->d_wvslot;
-    const size_t wlds = 4 * (size_t)a.wave_lds;
+    const size_t wlds = kWalkLdsBase + 4 * (size_t)a.wave_lds;
     const int64_t grid = std::min<int64_t>((n_tiles + 3) / 4, (int64_t)P->num_cus * 8);
     // kernel timing (cbx_plan_set_profiling): the walk is the decode; it has no post passes
     cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};
@@ -1088,14 +1204,29 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
         for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
         HIP_CHECK(hipEventRecord(ce.e[0], st));
     }
-    hipLaunchKernelGGL(walk_kernel, dim3((unsigned)grid), dim3(256), wlds, st, a);
-    HIP_CHECK(hipGetLastError());
+    // the copybook-specialised walk for large batches (cbx_jit_walk), else the table-driven one
+    hipFunction_t jfn = nullptr;
+    if (P->jit_min >= 0 && c.n_rec >= P->jit_min && !getenv("CBX_NO_JIT_WALK")) {
+        if (!P->walk_jit_tried) {
+            P->walk_jit_tried = true;
+            const std::string src = jit_walk_source(P);
+            if (!src.empty()) P->walk_jit_fn = jit_get(src, &P->jit_error, "cbx_jit_walk");
+        }
+        jfn = P->walk_jit_fn;
+    }
+    if (jfn) {
+        void* kargs[] = {&a};
+        HIP_CHECK(hipModuleLaunchKernel(jfn, (unsigned)grid, 1, 1, 256, 1, 1, (unsigned)wlds, st, kargs, nullptr));
+    } else {
+        hipLaunchKernelGGL(walk_kernel, dim3((unsigned)grid), dim3(256), wlds, st, a);
+        HIP_CHECK(hipGetLastError());
+    }
     if (P->profiling) {
         HIP_CHECK(hipEventRecord(ce.e[1], st));
         HIP_CHECK(hipEventRecord(ce.e[2], st));
         P->ev_calls.push_back(ce);
     }
-    P->last_kind = 2;
+    P->last_kind = jfn ? 3 : 2;
     return CBX_OK;
 }
 
@@ -2126,6 +2257,8 @@ extern "C" int cbx_plan_set_walk(cbx_plan* P, const cbx_walk_node* nodes, int32_
         return fail(CBX_E_UNSUPPORTED, "cbx_plan_set_walk: the copybook nests " + std::to_string(depth) + " levels, above " +
                                            std::to_string(kWalkDepth));
     P->walk_depth = depth;
+    P->h_wnodes.assign(nodes, nodes + n_nodes);
+    P->h_warr.assign(arrays, arrays + na);
     P->n_str_slots = ns;
     P->walk_root = root;
     P->walk_var = variable_size_occurs != 0;

@@ -22,6 +22,9 @@ namespace cbx {
 
 constexpr int kWalkDepth = 16;     // group / OCCURS nesting levels
 constexpr int kWalkDeps = 8;       // DEPENDING ON names (dependee slots)
+// the waves' LDS areas start past LDS address 0: the compiler the specialised walk is built with
+// (torch's hipRTC) takes a pointer to LDS address 0 for a null one
+constexpr int kWalkLdsBase = 16;
 
 struct WalkArgs {
     const uint8_t* data;
@@ -140,12 +143,12 @@ __device__ __forceinline__ int walk_count(const WalkArgs& a, int ai, const WalkD
 // One primitive element at record offset `off` (relative to the decode base) for the lanes with
 // `la` (wave-uniform call: the node, its field and slot are the wave's).  `element`: an element of a
 // primitive OCCURS -- extractArray decodes those with decodeTypeValue, which never touches
-// dependFields (RecordExtractors.scala:96-107), so they update no dependee.
-__device__ void walk_prim(const WalkArgs& a, const WalkLds& wl, const cbx_walk_node& nd, int off, int slot, const uint8_t* rec,
-                          int avail, int64_t r, int64_t tile, int lane, bool la, WalkDeps& dep, bool element) {
-    if (nd.field < 0) return;   // a FILLER that nothing depends on
-    const Field f = ldc(a.fields + nd.field);
-    const int size = nd.data_size;
+// dependFields (RecordExtractors.scala:96-107), so they update no dependee.  f, size (the node's
+// dataSize) and dep_slot come from the node: the table-driven walk loads them, the
+// copybook-specialised walk (cbx_jit_walk) passes constants, so its decoders fold to the field's.
+__device__ __forceinline__ void walk_prim_f(const WalkArgs& a, const WalkLds& wl, const Field& f, int size, int dep_slot, int off,
+                                            int slot, const uint8_t* rec, int avail, int64_t r, int64_t tile, int lane, bool la,
+                                            WalkDeps& dep, bool element) {
     const int o = a.start_off + off;
     const uint8_t* p = rec + o;
     const bool is_str = f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII || f.kind == CBX_K_HEX ||
@@ -199,7 +202,7 @@ __device__ void walk_prim(const WalkArgs& a, const WalkLds& wl, const cbx_walk_n
             ((u32x4*)c.values)[(int64_t)slot * a.pitch + r] = view;
         }
         walk_valid(a, wl, c.validity, f.column, slot, tile, lane, ok);
-        if (nd.dep_slot >= 0 && !element) {   // Right(s): the handler key it equals (occurs_mappings)
+        if (dep_slot >= 0 && !element) {   // Right(s): the handler key it equals (occurs_mappings)
             int key = 0;
             if (ok && len <= 64) {
                 uint8_t buf[64];
@@ -211,7 +214,7 @@ __device__ void walk_prim(const WalkArgs& a, const WalkLds& wl, const cbx_walk_n
                     if (eq) key = hd.key_id + 1;
                 }
             }
-            dep.set(nd.dep_slot, ok, WalkDep{2, key});
+            dep.set(dep_slot, ok, WalkDep{2, key});
         }
         return;
     }
@@ -227,12 +230,22 @@ __device__ void walk_prim(const WalkArgs& a, const WalkLds& wl, const cbx_walk_n
         else ((u32x4*)c.values)[at] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
     }
     walk_valid(a, wl, c.validity, f.column, slot, tile, lane, ok);
-    if (nd.dep_slot >= 0 && !element) {   // Left(Number.intValue)
+    if (dep_slot >= 0 && !element) {   // Left(Number.intValue)
         Val dv{0, 0, false};
         if (ok) dv = decode_count_int(f, p);
-        dep.set(nd.dep_slot, ok && dv.valid, WalkDep{1, (int32_t)dv.lo});
+        dep.set(dep_slot, ok && dv.valid, WalkDep{1, (int32_t)dv.lo});
     }
 }
+
+#ifndef CBX_JIT_WALK
+// The table-driven walk's primitive: the node's field from the plan tables.
+__device__ void walk_prim(const WalkArgs& a, const WalkLds& wl, const cbx_walk_node& nd, int off, int slot, const uint8_t* rec,
+                          int avail, int64_t r, int64_t tile, int lane, bool la, WalkDeps& dep, bool element) {
+    if (nd.field < 0) return;   // a FILLER that nothing depends on
+    walk_prim_f(a, wl, ldc(a.fields + nd.field), nd.data_size, nd.dep_slot, off, slot, rec, avail, r, tile, lane, la, dep, element);
+}
+
+#endif
 
 // A frame's wave-uniform part (the node, the loop position, the slot and the lanes taking part);
 // its per-lane part -- start and running offset, the array's element count -- lives in LDS rows
@@ -252,6 +265,7 @@ __device__ __forceinline__ WalkU walk_u(const WalkU* p) {
     return u;
 }
 
+#ifndef CBX_JIT_WALK
 // The walk of the tile's 64 records at once (extractRecord's getGroupValues / extractArray /
 // extractValue): every record has the copybook's shape, only its counts, segment and offsets
 // differ, so the wave walks the node tree in step -- an OCCURS loop runs to the largest count among
@@ -367,13 +381,18 @@ __device__ void walk_tile(const WalkArgs& a, const WalkLds& wl, uint8_t* stk, co
         VO[row] = off;
     }
 }
+#endif
 
-__global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
+// The tiles of a walk launch (one wave per tile of 64 records, lane = record): the tile's span
+// staged in LDS, the generated columns, body(a, wl, area, rec, avail, seg, r, tile, lane, act) for the
+// copybook's fields (the table-driven walk_tile, or the copybook-specialised walk of cbx_jit_walk),
+// then the tile's LDS validity words.
+template <typename Body>
+__device__ __forceinline__ void walk_tiles(const WalkArgs& a, uint8_t* wsm, const Body& body) {
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     // per wave: the frame stack, the tile's record bytes, then (vlds) the tile's words and cursors
-    uint8_t* area = wsm + wid * a.wave_lds;
+    uint8_t* area = wsm + kWalkLdsBase + wid * a.wave_lds;
     uint8_t* stage = area + a.stack_lds;
     WalkLds wl{nullptr, nullptr};
     if (a.vlds) {
@@ -398,14 +417,14 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
         // the tile's records are one byte span of the file: staged in LDS with 16-byte loads (the
         // decoders' byte reads then hit LDS, not HBM), unless it is wider than the stage
         {
-            const int64_t lo = wave_min64(act ? base : INT64_MAX);
+            const int64_t lo = wave_min64(act ? base : 0x7fffffffffffffffll);
             const int64_t hi = wave_max64(act ? base + avail : 0);
             if (hi > lo) {
-                const uintptr_t g0 = (uintptr_t)(a.data + lo);
+                const uint64_t g0 = (uint64_t)(size_t)(a.data + lo);
                 const int mis = (int)(g0 & 15);
                 const int64_t span = hi - lo + mis;
                 if (span <= a.stage_cap) {
-                    const u32x4* src = (const u32x4*)(g0 - mis);
+                    const u32x4* src = (const u32x4*)(size_t)(g0 - mis);
                     for (int q = lane; 16 * q < span; q += kWave) ((u32x4*)stage)[q] = src[q];
                     wave_sync_lds();
                     rec = stage + mis + (base - lo);
@@ -435,7 +454,7 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
             if (act) ((int64_t*)c.values)[r] = a.rec_id ? a.rec_id[r] : a.first_record_id + (a.rec_id_base ? *a.rec_id_base : 0) + r;
             walk_valid(a, wl, c.validity, a.rid_col, 0, tile, lane, act);
         }
-        walk_tile(a, wl, area, rec, avail, seg, r, tile, lane, act);
+        body(a, wl, area, rec, avail, seg, r, tile, lane, act);
         wave_sync_lds();
         if (a.vlds) {   // the tile's words: one plain store each (this wave owns them), then cleared
             for (int i = lane; i < a.n_vslots; i += kWave) {
@@ -447,6 +466,19 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
             wave_sync_lds();
         }
     }
+}
+
+#ifndef CBX_JIT_WALK
+struct TableWalk {
+    __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, const uint8_t* rec, int avail,
+                                               int seg, int64_t r, int64_t tile, int lane, bool act) const {
+        walk_tile(a, wl, area, rec, avail, seg, r, tile, lane, act);
+    }
+};
+
+__global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
+    walk_tiles(a, wsm, TableWalk{});
 }
 
 // ---- VarOccursRecordExtractor: record lengths by walking each record's dependees ----
@@ -589,5 +621,7 @@ __global__ void lenfield_frame_kernel(LenFieldArgs a, int64_t capacity, int64_t*
     }
     out[0] = k;
 }
+
+#endif  // CBX_JIT_WALK
 
 }  // namespace cbx

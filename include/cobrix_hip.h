@@ -294,7 +294,7 @@ int cbx_plan_set_profiling(cbx_plan* plan, int32_t enable);
 int cbx_plan_kernel_times(cbx_plan* plan, float* decode_ms, float* post_ms, int32_t max_calls, int32_t* n_calls);
 
 /* Which decode kernel the plan's last decode call ran: *kind = 0 the table-driven kernel,
- * 2 the record walk (cbx_plan_set_walk),
+ * 2 the record walk (cbx_plan_set_walk), 3 its copybook-specialised form,
  * 1 the copybook-specialised kernel.  If specialisation was attempted and failed, *kind = 0 and
  * the reason is in cbx_last_error() (the call itself succeeded on the table-driven kernel). */
 int cbx_plan_kernel_kind(cbx_plan* plan, int32_t* kind);

@@ -32,14 +32,34 @@ def _gpu():
         pytest.skip("no GPU")
 
 
+_JIT_MIN = -1
+
+
+@pytest.fixture(autouse=True, params=["table", "jit"])
+def _walk_kernel(request):
+    """Every test runs on both walks: the table-driven walk_kernel and the copybook-specialised
+    cbx_jit_walk (hipRTC), which a decode call uses from jit_min_records records on."""
+    global _JIT_MIN
+    _JIT_MIN = -1 if request.param == "table" else 1
+    yield request.param
+
+
 def _reader(copybook: str, options: dict, **params):
     import dataclasses
     from cobrix_amd.options import parse_options
     from cobrix_amd.reader import VarLenNestedReader
     p, var_len = parse_options(options)
     assert var_len
-    p = dataclasses.replace(p, **params)
+    p = dataclasses.replace(p, **{"jit_min_records": _JIT_MIN, **params})
     return VarLenNestedReader(copybook, p), p
+
+
+def _walk_kind(rd) -> int:
+    import ctypes
+    from cobrix_amd import native as N
+    k = ctypes.c_int32()
+    N.check(N.load().cbx_plan_kernel_kind(rd.native.handle, ctypes.byref(k)))
+    return k.value
 
 
 @pytest.mark.parametrize("var_size", [True, False])
@@ -50,6 +70,7 @@ def test_walk_nested_odo_rdw_vs_oracle(var_size):
     rd, p = _reader(NESTED, opts)
     assert rd.walk
     rows = rd.read(raw, file_id=1).to_rows()
+    assert _walk_kind(rd) == (3 if _JIT_MIN > 0 else 2)
     exp = RO.var_len_rows(rd.copybook, raw, p, file_id=1)
     assert len(rows) == len(exp) == 3000
     bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]

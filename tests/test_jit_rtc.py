@@ -23,7 +23,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "cobrix_amd", "csrc")
 HEADERS = [("cobrix_hip.h", os.path.join(ROOT, "include", "cobrix_hip.h"))] + [
-    (n, os.path.join(CSRC, n)) for n in ("cbx_decode.h", "cbx_internal.h", "cbx_device.h", "cbx_list.h")]
+    (n, os.path.join(CSRC, n)) for n in ("cbx_decode.h", "cbx_internal.h", "cbx_device.h", "cbx_list.h", "cbx_walk.h")]
 
 
 def _torch_hiprtc() -> str | None:
@@ -162,4 +162,54 @@ def test_list_kernel_compiles_with_hiprtc(compiler):
     if compiler >= len(COMPILERS):
         pytest.skip("no second hipRTC")
     err = _compile(LIST_KERNEL, COMPILERS[compiler])
+    assert not err, err[:3000]
+
+
+WALK_KERNEL = """#define CBX_STR_LAYOUT 1
+#define CBX_MODE 0
+#define CBX_JIT_WALK 1
+#include "cbx_device.h"
+#include "cbx_walk.h"
+namespace cbx {
+struct JitWalk {
+  __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, const uint8_t* rec,
+      int avail, int seg, int64_t r, int64_t tile, int lane, bool act) const {
+    WalkDeps dep;
+    dep.clear();
+    int off0 = 0;
+    { constexpr Field f = {7,1,1,1,1,0,0,0,0,72,4,0,{0,0,0,0},{0,0,0,0},{0,0,0,0},-1,1,1,4,-1,1,0,0,0,0,0,1ull,0ull};
+      walk_prim_f(a, wl, f, 1, 0, off0, 0, rec, avail, r, tile, lane, act, dep, false); }
+    if (act) off0 += 1;
+    {
+      const int cnt3 = act ? walk_count(a, 0, dep) : 0;
+      const int cmax3 = (int)wave_max64(cnt3);
+      int eo3 = off0;
+      for (int e3 = 0; e3 < cmax3; e3++) {
+        const bool le3 = act && e3 < cnt3;
+        const int s3 = (0) * 3 + e3;
+        { constexpr Field f = {5,1,5,3,5,0,0,0,0,9,4,1,{3,0,0,0},{3,0,0,0},{0,0,0,0},-1,2,3,1,-1,1,-1,0,0,0,0,1ull,0ull};
+          walk_prim_f(a, wl, f, 3, -1, eo3, s3, rec, avail, r, tile, lane, le3, dep, true); }
+        if (le3) eo3 += 3;
+      }
+      if (act) off0 += eo3 - off0;
+    }
+    { constexpr Field f = {1,7,8,3,0,0,0,0,0,0,4,0,{0,0,0,0},{0,0,0,0},{0,0,0,0},-1,3,1,6,0,1,-1,0,0,0,0,1ull,0ull};
+      walk_prim_f(a, wl, f, 3, -1, off0, 0, rec, avail, r, tile, lane, act, dep, false); }
+  }
+};
+}  // namespace cbx
+extern "C" __global__ __launch_bounds__(256) void cbx_jit_walk(cbx::WalkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
+  cbx::walk_tiles(a, wsm, cbx::JitWalk{});
+}
+"""
+
+
+@pytest.mark.parametrize("compiler", range(2), ids=["rocm", "torch"])
+def test_walk_kernel_compiles_with_hiprtc(compiler):
+    """The copybook-specialised record walk (jit_walk_source: a prim, an OCCURS of a COMP-3 element,
+    a string) compiles against the bundled headers with both compilers."""
+    if compiler >= len(COMPILERS):
+        pytest.skip("no second hipRTC")
+    err = _compile(WALK_KERNEL, COMPILERS[compiler])
     assert not err, err[:3000]

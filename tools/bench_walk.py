@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--records", type=int, default=30_000_000)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--table", action="store_true", help="the table-driven walk (no copybook-specialised kernel)")
     args = ap.parse_args()
     import torch
     import bench
@@ -43,6 +44,9 @@ def main():
     dev = torch.device("cuda", 0)
     t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
     p, _ = parse_options({"is_record_sequence": "true", "variable_size_occurs": "true", "generate_record_id": "true"})
+    if args.table:
+        import dataclasses
+        p = dataclasses.replace(p, jit_min_records=-1)
     rd = VarLenNestedReader(NESTED, p)
     assert rd.walk
     off, ln = rd.frame(t, len(raw))
@@ -72,7 +76,7 @@ def main():
     alg = bench.algorithmic_bytes(rd.plan, n_rec, in_bytes, payload, present)
     achieved = alg / (ms * 1e-3) / 1e9
     print(json.dumps({
-        "metric": "record walk (variable_size_occurs) decode: input GB/s + records/s", "kernel": "cbx::walk_kernel",
+        "metric": "record walk (variable_size_occurs) decode: input GB/s + records/s", "kernel": {2: "cbx::walk_kernel (table-driven)", 3: "cbx_jit_walk (copybook-specialised, hipRTC)"}.get(kind.value, "?"),
         "kernel_kind": kind.value, "records": n_rec, "input_bytes": in_bytes,
         "value": round(in_bytes / (ms * 1e-3) / 1e9, 2), "unit": "GB/s", "records_per_s": round(n_rec / (ms * 1e-3), 1),
         "walk_kernel_ms": round(ms, 4), "call_ms_wall": round(wall * 1e3, 4),
