@@ -1085,8 +1085,8 @@ struct WalkGen {
                 line(ind + 1, "const int cnt" + K + " = " + m + " ? walk_count(a, " + std::to_string(n.array) + ", dep) : 0;");
                 if (ar.count_column >= 0) {
                     const std::string cc = std::to_string(ar.count_column);
-                    line(ind + 1, "{ const DevColumn cc = ldc(a.cols + " + cc + "); if (" + m + ") ((int32_t*)cc.values)[(int64_t)(" + slot +
-                                      ") * a.pitch + r] = cnt" + K + "; walk_valid(a, wl, cc.validity, " + cc + ", " + slot +
+                    line(ind + 1, "{ const DevColumn cc = ldc(a.cols + " + cc + "); if (" + m + ") *gp((int32_t*)cc.values + (int64_t)(" + slot +
+                                      ") * a.pitch + r) = cnt" + K + "; walk_valid(a, wl, cc.validity, " + cc + ", " + slot +
                                       ", tile, lane, " + m + "); }");
                 }
                 line(ind + 1, "const int cmax" + K + " = (int)wave_max64(cnt" + K + ");");
@@ -1137,7 +1137,9 @@ static std::string jit_walk_source(const cbx_plan* P) {
     WalkGen g{P};
     g.o << "#define CBX_STR_LAYOUT 1\n#define CBX_MODE 0\n#define CBX_JIT_WALK 1\n#include \"cbx_device.h\"\n#include \"cbx_walk.h\"\n"
            "namespace cbx {\nstruct JitWalk {\n"
-           "  __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, const uint8_t* rec,\n"
+           "  static constexpr bool kTyped = true;\n"
+           "  template <typename RP>\n"
+           "  __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, RP rec,\n"
            "      int avail, int seg, int64_t r, int64_t tile, int lane, bool act) const {\n"
            "    WalkDeps dep;\n    dep.clear();\n    int off0 = 0;\n";
     g.body(P->walk_root, "off0", "0", "act", 2, 0);
@@ -1196,7 +1198,7 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
     a.stage_cap = getenv("CBX_WALK_NO_STAGE") ? 0 : 8192;
     a.wave_lds = a.stack_lds + a.stage_cap + (a.vlds ? words : 0);
     a.vslot_base = P->d_wvbase; a.vslot_col = P->d_wvcol; a.vslot_slot = P->d_wvslot;
-    const size_t wlds = kWalkLdsBase + 4 * (size_t)a.wave_lds;
+    const size_t wlds = kWalkLdsBase + kWalkLut + 4 * (size_t)a.wave_lds;
     const int64_t grid = std::min<int64_t>((n_tiles + 3) / 4, (int64_t)P->num_cus * 8);
     // kernel timing (cbx_plan_set_profiling): the walk is the decode; it has no post passes
     cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};

@@ -258,7 +258,8 @@ CBX_HD Val finalize_decimal(U128 M, bool m_ovf, int vs, bool neg, const Field& f
 // ------------------------------------------------------------------------------------------
 // COMP-3  (BCDNumberDecoders.decodeBCDIntegralNumber / decodeBigBCDNumber)
 // ------------------------------------------------------------------------------------------
-CBX_HD Val decode_bcd(const Field& f, const uint8_t* p) {
+template <typename BP>
+CBX_HD Val decode_bcd(const Field& f, BP p) {
     const int n = f.size;
     U128 M = u128(0);
     bool ovf = false;
@@ -298,7 +299,8 @@ CBX_HD Val decode_bcd(const Field& f, const uint8_t* p) {
 // ------------------------------------------------------------------------------------------
 // COMP / COMP-4 / COMP-5 / COMP-9
 // ------------------------------------------------------------------------------------------
-CBX_HD Val decode_binary(const Field& f, const uint8_t* p) {
+template <typename BP>
+CBX_HD Val decode_binary(const Field& f, BP p) {
     const int n = f.size;
     const bool be = (f.flags & CBX_F_BIG_ENDIAN) != 0;
     const bool sgn = (f.flags & CBX_F_SIGNED) != 0;
@@ -388,7 +390,8 @@ CBX_HD Val zoned_finish(const Field& f, bool malformed, int sign, int nd, int nd
     return finalize_decimal(D, ovf, -f.sf + nd, neg, f);
 }
 
-CBX_HD Val decode_zoned(const Field& f, const uint8_t* p) {
+template <typename BP>
+CBX_HD Val decode_zoned(const Field& f, BP p) {
     const int n = f.size;
     bool malformed = false;
     int sign = 0;  // 0 none, 1 '+', 2 '-'
@@ -430,7 +433,8 @@ constexpr int kAsciiNumMax = 64;
 
 // Integer.parseInt / Long.parseLong of decodeAsciiNumber(bytes): after the sign bytes are taken
 // out, the trimmed rest must be one non-empty run of '0'..'9'.
-CBX_HD Val ascii_integral(const Field& f, const uint8_t* p) {
+template <typename BP>
+CBX_HD Val ascii_integral(const Field& f, BP p) {
     const int n = f.size;
     int sign = 0, phase = 0, nd = 0;   // phase 0 leading spaces, 1 digits, 2 trailing spaces
     bool bad = false, big = false;
@@ -473,7 +477,8 @@ CBX_HD Val finalize_decimal_wide(U128 M, int64_t vs, int first_cut, bool neg, co
 
 // java.math.BigDecimal(String) (significand [+-]?digits[.digits] | .digits, exponent [eE][+-]?digits)
 // then the Spark conversion.
-CBX_HD Val parse_java_bigdecimal(const Field& f, const uint8_t* s, int n) {
+template <typename BP>
+CBX_HD Val parse_java_bigdecimal(const Field& f, BP s, int n) {
     int i = 0;
     bool neg = false;
     if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
@@ -516,7 +521,8 @@ CBX_HD Val parse_java_bigdecimal(const Field& f, const uint8_t* s, int n) {
     return finalize_decimal_wide(M, scale - cut, first_cut, neg, f);
 }
 
-CBX_HD Val decode_ascii_num(const Field& f, const uint8_t* p) {
+template <typename BP>
+CBX_HD Val decode_ascii_num(const Field& f, BP p) {
     if ((f.flags & CBX_F_INTEGRAL) && f.precision <= 18) return ascii_integral(f, p);
     const int n = f.size < kAsciiNumMax ? f.size : kAsciiNumMax;
     // decodeAsciiNumber -> s = [sign] + buf.trim
@@ -616,7 +622,8 @@ CBX_HD uint64_t ibm_double_bits(uint64_t m) {
     return sign + ((uint64_t)ce << 52) + (uint64_t)cf;
 }
 
-CBX_HD Val decode_float(const Field& f, const uint8_t* p) {
+template <typename BP>
+CBX_HD Val decode_float(const Field& f, BP p) {
     const bool le = (f.flags & CBX_F_LITTLE_ENDIAN_FP) != 0;
     uint32_t w = 0;
     for (int i = 0; i < 4; i++) w = (w << 8) | p[le ? 3 - i : i];
@@ -624,7 +631,8 @@ CBX_HD Val decode_float(const Field& f, const uint8_t* p) {
     return Val{bits, 0, true};
 }
 
-CBX_HD Val decode_double(const Field& f, const uint8_t* p) {
+template <typename BP>
+CBX_HD Val decode_double(const Field& f, BP p) {
     const bool le = (f.flags & CBX_F_LITTLE_ENDIAN_FP) != 0;
     uint64_t w = 0;
     for (int i = 0; i < 8; i++) w = (w << 8) | p[le ? 7 - i : i];
@@ -632,7 +640,8 @@ CBX_HD Val decode_double(const Field& f, const uint8_t* p) {
     return Val{bits, 0, true};
 }
 
-CBX_HD Val decode_numeric(const Field& f, const uint8_t* p) {
+template <typename BP>
+CBX_HD Val decode_numeric(const Field& f, BP p) {
     switch (f.kind) {
     case CBX_K_BCD: return decode_bcd(f, p);
     case CBX_K_BINARY: return decode_binary(f, p);
@@ -931,7 +940,8 @@ CBX_HD Val decode_value(const NumOp& op, const uint8_t* img, uint32_t addr, bool
 
 // OCCURS DEPENDING ON source (integral, precision <= 18, RecordExtractors.scala:126-134): the
 // value as a Java long (BCD wraps; zoned follows Integer/Long.parseInt; binary <= 8 bytes).
-CBX_HD Val decode_count_int(const Field& f, const uint8_t* p) {
+template <typename BP>
+CBX_HD Val decode_count_int(const Field& f, BP p) {
     const int n = f.size;
     if (f.kind == CBX_K_BCD) {
         uint64_t v = 0;
@@ -1013,7 +1023,8 @@ CBX_HD uint32_t ascii_lut(uint32_t b) {
 // surrogate are malformed(2), a high surrogate followed by a non-low unit is malformed(4) (both
 // units), a high surrogate or a lone byte at the end is malformed(rest); each malformed run is
 // one U+FFFD.  One token at byte `pos` of p[0, n): returns its byte length, code point in cp.
-CBX_HD int utf16_token(const uint8_t* p, int pos, int n, bool be, uint32_t& cp) {
+template <typename BP>
+CBX_HD int utf16_token(BP p, int pos, int n, bool be, uint32_t& cp) {
     const int r = n - pos;
     cp = 0xFFFDu;
     if (r < 2) return r;
@@ -1030,7 +1041,8 @@ CBX_HD int utf16_token(const uint8_t* p, int pos, int n, bool be, uint32_t& cp) 
 CBX_HD int utf8_width(uint32_t cp) { return cp < 0x80u ? 1 : cp < 0x800u ? 2 : cp < 0x10000u ? 3 : 4; }
 
 // Trimmed span (token boundaries) + UTF-8 length of a UTF-16 field; trimming drops chars <= U+0020.
-CBX_HD StrSpan utf16_span(int kind, int trim, const uint8_t* p, int n) {
+template <typename BP>
+CBX_HD StrSpan utf16_span(int kind, int trim, BP p, int n) {
     const bool be = kind == CBX_K_UTF16_BE;
     int pos = 0, first = -1, last_end = 0, run = 0, u8_first = 0, u8_last = 0;
     while (pos < n) {
@@ -1057,8 +1069,8 @@ CBX_HD StrSpan utf16_span(int kind, int trim, const uint8_t* p, int n) {
     return s;
 }
 
-template <typename LutFn>
-CBX_HD StrSpan string_span(int kind, int trim, const uint8_t* p, int n, LutFn lut) {
+template <typename BP, typename LutFn>
+CBX_HD StrSpan string_span(int kind, int trim, BP p, int n, LutFn lut) {
     StrSpan s{0, n, 0};
     if (kind == CBX_K_HEX) { s.utf8_len = 2 * n; return s; }
     if (kind == CBX_K_RAW) { s.utf8_len = n; return s; }
@@ -1074,8 +1086,8 @@ CBX_HD StrSpan string_span(int kind, int trim, const uint8_t* p, int n, LutFn lu
     return s;
 }
 
-template <typename LutFn>
-CBX_HD void string_write(int kind, const uint8_t* p, const StrSpan& s, uint8_t* out, LutFn lut) {
+template <typename BP, typename LutFn>
+CBX_HD void string_write(int kind, BP p, const StrSpan& s, uint8_t* out, LutFn lut) {
     if (kind == CBX_K_HEX) {
         const char* H = "0123456789ABCDEF";
         for (int i = s.begin; i < s.end; i++) {

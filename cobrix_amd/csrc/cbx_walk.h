@@ -25,6 +25,7 @@ constexpr int kWalkDeps = 8;       // DEPENDING ON names (dependee slots)
 // the waves' LDS areas start past LDS address 0: the compiler the specialised walk is built with
 // (torch's hipRTC) takes a pointer to LDS address 0 for a null one
 constexpr int kWalkLdsBase = 16;
+constexpr int kWalkLut = 1024;     // the workgroup's 256-entry code-page table
 
 struct WalkArgs {
     const uint8_t* data;
@@ -67,10 +68,16 @@ struct WalkArgs {
 };
 
 // The wave's LDS area of the tile being walked (vlds): validity words, then string cursors.
+typedef __attribute__((address_space(3))) const uint8_t walk_lds_cu8;
+typedef __attribute__((address_space(3))) uint32_t walk_lds_u32;
+typedef __attribute__((address_space(3))) uint64_t walk_lds_u64;
 struct WalkLds {
-    uint64_t* vw;     // [n_vslots]
-    uint32_t* cur;    // [n_sslots]
+    walk_lds_u64* vw;          // [n_vslots]
+    walk_lds_u32* cur;         // [n_sslots]
+    const walk_lds_u32* lut;   // the code page's UTF-8 table, staged per workgroup
 };
+// A plan table of the walk (read-only for the kernel's lifetime): a scalar load.
+__device__ __forceinline__ int64_t walk_tab(const int64_t* t, int64_t i) { return ldc((const CBX_CONST int64_t*)t + i); }
 
 struct WalkFrame {
     int32_t node;     // group (children loop) or OCCURS node (elements loop)
@@ -108,8 +115,8 @@ struct WalkDeps {
     }
 };
 
-__device__ __forceinline__ uint32_t walk_lut(const WalkArgs& a, int kind, uint32_t b) {
-    return kind == CBX_K_STRING_ASCII ? ascii_lut(b) : a.lut[b];
+__device__ __forceinline__ uint32_t walk_lut(const WalkArgs& a, const WalkLds& wl, int kind, uint32_t b) {
+    return kind == CBX_K_STRING_ASCII ? ascii_lut(b) : wl.lut[b];
 }
 
 // Validity of (column, slot) for the tile's lanes with v set (wave-uniform call): one OR of the
@@ -119,7 +126,7 @@ __device__ __forceinline__ void walk_valid(const WalkArgs& a, const WalkLds& wl,
     const uint64_t m = __ballot(v);
     if (m == 0) return;
     if (lane == 0) {
-        if (wl.vw) wl.vw[a.vslot_base[column] + slot] |= m;
+        if (wl.vw) wl.vw[walk_tab(a.vslot_base, column) + slot] |= m;
         else atomicOr((unsigned long long*)(validity + (int64_t)slot * a.n_tiles + tile), m);
     }
 }
@@ -146,11 +153,12 @@ __device__ __forceinline__ int walk_count(const WalkArgs& a, int ai, const WalkD
 // dependFields (RecordExtractors.scala:96-107), so they update no dependee.  f, size (the node's
 // dataSize) and dep_slot come from the node: the table-driven walk loads them, the
 // copybook-specialised walk (cbx_jit_walk) passes constants, so its decoders fold to the field's.
+template <typename RP>
 __device__ __forceinline__ void walk_prim_f(const WalkArgs& a, const WalkLds& wl, const Field& f, int size, int dep_slot, int off,
-                                            int slot, const uint8_t* rec, int avail, int64_t r, int64_t tile, int lane, bool la,
+                                            int slot, RP rec, int avail, int64_t r, int64_t tile, int lane, bool la,
                                             WalkDeps& dep, bool element) {
     const int o = a.start_off + off;
-    const uint8_t* p = rec + o;
+    const RP p = rec + o;
     const bool is_str = f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII || f.kind == CBX_K_HEX ||
                         f.kind == CBX_K_RAW || f.kind == CBX_K_UTF16_BE || f.kind == CBX_K_UTF16_LE;
     const DevColumn c = ldc(a.cols + f.column);
@@ -158,16 +166,16 @@ __device__ __forceinline__ void walk_prim_f(const WalkArgs& a, const WalkLds& wl
         // Primitive.decodeTypeValue (:102-128): offset past the end -> null, else truncated
         bool ok = la && o <= avail;
         const int n = ok ? (o + size <= avail ? size : avail - o) : 0;
-        auto lutf = [&](uint32_t b) { return walk_lut(a, f.kind, b); };
+        auto lutf = [&](uint32_t b) { return walk_lut(a, wl, f.kind, b); };
         StrSpan sp{};
         if (ok) sp = string_span(f.kind, f.trim, p, n, lutf);
         const int len = ok ? sp.utf8_len : 0;
         const bool lng = ok && len > 12;
         // a long value's place in its tile's region: a wave scan of the long lengths (vlds), else
         // one atomic per lane on the (slot, tile) cursor
-        const int64_t tb = a.tile_bytes[2 * f.column];
-        const int64_t tpb = a.tile_bytes[2 * f.column + 1];   // a power of two (view_tiles_per_buf)
-        const int64_t cs = a.str_slot_base[f.column] + slot;
+        const int64_t tb = walk_tab(a.tile_bytes, 2 * f.column);
+        const int64_t tpb = walk_tab(a.tile_bytes, 2 * f.column + 1);   // a power of two (view_tiles_per_buf)
+        const int64_t cs = walk_tab(a.str_slot_base, f.column) + slot;
         uint32_t at = 0;
         if (wl.cur) {
             uint32_t tot = 0;
@@ -193,13 +201,14 @@ __device__ __forceinline__ void walk_prim_f(const WalkArgs& a, const WalkLds& wl
                 view.z = inl[4] | (uint32_t)inl[5] << 8 | (uint32_t)inl[6] << 16 | (uint32_t)inl[7] << 24;
                 view.w = inl[8] | (uint32_t)inl[9] << 8 | (uint32_t)inl[10] << 16 | (uint32_t)inl[11] << 24;
             } else {
-                uint8_t* dst = c.data + (int64_t)slot * c.capacity + tile * tb + at;
+                uint8_t* dst = (uint8_t*)gp(c.data + (int64_t)slot * c.capacity + tile * tb + at);
                 string_write(f.kind, p, sp, dst, lutf);
-                view.y = dst[0] | (uint32_t)dst[1] << 8 | (uint32_t)dst[2] << 16 | (uint32_t)dst[3] << 24;
+                const CBX_GLOBAL uint8_t* d = gp(dst);
+                view.y = d[0] | (uint32_t)d[1] << 8 | (uint32_t)d[2] << 16 | (uint32_t)d[3] << 24;
                 view.z = (uint32_t)(tile >> __builtin_ctzll((unsigned long long)tpb));
                 view.w = (uint32_t)((tile & (tpb - 1)) * tb + at);
             }
-            ((u32x4*)c.values)[(int64_t)slot * a.pitch + r] = view;
+            *gp((u32x4*)c.values + (int64_t)slot * a.pitch + r) = view;
         }
         walk_valid(a, wl, c.validity, f.column, slot, tile, lane, ok);
         if (dep_slot >= 0 && !element) {   // Right(s): the handler key it equals (occurs_mappings)
@@ -225,9 +234,9 @@ __device__ __forceinline__ void walk_prim_f(const WalkArgs& a, const WalkLds& wl
     if (ok) {
         const int w = f.out_type == CBX_O_I32 || f.out_type == CBX_O_F32 ? 4 : f.out_type == CBX_O_DEC128 ? 16 : 8;
         const int64_t at = (int64_t)slot * a.pitch + r;
-        if (w == 4) ((uint32_t*)c.values)[at] = (uint32_t)x.lo;
-        else if (w == 8) ((uint64_t*)c.values)[at] = x.lo;
-        else ((u32x4*)c.values)[at] = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
+        if (w == 4) *gp((uint32_t*)c.values + at) = (uint32_t)x.lo;
+        else if (w == 8) *gp((uint64_t*)c.values + at) = x.lo;
+        else *gp((u32x4*)c.values + at) = u32x4{(uint32_t)x.lo, (uint32_t)(x.lo >> 32), (uint32_t)x.hi, (uint32_t)(x.hi >> 32)};
     }
     walk_valid(a, wl, c.validity, f.column, slot, tile, lane, ok);
     if (dep_slot >= 0 && !element) {   // Left(Number.intValue)
@@ -391,13 +400,19 @@ template <typename Body>
 __device__ __forceinline__ void walk_tiles(const WalkArgs& a, uint8_t* wsm, const Body& body) {
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    // per wave: the frame stack, the tile's record bytes, then (vlds) the tile's words and cursors
-    uint8_t* area = wsm + kWalkLdsBase + wid * a.wave_lds;
+    // the workgroup's code-page table, then per wave: the frame stack, the tile's record bytes, then
+    // (vlds) the tile's words and cursors
+    walk_lds_u32* lut = (walk_lds_u32*)((__attribute__((address_space(3))) uint8_t*)wsm + kWalkLdsBase);
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = a.lut[i];
+    __syncthreads();
+    uint8_t* area = wsm + kWalkLdsBase + kWalkLut + wid * a.wave_lds;
     uint8_t* stage = area + a.stack_lds;
-    WalkLds wl{nullptr, nullptr};
+    __attribute__((address_space(3))) uint8_t* stage_l = (__attribute__((address_space(3))) uint8_t*)wsm + kWalkLdsBase +
+                                                        kWalkLut + wid * a.wave_lds + a.stack_lds;
+    WalkLds wl{nullptr, nullptr, lut};
     if (a.vlds) {
-        wl.vw = (uint64_t*)(stage + a.stage_cap);
-        wl.cur = (uint32_t*)(stage + a.stage_cap + 8 * a.n_vslots);
+        wl.vw = (walk_lds_u64*)(stage_l + a.stage_cap);
+        wl.cur = (walk_lds_u32*)(stage_l + a.stage_cap + 8 * a.n_vslots);
         for (int i = lane; i < a.n_vslots; i += kWave) wl.vw[i] = 0;
         for (int i = lane; i < a.n_sslots; i += kWave) wl.cur[i] = 0;
         wave_sync_lds();
@@ -410,12 +425,13 @@ __device__ __forceinline__ void walk_tiles(const WalkArgs& a, uint8_t* wsm, cons
         int64_t base = 0;
         int avail = 0;
         if (act) {
-            if (a.rec_off) { base = a.rec_off[r]; avail = a.rec_len[r]; }
+            if (a.rec_off) { base = *gp(a.rec_off + r); avail = *gp(a.rec_len + r); }
             else { base = r * (int64_t)a.stride; avail = a.stride; }
         }
         const uint8_t* rec = a.data + base;
         // the tile's records are one byte span of the file: staged in LDS with 16-byte loads (the
         // decoders' byte reads then hit LDS, not HBM), unless it is wider than the stage
+        int stage_at = -1;   // the lane's record in the stage
         {
             const int64_t lo = wave_min64(act ? base : 0x7fffffffffffffffll);
             const int64_t hi = wave_max64(act ? base + avail : 0);
@@ -427,13 +443,14 @@ __device__ __forceinline__ void walk_tiles(const WalkArgs& a, uint8_t* wsm, cons
                     const u32x4* src = (const u32x4*)(size_t)(g0 - mis);
                     for (int q = lane; 16 * q < span; q += kWave) ((u32x4*)stage)[q] = src[q];
                     wave_sync_lds();
-                    rec = stage + mis + (base - lo);
+                    stage_at = act ? mis + (int)(base - lo) : 0;
+                    rec = stage + stage_at;
                 }
             }
         }
         int seg = -1;
         if (act) {
-            if (a.rec_seg) seg = a.rec_seg[r];
+            if (a.rec_seg) seg = *gp(a.rec_seg + r);
             else if (a.segmap) {
                 const int k = segment_key(a.segmap, a.lut, a.fields, rec, avail, a.start_off);
                 if (k >= 0) seg = a.segmap->key_segment[k];
@@ -441,25 +458,30 @@ __device__ __forceinline__ void walk_tiles(const WalkArgs& a, uint8_t* wsm, cons
         }
         if (a.seg_col >= 0) {
             const DevColumn c = ldc(a.cols + a.seg_col);
-            if (act) ((int32_t*)c.values)[r] = seg;
+            if (act) *gp((int32_t*)c.values + r) = seg;
             walk_valid(a, wl, c.validity, a.seg_col, 0, tile, lane, act);
         }
         if (a.fid_col >= 0) {
             const DevColumn c = ldc(a.cols + a.fid_col);
-            if (act) ((int32_t*)c.values)[r] = a.file_id;
+            if (act) *gp((int32_t*)c.values + r) = a.file_id;
             walk_valid(a, wl, c.validity, a.fid_col, 0, tile, lane, act);
         }
         if (a.rid_col >= 0) {
             const DevColumn c = ldc(a.cols + a.rid_col);
-            if (act) ((int64_t*)c.values)[r] = a.rec_id ? a.rec_id[r] : a.first_record_id + (a.rec_id_base ? *a.rec_id_base : 0) + r;
+            if (act) *gp((int64_t*)c.values + r) = a.rec_id ? *gp(a.rec_id + r) : a.first_record_id + (a.rec_id_base ? *gp(a.rec_id_base) : 0) + r;
             walk_valid(a, wl, c.validity, a.rid_col, 0, tile, lane, act);
         }
-        body(a, wl, area, rec, avail, seg, r, tile, lane, act);
+        // the copybook's fields, reading the record through a typed pointer: LDS (ds_read) when
+        // staged, global otherwise -- a generic one would make every byte read wait for the tile's
+        // outstanding stores
+        if (!Body::kTyped) body(a, wl, area, rec, avail, seg, r, tile, lane, act);
+        else if (__builtin_amdgcn_readfirstlane(stage_at) >= 0) body(a, wl, area, (walk_lds_cu8*)stage_l + stage_at, avail, seg, r, tile, lane, act);
+        else body(a, wl, area, gp(a.data) + base, avail, seg, r, tile, lane, act);
         wave_sync_lds();
         if (a.vlds) {   // the tile's words: one plain store each (this wave owns them), then cleared
             for (int i = lane; i < a.n_vslots; i += kWave) {
-                const DevColumn c = ldc(a.cols + a.vslot_col[i]);
-                c.validity[(int64_t)a.vslot_slot[i] * a.n_tiles + tile] = wl.vw[i];
+                const DevColumn c = ldc(a.cols + *gp(a.vslot_col + i));
+                *gp(c.validity + (int64_t)*gp(a.vslot_slot + i) * a.n_tiles + tile) = wl.vw[i];
                 wl.vw[i] = 0;
             }
             for (int i = lane; i < a.n_sslots; i += kWave) wl.cur[i] = 0;
@@ -470,9 +492,11 @@ __device__ __forceinline__ void walk_tiles(const WalkArgs& a, uint8_t* wsm, cons
 
 #ifndef CBX_JIT_WALK
 struct TableWalk {
-    __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, const uint8_t* rec, int avail,
+    static constexpr bool kTyped = false;   // one instantiation, generic record pointer
+    template <typename RP>
+    __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, RP rec, int avail,
                                                int seg, int64_t r, int64_t tile, int lane, bool act) const {
-        walk_tile(a, wl, area, rec, avail, seg, r, tile, lane, act);
+        walk_tile(a, wl, area, (const uint8_t*)rec, avail, seg, r, tile, lane, act);
     }
 };
 
@@ -543,7 +567,7 @@ __device__ int walk_length(const WalkArgs& a, const uint8_t* rec, int avail) {
             const int size = ch.actual_size < 64 ? ch.actual_size : 64;
             for (int i = 0; i < size; i++) zb[i] = fr.off + i < avail ? rec[fr.off + i] : 0;
             if (f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII) {
-                auto lutf = [&](uint32_t b) { return walk_lut(a, f.kind, b); };
+                auto lutf = [&](uint32_t b) { return f.kind == CBX_K_STRING_ASCII ? ascii_lut(b) : a.lut[b]; };
                 const StrSpan s = string_span(f.kind, f.trim, zb, size, lutf);
                 uint8_t buf[64];
                 int key = 0;

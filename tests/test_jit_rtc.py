@@ -172,7 +172,9 @@ WALK_KERNEL = """#define CBX_STR_LAYOUT 1
 #include "cbx_walk.h"
 namespace cbx {
 struct JitWalk {
-  __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, const uint8_t* rec,
+  static constexpr bool kTyped = true;
+  template <typename RP>
+  __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, RP rec,
       int avail, int seg, int64_t r, int64_t tile, int lane, bool act) const {
     WalkDeps dep;
     dep.clear();
