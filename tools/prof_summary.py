@@ -5,9 +5,10 @@ rocprofv3 kernel trace of the SAME process and the PMC passes of a 1-step run.
   (dispatches warmup .. warmup + steps - 1: warm-up first, the end-to-end pass's chunks after);
 * roofline recomputed from the trace: algorithmic bytes (from the bench line) / the traced average
   of the decode kernel over the timed steps, next to the bench's HIP-event figure;
-* HBM traffic per launch: FETCH_SIZE (KiB) x 2 for the kernels that read with 16-byte-per-lane
-  streaming loads (MI355X_MICROARCH.md, HBM: gfx950 counts half of those), WRITE_SIZE as is, each
-  from the last dispatch of the kernel in the pass;
+* HBM traffic per step: FETCH_SIZE (KiB) x 2 for the kernels that read with 16-byte-per-lane
+  streaming loads (MI355X_MICROARCH.md, HBM: gfx950 counts half of those), WRITE_SIZE as is, from
+  the last dispatch of the kernel in the pass (the last KPS dispatches, summed, when the step decodes
+  its shard in KPS batches);
 * SQ counters per launch of each cbx kernel (the last dispatch).
 Usage: prof_summary.py <workload dir> -> JSON on stdout."""
 import collections
@@ -50,12 +51,15 @@ spans = collections.defaultdict(list)   # kernel -> [(start, end)] in ns, launch
 for r in sorted(trace, key=lambda r: int(r["Start_Timestamp"])):
     per[base(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     spans[base(r["Kernel_Name"])].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+# launches of the record kernel per step: a fixed-length shard decoded in batches (C3's 64 GB job)
+# runs one call per batch
+KPS = int(bench["config"].get("batches_per_gpu", 1) or 1)
 kernels = {}
 for k, d in per.items():
     if not (k.startswith("cbx") or "cbx" in k):
         continue
-    w0 = bench.get("warmup", 0)     # one launch per step: warm-up launches, the timed steps, then end-to-end chunks
-    timed = d[w0:w0 + steps] if len(d) >= w0 + steps else d
+    w0 = bench.get("warmup", 0) * KPS     # warm-up launches, the timed steps', then end-to-end chunks
+    timed = d[w0:w0 + steps * KPS] if len(d) >= w0 + steps * KPS else d
     kernels[k] = {"calls": len(d), "avg_ms_all": round(sum(d) / len(d), 4), "avg_ms_timed_steps": round(sum(timed) / len(timed), 4),
                   "max_ms": round(max(d), 4)}
 
@@ -71,10 +75,10 @@ if dec:
     # (the end-to-end pieces may run the table-driven kernel), a count/scan kernel from the END of
     # the last warm-up record launch up to the START of the last timed one -- so the warm-up step's
     # list kernels and the end-to-end pieces' parts (smaller batches) do not count
-    w0 = bench.get("warmup", 0)
+    w0 = bench.get("warmup", 0) * KPS
     sp = spans[k]
-    n_t = min(steps, len(sp) - w0)
-    first, last = sp[w0][0], sp[w0 + n_t - 1][0]
+    n_t = min(steps, (len(sp) - w0) // KPS)     # timed steps in the trace
+    first, last = sp[w0][0], sp[w0 + n_t * KPS - 1][0]
     lo = sp[w0 - 1][1] if w0 > 0 else 0
     after = [s0 for x in dec for s0, _ in spans[x] if s0 > last]
     hi = min(after) if after else float("inf")
@@ -108,7 +112,8 @@ for i in range(1, 9):
         d[int(r["Dispatch_Id"])] = d.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
 counters, traffic = {}, {}
 for k, cs in pmc.items():
-    last = {c: v[max(v)] for c, v in cs.items()}
+    # the last step of the 1-step pass: its KPS dispatches (one per batch) summed; one dispatch otherwise
+    last = {c: sum(v[d] for d in sorted(v)[-KPS:]) if len(v) >= KPS else v[max(v)] for c, v in cs.items()}
     counters[k] = {c: int(v) for c, v in sorted(last.items())}
     if "FETCH_SIZE" in last or "WRITE_SIZE" in last:
         f = last.get("FETCH_SIZE", 0.0) * 1024.0
@@ -124,7 +129,9 @@ for k, cs in pmc.items():
         counters[k]["lds_idx_active_per_cu_cycle"] = round(last["SQ_LDS_IDX_ACTIVE"] / (last["GRBM_GUI_ACTIVE"] / 8.0 * 256.0), 3)
     if last.get("SQ_WAVE_CYCLES"):
         counters[k]["wait_any_frac"] = round(last.get("SQ_WAIT_ANY", 0) / last["SQ_WAVE_CYCLES"], 3)
-dec_traffic = sum(v["traffic_bytes"] for k, v in traffic.items() if k.startswith(STAGED16))
+# the decode chain's traffic (the kernels the HIP-event window covers; framing kernels apart)
+chain = check.get("kernel", "").split(" + ") if check else []
+dec_traffic = sum(v["traffic_bytes"] for k, v in traffic.items() if k in chain)
 print(json.dumps({"workload": bench["config"]["workload"][:60], "records": bench["config"]["records_per_gpu"],
                   "bench": {k: bench[k] for k in ("value", "ms_per_step", "kernel_ms", "roofline", "hbm_frac_step")},
                   "kernels": kernels, "check": check, "traffic": traffic,
