@@ -336,6 +336,34 @@ class _Fixed:
                        "cbx_decode_fixed of the previous chunk (double-buffered), per rank"}
 
 
+def _host_staged() -> bool:
+    """gloo backend (--dist-backend gloo): collectives on device tensors go through host copies."""
+    import torch.distributed as dist
+    return dist.is_initialized() and dist.get_backend() == "gloo"
+
+
+def _all_reduce(t, op=None):
+    import torch.distributed as dist
+    op = op if op is not None else dist.ReduceOp.SUM
+    if _host_staged() and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+
+
+def _all_gather_into(out, inp):
+    import torch
+    import torch.distributed as dist
+    if _host_staged() and inp.is_cuda:
+        parts = [torch.empty_like(inp, device="cpu") for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, inp.cpu())
+        out.copy_(torch.cat(parts))
+    else:
+        dist.all_gather_into_tensor(out, inp)
+
+
 def _frame_rdw(L, data, n_bytes, seeds, prm, cap, dev, stream):
     """cbx_frame_rdw into fresh (offsets, lengths) tensors of `cap` records -> (off, len, n)."""
     import torch
@@ -500,7 +528,7 @@ class _VarLen:
                                            self.state.data_ptr(), 0, self.stream))
         self.fr1.record()
         if world > 1:   # Record_Id base = exclusive prefix of the ranks' counts, computed on the device
-            dist.all_gather_into_tensor(self.gathered, self.state[:1])
+            _all_gather_into(self.gathered, self.state[:1])
             self.base.copy_(self.gathered[: self.rank].sum().view(1))
         N.check(self.L.cbx_decode_var(self.h, self.raw.data_ptr(), self.in_bytes, self.off.data_ptr(),
                                       self.ln.data_ptr(), self.n_rec, 0, 0, self.cs, self.stream))
@@ -786,6 +814,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU plumbing only (gloo): launcher, all-gather, timing")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL, the measured path) or gloo: ranks may then share one GPU and collectives "
+                         "go through host copies -- a correctness run of the multi-rank path on a one-GPU box, "
+                         "not a measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -804,10 +836,15 @@ def main():
 
     from cobrix_amd import native as N
 
+    if args.dist_backend == "gloo":   # ranks may share the box's GPUs (correctness runs of the N > 1 path)
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     W = WORKLOADS[args.workload]
     n_req = args.records or W["records"]
@@ -865,7 +902,7 @@ def main():
     N.check(L.cbx_plan_set_profiling(h, 0))
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        _all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     check = job.verify(world)
 
@@ -874,7 +911,7 @@ def main():
     # job totals: every rank's input bytes and records (var-len runs differ in size)
     tot = torch.tensor([job.in_bytes, n_rec], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(tot)
+        _all_reduce(tot)
     job_bytes, job_recs = float(tot[0].item()), float(tot[1].item())
     steps = args.steps
     ms_per_step = elapsed / steps * 1e3

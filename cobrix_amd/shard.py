@@ -116,25 +116,37 @@ def index_chain(buf, tail_room: int, index_fn, group=None) -> dict:
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    meta = torch.zeros(3, dtype=torch.int64, device=buf.device)   # file offset, record index, tail bytes
+    # gloo moves host tensors only: device buffers then go through host copies
+    host = buf.is_cuda and dist.is_initialized() and dist.get_backend(group) == "gloo"
+    cdev = "cpu" if host else buf.device
+
+    def recv_into(t, src):
+        if host:
+            h = torch.empty(t.shape, dtype=t.dtype)
+            dist.recv(h, src=src, group=group)
+            t.copy_(h)
+        else:
+            dist.recv(t, src=src, group=group)
+
+    meta = torch.zeros(3, dtype=torch.int64, device=cdev)   # file offset, record index, tail bytes
     if rank > 0:
         dist.recv(meta, src=rank - 1, group=group)
     r_off, r_rec, tail = (int(x) for x in meta.tolist())
     if tail < 0:
         raise RuntimeError(f"index_chain: rank {rank - 1} had a tail larger than the {tail_room}-byte room")
     if tail > 0:
-        dist.recv(buf[tail_room - tail:tail_room], src=rank - 1, group=group)
+        recv_into(buf[tail_room - tail:tail_room], rank - 1)
     res, fwd = chain_step(buf[tail_room - tail:], index_fn, r_off, r_rec, rank == world - 1)
     if fwd is not None:
         f_off, f_rec, f_bytes = fwd
         ok = f_bytes.numel() <= tail_room
-        out = torch.tensor([f_off, f_rec, f_bytes.numel() if ok else -1], dtype=torch.int64, device=buf.device)
+        out = torch.tensor([f_off, f_rec, f_bytes.numel() if ok else -1], dtype=torch.int64, device=cdev)
         dist.send(out, dst=rank + 1, group=group)
         if not ok:
             raise RuntimeError(f"index_chain: {f_bytes.numel()}-byte tail for rank {rank + 1} exceeds the "
                                f"{tail_room}-byte room")
         if f_bytes.numel() > 0:
-            dist.send(f_bytes.contiguous(), dst=rank + 1, group=group)
+            dist.send(f_bytes.cpu() if host else f_bytes.contiguous(), dst=rank + 1, group=group)
     return res
 
 
