@@ -1065,7 +1065,7 @@ struct WalkGen {
 
     void prim(const cbx_walk_node& n, const std::string& off, const std::string& slot, const std::string& m, bool element, int ind) {
         if (n.field < 0) return;   // a FILLER that nothing depends on
-        if (++prims > 4096) { ok = false; return; }
+        if (++prims > kJitMaxOps) { ok = false; return; }   // (hipRTC time grows with the unrolled code)
         line(ind, "{ constexpr Field f = " + field_literal(P->dfields_h[n.field]) + ";");
         line(ind + 1, "walk_prim_f(a, wl, f, " + std::to_string(n.data_size) + ", " + std::to_string(n.dep_slot) + ", " + off + ", " +
                           slot + ", rec, avail, r, tile, lane, " + m + ", dep, " + (element ? "true" : "false") + "); }");
