@@ -1481,9 +1481,11 @@ static int frame_rdw_impl(const uint8_t* d_data, int64_t n_bytes, const int64_t*
     const bool async = d_state != nullptr;
     keep_pool_memory();
     // seed ranges cut into chunks (rdw_wave_kernel: speculation + walk, fix rounds; rdw_place_kernel)
-    // 64 KiB chunks: C4's 65-byte records ~1,000 per chunk; C5's 16 KB records still leave every
-    // chunk a few headers (framing 13.9 ms at 16 KiB -> 3.4 ms; C4 4.6 -> 4.5 ms)
-    int64_t chunk = 64 * 1024;
+    // 256 KiB chunks: every chunk pays one speculated entry, so C5's 16 KB records want few of them
+    // (framing 21.1 / 2.30 / 1.59 / 1.23 / 1.10 ms at 16 / 64 / 128 / 256 / 512 KiB), while C4's
+    // 65-byte records walk ~4,000 per chunk at no loss (4.02 / 3.97 / 3.96 / 4.11 ms at 64 / 128 /
+    // 256 / 512 KiB; same-box runs, tools/gpu_r04_chunk.sh)
+    int64_t chunk = 256 * 1024;
     if (const char* e = getenv("CBX_RDW_CHUNK_BYTES")) chunk = std::max<int64_t>(8, atoll(e));   // tests: many chunks
     std::vector<int64_t> hs;
     if (n_seeds <= 0) hs.push_back(0);
