@@ -1,5 +1,6 @@
-"""Timing line for the record walk (cbx_walk.h: extractRecord with data-dependent offsets, one lane per
-record; SURVEY.md 8(f)4 -- RecordExtractors.scala:66-134 with variable_size_occurs = true).
+"""Timing line for the record walk (cbx_walk.h: extractRecord with data-dependent offsets, a tile of
+64 records walked in step -- the copybook-specialised cbx_jit_walk, or with --table the table-driven
+walk_kernel; SURVEY.md 8(f)4 -- RecordExtractors.scala:66-134 with variable_size_occurs = true).
 
 The layout is cobrix_amd/synth.py's WALK_NESTED copybook (an OCCURS 0 TO 3 DEPENDING ON holding an
 OCCURS 1 TO 4 DEPENDING ON, COMP-3 / zoned / strings around them), records laid out as
