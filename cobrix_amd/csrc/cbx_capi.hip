@@ -124,7 +124,7 @@ struct cbx_plan {
     int num_cus = 256;
     // record walk (cbx_plan_set_walk, cbx_walk.h)
     bool walk = false;
-    int32_t walk_root = 0, walk_var = 0, walk_n_handlers = 0, walk_depth = 1;
+    int32_t walk_root = 0, walk_var = 0, walk_n_handlers = 0, walk_depth = 1, walk_max_rec = 0;
     cbx_walk_node* d_wnodes = nullptr;
     std::vector<cbx_walk_node> h_wnodes;   // host copies: the copybook-specialised walk's source
     std::vector<cbx_walk_array> h_warr;
@@ -1188,24 +1188,9 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
     // per-wave LDS words (validity of every column slot, string cursors) when they fit 8 KiB a wave
     a.n_vslots = P->n_vslots;
     a.n_sslots = (int32_t)P->n_str_slots;
-    // per wave: the frame stack (uniform part + three 64-lane rows per level), then the tile's
-    // validity words and string cursors when they fit 8 KiB
+    // per wave: the frame stack (uniform part + three 64-lane rows per level), the tile's record
+    // bytes, then the tile's validity words and string cursors when they fit 8 KiB
     a.depth = P->walk_depth;
-    a.stack_lds = (int32_t)((a.depth * (sizeof(WalkU) + 3 * sizeof(int32_t) * kWave) + 15) & ~(size_t)15);
-    const int32_t words = (int32_t)((8 * (int64_t)P->n_vslots + 4 * P->n_str_slots + 15) & ~15ll);
-    a.vlds = P->n_vslots > 0 && words <= 8192 && !getenv("CBX_WALK_GLOBAL_ATOMICS") ? 1 : 0;
-    // the tile's record bytes: 8 KiB covers 64 records of up to 128 bytes (wider tiles read HBM)
-    a.stage_cap = getenv("CBX_WALK_NO_STAGE") ? 0 : 8192;
-    a.wave_lds = a.stack_lds + a.stage_cap + (a.vlds ? words : 0);
-    a.vslot_base = P->d_wvbase; a.vslot_col = P->d_wvcol; a.vslot_slot = P->d_wvslot;
-    const size_t wlds = kWalkLdsBase + kWalkLut + 4 * (size_t)a.wave_lds;
-    const int64_t grid = std::min<int64_t>((n_tiles + 3) / 4, (int64_t)P->num_cus * 8);
-    // kernel timing (cbx_plan_set_profiling): the walk is the decode; it has no post passes
-    cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};
-    if (P->profiling) {
-        for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
-        HIP_CHECK(hipEventRecord(ce.e[0], st));
-    }
     // the copybook-specialised walk for large batches (cbx_jit_walk), else the table-driven one
     hipFunction_t jfn = nullptr;
     if (P->jit_min >= 0 && c.n_rec >= P->jit_min && !getenv("CBX_NO_JIT_WALK")) {
@@ -1215,6 +1200,26 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
             if (!src.empty()) P->walk_jit_fn = jit_get(src, &P->jit_error, "cbx_jit_walk");
         }
         jfn = P->walk_jit_fn;
+    }
+    // the table-driven walk's frame stack (the specialised walk keeps its frames in registers)
+    a.stack_lds = jfn ? 0 : (int32_t)((a.depth * (sizeof(WalkU) + 3 * sizeof(int32_t) * kWave) + 15) & ~(size_t)15);
+    const int32_t words = (int32_t)((8 * (int64_t)P->n_vslots + 4 * P->n_str_slots + 15) & ~15ll);
+    a.vlds = P->n_vslots > 0 && words <= 8192 && !getenv("CBX_WALK_GLOBAL_ATOMICS") ? 1 : 0;
+    // the tile's record bytes: 64 records of the copybook's largest form + 8 bytes of framing each
+    // (RDW headers, line ends), at most 8 KiB -- the resident waves per CU are LDS-bound; a wider
+    // tile reads its records from HBM
+    a.stage_cap = getenv("CBX_WALK_NO_STAGE")
+                      ? 0
+                      : (int32_t)std::min<int64_t>(8192, (kWave * (int64_t)(P->walk_max_rec + c.start_off + 8) + 31) & ~15ll);
+    a.wave_lds = a.stack_lds + a.stage_cap + (a.vlds ? words : 0);
+    a.vslot_base = P->d_wvbase; a.vslot_col = P->d_wvcol; a.vslot_slot = P->d_wvslot;
+    const size_t wlds = kWalkLdsBase + kWalkLut + 4 * (size_t)a.wave_lds;
+    const int64_t grid = std::min<int64_t>((n_tiles + 3) / 4, (int64_t)P->num_cus * 8);
+    // kernel timing (cbx_plan_set_profiling): the walk is the decode; it has no post passes
+    cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};
+    if (P->profiling) {
+        for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
+        HIP_CHECK(hipEventRecord(ce.e[0], st));
     }
     if (jfn) {
         void* kargs[] = {&a};
@@ -2261,6 +2266,10 @@ extern "C" int cbx_plan_set_walk(cbx_plan* P, const cbx_walk_node* nodes, int32_
         return fail(CBX_E_UNSUPPORTED, "cbx_plan_set_walk: the copybook nests " + std::to_string(depth) + " levels, above " +
                                            std::to_string(kWalkDepth));
     P->walk_depth = depth;
+    // the largest record the copybook describes (the root group's children at their static sizes)
+    int32_t max_rec = 0;
+    for (int c = nodes[root].child, k = 0; c >= 0 && k < n_nodes; c = nodes[c].next, k++) max_rec = std::max(max_rec, nodes[c].actual_size);
+    P->walk_max_rec = max_rec;
     P->h_wnodes.assign(nodes, nodes + n_nodes);
     P->h_warr.assign(arrays, arrays + na);
     P->n_str_slots = ns;
