@@ -265,5 +265,6 @@ def parse_options(options: Mapping[str, object]) -> Tuple[ReaderParameters, bool
         # VariableLengthParameters.inputFileNameColumn: only the variable-length readers generate the
         # column (the fixed-length defaults carry "", DefaultSource.scala:141-162)
         input_file_name_column=opts.get("with_input_file_name_col", "") if var_len else "",
+        debug_ignore_file_size=_bool(opts.get("debug_ignore_file_size", "false"), "debug_ignore_file_size"),
     )
     return p, var_len

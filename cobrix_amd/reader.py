@@ -94,6 +94,10 @@ class ReaderParameters:
     # with_input_file_name_col (ReaderParameters.inputFileNameColumn): a string column holding the
     # name of the file each record came from (RecordExtractors.applyRecordPostProcessing)
     input_file_name_column: str = ""
+    # debug_ignore_file_size (CobolParametersParser.PARAM_DEBUG_IGNORE_FILE_SIZE): a fixed-length file
+    # whose size is not a multiple of the record size (record_length included) is read anyway, its
+    # partial last record dropped, instead of being rejected (CobolScanners.scala:86-90)
+    debug_ignore_file_size: bool = False
 
 
 @dataclass
@@ -818,7 +822,14 @@ class FixedLenNestedReader(_BaseReader):
         return inner + self.params.start_offset + self.params.end_offset
 
     def check_binary_data_validity(self, n_bytes: int) -> None:
-        # FixedLenNestedReader.checkBinaryDataValidity (:71-90) applied to a whole split
+        """FixedLenNestedReader.checkBinaryDataValidity (CP/reader/FixedLenNestedReader.scala:71-90)
+        and the file-size rule of the fixed-length Spark scan (SC/source/scanners/CobolScanners.scala:
+        86-90), applied to a whole file / split.
+
+        The reference runs the first check on each record Spark's binaryRecords cut at getRecordSize,
+        and the second on each file before the scan: a file whose size is not a multiple of
+        getRecordSize -- `record_length` included -- is rejected unless `debug_ignore_file_size` is
+        set.  With it set the records are the file's whole records (the partial last one dropped)."""
         p = self.params
         if p.start_offset < 0:
             raise ValueError(f"Invalid record start offset = {p.start_offset}. A record start offset cannot be negative.")
@@ -828,7 +839,11 @@ class FixedLenNestedReader(_BaseReader):
             if p.record_length < 1:
                 raise ValueError(f"The specified record size {p.record_length} cannot be used. "
                                  "The record length should be greater then zero.")
-        else:
+            if not p.debug_ignore_file_size and n_bytes % self.get_record_size() > 0:
+                raise ValueError("There are some files in the input that are NOT DIVISIBLE by the RECORD SIZE calculated "
+                                 f"from the copybook ({self.get_record_size()} bytes per record). "
+                                 "Check the logs for the names of the files.")
+        elif not p.debug_ignore_file_size:
             exp = self.copybook.record_size + p.start_offset + p.end_offset
             if n_bytes < exp:
                 raise ValueError(f"Binary record too small. Expected binary record size = {exp}, got {n_bytes} ")

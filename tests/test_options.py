@@ -79,3 +79,42 @@ def test_segment_children_with_levels():
     with pytest.raises(ValueError, match="cannot be used with 'segment_id_level\\*' or 'segment_id_root'"):
         parse_options({"is_record_sequence": "true", "segment_field": "S", "segment_id_level0": "1",
                        "segment-children:1": "A => B"})
+
+
+def _fixed_reader(opts):
+    """A FixedLenNestedReader's host half (parameters + copybook) without the device plan: the
+    size checks are host logic."""
+    from cobrix_amd.reader import FixedLenNestedReader
+    p, var_len = parse_options(opts)
+    assert not var_len
+    rd = object.__new__(FixedLenNestedReader)
+    rd.params = p
+    rd.copybook = parse_copybook_for("       01  R.\n          05  A  PIC X(5).\n          05  B  PIC X(11).\n", p)
+    return rd
+
+
+def test_file_size_rule():
+    """A file whose size is not a multiple of getRecordSize is rejected -- `record_length`
+    included -- unless debug_ignore_file_size is set (CobolScanners.scala:86-90;
+    Test1FixedLengthRecordsSpec.scala:62-105)."""
+    rd = _fixed_reader({})
+    rd.check_binary_data_validity(32)
+    with pytest.raises(ValueError, match="Binary record size 16 does not divide data size 33."):
+        rd.check_binary_data_validity(33)
+    with pytest.raises(ValueError, match="Binary record too small"):
+        rd.check_binary_data_validity(10)
+    rd = _fixed_reader({"record_length": "10"})
+    assert rd.get_record_size() == 10
+    rd.check_binary_data_validity(30)
+    with pytest.raises(ValueError, match=r"NOT DIVISIBLE by the RECORD SIZE calculated from the copybook \(10 bytes"):
+        rd.check_binary_data_validity(33)
+    rd = _fixed_reader({"record_length": "10", "record_start_offset": "2"})
+    with pytest.raises(ValueError, match=r"\(12 bytes per record\)"):
+        rd.check_binary_data_validity(30)
+    for opts in ({"debug_ignore_file_size": "true"}, {"debug_ignore_file_size": "true", "record_length": "10"}):
+        rd = _fixed_reader(opts)
+        assert rd.params.debug_ignore_file_size
+        rd.check_binary_data_validity(33)
+        rd.check_binary_data_validity(7)
+    with pytest.raises(ValueError):
+        parse_options({"debug_ignore_file_size": "yes"})
