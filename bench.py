@@ -29,7 +29,7 @@ offset per list; absent ODO elements count nothing.  The layout actually written
 views, int64 offsets, count / segment columns) is reported as `layout_overhead` beside it, never in
 `achieved`.  achieved = algorithmic bytes / the decode kernel's average duration (HIP events recorded
 by the library on the launch stream over the timed steps, cbx_plan_kernel_times); the rocprofv3
-summary of the same command is committed under profiles/ (tools/gpu_r03.sh).
+summary of the same command is committed under profiles/ (tools/evidence.sh).
 
 end_to_end (N = 1): the same shard streamed from pinned host memory -- fixed-length: 2.5 M-record
 chunks; variable-length: pieces of whole index entries (their offsets seed the framing of the
@@ -185,7 +185,7 @@ def _round_key(path: str):
 
 def measured_traffic(tag: str):
     """HBM bytes per decode-kernel launch from the newest committed rocprofv3 FETCH_SIZE/WRITE_SIZE
-    passes of this configuration (tools/gpu_r03.sh -> profiles/<round tag>/traffic_<tag>.json)."""
+    passes of this configuration (tools/evidence.sh -> profiles/<round tag>/traffic_<tag>.json)."""
     import glob
     found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_{tag}.json")), key=_round_key)
     if not found:

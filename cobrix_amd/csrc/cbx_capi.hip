@@ -118,6 +118,9 @@ struct cbx_plan {
     // + [4 (kPre + 1)] the specialised list kernel
     bool jit_tried[4 * kPre + 5] = {};
     hipFunction_t jit_fn[4 * kPre + 5] = {};
+    // the cooperative-tile decision each specialised kernel was compiled with (jit_coop_of reads env
+    // knobs: launches reuse the compile-time answer, never re-derive it)
+    bool jit_coop[4 * kPre + 5] = {};
     // the one-pass Arrow Utf8 kernel (cbx_utf8.h) by prefetch depth, with its staging bytes
     bool u8_tried[kPre + 1] = {};
     hipFunction_t u8_fn[kPre + 1] = {};
@@ -967,6 +970,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // resident blocks per CU: the LDS bound and the runtime's occupancy (registers)
     // copybook-specialised kernel for large contiguous batches (cbx_jit.h)
     hipFunction_t jfn = span_fn;
+    int jk = -1;   // jit_fn slot of jfn (-1: the span kernel or none -- never cooperative)
     if (!span && mode == 0 && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
         const int k = contig ? contig_kp(sdw) : 0;
         if (!P->jit_tried[k]) {
@@ -980,16 +984,19 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                 P->jit_error = "layout has " + std::to_string(elems) + " elements in " + std::to_string(S.win.size()) +
                                " windows, above the specialised-kernel limits (" + std::to_string(kJitMaxOps) + ", " +
                                std::to_string(kJitMaxWindows) + ")";
-            else
+            else {
+                CoopSplit cs;
+                P->jit_coop[k] = jit_coop_of(contig, span, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false, &cs);
                 P->jit_fn[k] = jit_get(jit_source(contig, k, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false), &P->jit_error);
+            }
         }
         jfn = P->jit_fn[k];
+        jk = k;
     }
     P->last_kind = jfn ? 1 : 0;
     // cooperative tiles (cbx_jit.h jit_coop, cbx_device.h coop_loop): one image per workgroup,
     // one tile per workgroup
-    CoopSplit coop_split;
-    const bool coop = jfn && jit_coop_of(contig, span, jit_pro(P), str_layout_of(P), S.win, S.nops, S.batches, S.sops, false, &coop_split);
+    const bool coop = jfn && jk >= 0 && P->jit_coop[jk];
     const size_t lds = coop ? kLutLds + (size_t)a.lds_rows + (size_t)kWavesPerBlock * (a.lds_wave - a.lds_rows) : lds_own;
     if (lds > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
     int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / lds));
@@ -1015,16 +1022,20 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // span-staged batches count with a specialised kernel of the same staging; windowed ones (and a
     // failed specialisation) with a mode-1 call of the table-driven kernel.
     hipFunction_t cfn = nullptr;
+    int ck = 0;
     if (mode == 0 && P->packed && P->n_seq > 0 && (contig || span) && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
         const int kp = contig ? contig_kp(sdw) : span_kp;
         const int k = (contig ? 2 : 3) * (kPre + 1) + kp;
         if (!P->jit_tried[k]) {
             P->jit_tried[k] = true;
             std::string err;
+            CoopSplit cs;
+            P->jit_coop[k] = jit_coop_of(true, span, jit_pro(P), 2, S.win, S.nops, S.batches, S.sops, true, &cs);
             P->jit_fn[k] = jit_get(jit_source(true, kp, jit_pro(P), 2, S.win, S.nops, S.batches, S.sops, span, true),
                                    &err, "cbx_jit_count");
         }
         cfn = P->jit_fn[k];
+        ck = k;
     }
     if (mode == 0 && P->packed && P->n_seq > 0 && !cfn && !contig) {
         const int kind = P->last_kind;
@@ -1036,8 +1047,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         // the specialised count kernel: no string staging per wave (it only scans lengths), two LUT
         // copies in front (full + count_lut_byte)
         size_t clds = lds_own;
-        CoopSplit csplit;
-        const bool ccoop = cfn && jit_coop_of(true, span, jit_pro(P), 2, S.win, S.nops, S.batches, S.sops, true, &csplit);
+        const bool ccoop = cfn && P->jit_coop[ck];
         if (cfn) {
             ac.lds_wave = (a.lds_rows + a.lds_counts + 16 + 15) & ~15;
             clds = 1024 + kLutLds + (ccoop ? (size_t)a.lds_rows + (size_t)kWavesPerBlock * (ac.lds_wave - a.lds_rows)
@@ -1541,8 +1551,10 @@ static int upload_no_wait(const void* src, size_t n, void* dst, hipStream_t st) 
     next = (next + 1) % 4;
     int dev = 0;
     HIP_CHECK(hipGetDevice(&dev));
-    if (sl.ev && sl.dev == dev) HIP_CHECK(hipEventSynchronize(sl.ev));
-    if (sl.ev && sl.dev != dev) {   // a slot last used on another device: start it over
+    // the copy that last read the slot's buffer must be done before it is overwritten or freed --
+    // also when it ran on another device (then the slot starts over with an event of this one)
+    if (sl.ev) HIP_CHECK(hipEventSynchronize(sl.ev));
+    if (sl.ev && sl.dev != dev) {
         (void)hipEventDestroy(sl.ev);
         sl.ev = nullptr;
     }
@@ -1583,7 +1595,7 @@ static int frame_rdw_impl(const uint8_t* d_data, int64_t n_bytes, const int64_t*
     // 256 KiB chunks: every chunk pays one speculated entry, so C5's 16 KB records want few of them
     // (framing 21.1 / 2.30 / 1.59 / 1.23 / 1.10 ms at 16 / 64 / 128 / 256 / 512 KiB), while C4's
     // 65-byte records walk ~4,000 per chunk at no loss (4.02 / 3.97 / 3.96 / 4.11 ms at 64 / 128 /
-    // 256 / 512 KiB; same-box runs, tools/gpu_r04_chunk.sh)
+    // 256 / 512 KiB; same-box runs, tools/gpu.sh A/B)
     int64_t chunk = 256 * 1024;
     if (const char* e = getenv("CBX_RDW_CHUNK_BYTES")) chunk = std::max<int64_t>(8, atoll(e));   // tests: many chunks
     std::vector<int64_t> hs;

@@ -161,11 +161,15 @@ struct U8Ring {
     uint32_t head, tail;   // next allocation, oldest entry
     int np, first;         // pending entries, FIFO slot of the oldest
     uint32_t f_op, f_tile, f_off, f_tot;
+    uint32_t f_base;       // the entry's place when a batched probe resolved it (kU8NoBase: not yet)
 };
+
+constexpr uint32_t kU8NoBase = 0xFFFFFFFFu;
 
 __device__ __forceinline__ void u8_ring_init(U8Ring& r, uint32_t rb, uint32_t rw) {
     r.rb = rb; r.rw = rw; r.head = r.tail = 0; r.np = 0; r.first = 0;
     r.f_op = r.f_tile = r.f_off = r.f_tot = 0;
+    r.f_base = kU8NoBase;
 }
 
 // whether an entry of `need` bytes fits (contiguous: at the head or, wrapping, at the ring start)
@@ -187,7 +191,7 @@ __device__ __forceinline__ uint32_t u8_alloc(U8Ring& r, uint32_t need) {
 
 __device__ __forceinline__ void u8_push(U8Ring& r, int lane, int op, int64_t tile, uint32_t off, uint32_t tot) {
     const int slot = (r.first + r.np) & (kWave - 1);
-    if (lane == slot) { r.f_op = (uint32_t)op; r.f_tile = (uint32_t)tile; r.f_off = off; r.f_tot = tot; }
+    if (lane == slot) { r.f_op = (uint32_t)op; r.f_tile = (uint32_t)tile; r.f_off = off; r.f_tot = tot; r.f_base = kU8NoBase; }
     r.np++;
 }
 
@@ -410,20 +414,83 @@ __device__ __forceinline__ int64_t u8_place(const KernelArgs& a, const StrOp& op
     return (int64_t)acc + intra;
 }
 
+// The places of the oldest entries of one earlier round's tile (up to kU8Batch of the FIFO's head):
+// every probe of the batch -- the totals of the tiles before it in its block, the block totals B
+// and inclusive prefixes P of the 64 blocks before it -- is issued before any is waited on, so the
+// batch costs one memory round trip.  An entry whose answers are complete (every total it needs
+// published, a P within the window or the window reaching block 0) gets its place in f_base; the
+// others keep kU8NoBase and take the polling look-back (u8_place) when flushed.
+constexpr int kU8Batch = 4;
+
+__device__ __forceinline__ void u8_probe_lagged(const KernelArgs& a, U8Ring& r, int lane) {
+    const int64_t tile = u8_oldest_tile(r);
+    const int64_t blk = tile / kLbBlock;
+    const int k = (int)(tile & (kLbBlock - 1));
+    const int64_t bq = blk - 1 - lane;   // lane j: block blk - 1 - j
+    int seq[kU8Batch];
+    int m = 0;
+    for (; m < kU8Batch && m < r.np; m++) {
+        const int s = (r.first + m) & (kWave - 1);
+        if ((uint32_t)__builtin_amdgcn_readlane((int)r.f_tile, s) != (uint32_t)tile) break;
+        seq[m] = ldc(a.sops + __builtin_amdgcn_readlane((int)r.f_op, s)).seq;
+    }
+    uint64_t ga[kU8Batch], gb[kU8Batch], gq[kU8Batch];
+#pragma unroll
+    for (int e = 0; e < kU8Batch; e++) {
+        ga[e] = gb[e] = gq[e] = 0;
+        if (e < m) {
+            const uint64_t* pt = a.lb_tile + (int64_t)seq[e] * a.n_tiles + blk * kLbBlock;
+            const uint64_t* pb = a.lb_blk + (int64_t)seq[e] * a.lb_nblk * 2;
+            if (lane < k) ga[e] = lb_ld(pt + lane);
+            if (bq >= 0) {
+                gb[e] = lb_ld(pb + 2 * bq);
+                gq[e] = lb_ld(pb + 2 * bq + 1);
+            }
+        }
+    }
+    if (a.lb_force) return;
+#pragma unroll
+    for (int e = 0; e < kU8Batch; e++) {
+        if (e >= m) break;
+        const uint32_t tag = a.lb_tag;
+        const bool has_p = bq >= 0 && (uint32_t)(gq[e] >> 32) == tag;
+        const uint64_t pm = __ballot(has_p);
+        const int jp = pm ? (int)__builtin_ctzll(pm) : kWave;
+        const bool a_in = lane < k, b_in = bq >= 0 && lane < jp;
+        const bool bad = (a_in && (uint32_t)(ga[e] >> 32) != tag) || (b_in && (uint32_t)(gb[e] >> 32) != tag);
+        if (__ballot(bad) || (jp == kWave && blk > kWave)) continue;
+        const uint32_t v = (a_in ? (uint32_t)ga[e] : 0u) + (b_in ? (uint32_t)gb[e] : 0u);
+        const uint64_t base = (uint64_t)wave_sum32(v, lane) + (jp < kWave ? (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gq[e], jp) : 0u);
+        if (base < kU8NoBase && lane == ((r.first + e) & (kWave - 1))) r.f_base = (uint32_t)base;
+    }
+}
+
 // Flush the oldest pending entry: its place, the element's int32 offsets (place + tile-local start)
 // and the payload.  cur_tile: the tile the wave is composing (-1 after its last): an entry of the
-// same round looks back in sync mode.
+// same round looks back in sync mode; an entry of an earlier round first has its batch probed.
 __device__ __forceinline__ void u8_flush_oldest(const KernelArgs& a, U8Ring& r, int lane, int64_t cur_tile) {
+    const int64_t G = (int64_t)gridDim.x;
+    const int64_t tile0 = u8_oldest_tile(r);
+    const bool lagged = cur_tile < 0 || tile0 / G != cur_tile / G;
+    if (lagged && !(CBX_DIAG & 64) && (uint32_t)__builtin_amdgcn_readlane((int)r.f_base, r.first) == kU8NoBase)
+        u8_probe_lagged(a, r, lane);
     const int s = r.first;
     const int i = __builtin_amdgcn_readlane((int)r.f_op, s);
-    const int64_t tile = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)r.f_tile, s);
+    const int64_t tile = tile0;
     const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)r.f_off, s);
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)r.f_tot, s);
+    const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)r.f_base, s);
     const StrOp op = ldc(a.sops + i);
-    const int64_t G = (int64_t)gridDim.x;
     int64_t sync_blk = 0x7fffffffffffffffll;
-    if (cur_tile >= 0 && tile / G == cur_tile / G) sync_blk = (tile / G) * G / kLbBlock;
-    const int64_t base = u8_place(a, op, tile, lane, tot, sync_blk);
+    if (!lagged) sync_blk = (tile / G) * G / kLbBlock;
+    int64_t base;
+    if (fb != kU8NoBase) {
+        base = fb;
+        if ((tile & (kLbBlock - 1)) == kLbBlock - 1 && lane == 0)   // the block's inclusive prefix
+            lb_st(a.lb_blk + ((int64_t)op.seq * a.lb_nblk + tile / kLbBlock) * 2 + 1, lb_gran(a.lb_tag, (uint64_t)base + tot));
+    } else {
+        base = u8_place(a, op, tile, lane, tot, sync_blk);
+    }
     const uint32_t entry = r.rb + off;
     const uint32_t ex = lds_ld<uint16_t>(entry + 2u * (uint32_t)lane);
     const StrCall c = ldc(a.scall + i);
@@ -500,6 +567,8 @@ __device__ __forceinline__ void u8_loop(const KernelArgs& a, const U8Lds& l, int
     body.range(wid, lo, hi);
     U8Ring ring;
     u8_ring_init(ring, l.stage + (uint32_t)wid * (uint32_t)a.lb_ring, (uint32_t)a.lb_ring);
+    Stamps st;   // (diagnostic build: 0 stage, 1 barrier + prefetch, 2 compose, 3 flush, 4 block totals, 5 end barrier)
+    st.init();
     int64_t tile = (int64_t)blockIdx.x;
     const int64_t tstep = (int64_t)gridDim.x;
     if (tile < a.n_tiles) u8_issue<KP, NW>(a, contig_span(a, tile), wid, lane, buf);
@@ -514,21 +583,26 @@ __device__ __forceinline__ void u8_loop(const KernelArgs& a, const U8Lds& l, int
                 if (c < sp.nch) contig_put(a, sp, c, buf[v], l.img);
             }
         }
+        st.mark(0);
         __syncthreads();   // the tile's image complete
         const int64_t next = tile + tstep;
         u8_issue<KP, NW>(a, contig_span(a, next), wid, lane, buf);
+        st.mark(1);
         TileCtx t = tile_ctx<false>(a, tile, lane);
         const uint32_t rec0 = (uint32_t)(lane * a.cpitch + 4 * sp.mis_dw);
-        body.run(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, ring, tile);
+        body.run(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, ring, tile, st);
         u8_publish_b(a, lo, hi, tile, lane);
+        st.mark(4);
         __syncthreads();   // every wave done with the image
+        st.mark(5);
         tile = next;
     }
     // every pending entry (the last round's block totals are out)
 #ifndef U8_NO_FINAL
     TileCtx t0 = tile_ctx<false>(a, 0, lane);
-    body.run(a, t0, (const uint8_t*)l.img, 0u, l, lane, ring, -1);
+    body.run(a, t0, (const uint8_t*)l.img, 0u, l, lane, ring, -1, st);
 #endif
+    st.flush(a, lane);
 }
 
 }  // namespace cbx

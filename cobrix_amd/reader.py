@@ -1101,7 +1101,9 @@ class VarLenNestedReader(_BaseReader):
     def decode_device(self, d_data, n_bytes: int, rec_off, rec_len, first_record_id: int = 0,
                       stream=None, exact_strings: bool = False) -> DecodedBatch:
         """Decode framed records as one index entry starting at first_record_id, without the
-        selection stage (cbx_decode_var: Record_Id = first_record_id + r)."""
+        selection stage (cbx_decode_var: Record_Id = first_record_id + r).  The device-level entry
+        points leave with_input_file_name_col's column to the caller (`batch.input_file`); `read`
+        and `decode` set it from their input_file_name."""
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream()
         n_rec = int(rec_off.numel())
@@ -1236,9 +1238,16 @@ class VarLenNestedReader(_BaseReader):
             offsets[s] = o.cpu().numpy()
         return HierBatch(flat, table_rows, offsets, self.collapse_root, self.params.generate_record_id)
 
-    def _file_column(self, batch, input_file_name: str):
-        """with_input_file_name_col: the batch's file-name column (SimpleStream.inputFileName)."""
+    def _file_column(self, batch, input_file_name: Optional[str], check_only: bool = False):
+        """with_input_file_name_col: the batch's file-name column (SimpleStream.inputFileName).  The
+        schema lists the column whenever the option is set, so an entry point given no file name
+        refuses rather than return a batch without it (or with empty names)."""
         if self.params.input_file_name_column:
+            if not input_file_name:
+                raise ValueError(f"with_input_file_name_col = '{self.params.input_file_name_column}' needs the "
+                                 "input file's name (input_file_name=...)")
+            if check_only:
+                return batch
             batch.input_file = (self.params.input_file_name_column, input_file_name)
         return batch
 
@@ -1249,9 +1258,10 @@ class VarLenNestedReader(_BaseReader):
         order: the root record's groups, then each segment's children (extractChildren, :300-322).
         The records' own bytes give the same count when the dependee sits in the array's own segment and
         is not null there; otherwise (a dependee of the parent segment, of the common header, or a null
-        one) the count is the value of the last record BEFORE this one, in the same hierarchical record,
-        whose segment holds the dependee and gives it a value: same-type records are walked in record
-        order, and an ancestor of the array's segment is walked before its subtree.  Returns the counts
+        one) the count is the value of the last record BEFORE this one in the walk of the same
+        hierarchical record whose segment holds the dependee and gives it a value -- the walk's order,
+        not the file's: a sibling type's records come after the array's own subtree when the sibling
+        follows in the copybook, whatever their file positions.  Returns the counts
         where they differ from the first decode (int32 [n_arrays, rows], -1 elsewhere), or None."""
         torch = _torch()
         plan = self.plan
@@ -1277,6 +1287,28 @@ class VarLenNestedReader(_BaseReader):
                 break
             root_of = nxt
         off = rec_off.cpu().numpy()
+        # every row's place in the walk (extractHierarchicalRecord, RecordExtractors.scala:324-370): a
+        # hierarchical record's root, then per child type in copybook order (getParentToChildrenMap,
+        # CopybookParser.scala:702-727) each instance in record order followed by its own subtree -- a
+        # lexicographic order of the rows' paths (child type, record position) from the root
+        anc = [np.arange(n)]
+        while True:
+            up = np.where(anc[-1] >= 0, par[np.maximum(anc[-1], 0)], -1)
+            if not (up >= 0).any():
+                break
+            anc.append(up)
+        A = np.stack(anc)                                # A[k, x]: the k-th ancestor of row x (-1: none)
+        depth = (A >= 0).sum(axis=0) - 1                 # 0 for the roots
+        trank = np.array([order[id(g)] for g in segs], np.int64)
+        keys = []
+        for lvl in range(len(anc) - 1, 0, -1):           # deepest level first: np.lexsort's last key leads
+            k = depth - lvl
+            node = np.where(k >= 0, A[np.maximum(k, 0), np.arange(n)], -1)
+            keys.append(np.where(node >= 0, off[np.maximum(node, 0)], -1))
+            keys.append(np.where(node >= 0, trank[seg_row[np.maximum(node, 0)]], -1))
+        keys.append(root_of)
+        walk = np.empty(n, np.int64)
+        walk[np.lexsort(keys)] = np.arange(n)
         out = np.full((len(plan.arrays), n), -1, np.int32)
         changed = False
         for ai, ar in arrays:
@@ -1313,10 +1345,10 @@ class VarLenNestedReader(_BaseReader):
             else:
                 incl = df.segment == ar.segment and order[id(dcol.node)] < order[id(anode)]
                 ys = np.nonzero((seg_row == df.segment) & dok)[0]
-                key_y = root_of[ys].astype(np.int64) * (1 << 40) + off[ys]
+                key_y = walk[ys]
                 srt = np.argsort(key_y, kind="stable")
                 ys, key_y = ys[srt], key_y[srt]
-                key_x = root_of[xs].astype(np.int64) * (1 << 40) + off[xs]
+                key_x = walk[xs]
                 pos = np.searchsorted(key_y, key_x, side="right" if incl else "left") - 1
                 hit = (pos >= 0)
                 yy = ys[np.maximum(pos, 0)]
@@ -1332,10 +1364,11 @@ class VarLenNestedReader(_BaseReader):
                 changed = True
         return torch.as_tensor(out, device=parent_row.device) if changed else None
 
-    def read(self, data: bytes, file_id: int = 0, input_file_name: str = "") -> DecodedBatch:
+    def read(self, data: bytes, file_id: int = 0, input_file_name: Optional[str] = None) -> DecodedBatch:
         """A whole file, as the reference reads it: sparse-index entries (when index generation
         applies) each read by its own VarLenNestedIterator, concatenated in file order.
         input_file_name: the file's name for the with_input_file_name_col column."""
+        self._file_column(None, input_file_name, check_only=True)
         t = self._device_file(data)
         off, ln, vb = self.frame_file(t, len(data))
         if self.hierarchical:
@@ -1346,17 +1379,19 @@ class VarLenNestedReader(_BaseReader):
         sel = self.select(t, vb, off, ln, entries, file_id)
         return self._file_column(self.decode_selected(t, vb, sel), input_file_name)
 
-    def decode(self, data: bytes, seeds: Optional[Sequence[int]] = None, first_record_id: int = 0) -> DecodedBatch:
-        """Frame + decode as one entry (no selection stage)."""
+    def decode(self, data: bytes, seeds: Optional[Sequence[int]] = None, first_record_id: int = 0,
+               input_file_name: Optional[str] = None) -> DecodedBatch:
+        """Frame + decode as one entry (no selection stage).  input_file_name: as in `read`."""
+        self._file_column(None, input_file_name, check_only=True)
         t = self._device_file(data)
         if self.params.is_text or self.var_occurs_extractor() or (
                 self.params.record_length_field is not None and not self.params.is_record_sequence):
             # framings that are not seeded by RDW headers: text lines, VarOccursRecordExtractor,
             # record_length_field (VRLRecordReader.fetchRecordUsingRecordLengthField)
             off, ln, vb = self.frame_file(t, len(data))
-            return self.decode_device(t, vb, off, ln, first_record_id)
+            return self._file_column(self.decode_device(t, vb, off, ln, first_record_id), input_file_name)
         off, ln = self.frame(t, len(data), seeds) if self.params.is_record_sequence else self.frame_fixed(t, len(data))
-        return self.decode_device(t, len(data), off, ln, first_record_id)
+        return self._file_column(self.decode_device(t, len(data), off, ln, first_record_id), input_file_name)
 
     def get_row_iterator(self, data: bytes) -> Iterator[dict]:
         return iter(self.read(data).to_rows())

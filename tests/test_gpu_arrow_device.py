@@ -250,6 +250,8 @@ def test_device_export_input_file_column(gen_id):
     assert var_len
     rd = VarLenNestedReader(GC.copybook_text({"copybook": "test4_copybook.cob"}), p)
     data = GC.data_bytes({"data": "test4_data/COMP.DETAILS.SEP30.DATA.dat"})
+    with pytest.raises(ValueError, match="needs the input file's name"):
+        rd.read(data)
     batch = rd.read(data, input_file_name="COMP.DETAILS.SEP30.DATA.dat")
     from cobrix_amd import arrow_device as AD
     da, schema, kids = AD.export_device(batch)

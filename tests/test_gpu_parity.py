@@ -629,18 +629,64 @@ def test_wide_odo_forced_counts_vs_oracle(jit):
         assert (cnts == c).any()
 
 
+def _check_framing(off, ln, hdr, n_bytes):
+    """Every framed record against the generator's RDW header list: payload at header + 4, length up to
+    the next header (the file end for the last)."""
+    hdr = hdr.to(off.device)
+    assert off.numel() == hdr.numel(), (off.numel(), hdr.numel())
+    assert torch.equal(off, hdr + 4)
+    nxt = torch.cat([hdr[1:], torch.tensor([n_bytes], dtype=hdr.dtype, device=hdr.device)])
+    assert torch.equal(ln.to(torch.int64), nxt - hdr - 4)
+
+
+def test_rdw_narrow_full_size_framing_and_sample():
+    """C4 as the bench runs it: 150 M RDW records (9.8 GB) framed by cbx_frame_rdw from seeds at the
+    100 MB index spacing -- every record's offset and length equal to the generator's header list --
+    then decoded (string views, the bench's layout); 2,000 records sampled across the batch are
+    bit-exact against the oracle's decode of the same records."""
+    from parity import compare_sample
+    from cobrix_amd.synth import RDW_NARROW_COPYBOOK, RDW_NARROW_SEGMENTS, rdw_narrow_large
+    n = 150_000_000
+    raw_t, hdr = rdw_narrow_large(n, device="cuda")
+    n_bytes = int(raw_t.numel())
+    params = ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
+                              segment_id_redefine_map=RDW_NARROW_SEGMENTS, string_views=True)
+    rd = VarLenNestedReader(RDW_NARROW_COPYBOOK, params)
+    marks = torch.arange(0, n_bytes, 100 * 1024 * 1024, device="cuda")
+    seeds = torch.unique(hdr[torch.searchsorted(hdr, marks).clamp(max=n - 1)]).tolist()
+    off, ln = rd.frame(raw_t, n_bytes, seeds=seeds)
+    _check_framing(off, ln, hdr, n_bytes)
+    del hdr
+    torch.cuda.empty_cache()
+    batch = rd.decode_device(raw_t, n_bytes, off, ln)
+    assert batch.n_rec == n
+    rng = np.random.default_rng(13)
+    idx = np.unique(np.concatenate([np.arange(64), n - 64 + np.arange(64), rng.integers(0, n, 1872)]))
+    offs = off[torch.as_tensor(idx, device="cuda")].cpu().numpy()
+    lens = ln[torch.as_tensor(idx, device="cuda")].cpu().numpy()
+    recs = [raw_t[o:o + l].cpu().numpy().tobytes() for o, l in zip(offs, lens)]
+    segs = [{"C": "STATIC_DETAILS", "P": "CONTACTS"}.get(G.java_trim(r[:5].decode("cp037"))) for r in recs]
+    res = O.decode_records(rd.copybook, recs, active_segments=segs)
+    errs = compare_sample(batch, idx, res)
+    assert not errs, errs
+    del batch, raw_t, off, ln
+    torch.cuda.empty_cache()
+
+
 def test_wide_odo_full_size_sampled_parity():
     """C5 as the bench runs it (770,000 roots + children = 2.31 M records, 12.5 GB, list layout, the
-    specialised kernels): 2,000 records sampled across the batch -- counts, list offsets and every
-    present element -- bit-exact against the oracle's decode of the same records."""
+    specialised kernels): the framing against the generator's header list, then 2,000 records sampled
+    across the batch -- counts, list offsets and every present element -- bit-exact against the
+    oracle's decode of the same records."""
     from parity import compare_sample_lists, compare_sample
     from cobrix_amd.synth import WIDE_ODO_COPYBOOK, WIDE_ODO_SEGMENTS, wide_odo
-    raw_t, _ = wide_odo(770_000, seed=20261018, device="cuda")
+    raw_t, hdr = wide_odo(770_000, seed=20261018, device="cuda")
     params = ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID",
                               segment_id_redefine_map=WIDE_ODO_SEGMENTS, occurs_lists=True, string_views=True)
     rd = VarLenNestedReader(WIDE_ODO_COPYBOOK, params)
     n_bytes = int(raw_t.numel())
     off, ln = rd.frame(raw_t, n_bytes)
+    _check_framing(off, ln, hdr, n_bytes)
     batch = rd.decode_device(raw_t, n_bytes, off, ln)
     assert batch.n_rec > 2_000_000 and _kernel_kind(rd) in (1, 4)
     rng = np.random.default_rng(12)

@@ -88,3 +88,41 @@ def test_children_skip_record_start_offset():
     assert r["SEGMENT_ID"] == "P" and r["PARENT_SEG"]["P_NAME"] == "NAME"
     # the child group (offset 2) read from the child's byte 2 -- the start offset is not applied
     assert r["PARENT_SEG"]["CHILD_SEG"][0]["C_NAME"] == "C9A"
+
+
+SIBLING_COPYBOOK = """
+       01  REC.
+           05  SEGMENT-ID        PIC X(1).
+           05  PARENT-SEG.
+               10  P-CNT         PIC 9(1).
+               10  P-NAME        PIC X(3).
+           05  SIB-A REDEFINES PARENT-SEG.
+               10  A-CNT         PIC 9(1).
+               10  A-ITEMS OCCURS 0 TO 5 TIMES DEPENDING ON P-CNT.
+                   15  A-V       PIC X(2).
+           05  SIB-B REDEFINES PARENT-SEG.
+               10  B-CNT         PIC 9(1).
+               10  B-ITEMS OCCURS 0 TO 5 TIMES DEPENDING ON A-CNT.
+                   15  B-V       PIC X(1).
+               10  B-P OCCURS 0 TO 5 TIMES DEPENDING ON P-CNT.
+                   15  B-PV      PIC X(1).
+"""
+
+SIBLING_OPTS = {"is_record_sequence": "true", "segment_field": "SEGMENT_ID",
+                "redefine_segment_id_map:1": "PARENT-SEG => P", "redefine-segment-id-map:2": "SIB-A => A",
+                "redefine-segment-id-map:3": "SIB-B => B", "segment-children:1": "PARENT-SEG => SIB-A,SIB-B"}
+
+
+def test_sibling_dependees_follow_the_walk_not_the_file():
+    """Sibling segment types under one parent, B's array DEPENDING ON A's field, the B record placed
+    before the A record in the file: extractHierarchicalRecord walks the child types in copybook order
+    (RecordExtractors.scala:364-370, getParentToChildrenMap), so A is decoded first and B's B-ITEMS
+    sees A-CNT = 3 (by file order nothing would be registered yet: the maximum, 5)."""
+    p, _ = parse_options(SIBLING_OPTS)
+    data = rdw("P1ABC") + rdw("B2" + "x" * 10) + rdw("A3" + "yy" * 5)
+    rows = RO.var_len_rows(parse_copybook_for(SIBLING_COPYBOOK, p), data, p)
+    assert len(rows) == 1
+    par = rows[0]["REC"]["PARENT_SEG"]
+    (a,), (b,) = par["SIB_A"], par["SIB_B"]
+    assert a["A_CNT"] == 3 and len(a["A_ITEMS"]) == 1
+    assert b["B_CNT"] == 2 and len(b["B_ITEMS"]) == 3 and len(b["B_P"]) == 1

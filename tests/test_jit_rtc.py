@@ -238,17 +238,18 @@ def _utf8_onepass_kernel(n_str: int = 10, numerics: bool = False) -> str:
             nums += ("      { constexpr NumOp g[1] = {{" + str(20 * n_str) + ",0,8,2,0,0,0,0,0,10,0,-1,-1,0,0xffffffffffffffffull,0x0ull,"
                      "0x1ull,0x0ull,0x0ull,0x0ull,{0,0,0,0},{0,0,0,0}}}; num_group<0,8,false,1>(a, g, 0, t, img, rec_addr, l.cnt, lane, vw); }\n")
     body = ("    uint32_t todo = 0;\n    if (cur >= 0) { int lo = 0, hi = 0; range(l.wid, lo, hi); todo = (1u << (hi - lo)) - 1u; }\n"
-            "    bool num = cur < 0;\n    for (;;) {\n" + comp + "      }\n"
+            "    bool num = cur < 0;\n    for (;;) {\n" + comp + "      }\n      st.mark(2);\n"
             "      if (!todo && !num) {\n        num = true;\n" + nums + "        }\n      }\n"
             "      if (!todo && (ring.np == 0 || u8_oldest_tile(ring) == cur)) break;\n"
             "      if (todo && ring.np == 0) { if (lane == 0) atomicOr(a.status, 1); break; }\n"
-            "      u8_flush_oldest(a, ring, lane, cur);\n    }\n")
+            "      u8_flush_oldest(a, ring, lane, cur);\n      st.mark(3);\n    }\n")
     return ("#define CBX_STR_LAYOUT 2\n#define CBX_MODE 0\n#include \"cbx_utf8.h\"\nnamespace cbx {\nstruct JitU8Body {\n"
             "  __device__ __forceinline__ void range(int wid, int& lo, int& hi) const {\n" + rng + "  }\n"
             "  __device__ __forceinline__ void run(const KernelArgs& a, const TileCtx& t, const uint8_t* img, uint32_t rec_addr,\n"
-            "                                      const U8Lds& l, int lane, U8Ring& ring, int64_t cur) {\n    Stamps st;\n    DirectSink vw;\n"
+            "                                      const U8Lds& l, int lane, U8Ring& ring, int64_t cur, Stamps& st) {\n    DirectSink vw;\n"
             "    (void)img; (void)rec_addr;\n" + body + "  }\n};\n}  // namespace cbx\n"
-            "extern \"C\" __global__ __launch_bounds__(cbx::kWave * cbx::kU8Waves) void cbx_jit_utf8(cbx::KernelArgs a) {\n"
+            "extern \"C\" __global__ __launch_bounds__(cbx::kWave * cbx::kU8Waves) __attribute__((amdgpu_waves_per_eu(4))) "
+            "void cbx_jit_utf8(cbx::KernelArgs a) {\n"
             "  using namespace cbx;\n  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
             "  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);\n  const int lane = threadIdx.x % kWave;\n"
             "  if (!lds_base_ok(smem)) { if (threadIdx.x == 0) atomicOr(a.status, 4); return; }\n"

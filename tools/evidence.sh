@@ -1,14 +1,14 @@
 #!/bin/bash
-# Round-4 GPU evidence.  Usage: tools/gpu_r04.sh TAG [--no-tests] WORKLOAD[:extra bench args,comma-separated]...
+# A round's GPU evidence for the bench configurations.  Usage: tools/evidence.sh TAG [--no-tests] WORKLOAD[:extra bench args,comma-separated]...
 # 1. the -m gpu suite (unless --no-tests);
 # 2. per workload: the bench command itself under rocprofv3 --kernel-trace --stats (the JSON line and the
 #    kernel trace come from ONE process, so roofline.frac can be recomputed from the trace), then PMC
 #    passes of a 1-step run, one counter group per pass (FETCH_SIZE; WRITE_SIZE; two SQ groups);
-# 3. tools/prof_summary.py -> gpurun_out/r04_TAG/<workload>/summary.json.
+# 3. tools/prof_summary.py -> gpurun_out/TAG/<workload>/summary.json (copied into profiles/TAG/).
 set -u
 TAG=$1; shift
 ROOTDIR=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOTDIR/gpurun_out/r04_$TAG
+OUT=$ROOTDIR/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 cd $ROOTDIR

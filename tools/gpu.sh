@@ -7,7 +7,7 @@
 #   BENCH="W[:args] ..."                      short bench lines (5 steps, no CPU baseline / end-to-end);
 #                                             args comma-separated, e.g. synstr200:--records,50000000
 #   PROF="W[:args] ..."                       the bench under rocprofv3 --kernel-trace --stats (10 steps)
-#   PMC="W[:args] ..."                        FETCH/WRITE + SQ counter passes of a 1-step run (tools/gpu_r04.sh groups)
+#   PMC="W[:args] ..."                        FETCH/WRITE + SQ counter passes of a 1-step run (tools/evidence.sh groups)
 #   ENVS="K=V ..."                            exported before every step (A/B knobs)
 # Every GPU step has its own time limit and the script stops at the first failure.
 set -u

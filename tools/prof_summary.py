@@ -1,4 +1,4 @@
-"""Summary of one workload's round-3 GPU evidence (tools/gpu_r03.sh): the bench JSON line, the
+"""Summary of one workload's GPU evidence (tools/evidence.sh): the bench JSON line, the
 rocprofv3 kernel trace of the SAME process and the PMC passes of a 1-step run.
 
 * per kernel: calls, rocprof average over all calls, and the average over the timed steps only
