@@ -211,7 +211,9 @@ WORKLOADS = {
                            "-- BASELINE config C3 (64 GB strong-scaled over the job)",
                       data="synthetic (cobrix_amd/synth.py SYNSTR200: lengths 0-20, 25% accented, 10% leading "
                            "spaces, 1% control bytes)"),
-    "rdw_narrow": dict(records=150_000_000, config="C4", strings="views",
+    # C4 in the Utf8 layout (--strings offsets): batches whose int32 offsets fit the widest column's worst
+    # case (X(28) -> <= 56 UTF-8 bytes per value)
+    "rdw_narrow": dict(records=150_000_000, config="C4", strings="views", batch_records=37_500_000,
                        desc="RDW multisegment file, exp2/test5 layout (C 68 B / P 64 B records, segment redefines, "
                             "File_Id + Record_Id), GPU RDW offset discovery seeded by sparse-index entries + var-len "
                             "decode -- BASELINE config C4",
@@ -387,7 +389,7 @@ class _VarLen:
     RDW framing of the run seeded by its entries + (N > 1) one device all-gather of the run's record
     count, whose exclusive prefix is the run's Record_Id base + decode."""
 
-    def __init__(self, name, n_rec, dev, rank, world, window, strings, lists=True, seed_mb=100):
+    def __init__(self, name, n_rec, dev, rank, world, window, strings, lists=True, seed_mb=100, batch_records=0):
         import torch
         import torch.distributed as dist
         from cobrix_amd import native as N
@@ -403,6 +405,7 @@ class _VarLen:
             size = lambda b: synth.wide_odo_size(n_rec, seed=20261018 + b, device=dev)  # noqa: E731
             cb, segs = synth.WIDE_ODO_COPYBOOK, synth.WIDE_ODO_SEGMENTS
         self.dev, self.world, self.rank = dev, world, rank
+        self.batch = batch_records
         L = N.load()
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         opts = dict(is_record_sequence=True, segment_field="SEGMENT-ID", segment_id_redefine_map=segs,
@@ -508,8 +511,17 @@ class _VarLen:
         self.sd = (ctypes.c_int64 * len(self.seeds))(*self.seeds)
         self.state = torch.zeros(3, dtype=torch.int64, device=self.dev)   # cbx_frame_rdw_async outcome
         self.n_rec = self.n_expected
-        self.cols, self.cs = _alloc_columns(self.rd.plan, self.n_rec, string_capacity(self.rd.native, self.n_rec),
-                                            self.dev)
+        # parts: (first record, records, columns, cbx_column table) per decode call -- the Utf8 layout
+        # decodes the run in batches whose int32 offsets fit (one Arrow array per batch and column)
+        self.batch = self.batch if 0 < self.batch < self.n_rec else max(1, self.n_rec)
+        self.parts = []
+        for r0 in range(0, max(1, self.n_rec), self.batch):
+            m = min(self.batch, self.n_rec - r0)
+            cols, cs = _alloc_columns(self.rd.plan, m, string_capacity(self.rd.native, m), self.dev)
+            self.parts.append((r0, m, cols, cs))
+        self.cols, self.cs = self.parts[0][2], self.parts[0][3]
+        if len(self.parts) > 1:
+            self.shard_note += f"; decoded in {len(self.parts)} batches of <= {self.batch} records"
         self.fr0, self.fr1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # the run's Record_Id base lives on the device: the decode kernels read it (cbx_plan_set_record_base)
         self.base = torch.zeros(1, dtype=torch.int64, device=self.dev)
@@ -530,9 +542,20 @@ class _VarLen:
         if world > 1:   # Record_Id base = exclusive prefix of the ranks' counts, computed on the device
             _all_gather_into(self.gathered, self.state[:1])
             self.base.copy_(self.gathered[: self.rank].sum().view(1))
-        N.check(self.L.cbx_decode_var(self.h, self.raw.data_ptr(), self.in_bytes, self.off.data_ptr(),
-                                      self.ln.data_ptr(), self.n_rec, 0, 0, self.cs, self.stream))
+        for r0, m, _, cs in self.parts:
+            N.check(self.L.cbx_decode_var(self.h, self.raw.data_ptr(), self.in_bytes, self.off.data_ptr() + 8 * r0,
+                                          self.ln.data_ptr() + 4 * r0, m, 0, r0, cs, self.stream))
         return (self.fr0, self.fr1)
+
+    def calls_per_step(self) -> int:
+        return len(self.parts)
+
+    def part_bytes(self, i: int) -> int:
+        """Input bytes of part i's records (payloads + their 4-byte RDW headers), from the framing."""
+        r0, m, _, _ = self.parts[i]
+        if len(self.parts) == 1:
+            return self.in_bytes
+        return int(self.ln[r0:r0 + m].to(dtype=self.off.dtype).sum().item()) + 4 * m
 
     def verify(self, world):
         """After timing: the device base equals the records before this run in the setup framing, and
@@ -544,9 +567,11 @@ class _VarLen:
         if nfr.value != self.n_expected:
             raise RuntimeError(f"framing found {nfr.value} records, the index run holds {self.n_expected}")
         got = int(self.base.item()) if world > 1 else 0
-        rid = self.cols[self.rd.plan.record_id_column]["values"][: max(1, self.n_rec)]
-        first = int(rid[0].item()) if self.n_rec else got
-        last = int(rid[self.n_rec - 1].item()) if self.n_rec else got - 1
+        rid0 = self.parts[0][2][self.rd.plan.record_id_column]["values"]
+        r0, m, cols, _ = self.parts[-1]
+        rid1 = cols[self.rd.plan.record_id_column]["values"]
+        first = int(rid0[0].item()) if self.n_rec else got
+        last = int(rid1[m - 1].item()) if self.n_rec else got - 1
         torch.cuda.synchronize()
         ok = got == self.expected_base and first == got and last == got + self.n_rec - 1
         return {"record_id_base": got, "expected": self.expected_base, "ok": ok}
@@ -866,7 +891,7 @@ def main():
         job = _Fixed(args.workload, n_req, dev, rank, args.window, strings, batch, rec_base)
     else:
         job = _VarLen(args.workload, n_req, dev, rank, world, args.window, strings, args.occurs == "lists",
-                      args.seed_mb)
+                      args.seed_mb, batch)
     st = torch.cuda.current_stream()
     progress(f"{job.in_bytes / 1e9:.2f} GB on this rank; allocating columns")
     job.prepare(st)
@@ -921,10 +946,10 @@ def main():
     parts = getattr(job, "parts", None) or [(0, n_rec, job.cols, None)]
     alg = lay = absent = 0
     has_lists = any(c.list_array >= 0 for c in plan.columns)
-    for _, m, cols, _ in parts:
+    for i, (_, m, cols, _) in enumerate(parts):
         present = present_elements(plan, cols, m)
         payload = string_payload(plan, cols, m)
-        in_b = m * job.stride if len(parts) > 1 else job.in_bytes
+        in_b = job.part_bytes(i) if hasattr(job, "part_bytes") else m * job.stride if len(parts) > 1 else job.in_bytes
         alg += algorithmic_bytes(plan, m, in_b, payload, present)
         lay += layout_bytes(plan, cols, m, in_b, payload, present)
         # OCCURS lists: the 8(d) input term counts every record byte, absent ODO elements included;

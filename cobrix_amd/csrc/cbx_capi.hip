@@ -1058,6 +1058,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
                                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&cocc, decode_kernel, kWave * kWavesPerBlock, clds);
         int cbpc = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / clds));
         if (ce2 == hipSuccess && cocc > 0) cbpc = std::min(cbpc, cocc);
+        if (const char* e = getenv("CBX_MAX_BLOCKS_PER_CU")) cbpc = std::max(1, std::min(cbpc, atoi(e)));   // tuning
         const int64_t cneeded = ccoop ? n_tiles : (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
         const int64_t cgrid = std::min<int64_t>(cneeded, (int64_t)P->num_cus * cbpc);
         if (cfn) {

@@ -211,6 +211,73 @@ __device__ __forceinline__ uint64_t le32_ending_ptr(const uint8_t* e) {
     return (uint64_t)align_bytes(p[1], p[0], sh) << 32;
 }
 
+// The lane's element bytes as whole aligned 8-byte words: ds_read_b64 of lanes 8 bytes apart
+// (an 8-byte element stride) covers one 256-byte bank row per 32 lanes -- no bank conflict, where
+// the per-field dword reads of lanes 8 bytes apart put two lanes on every ds_read_b32 bank (C5's
+// list kernel: SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS 4.0) and read each dword once per field.
+// Words K0 .. K0 + NW - 1 around el's 8-byte aligned address (K0 <= 0: bytes before the element);
+// ph: el's byte phase in its word.  d holds 2 NW dwords + 2 zero dwords (selects past the end).
+template <int K0, int NW>
+__device__ __forceinline__ void list_words(const uint8_t* el, uint32_t& ph, uint32_t (&d)[2 * NW + 2]) {
+    const uint32_t a = lds_addr(el);
+    ph = a & 7u;
+    const uint32_t a8 = (a & ~7u) + (uint32_t)(8 * K0);
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+        // (each word its own ds_read_b64: 2 LDS cycles, conflict-free; the pair merged into one
+        // ds_read2_b64 would take 8 -- MI355X_MICROARCH.md LDS table)
+        uint32_t ak = a8 + 8u * (uint32_t)k;
+        if (k) asm volatile("" : "+v"(ak));
+        const uint64_t w = lds_ld<uint64_t>(ak);
+        d[2 * k] = (uint32_t)w;
+        d[2 * k + 1] = (uint32_t)(w >> 32);
+    }
+    d[2 * NW] = d[2 * NW + 1] = 0u;
+}
+
+// The 8 bytes at window byte C + ph (C: a compile-time offset, ph: the lane's phase 0..7) as a
+// little-endian u64: dword j = (C + ph) / 4 is one of three candidates, picked by selects.
+template <int C, int NW>
+__device__ __forceinline__ uint64_t list_win8(const uint32_t (&d)[2 * NW + 2], uint32_t ph) {
+    static_assert(C >= 0 && (C + 7) / 4 + 2 <= 2 * NW + 1, "element window too small");
+    constexpr int J = C / 4;
+    const uint32_t o = (uint32_t)C + ph;
+    const uint32_t j = o >> 2, sh = o & 3u;
+    uint32_t x0 = d[J], x1 = d[J + 1], x2 = d[J + 2];
+    if (j >= (uint32_t)J + 1) { x0 = d[J + 1]; x1 = d[J + 2]; x2 = d[J + 3 < 2 * NW + 2 ? J + 3 : 2 * NW + 1]; }
+    if (j >= (uint32_t)J + 2) { x0 = d[J + 2]; x1 = d[J + 3 < 2 * NW + 2 ? J + 3 : 2 * NW + 1]; x2 = d[J + 4 < 2 * NW + 2 ? J + 4 : 2 * NW + 1]; }
+    return ((uint64_t)align_bytes(x2, x1, sh) << 32) | align_bytes(x1, x0, sh);
+}
+
+// list_jit_field from the element's words: E = the field's end within the element, K0 the window's
+// first word (list_words).
+template <int V, int W, bool SMALL, int E, int K0, int NW>
+__device__ __forceinline__ void list_jit_field_w(const NumOp& op, const DevColumn& col, const uint32_t (&d)[2 * NW + 2],
+                                                 uint32_t ph, int64_t cstart, bool present, int lane, bool& deferred) {
+    // SMALL: a field of <= 4 bytes of the BCD8 / BIN8 / FP decoders, its bytes in the high half
+    uint64_t r1;
+    if constexpr (SMALL) r1 = list_win8<E - 4 - 8 * K0, NW>(d, ph) << 32;
+    else r1 = list_win8<E - 8 - 8 * K0, NW>(d, ph);
+    uint64_t r0 = 0ull;
+    if constexpr (V == V_BCD16 || V == V_ZONED16) r0 = list_win8<E - 16 - 8 * K0, NW>(d, ph);
+    bool slow = false;
+    Val x;
+    if (V == V_BCD8) x = bcd8_raw<W>(op, r1);
+    else if (V == V_BCD16) x = bcd16_raw<W>(op, r1, r0);
+    else if (V == V_BIN8) x = bin8_raw<W>(op, r1);
+    else if (V == V_ZONED16) x = zoned16_raw<W>(op, r1, r0, slow);
+    else x = fp_raw(op, r1);
+    if (V == V_ZONED16) {
+        slow &= present;
+        deferred |= __ballot(slow) != 0;
+        x.valid &= !slow;
+    }
+    x.valid &= present;
+    store_w<W>(col.values, cstart >> 6, lane, x, op.out_type);
+    const uint64_t vm = __ballot(x.valid);
+    gp(col.validity)[cstart >> 6] = vm;
+}
+
 template <int V, int W>
 __device__ __forceinline__ void list_jit_field(const NumOp& op, const DevColumn& col, const uint8_t* e, int64_t cstart,
                                                bool present, int lane, bool& deferred) {

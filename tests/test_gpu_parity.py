@@ -701,3 +701,30 @@ def test_wide_odo_full_size_sampled_parity():
     assert not errs, errs
     del batch, raw_t
     torch.cuda.empty_cache()
+
+
+def test_var_utf8_batches_vs_oracle():
+    """C4 in the Arrow Utf8 layout decoded in batches whose int32 offsets fit (bench.py --strings
+    offsets: one Arrow array per batch and column): each batch of framed records -- cut mid-run, at
+    ragged sizes -- is bit-exact against the oracle, and its Record_Id continues from the batch's
+    first record."""
+    from cobrix_amd.synth import RDW_NARROW_COPYBOOK, RDW_NARROW_SEGMENTS, rdw_narrow
+    raw_t, _ = rdw_narrow(200_003, seed=31)
+    raw = raw_t.numpy().tobytes()
+    params = ReaderParameters(is_record_sequence=True, segment_field="SEGMENT-ID", generate_record_id=True,
+                              segment_id_redefine_map=RDW_NARROW_SEGMENTS, string_utf8=True)
+    rd = VarLenNestedReader(RDW_NARROW_COPYBOOK, params)
+    t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+    off, ln = rd.frame(t, len(raw))
+    eo, el = O.frame_rdw(raw)
+    assert np.array_equal(off.cpu().numpy(), eo)
+    n = len(eo)
+    cuts = [0, 64_000, 64_001, 131_072 + 37, n]
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        batch = rd.decode_device(t, len(raw), off[r0:r1], ln[r0:r1], first_record_id=r0)
+        recs = [raw[o:o + l] for o, l in zip(eo[r0:r1], el[r0:r1])]
+        segs = [{"C": "STATIC_DETAILS", "P": "CONTACTS"}.get(G.java_trim(r[:5].decode("cp037"))) for r in recs]
+        errs = compare_batch(batch, O.decode_records(rd.copybook, recs, active_segments=segs))
+        assert not errs, (r0, errs)
+        rid = batch.cols[rd.plan.record_id_column]["values"][: r1 - r0].cpu().numpy()
+        assert np.array_equal(rid, np.arange(r0, r1)), r0

@@ -157,11 +157,23 @@ def test_record_kernel_compiles_with_hiprtc(layout, count, loop, pair, coop, com
     assert not err, err[:3000]
 
 
+# the element's fields from aligned 8-byte words (list_words / list_jit_field_w: C5's element of a
+# 4-byte binary + a 4-byte COMP-3 field, 8-byte stride)
+LIST_KERNEL_WORDS = LIST_KERNEL.replace(
+    "        list_jit_field<3, 4>(op0, c0, el + 4, r.rstart + cb, cb + lane < r.rlen, lane, deferred);\n",
+    "        uint32_t ph, d[6];\n        list_words<0, 2>(el, ph, d);\n"
+    "        list_jit_field_w<3, 4, true, 4, 0, 2>(op0, c0, d, ph, r.rstart + cb, cb + lane < r.rlen, lane, deferred);\n"
+    "        list_jit_field_w<1, 8, true, 8, 0, 2>(op0, c0, d, ph, r.rstart + cb, cb + lane < r.rlen, lane, deferred);\n")
+
+
+@pytest.mark.parametrize("words", [False, True])
 @pytest.mark.parametrize("compiler", range(2), ids=["rocm", "torch"])
-def test_list_kernel_compiles_with_hiprtc(compiler):
+def test_list_kernel_compiles_with_hiprtc(compiler, words):
     if compiler >= len(COMPILERS):
         pytest.skip("no second hipRTC")
-    err = _compile(LIST_KERNEL, COMPILERS[compiler])
+    src = LIST_KERNEL_WORDS if words else LIST_KERNEL
+    assert words == ("list_words" in src)
+    err = _compile(src, COMPILERS[compiler])
     assert not err, err[:3000]
 
 
