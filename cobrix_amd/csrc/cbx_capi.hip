@@ -2291,6 +2291,53 @@ extern "C" int cbx_hier_list_offsets(const int64_t* d_parent_row, int64_t child_
     return CBX_OK;
 }
 
+extern "C" int cbx_hier_dependee_counts(const cbx_hier_walk* walk, const cbx_hier_dependee* deps, int32_t n_deps,
+                                        const cbx_hier_odo_array* arrays, int32_t n_arrays, int32_t* d_counts, int64_t pitch,
+                                        int32_t* d_changed, void* stream) {
+    if (!walk || n_deps < 0 || n_deps > CBX_HIER_MAX_DEPS || n_arrays < 0 || n_arrays > CBX_HIER_MAX_DEPS ||
+        (n_deps && !deps) || (n_arrays && !arrays) || !d_changed || pitch < 0 || (n_arrays && !d_counts) ||
+        walk->n_segments < 1 || walk->n_segments > CBX_HIER_MAX_SEG || walk->root_segment < 0 ||
+        walk->root_segment >= walk->n_segments)
+        return fail(CBX_E_ARGUMENT, "cbx_hier_dependee_counts: invalid arguments");
+    HierDepArgs a{};
+    a.w = *walk;
+    a.n_deps = n_deps;
+    a.n_arrays = n_arrays;
+    for (int i = 0; i < n_deps; i++) {
+        const int ot = deps[i].out_type;
+        if (!deps[i].values || !deps[i].validity || (ot != CBX_O_I32 && ot != CBX_O_I64 && ot != CBX_O_DEC128))
+            return fail(CBX_E_ARGUMENT, "cbx_hier_dependee_counts: a dependee column must be I32, I64 or DEC128");
+        a.dep[i] = deps[i];
+    }
+    for (int i = 0; i < n_arrays; i++) {
+        if (arrays[i].dependee < 0 || arrays[i].dependee >= n_deps)
+            return fail(CBX_E_ARGUMENT, "cbx_hier_dependee_counts: array dependee out of range");
+        a.arr[i] = arrays[i];
+    }
+    // every event names a known dependee / array, every child segment has its offsets
+    for (int s = 0; s <= CBX_HIER_MAX_SEG; s++)
+        for (int k = 0; k < CBX_HIER_MAX_EVENTS; k++) {
+            const int e = walk->events[s][k];
+            if (e == -32768) break;
+            if ((e >= 0 && e >= n_deps) || (e < 0 && -e - 1 >= n_arrays))
+                return fail(CBX_E_ARGUMENT, "cbx_hier_dependee_counts: event out of range");
+        }
+    for (int s = 0; s < walk->n_segments; s++)
+        for (int k = 0; k < CBX_HIER_MAX_SEG && walk->children[s][k] >= 0; k++) {
+            const int c = walk->children[s][k];
+            if (c >= walk->n_segments || !walk->child_offsets[c])
+                return fail(CBX_E_ARGUMENT, "cbx_hier_dependee_counts: child segment without list offsets");
+        }
+    hipStream_t st = (hipStream_t)stream;
+    HIP_CHECK(hipMemsetAsync(d_changed, 0, sizeof(int32_t), st));
+    const int64_t n = walk->table_rows[0];
+    if (n > 0) {
+        hipLaunchKernelGGL(hier_dep_kernel, dim3(blocks_for(n, 64)), dim3(64), 0, st, a, d_counts, pitch, d_changed);
+        HIP_CHECK(hipGetLastError());
+    }
+    return CBX_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // The record walk: node tables (cbx_plan_set_walk) and VarOccursRecordExtractor framing.
 // ---------------------------------------------------------------------------------------------

@@ -251,4 +251,81 @@ __global__ void hier_offsets_kernel(const int64_t* parent_row, int64_t child_beg
     offsets[k] = (int32_t)lo;
 }
 
+// ---- the shared dependFields map (cbx_hier_dependee_counts) ----
+// One thread per hierarchical record (root row r): the reference's recursive walk as an explicit
+// stack of (row, segment, child-type cursor, child-row range), each row's events replayed in field
+// order -- registrations into the thread's map (value + known bit per dependee), resolutions into
+// the counts.  Trees are small (a root and its children): the walk is a few dependent loads per row.
+static_assert(kHierMaxSeg == CBX_HIER_MAX_SEG, "hierarchical segment limit");
+
+struct HierDepArgs {
+    cbx_hier_walk w;
+    cbx_hier_dependee dep[CBX_HIER_MAX_DEPS];
+    cbx_hier_odo_array arr[CBX_HIER_MAX_DEPS];
+    int32_t n_deps, n_arrays;
+};
+
+__device__ __forceinline__ void hier_dep_events(const HierDepArgs& a, int ev_row, int64_t x, bool root, int32_t* regv,
+                                                uint32_t& regok, int32_t* counts, int64_t pitch, int32_t* changed) {
+    for (int k = 0; k < CBX_HIER_MAX_EVENTS; k++) {
+        const int e = a.w.events[ev_row][k];
+        if (e == -32768) break;
+        if (e >= 0) {
+            const cbx_hier_dependee& d = a.dep[e];
+            if (!((d.validity[x >> 6] >> (x & 63)) & 1ull)) continue;   // a null value registers nothing
+            int32_t v;
+            if (d.out_type == CBX_O_I32) v = ((const int32_t*)d.values)[x];
+            else if (d.out_type == CBX_O_I64) v = (int32_t)((const int64_t*)d.values)[x];
+            else v = (int32_t)((const int64_t*)d.values)[2 * x];   // DEC128: the low 64 bits (intValue)
+            regv[e] = v;
+            regok |= 1u << e;
+        } else {
+            const cbx_hier_odo_array& A = a.arr[-e - 1];
+            const int dd = A.dependee;
+            const int32_t v = regv[dd];
+            const int32_t c = ((regok >> dd) & 1u) && v >= A.min_count && v <= A.max_count ? v : A.max_count;
+            counts[(int64_t)A.out_row * pitch + x] = root ? -1 : c;
+            if (!root && A.first_counts && A.first_counts[x] != c) *changed = 1;
+        }
+    }
+}
+
+__global__ void hier_dep_kernel(HierDepArgs a, int32_t* counts, int64_t pitch, int32_t* changed) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.w.table_rows[0]) return;
+    int32_t regv[CBX_HIER_MAX_DEPS];
+    uint32_t regok = 0;
+    for (int k = 0; k < CBX_HIER_MAX_DEPS; k++) regv[k] = 0;
+    // stack frames: row, segment, next child type (index into children[seg]), child rows [lo, hi)
+    int64_t f_row[kHierMaxSeg + 1], f_lo[kHierMaxSeg + 1], f_hi[kHierMaxSeg + 1];
+    int f_seg[kHierMaxSeg + 1], f_ci[kHierMaxSeg + 1];
+    const int root = a.w.root_segment;
+    hier_dep_events(a, CBX_HIER_MAX_SEG, r, true, regv, regok, counts, pitch, changed);
+    hier_dep_events(a, root, r, true, regv, regok, counts, pitch, changed);
+    int d = 0;
+    f_row[0] = r; f_seg[0] = root; f_ci[0] = -1; f_lo[0] = f_hi[0] = 0;
+    while (d >= 0) {
+        if (f_lo[d] < f_hi[d]) {   // the next child row of the current type: visit it, then its subtree
+            const int c = a.w.children[f_seg[d]][f_ci[d]];
+            const int64_t x = a.w.table_base[1 + c] + f_lo[d]++;
+            hier_dep_events(a, c, x, false, regv, regok, counts, pitch, changed);
+            if (d + 1 <= kHierMaxSeg) {
+                d++;
+                f_row[d] = x; f_seg[d] = c; f_ci[d] = -1; f_lo[d] = f_hi[d] = 0;
+            }
+            continue;
+        }
+        // the next child type of the row
+        const int s = f_seg[d];
+        const int ci = ++f_ci[d];
+        const int c = ci < kHierMaxSeg ? a.w.children[s][ci] : -1;
+        if (c < 0) { d--; continue; }
+        // the row's index in its own table (the child's list offsets run over it)
+        const int64_t pt = s == root ? 0 : 1 + s;
+        const int64_t k = f_row[d] - a.w.table_base[pt];
+        f_lo[d] = a.w.child_offsets[c][k];
+        f_hi[d] = a.w.child_offsets[c][k + 1];
+    }
+}
+
 }  // namespace cbx

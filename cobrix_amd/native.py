@@ -43,8 +43,8 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
                     "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs",
                     "cbx_plan_set_record_base", "cbx_frame_length_field", "cbx_plan_set_odo_counts",
-                    "cbx_plan_lookback_stats")
-ABI_VERSION = 13
+                    "cbx_plan_lookback_stats", "cbx_hier_dependee_counts")
+ABI_VERSION = 14
 
 
 class NativeLibraryError(RuntimeError):
@@ -150,6 +150,29 @@ class CbxHierParams(ctypes.Structure):
                 ("start_offset", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+CBX_HIER_MAX_SEG, CBX_HIER_MAX_EVENTS, CBX_HIER_MAX_DEPS = 16, 32, 16
+HIER_EVENT_END = -32768
+
+
+class CbxHierDependee(ctypes.Structure):
+    _fields_ = [("values", ctypes.c_void_p), ("validity", ctypes.c_void_p), ("out_type", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class CbxHierOdoArray(ctypes.Structure):
+    _fields_ = [("dependee", ctypes.c_int32), ("out_row", ctypes.c_int32), ("min_count", ctypes.c_int32),
+                ("max_count", ctypes.c_int32), ("first_counts", ctypes.c_void_p)]
+
+
+class CbxHierWalk(ctypes.Structure):
+    _fields_ = [("n_segments", ctypes.c_int32), ("root_segment", ctypes.c_int32),
+                ("table_base", ctypes.c_int64 * (CBX_HIER_MAX_SEG + 1)),
+                ("table_rows", ctypes.c_int64 * (CBX_HIER_MAX_SEG + 1)),
+                ("child_offsets", ctypes.c_void_p * CBX_HIER_MAX_SEG),
+                ("children", (ctypes.c_int8 * CBX_HIER_MAX_SEG) * CBX_HIER_MAX_SEG),
+                ("events", (ctypes.c_int16 * CBX_HIER_MAX_EVENTS) * (CBX_HIER_MAX_SEG + 1))]
+
+
 _lib = None
 
 
@@ -199,7 +222,8 @@ def load():
                      ("cbx_frame_var_occurs", [P, P, i64, i64, P, P, i64, P, P, P]),
                      ("cbx_plan_set_record_base", [P, P]),
                      ("cbx_frame_length_field", [P, P, i64, i32, i32, i32, i32, P, P, i64, P, P]),
-                     ("cbx_plan_set_odo_counts", [P, P, i64])):
+                     ("cbx_plan_set_odo_counts", [P, P, i64]),
+                     ("cbx_hier_dependee_counts", [P, P, i32, P, i32, P, i64, P, P])):
         if hasattr(L, name):   # (diagnostic builds of older revisions lack the newest entry points)
             getattr(L, name).argtypes = at
     if L.cbx_abi_version() != ABI_VERSION:

@@ -1202,7 +1202,6 @@ class VarLenNestedReader(_BaseReader):
                                   ctypes.byref(prm), ctypes.byref(cs), parent_row.data_ptr(), rows, ctypes.byref(n_rows), sp))
         table_rows = [int(x) for x in rows]
         sel["n"], sel["struct"] = n_rows.value, cs
-        rec_off0 = sel["rec_off"][: n_rows.value].clone()   # record order (before any start-offset shift)
         s0 = self.params.start_offset
         if s0 and n_rows.value > table_rows[0]:
             # extractHierarchicalRecord decodes the root record from offsetBytes = record_start_offset
@@ -1217,7 +1216,18 @@ class VarLenNestedReader(_BaseReader):
             kid_off -= s0
             sel["rec_len"][table_rows[0]:n_rows.value] += s0
         flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
-        odo = self._hier_dependee_counts(flat, table_rows, parent_row, rec_off0, prm.root_segment)
+        # every child segment's list offsets over its parent table (device)
+        base = np.concatenate([[0], np.cumsum(table_rows)]).astype(np.int64)
+        d_offsets: Dict[int, Any] = {}
+        for s, g in enumerate(segs):
+            if g.parent_segment is None:
+                continue
+            ps = segs.index(g.parent_segment)
+            pb, pn = (0, table_rows[0]) if g.parent_segment.parent_segment is None else (int(base[1 + ps]), table_rows[1 + ps])
+            o = torch.empty(pn + 1, dtype=torch.int32, device=dev)
+            N.check(L.cbx_hier_list_offsets(parent_row.data_ptr(), int(base[1 + s]), table_rows[1 + s], pb, pn, o.data_ptr(), sp))
+            d_offsets[s] = o
+        odo = self._hier_dependee_counts(flat, table_rows, d_offsets, prm.root_segment, st)
         if odo is not None:
             # arrays whose count comes from a dependee another segment of the hierarchical record
             # registered: decode again with those counts
@@ -1226,16 +1236,7 @@ class VarLenNestedReader(_BaseReader):
                 flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
             finally:
                 N.check(L.cbx_plan_set_odo_counts(self.native.handle, None, 0))
-        base = np.concatenate([[0], np.cumsum(table_rows)]).astype(np.int64)
-        offsets: Dict[int, np.ndarray] = {}
-        for s, g in enumerate(segs):
-            if g.parent_segment is None:
-                continue
-            ps = segs.index(g.parent_segment)
-            pb, pn = (0, table_rows[0]) if g.parent_segment.parent_segment is None else (int(base[1 + ps]), table_rows[1 + ps])
-            o = torch.empty(pn + 1, dtype=torch.int32, device=dev)
-            N.check(L.cbx_hier_list_offsets(parent_row.data_ptr(), int(base[1 + s]), table_rows[1 + s], pb, pn, o.data_ptr(), sp))
-            offsets[s] = o.cpu().numpy()
+        offsets = {s: o.cpu().numpy() for s, o in d_offsets.items()}
         return HierBatch(flat, table_rows, offsets, self.collapse_root, self.params.generate_record_id)
 
     def _file_column(self, batch, input_file_name: Optional[str], check_only: bool = False):
@@ -1251,18 +1252,18 @@ class VarLenNestedReader(_BaseReader):
             batch.input_file = (self.params.input_file_name_column, input_file_name)
         return batch
 
-    def _hier_dependee_counts(self, flat: DecodedBatch, table_rows: List[int], parent_row, rec_off, root_seg: int):
+    def _hier_dependee_counts(self, flat: DecodedBatch, table_rows: List[int], child_offsets, root_seg: int, stream):
         """extractHierarchicalRecord shares ONE dependFields map between the segments of a hierarchical
         record (RecordExtractors.scala:224-245): a DEPENDING ON field registers its value when a record's
         group holding it is decoded, and an array reads the value registered last -- in the walk's
-        order: the root record's groups, then each segment's children (extractChildren, :300-322).
-        The records' own bytes give the same count when the dependee sits in the array's own segment and
-        is not null there; otherwise (a dependee of the parent segment, of the common header, or a null
-        one) the count is the value of the last record BEFORE this one in the walk of the same
-        hierarchical record whose segment holds the dependee and gives it a value -- the walk's order,
-        not the file's: a sibling type's records come after the array's own subtree when the sibling
-        follows in the copybook, whatever their file positions.  Returns the counts
-        where they differ from the first decode (int32 [n_arrays, rows], -1 elsewhere), or None."""
+        order (:324-370): the root record's groups, then per child segment in copybook order each child
+        record followed by its own subtree.  The records' own bytes give the same count when the
+        dependee sits in the array's own segment and is not null there; otherwise (a dependee of the
+        parent segment, of a sibling segment walked earlier, of the common header, or a null one) the
+        count is the value registered last in the walk.  Resolved on the device
+        (cbx_hier_dependee_counts: one thread per hierarchical record replays the walk's events);
+        returns the counts (int32 [n_arrays, rows], -1 where the first decode's own count stands)
+        when some differ from the first decode, else None."""
         torch = _torch()
         plan = self.plan
         arrays = [(ai, ar) for ai, ar in enumerate(plan.arrays) if ar.dependee >= 0 and ar.segment >= 0]
@@ -1278,39 +1279,9 @@ class VarLenNestedReader(_BaseReader):
         dfs(self.copybook.ast)
         segs = plan.segment_groups
         root_pos = order[id(segs[root_seg])]
-        seg_row = np.repeat(np.array([root_seg] + list(range(len(segs))), np.int64), table_rows)
-        par = parent_row[:n].cpu().numpy()
-        root_of = np.where(par < 0, np.arange(n), par)
-        for _ in range(len(segs) + 1):   # chase the parents up to the root rows (table 0)
-            nxt = np.where(root_of >= table_rows[0], par[np.minimum(root_of, n - 1)], root_of)
-            if np.array_equal(nxt, root_of):
-                break
-            root_of = nxt
-        off = rec_off.cpu().numpy()
-        # every row's place in the walk (extractHierarchicalRecord, RecordExtractors.scala:324-370): a
-        # hierarchical record's root, then per child type in copybook order (getParentToChildrenMap,
-        # CopybookParser.scala:702-727) each instance in record order followed by its own subtree -- a
-        # lexicographic order of the rows' paths (child type, record position) from the root
-        anc = [np.arange(n)]
-        while True:
-            up = np.where(anc[-1] >= 0, par[np.maximum(anc[-1], 0)], -1)
-            if not (up >= 0).any():
-                break
-            anc.append(up)
-        A = np.stack(anc)                                # A[k, x]: the k-th ancestor of row x (-1: none)
-        depth = (A >= 0).sum(axis=0) - 1                 # 0 for the roots
-        trank = np.array([order[id(g)] for g in segs], np.int64)
-        keys = []
-        for lvl in range(len(anc) - 1, 0, -1):           # deepest level first: np.lexsort's last key leads
-            k = depth - lvl
-            node = np.where(k >= 0, A[np.maximum(k, 0), np.arange(n)], -1)
-            keys.append(np.where(node >= 0, off[np.maximum(node, 0)], -1))
-            keys.append(np.where(node >= 0, trank[seg_row[np.maximum(node, 0)]], -1))
-        keys.append(root_of)
-        walk = np.empty(n, np.int64)
-        walk[np.lexsort(keys)] = np.arange(n)
-        out = np.full((len(plan.arrays), n), -1, np.int32)
-        changed = False
+        deps: List[int] = []               # dependee field indices, in the device table's order
+        events: Dict[int, List[Tuple[int, int]]] = {}   # event row -> [(field order, event)]
+        odo: List[Tuple[int, Any]] = []
         for ai, ar in arrays:
             df = plan.fields[ar.dependee]
             dcol = plan.columns[df.column]
@@ -1322,47 +1293,68 @@ class VarLenNestedReader(_BaseReader):
                 continue
             if any(order[id(g)] < root_pos for g in segs if g is not segs[root_seg]) and df.segment != ar.segment:
                 # the root record decodes a segment group placed before the root's from its own bytes,
-                # ahead of the children -- registrations this restatement does not model
+                # ahead of the children -- registrations this walk does not model
                 raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a segment group before the root "
                                                       "segment's with a cross-segment DEPENDING ON")
-            h = flat.host_column(df.column)
-            raw = np.asarray(h["values"])
-            if dcol.out_type == N.O_DEC128:
-                raw = raw.reshape(-1, 2)[:, 0]
-            dv = raw.reshape(dcol.n_slots, -1)[0, :n].astype(np.int64)
-            dok = np.asarray(h["validity"])[0, :n].astype(bool)
-            dv = ((dv + (1 << 31)) % (1 << 32) - (1 << 31)).astype(np.int64)   # Number.intValue
-            xs = np.nonzero(seg_row == ar.segment)[0]
-            if not len(xs):
-                continue
-            own = xs < table_rows[0]   # root rows: their own decode (the first record of the walk)
-            if df.segment < 0:
-                # the common header: only the root record decodes it, ahead of the children when it
-                # precedes the root's segment group
-                r = root_of[xs]
-                known = dok[r] & (order[id(dcol.node)] < root_pos)
-                val = dv[r]
-            else:
-                incl = df.segment == ar.segment and order[id(dcol.node)] < order[id(anode)]
-                ys = np.nonzero((seg_row == df.segment) & dok)[0]
-                key_y = walk[ys]
-                srt = np.argsort(key_y, kind="stable")
-                ys, key_y = ys[srt], key_y[srt]
-                key_x = walk[xs]
-                pos = np.searchsorted(key_y, key_x, side="right" if incl else "left") - 1
-                hit = (pos >= 0)
-                yy = ys[np.maximum(pos, 0)]
-                hit &= root_of[yy] == root_of[xs]
-                val = dv[yy]
-                known = hit
-            cnt = np.where(known & (val >= ar.min_count) & (val <= ar.max_count), val, ar.max_count)
-            cnt = np.where(own, -1, cnt)
-            got = np.asarray(flat.host_column(ar.count_column)["values"]).reshape(-1)[:n][xs]
-            diff = (cnt >= 0) & (cnt != got)
-            if diff.any():
-                out[ai, xs[diff]] = cnt[diff]
-                changed = True
-        return torch.as_tensor(out, device=parent_row.device) if changed else None
+            if dcol.out_type not in (N.O_I32, N.O_I64, N.O_DEC128):
+                raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a DEPENDING ON field decoded as "
+                                                      "floating point")
+            if ar.dependee not in deps:
+                deps.append(ar.dependee)
+                e = deps.index(ar.dependee)
+                if df.segment < 0:
+                    # the common header: only the root record decodes it, ahead of the children when
+                    # it precedes the root's segment group (after it: once the children are walked)
+                    if order[id(dcol.node)] < root_pos:
+                        events.setdefault(N.CBX_HIER_MAX_SEG, []).append((order[id(dcol.node)], e))
+                else:
+                    events.setdefault(df.segment, []).append((order[id(dcol.node)], e))
+            odo.append((ai, ar))
+            events.setdefault(ar.segment, []).append((order[id(anode)], -len(odo)))
+        if not odo:
+            return None
+        if len(deps) > N.CBX_HIER_MAX_DEPS or len(odo) > N.CBX_HIER_MAX_DEPS or \
+                any(len(v) > N.CBX_HIER_MAX_EVENTS for v in events.values()):
+            raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: more DEPENDING ON fields / arrays than "
+                                                  "cbx_hier_dependee_counts takes")
+        w = N.CbxHierWalk()
+        w.n_segments, w.root_segment = len(segs), root_seg
+        base = np.concatenate([[0], np.cumsum(table_rows)]).astype(np.int64)
+        for t in range(len(table_rows)):
+            w.table_base[t], w.table_rows[t] = int(base[t]), int(table_rows[t])
+        for sgi in range(N.CBX_HIER_MAX_SEG):
+            for k in range(N.CBX_HIER_MAX_SEG):
+                w.children[sgi][k] = -1
+            for k in range(N.CBX_HIER_MAX_EVENTS):
+                w.events[sgi][k] = N.HIER_EVENT_END
+        for k in range(N.CBX_HIER_MAX_EVENTS):
+            w.events[N.CBX_HIER_MAX_SEG][k] = N.HIER_EVENT_END
+        for sgi, g in enumerate(segs):
+            kids = sorted((c for c, h in enumerate(segs) if h.parent_segment is g), key=lambda c: order[id(segs[c])])
+            for k, c in enumerate(kids):
+                w.children[sgi][k] = c
+            if sgi in child_offsets:
+                w.child_offsets[sgi] = child_offsets[sgi].data_ptr()
+        for row, evs in events.items():
+            for k, (_, e) in enumerate(sorted(evs)):
+                w.events[row][k] = e
+        dt = (N.CbxHierDependee * max(1, len(deps)))()
+        for e, fi in enumerate(deps):
+            ci = plan.fields[fi].column
+            dt[e].values = flat.cols[ci]["values"].data_ptr()
+            dt[e].validity = flat.cols[ci]["validity"].data_ptr()
+            dt[e].out_type = plan.columns[ci].out_type
+        at = (N.CbxHierOdoArray * len(odo))()
+        for k, (ai, ar) in enumerate(odo):
+            at[k].dependee, at[k].out_row = deps.index(ar.dependee), ai
+            at[k].min_count, at[k].max_count = ar.min_count, ar.max_count
+            at[k].first_counts = flat.cols[ar.count_column]["values"].data_ptr()
+        dev = flat.cols[0]["validity"].device
+        out = torch.full((len(plan.arrays), n), -1, dtype=torch.int32, device=dev)
+        changed = torch.zeros(1, dtype=torch.int32, device=dev)
+        N.check(N.load().cbx_hier_dependee_counts(ctypes.byref(w), dt, len(deps), at, len(odo), out.data_ptr(), n,
+                                                  changed.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+        return out if int(changed.item()) else None
 
     def read(self, data: bytes, file_id: int = 0, input_file_name: Optional[str] = None) -> DecodedBatch:
         """A whole file, as the reference reads it: sparse-index entries (when index generation

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 13
+#define CBX_ABI_VERSION 14
 
 /* status codes */
 #define CBX_OK 0
@@ -497,7 +497,7 @@ int cbx_frame_length_field(cbx_plan* plan, const uint8_t* d_data, int64_t n_byte
  * decodes the child rows as records starting start_offset bytes earlier.  The dependFields map the
  * reference shares between the segments of a hierarchical record (:224-245: a child's array DEPENDING
  * ON a field of its parent segment or of the common header, or on a null field of its own segment)
- * is resolved by the host from the decoded rows and applied with cbx_plan_set_odo_counts.
+ * is resolved on the device by cbx_hier_dependee_counts and applied with cbx_plan_set_odo_counts.
  * Not covered (reported by the host, CBX_E_UNSUPPORTED, never decoded differently): several segment
  * ids mapped to one parent segment; a cross-segment DEPENDING ON when a segment group precedes the
  * root segment's in the copybook; a string DEPENDING ON field outside the array's segment. */
@@ -519,6 +519,51 @@ int cbx_hier_select(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, cons
  * below parent_begin + k.  Asynchronous on `stream`. */
 int cbx_hier_list_offsets(const int64_t* d_parent_row, int64_t child_begin, int64_t n_child, int64_t parent_begin,
                           int64_t n_parent, int32_t* d_offsets, void* stream);
+
+/* The dependFields map extractHierarchicalRecord shares between the segments of one hierarchical
+ * record (RecordExtractors.scala:224-245, walk order :324-370), on the device: one thread per
+ * hierarchical record walks its rows as the reference does -- the root, then per child segment in
+ * copybook order (getParentToChildrenMap, CopybookParser.scala:702-727) each child row followed by
+ * its own subtree -- replaying at every row its segment's events in field order: a numeric DEPENDING
+ * ON field registers its value (Number.intValue) when the row decodes it non-null; an array takes the
+ * value registered last (its maximum when none is, or the value is outside [min, max]).
+ * counts (device, [n_arrays_out][pitch] int32) receives the count of every array event's rows --
+ * -1 for root rows, whose own decode resolves them -- and *d_changed (device int32) is set to 1
+ * when some count differs from the first decode's (first_counts); apply with
+ * cbx_plan_set_odo_counts and decode again.  Rows as cbx_hier_select emits them. */
+#define CBX_HIER_MAX_SEG 16       /* segments of a hierarchical layout (cbx_hier_select's limit) */
+#define CBX_HIER_MAX_EVENTS 32    /* events per segment */
+#define CBX_HIER_MAX_DEPS 16      /* dependees and arrays of one cbx_hier_dependee_counts call */
+typedef struct {
+    const void* values;               /* device: the dependee column's values, slot 0 (row-indexed) */
+    const uint64_t* validity;         /* device: its validity words, slot 0 */
+    int32_t out_type;                 /* CBX_O_I32 / CBX_O_I64 / CBX_O_DEC128 */
+    int32_t reserved;
+} cbx_hier_dependee;
+
+typedef struct {
+    int32_t dependee;                 /* index into the dependee table */
+    int32_t out_row;                  /* row of `counts` receiving this array's counts (the plan array index) */
+    int32_t min_count, max_count;
+    const int32_t* first_counts;      /* device: the first decode's counts of the array (row-indexed), may be NULL */
+} cbx_hier_odo_array;
+
+typedef struct {
+    int32_t n_segments;
+    int32_t root_segment;
+    int64_t table_base[CBX_HIER_MAX_SEG + 1];        /* first row of table t (0: roots, 1 + s: segment s) */
+    int64_t table_rows[CBX_HIER_MAX_SEG + 1];
+    const int32_t* child_offsets[CBX_HIER_MAX_SEG];  /* device: segment s's list offsets over its parent table */
+    int8_t children[CBX_HIER_MAX_SEG][CBX_HIER_MAX_SEG]; /* child segments of s in copybook order, -1 ends */
+    /* events of a row of segment s in field order (s = CBX_HIER_MAX_SEG: the root record's common-header
+     * registrations before the root segment's group): e >= 0 registers dependee e, e < 0 resolves
+     * array -e - 1; -32768 ends */
+    int16_t events[CBX_HIER_MAX_SEG + 1][CBX_HIER_MAX_EVENTS];
+} cbx_hier_walk;
+
+int cbx_hier_dependee_counts(const cbx_hier_walk* walk, const cbx_hier_dependee* deps, int32_t n_deps,
+                             const cbx_hier_odo_array* arrays, int32_t n_arrays, int32_t* d_counts, int64_t pitch,
+                             int32_t* d_changed, void* stream);
 
 /* Text record framing (is_text = true) on the GPU: replaces TextRecordExtractor
  * (cobol-parser/.../reader/extractors/raw/TextRecordExtractor.scala:26-108, chosen by

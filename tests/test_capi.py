@@ -30,7 +30,8 @@ STRUCTS = {"cbx_field": N.CbxField, "cbx_array": N.CbxArray, "cbx_segment_map": 
            "cbx_plan_options": N.CbxPlanOptions, "cbx_column": N.CbxColumn, "cbx_rdw_params": N.CbxRdwParams,
            "cbx_index_entry": N.CbxIndexEntry, "cbx_index_params": N.CbxIndexParams, "cbx_selection": N.CbxSelection,
            "cbx_hier_params": N.CbxHierParams, "cbx_walk_node": N.CbxWalkNode, "cbx_walk_array": N.CbxWalkArray,
-           "cbx_walk_handler": N.CbxWalkHandler}
+           "cbx_walk_handler": N.CbxWalkHandler, "cbx_hier_dependee": N.CbxHierDependee,
+           "cbx_hier_odo_array": N.CbxHierOdoArray, "cbx_hier_walk": N.CbxHierWalk}
 
 
 def test_struct_layout_matches_header(tmp_path):
