@@ -2233,6 +2233,64 @@ extern "C" int cbx_hier_select(cbx_plan* P, const uint8_t* d_data, int64_t n_byt
     *n_rows = 0;
     for (int t = 0; t <= S; t++) table_rows[t] = 0;
     if (n_rec == 0) return CBX_OK;
+    if (prm->flags & 1) {
+        // the general walk (several segment ids per segment with children): one thread per
+        // hierarchical record, rows counted, scanned, then written; a record may sit under several
+        // parents, so the rows can outnumber the records -- CBX_E_CAPACITY (with *n_rows and
+        // table_rows set) when they do not fit the n_rec rows the outputs hold
+        const int T = S + 1;
+        const size_t o_key = ((size_t)n_rec + 15) & ~(size_t)15;
+        const size_t o_flag = (o_key + (size_t)n_rec + 15) & ~(size_t)15;
+        const size_t o_excl = (o_flag + 4 * (size_t)(n_rec + 1) + 15) & ~(size_t)15;
+        const size_t o_sums = o_excl + 8 * (size_t)(n_rec + 1);
+        const int64_t nb0 = scan_sums_len(n_rec + 1);
+        AsyncBlock blk(st);
+        HIP_CHECK(hipMallocAsync(&blk.p, o_sums + 8 * (size_t)nb0 + 64, st));
+        uint8_t* b = (uint8_t*)blk.p;
+        a.data = d_data; a.rec_off = d_rec_off; a.rec_len = d_rec_len; a.n = n_rec;
+        a.m = (const CBX_CONST cbx_segment_map*)P->d_segmap;
+        a.lut = P->d_lut;
+        a.fields = (const CBX_CONST Field*)P->d_fields;
+        a.type = (int8_t*)b; a.key = (int8_t*)(b + o_key);
+        uint32_t* flag = (uint32_t*)(b + o_flag);
+        int64_t* excl = (int64_t*)(b + o_excl);
+        hipLaunchKernelGGL(hier_type_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(hier_root_flag_kernel, dim3(blocks_for(n_rec + 1, 256)), dim3(256), 0, st, a, flag);
+        device_scan(flag, n_rec + 1, excl, (int64_t*)(b + o_sums), st);
+        int64_t G = 0;
+        HIP_CHECK(hipMemcpyAsync(&G, excl + n_rec, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        if (G == 0) return CBX_OK;   // no root record: no hierarchical record
+        const int64_t n_cnt = (int64_t)T * G;
+        const int64_t nb = scan_sums_len(n_cnt + 1);
+        const size_t o_cnt = ((size_t)8 * G + 15) & ~(size_t)15;
+        const size_t o_base = (o_cnt + 4 * (size_t)(n_cnt + 1) + 15) & ~(size_t)15;
+        const size_t o_s2 = o_base + 8 * (size_t)(n_cnt + 1);
+        AsyncBlock blk2(st);
+        HIP_CHECK(hipMallocAsync(&blk2.p, o_s2 + 8 * (size_t)nb + 64, st));
+        uint8_t* b2 = (uint8_t*)blk2.p;
+        int64_t* root_pos = (int64_t*)b2;
+        uint32_t* cnt = (uint32_t*)(b2 + o_cnt);
+        int64_t* base = (int64_t*)(b2 + o_base);
+        hipLaunchKernelGGL(hier_root_pos_kernel, dim3(blocks_for(n_rec, 256)), dim3(256), 0, st, a, (const int64_t*)excl, root_pos);
+        HIP_CHECK(hipMemsetAsync(cnt + n_cnt, 0, sizeof(uint32_t), st));
+        hipLaunchKernelGGL(hier_walk_kernel, dim3(blocks_for(G, 64)), dim3(64), 0, st, a, (const int64_t*)root_pos, G, 0, cnt,
+                           (const int64_t*)nullptr, prm->first_record_id, *out, d_parent_row);
+        device_scan(cnt, n_cnt + 1, base, (int64_t*)(b2 + o_s2), st);
+        std::vector<int64_t> tb(T + 1);
+        for (int t = 0; t < T; t++)
+            HIP_CHECK(hipMemcpyAsync(&tb[t], base + (int64_t)t * G, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipMemcpyAsync(&tb[T], base + n_cnt, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        for (int t = 0; t < T; t++) table_rows[t] = tb[t + 1] - tb[t];
+        *n_rows = tb[T];
+        if (tb[T] > (prm->row_capacity > 0 ? prm->row_capacity : n_rec)) return fail(CBX_E_CAPACITY, "cbx_hier_select: the rows (records under several parents) "
+                                                       "outnumber the output capacity; call again with n_rows rows");
+        hipLaunchKernelGGL(hier_walk_kernel, dim3(blocks_for(G, 64)), dim3(64), 0, st, a, (const int64_t*)root_pos, G, 1, cnt,
+                           (const int64_t*)base, prm->first_record_id, *out, d_parent_row);
+        HIP_CHECK(hipGetLastError());
+        return CBX_OK;
+    }
     const int64_t n_blk = (n_rec + kHierTile - 1) / kHierTile;   // last-position blocks
     const int64_t n_eb = (n_rec + 255) / 256;                     // compaction blocks
     const int64_t n_cnt = (int64_t)(S + 1) * n_eb;

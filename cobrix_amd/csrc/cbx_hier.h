@@ -43,6 +43,7 @@ struct HierArgs {
     int32_t parent[kHierMaxSeg];      // parent segment, -1 for the root / unused
     uint32_t anc[kHierMaxSeg];        // strict non-root ancestors of the parent of each segment (bits)
     int8_t* type;                     // per record: segment, -1 none
+    int8_t* key;                      // per record: segment id key, -1 none (the general walk only; may be null)
     int8_t* st;                       // per record: 0 not in the tree, 1 root, 2 child candidate
     int8_t* tab;                      // per record: table, -1 none
     int64_t* par;                     // per record: parent record (candidates)
@@ -57,6 +58,7 @@ __global__ void hier_type_kernel(HierArgs a) {
     int s = -1;
     if (k >= 0) s = a.m->key_segment[k];
     a.type[i] = (int8_t)(s >= 0 && s < a.n_seg ? s : -1);
+    if (a.key) a.key[i] = (int8_t)(s >= 0 && s < a.n_seg ? k : -1);
 }
 
 // mode 0: last position of every type in the block -> blk_lp[block][k].
@@ -249,6 +251,82 @@ __global__ void hier_offsets_kernel(const int64_t* parent_row, int64_t child_beg
         if (parent_row[child_begin + mid] < target) lo = mid + 1; else hi = mid;
     }
     offsets[k] = (int32_t)lo;
+}
+
+// ---- the general walk (segments with children mapped from several segment ids) ----
+// extractChildren breaks a parent's child list at a record whose segment ID is the parent's own or
+// one of its ancestors' -- ids, not segments: with several ids per segment a record of the parent's
+// segment under another id does not end the list, and one child record then sits under several
+// parents (RecordExtractors.scala:298-322).  One thread per hierarchical record (its root to the next
+// root) runs that recursion as the reference does, an explicit stack of (record, row, segment, child
+// type, scan position); mode 0 counts the rows per table, mode 1 writes them at the scanned bases
+// (cnt / base: [table][group]).  Rows of a table come out grouped by parent row in parent order.
+__global__ void hier_walk_kernel(HierArgs a, const int64_t* root_pos, int64_t G, int mode, uint32_t* cnt,
+                                 const int64_t* base, int64_t first_id, cbx_selection out, int64_t* parent_row) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const int64_t r0 = root_pos[g], r1 = g + 1 < G ? root_pos[g + 1] : a.n;
+    const int T = a.n_seg + 1;
+    int64_t nxt[kHierMaxSeg + 1];
+    for (int t = 0; t < T; t++) nxt[t] = mode ? base[(int64_t)t * G + g] : 0;
+    auto emit = [&](int t, int64_t rec, int64_t prow) -> int64_t {
+        const int64_t row = nxt[t]++;
+        if (mode) {
+            out.rec_off[row] = a.rec_off[rec];
+            out.rec_len[row] = a.rec_len[rec];
+            out.segment[row] = a.type[rec];
+            out.record_id[row] = first_id + (t == 0 ? r1 : rec);   // a root: the index of the next root (or the end)
+            parent_row[row] = prow;
+        }
+        return row;
+    };
+    int64_t f_rec[kHierMaxSeg + 1], f_row[kHierMaxSeg + 1], f_j[kHierMaxSeg + 1];
+    int f_seg[kHierMaxSeg + 1], f_c[kHierMaxSeg + 1], f_key[kHierMaxSeg + 1];
+    int d = 0;
+    f_rec[0] = r0; f_row[0] = emit(0, r0, -1); f_seg[0] = a.root; f_c[0] = -1; f_j[0] = r1; f_key[0] = a.key[r0];
+    while (d >= 0) {
+        const int c = f_c[d];
+        bool pushed = false;
+        if (c >= 0) {
+            for (int64_t j = f_j[d]; j < r1; j++) {
+                if (a.type[j] == c) {   // a child of this type: its row, then its own subtree
+                    f_j[d] = j + 1;
+                    const int64_t row = emit(1 + c, j, f_row[d]);
+                    if (d + 1 <= kHierMaxSeg) {
+                        d++;
+                        f_rec[d] = j; f_row[d] = row; f_seg[d] = c; f_c[d] = -1; f_j[d] = r1; f_key[d] = a.key[j];
+                    }
+                    pushed = true;
+                    break;
+                }
+                const int kj = a.key[j];
+                bool brk = false;
+                for (int u = 0; u <= d; u++) brk |= kj >= 0 && kj == f_key[u];
+                if (brk) break;
+            }
+        }
+        if (pushed) continue;
+        // the next child segment of the frame's segment (segment order = copybook order)
+        int nc = -1;
+        for (int s = c + 1; s < a.n_seg; s++)
+            if (a.parent[s] == f_seg[d]) { nc = s; break; }
+        if (nc < 0) { d--; continue; }
+        f_c[d] = nc;
+        f_j[d] = f_rec[d] + 1;
+    }
+    if (!mode)
+        for (int t = 0; t < T; t++) cnt[(int64_t)t * G + g] = (uint32_t)nxt[t];
+}
+
+// the root records' indices (excl: the exclusive scan of the root flags)
+__global__ void hier_root_flag_kernel(HierArgs a, uint32_t* flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.n) flag[i] = a.type[i] == a.root ? 1u : 0u;
+    if (i == a.n) flag[i] = 0u;
+}
+__global__ void hier_root_pos_kernel(HierArgs a, const int64_t* excl, int64_t* root_pos) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.n && a.type[i] == a.root) root_pos[excl[i]] = i;
 }
 
 // ---- the shared dependFields map (cbx_hier_dependee_counts) ----

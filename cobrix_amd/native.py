@@ -147,7 +147,7 @@ class CbxWalkHandler(ctypes.Structure):
 class CbxHierParams(ctypes.Structure):
     _fields_ = [("n_segments", ctypes.c_int32), ("root_segment", ctypes.c_int32),
                 ("parent", ctypes.c_int32 * CBX_MAX_SEG_KEYS), ("first_record_id", ctypes.c_int64),
-                ("start_offset", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("start_offset", ctypes.c_int32), ("flags", ctypes.c_int32), ("row_capacity", ctypes.c_int64)]
 
 
 CBX_HIER_MAX_SEG, CBX_HIER_MAX_EVENTS, CBX_HIER_MAX_DEPS = 16, 32, 16

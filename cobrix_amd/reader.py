@@ -632,6 +632,18 @@ def hier_root_keys(cb: cbk.Copybook, params: ReaderParameters) -> List[str]:
     return [sid for sid, grp in params.segment_id_redefine_map.items() if cbk._transform_identifier(grp) in roots]
 
 
+def hier_general_walk(params: ReaderParameters, plan: DecodePlan) -> bool:
+    """Whether a segment with children is mapped from several segment ids: extractChildren stops a
+    parent's children at a record with the parent's own id (or an ancestor's), so the lists then
+    depend on ids, not segments, and one record can sit under several parents (cbx_hier_select's
+    general walk, cbx_hier_params.flags bit 0)."""
+    ids: Dict[str, List[str]] = {}
+    for sid, grp in params.segment_id_redefine_map.items():
+        ids.setdefault(cbk._transform_identifier(grp), []).append(sid)
+    parents = {g.parent_segment.name for g in plan.segment_groups if g.parent_segment is not None}
+    return any(g.name in parents and len(ids.get(g.name, [])) > 1 for g in plan.segment_groups)
+
+
 def check_hierarchical(cb: cbk.Copybook, params: ReaderParameters, plan: DecodePlan) -> None:
     """What the GPU hierarchical path assumes (cobrix_hip.h cbx_hier_select); anything else is
     reported, never decoded differently."""
@@ -640,17 +652,6 @@ def check_hierarchical(cb: cbk.Copybook, params: ReaderParameters, plan: DecodeP
     segs = plan.segment_groups
     if len(segs) > 16:
         raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: more than 16 segment redefines")
-    ids: Dict[str, List[str]] = {}
-    for sid, grp in params.segment_id_redefine_map.items():
-        ids.setdefault(cbk._transform_identifier(grp), []).append(sid)
-    parents = {g.parent_segment.name for g in segs if g.parent_segment is not None}
-    for g in segs:
-        if g.name in parents and len(ids.get(g.name, [])) > 1:
-            # extractChildren stops a parent's children at a record with the parent's own id: with
-            # several ids per parent segment the lists depend on ids, not types (one record can then
-            # sit under several parents) -- not on the GPU path
-            raise N.CbxError(N.CBX_E_UNSUPPORTED, f"hierarchical records: segment {g.name} has children and "
-                                                  f"{len(ids[g.name])} segment ids")
 
 
 class HierBatch:
@@ -1187,19 +1188,28 @@ class VarLenNestedReader(_BaseReader):
             prm.parent[i] = segs.index(g.parent_segment) if g.parent_segment is not None else -1
         prm.first_record_id = first_record_id
         prm.start_offset = self.params.start_offset
-        sel = {"rec_off": torch.empty(max(1, n), dtype=torch.int64, device=dev),
-               "rec_len": torch.empty(max(1, n), dtype=torch.int32, device=dev),
-               "record_id": torch.empty(max(1, n), dtype=torch.int64, device=dev),
-               "segment": torch.empty(max(1, n), dtype=torch.int32, device=dev)}
-        parent_row = torch.empty(max(1, n), dtype=torch.int64, device=dev)
-        cs = N.CbxSelection()
-        for k in ("rec_off", "rec_len", "record_id", "segment"):
-            setattr(cs, k, sel[k].data_ptr())
-        cs.file_id = file_id
-        rows = (ctypes.c_int64 * (len(segs) + 1))()
-        n_rows = ctypes.c_int64(0)
-        N.check(L.cbx_hier_select(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(), rec_len.data_ptr(), n,
-                                  ctypes.byref(prm), ctypes.byref(cs), parent_row.data_ptr(), rows, ctypes.byref(n_rows), sp))
+        prm.flags = 1 if hier_general_walk(self.params, self.plan) else 0
+        cap = max(1, n)
+        while True:
+            sel = {"rec_off": torch.empty(cap, dtype=torch.int64, device=dev),
+                   "rec_len": torch.empty(cap, dtype=torch.int32, device=dev),
+                   "record_id": torch.empty(cap, dtype=torch.int64, device=dev),
+                   "segment": torch.empty(cap, dtype=torch.int32, device=dev)}
+            parent_row = torch.empty(cap, dtype=torch.int64, device=dev)
+            cs = N.CbxSelection()
+            for k in ("rec_off", "rec_len", "record_id", "segment"):
+                setattr(cs, k, sel[k].data_ptr())
+            cs.file_id = file_id
+            rows = (ctypes.c_int64 * (len(segs) + 1))()
+            n_rows = ctypes.c_int64(0)
+            prm.row_capacity = cap
+            rc = L.cbx_hier_select(self.native.handle, d_data.data_ptr(), n_bytes, rec_off.data_ptr(), rec_len.data_ptr(), n,
+                                   ctypes.byref(prm), ctypes.byref(cs), parent_row.data_ptr(), rows, ctypes.byref(n_rows), sp)
+            if rc == N.CBX_E_CAPACITY and prm.flags and n_rows.value > cap:
+                cap = n_rows.value   # the general walk: records under several parents -- more rows than records
+                continue
+            N.check(rc)
+            break
         table_rows = [int(x) for x in rows]
         sel["n"], sel["struct"] = n_rows.value, cs
         s0 = self.params.start_offset

@@ -480,8 +480,9 @@ int cbx_frame_length_field(cbx_plan* plan, const uint8_t* d_data, int64_t n_byte
  * framed records of a stream are grouped by root segment (records before the first root dropped) and
  * each record is placed under its parent instance (extractChildren's rule, :298-322: the children of
  * type C of a parent p are the C records after p up to the first record of p's segment or of one of
- * its ancestors).  Requires one segment id per segment that has children (the host checks it; the
- * reference's rule then depends on types only) and at most 16 segments.
+ * its ancestors).  With one segment id per segment that has children the reference's rule depends on
+ * types only (parallel passes over the records); else flags bit 0 selects the general walk.  At most
+ * 16 segments.
  *
  * Output: one cbx_selection of rows in table order -- table 0 = the root records (one row per
  * hierarchical record, Record_Id = first_record_id + the index of the next root record or n_rec,
@@ -498,16 +499,22 @@ int cbx_frame_length_field(cbx_plan* plan, const uint8_t* d_data, int64_t n_byte
  * reference shares between the segments of a hierarchical record (:224-245: a child's array DEPENDING
  * ON a field of its parent segment or of the common header, or on a null field of its own segment)
  * is resolved on the device by cbx_hier_dependee_counts and applied with cbx_plan_set_odo_counts.
- * Not covered (reported by the host, CBX_E_UNSUPPORTED, never decoded differently): several segment
- * ids mapped to one parent segment; a cross-segment DEPENDING ON when a segment group precedes the
- * root segment's in the copybook; a string DEPENDING ON field outside the array's segment. */
+ * Several segment ids mapped to one segment that has children: flags bit 0 (the general walk: one
+ * thread per hierarchical record runs extractChildren's recursion with its id-based break rule).
+ * Not covered (reported by the host, CBX_E_UNSUPPORTED, never decoded differently): a cross-segment
+ * DEPENDING ON when a segment group precedes the root segment's in the copybook; a string DEPENDING
+ * ON field outside the array's segment. */
 typedef struct {
     int32_t n_segments;               /* segment redefines (cbx_field.segment / key_segment indices) */
     int32_t root_segment;             /* the segment without a parent */
     int32_t parent[CBX_MAX_SEG_KEYS]; /* parent segment of each segment, -1 for the root */
     int64_t first_record_id;          /* startRecordId of the stream (entry.record_index) */
     int32_t start_offset;             /* record_start_offset: the segment id is read past it (VRLRecordReader) */
-    int32_t reserved;
+    int32_t flags;                    /* bit 0: the general walk -- a segment with children mapped from several
+                                       * segment ids (one record can then sit under several parents: rows may
+                                       * outnumber n_rec; CBX_E_CAPACITY with *n_rows / table_rows set when they
+                                       * do not fit, call again with that capacity) */
+    int64_t row_capacity;             /* rows the outputs hold (0: n_rec) */
 } cbx_hier_params;
 
 int cbx_hier_select(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,

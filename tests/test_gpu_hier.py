@@ -125,10 +125,42 @@ def test_hier_empty_and_rootless():
     assert rd.read(bytes(recs)).to_rows() == RO.var_len_rows(rd.copybook, bytes(recs), p) == []
 
 
-def test_hier_unsupported_layouts():
-    from cobrix_amd import native as N
-    with pytest.raises(N.CbxError):   # a parent segment with two ids
-        _reader({"redefine-segment-id-map:2": "DEPT => 2,8"})
+MULTI_IDS = {"redefine_segment_id_map:1": "COMPANY => 1,0", "redefine-segment-id-map:2": "DEPT => 2,8",
+             "redefine-segment-id-map:5": "CUSTOMER => 5,9"}
+
+
+def _multi_id_stream(n: int, seed: int, tree_like: float) -> bytes:
+    """hier_stream with the parent segments' records under either of their two ids (company 1 / 0,
+    department 2 / 8, customer 5 / 9), so a department under id 8 does not end the children of one
+    under id 2 (extractChildren's break compares ids): records then sit under several parents."""
+    rnd = random.Random(seed + 1000)
+    swap = {1: 0, 2: 8, 5: 9}
+    raw = bytearray(hier_stream(n, seed, tree_like))
+    i = 0
+    while i < len(raw):
+        ln = raw[i + 2] | (raw[i + 3] << 8)
+        sid = raw[i + 4] - 0xF0 if ln else -1
+        if sid in swap and rnd.random() < 0.5:
+            raw[i + 4] = 0xF0 + swap[sid]
+        i += 4 + ln
+    return bytes(raw)
+
+
+@pytest.mark.parametrize("seed,n,tree_like", [(11, 300, 1.0), (12, 4000, 0.8), (13, 4000, 0.3)])
+@pytest.mark.parametrize("views", [False, True])
+def test_hier_multi_id_parents_vs_oracle(seed, n, tree_like, views):
+    """Parent segments mapped from several segment ids (CobolParametersParser.scala:389-404 splits the
+    comma list): the general walk (cbx_hier_params.flags) breaks a parent's children only at its own
+    id or an ancestor's (RecordExtractors.scala:306-316), so a child record can appear under several
+    parents -- rows equal the oracle's literal walk, with more rows than records."""
+    raw = _multi_id_stream(n, seed, tree_like)
+    for jit in (-1, 1):
+        rd, p = _reader(MULTI_IDS, string_views=views, jit_min_records=jit)
+        rows = rd.read(raw, file_id=2).to_rows()
+        exp = RO.var_len_rows(rd.copybook, raw, p, file_id=2)
+        assert len(rows) == len(exp)
+        bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
+        assert not bad, (jit, bad[:5], rows[bad[0]], exp[bad[0]])
 
 
 @pytest.mark.parametrize("start", [3, 8])
