@@ -25,6 +25,7 @@
 #include "cbx_text.h"
 #include "cbx_hier.h"
 #include "cbx_walk.h"
+#include "cbx_chain.h"
 #include "cbx_utf8.h"
 
 using namespace cbx;
@@ -2492,6 +2493,69 @@ extern "C" int cbx_plan_set_walk(cbx_plan* P, const cbx_walk_node* nodes, int32_
     return CBX_OK;
 }
 
+namespace {
+// Chunk-parallel framing of a record chain (cbx_chain.h) from `first` over [first, n_bytes).
+// h: [0] records, [1] the chain's end position, [2] error kind (the step's), [3] error position.
+template <typename Step>
+int frame_chain(const Step& s, int64_t first, int64_t n_bytes, int64_t capacity, int64_t* d_rec_off, int32_t* d_rec_len,
+                hipStream_t st, int64_t h[4]) {
+    h[0] = 0; h[1] = first; h[2] = 0; h[3] = 0;
+    const int64_t span = n_bytes - first;
+    if (span <= 0) return CBX_OK;
+    // chunks: ~32 k lanes of walkers for a large stream, >= 1 KiB each (env CBX_CHAIN_CHUNK: tests force
+    // small chunks, so chains cross many of them)
+    int64_t chunk = std::min<int64_t>(65536, std::max<int64_t>(1024, span / 32768));
+    if (const char* e = getenv("CBX_CHAIN_CHUNK")) chunk = std::max<int64_t>(32, atoll(e));
+    chunk = (chunk + 31) & ~(int64_t)31;
+    const int64_t K = (span + chunk - 1) / chunk;
+    const int64_t nw = (span + 31) / 32 + 1;
+    const int64_t nsum = scan_sums_len(K);
+    auto r16 = [](size_t n) { return (n + 15) & ~(size_t)15; };
+    const size_t bytes = r16((size_t)nw * 4) + 6 * r16((size_t)K * 8) + r16((size_t)K * 4) + r16((size_t)nsum * 8 + 8) + r16(16 * 8);
+    AsyncBlock blk(st);
+    HIP_CHECK(hipMallocAsync(&blk.p, bytes, st));
+    uint8_t* q = (uint8_t*)blk.p;
+    auto take = [&](size_t n) { uint8_t* r = q; q += (n + 15) & ~(size_t)15; return r; };
+    ChainArgs c{};
+    c.first = first; c.chunk = chunk; c.n_chunks = K; c.n_bits = span;
+    c.bits = (uint32_t*)take((size_t)nw * 4);
+    c.ent = (int64_t*)take((size_t)K * 8);
+    c.spec_exit = (int64_t*)take((size_t)K * 8);
+    c.spec_cnt = (int64_t*)take((size_t)K * 8);
+    int64_t* ex[2] = {(int64_t*)take((size_t)K * 8), (int64_t*)take((size_t)K * 8)};
+    int64_t* base = (int64_t*)take((size_t)K * 8);
+    c.cnt = (uint32_t*)take((size_t)K * 4);
+    int64_t* sums = (int64_t*)take((size_t)nsum * 8 + 8);
+    c.out = (int64_t*)take(16 * 8);
+    HIP_CHECK(hipMemsetAsync(c.bits, 0, (size_t)nw * 4, st));
+    HIP_CHECK(hipMemsetAsync(c.out, 0, 16 * 8, st));
+    const unsigned g = (unsigned)((K + 255) / 256);
+    hipLaunchKernelGGL(chain_sample<Step>, dim3(1), dim3(1), 0, st, s, c, 256);
+    hipLaunchKernelGGL(chain_spec<Step>, dim3(g), dim3(256), 0, st, s, c);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(ex[0], c.spec_exit, (size_t)K * 8, hipMemcpyDeviceToDevice, st));
+    int cur = 0;
+    bool changed = K > 1;
+    for (int r = 0; r < kChainRounds && changed; r++) {
+        HIP_CHECK(hipMemsetAsync(c.out + 4, 0, 8, st));
+        hipLaunchKernelGGL(chain_fix<Step>, dim3(g), dim3(256), 0, st, s, c, (const int64_t*)ex[cur], ex[cur ^ 1]);
+        HIP_CHECK(hipGetLastError());
+        cur ^= 1;
+        int64_t flag = 0;
+        HIP_CHECK(hipMemcpyAsync(&flag, c.out + 4, 8, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        changed = flag != 0;
+    }
+    if (changed) hipLaunchKernelGGL(chain_settle<Step>, dim3(1), dim3(1), 0, st, s, c, ex[cur]);
+    device_scan(c.cnt, K, base, sums, st);
+    hipLaunchKernelGGL(chain_write<Step>, dim3(g), dim3(256), 0, st, s, c, (const int64_t*)base, capacity, d_rec_off, d_rec_len);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(h, c.out, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    return CBX_OK;
+}
+}  // namespace
+
 extern "C" int cbx_frame_length_field(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, int32_t field,
                                       int32_t start_offset, int32_t end_offset, int32_t adjustment, int64_t* d_rec_off,
                                       int32_t* d_rec_len, int64_t capacity, int64_t* n_records, void* stream) {
@@ -2510,18 +2574,12 @@ extern "C" int cbx_frame_length_field(cbx_plan* P, const uint8_t* d_data, int64_
     a.field = (const CBX_CONST Field*)P->d_fields + field;
     a.start_off = start_offset; a.end_off = end_offset; a.adjustment = adjustment;
     a.lfb = hf.offset + hf.size;
-    AsyncBlock blk(st);
-    HIP_CHECK(hipMallocAsync(&blk.p, 3 * sizeof(int64_t), st));
-    int64_t* d_out = (int64_t*)blk.p;
-    HIP_CHECK(hipMemsetAsync(d_out, 0, 3 * sizeof(int64_t), st));
-    hipLaunchKernelGGL(lenfield_frame_kernel, dim3(1), dim3(1), 0, st, a, capacity, d_rec_off, d_rec_len, d_out);
-    HIP_CHECK(hipGetLastError());
-    int64_t h[3] = {0, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(h, d_out, sizeof(h), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    int64_t h[4];
+    int r;
+    if ((r = frame_chain(LenFieldStep{a}, 0, n_bytes, capacity, d_rec_off, d_rec_len, st, h))) return r;
     *n_records = h[0];
-    if (h[1] == 1)
-        return fail(CBX_E_STATE, "Record length value of the field at byte " + std::to_string(h[2]) +
+    if (h[2] == 1)
+        return fail(CBX_E_STATE, "Record length value of the field at byte " + std::to_string(h[3]) +
                                      " must be an integral type.");
     if (h[0] > capacity) return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(h[0]));
     return CBX_OK;
@@ -2545,16 +2603,10 @@ extern "C" int cbx_frame_var_occurs(cbx_plan* P, const uint8_t* d_data, int64_t 
     a.handlers = (const CBX_CONST cbx_walk_handler*)P->d_whand; a.n_handlers = P->walk_n_handlers;
     a.arrays = (const CBX_CONST cbx_array*)P->d_arrays; a.fields = (const CBX_CONST Field*)P->d_fields;
     a.lut = P->d_lut;
-    AsyncBlock blk(st);
-    HIP_CHECK(hipMallocAsync(&blk.p, 3 * sizeof(int64_t), st));
-    int64_t* d_out = (int64_t*)blk.p;
-    HIP_CHECK(hipMemsetAsync(d_out, 0, 3 * sizeof(int64_t), st));
-    hipLaunchKernelGGL(walk_frame_kernel, dim3(1), dim3(1), 0, st, a, first_offset, n_bytes, capacity, d_rec_off, d_rec_len, d_out);
-    HIP_CHECK(hipGetLastError());
-    int64_t h[3] = {0, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(h, d_out, sizeof(h), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    if (h[2] < 0) return fail(CBX_E_UNSUPPORTED, "cbx_frame_var_occurs: copybook nesting deeper than the walk's frame stack");
+    int64_t h[4];
+    int r;
+    if ((r = frame_chain(VarOccursStep{a, n_bytes}, first_offset, n_bytes, capacity, d_rec_off, d_rec_len, st, h))) return r;
+    if (h[2] == 2) return fail(CBX_E_UNSUPPORTED, "cbx_frame_var_occurs: copybook nesting deeper than the walk's frame stack");
     *n_records = h[0];
     *virtual_bytes = std::max(n_bytes, h[1]);
     if (h[0] > capacity) return fail(CBX_E_CAPACITY, "record capacity " + std::to_string(capacity) + " < " + std::to_string(h[0]));

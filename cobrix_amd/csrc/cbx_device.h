@@ -1162,19 +1162,19 @@ __device__ __forceinline__ void utf8_store_slot(CBX_GLOBAL uint8_t* dst, int len
 }
 
 // Utf8 decode of a register-path element of a 2-byte code page: the LUT entries, trim range and
-// length first (str_lane_compose's first half and str_lane_group2's group build), then the tile
-// scan, then the groups placed in the lane's slot at the destination's phase (utf8_store_slot).
-__device__ __forceinline__ void str_utf8_fast2(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
-                                               const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
-                                               const uint8_t* src, uint32_t rec_addr, uint8_t* s_str, int lane) {
-    bool el = t.active && (op.segment < 0 || op.segment == t.seg);
-    if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
-    const int o = a.start_off + op.eo;
-    const bool ok = el && o <= t.avail;
-    const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
-    const int smax = op.size;
+// length first (str_lane_compose's first half and str_lane_group2's group build: g2_prep), then the
+// tile scan, then the groups placed in the lane's slot at the destination's phase (g2_store:
+// group2_put + utf8_store_slot).
+struct G2 {   // a lane's composed value: byte pairs, byte counts and selectors per group of 4 characters
+    uint32_t u01[kStrNG], u23[kStrNG], nb[kStrNG];
+    uint2 sel[kStrNG];
+    int b, e, len;   // kept characters [b, e), UTF-8 length (0 when !ok)
+};
+
+// smax: the compile-time bound of the field's bytes; bytes [eo, eo + n) of the lane's record at rec_addr.
+__device__ __forceinline__ void g2_prep(int trim, int smax, int eo, int n, bool ok, const uint8_t* src, uint32_t rec_addr, G2& g) {
     uint32_t w[8], ev[kStrFastBytes];
-    img_bytes32(src, rec_addr + (ok ? (uint32_t)op.eo : 0u), smax, w);
+    img_bytes32(src, rec_addr + (ok ? (uint32_t)eo : 0u), smax, w);
 #pragma unroll
     for (int j = 0; j < kStrFastBytes; j++)
         ev[j] = j < smax ? lds_ld<uint32_t>(byte_x4(w[j >> 2], j & 3)) : 0u;   // (the LUT at LDS 0)
@@ -1184,36 +1184,118 @@ __device__ __forceinline__ void str_utf8_fast2(const KernelArgs& a, const StrOp&
         if (j < smax) tr = __builtin_amdgcn_alignbit(tr, ev[j], 31);
     const uint32_t keep = ~(__builtin_bitreverse32(tr) >> (32 - smax)) & bits_below(n);
     int b = 0, e = n;
-    if (op.trim == CBX_TRIM_LEFT || op.trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;
-    if (op.trim == CBX_TRIM_RIGHT || op.trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
-    uint32_t u01[kStrNG], u23[kStrNG], nb[kStrNG];
-    uint2 sel[kStrNG];
+    if (trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH) b = keep ? (int)ctz32(keep) : n;
+    if (trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH) e = keep ? 32 - (int)clz32(keep) : b;
     uint32_t wide = 0;
 #pragma unroll
-    for (int g = 0; g < kStrNG; g++) {
-        if (4 * g >= smax) break;
-        const uint32_t e0 = ev[4 * g], e1 = 4 * g + 1 < smax ? ev[4 * g + 1] : 0u;
-        const uint32_t e2 = 4 * g + 2 < smax ? ev[4 * g + 2] : 0u, e3 = 4 * g + 3 < smax ? ev[4 * g + 3] : 0u;
-        u01[g] = __builtin_amdgcn_perm(e1, e0, 0x05040100u);
-        u23[g] = __builtin_amdgcn_perm(e3, e2, 0x05040100u);
+    for (int q = 0; q < kStrNG; q++) {
+        if (4 * q >= smax) break;
+        const uint32_t e0 = ev[4 * q], e1 = 4 * q + 1 < smax ? ev[4 * q + 1] : 0u;
+        const uint32_t e2 = 4 * q + 2 < smax ? ev[4 * q + 2] : 0u, e3 = 4 * q + 3 < smax ? ev[4 * q + 3] : 0u;
+        g.u01[q] = __builtin_amdgcn_perm(e1, e0, 0x05040100u);
+        g.u23[q] = __builtin_amdgcn_perm(e3, e2, 0x05040100u);
         const uint32_t lb = __builtin_amdgcn_perm(e1, e0, 0x0C0C0703u) | __builtin_amdgcn_perm(e3, e2, 0x07030C0Cu);
         const uint32_t so = __builtin_amdgcn_udot4(lb & 0x02020202u, 0x20100804u, 0u, false);
-        nb[g] = __builtin_amdgcn_udot4(lb & 0x03030303u, 0x01010101u, 0u, false);
-        wide |= g == 0 ? so >> 3 : so << (4 * g - 3);
-        sel[g] = group2_sel(so);
+        g.nb[q] = __builtin_amdgcn_udot4(lb & 0x03030303u, 0x01010101u, 0u, false);
+        wide |= q == 0 ? so >> 3 : so << (4 * q - 3);
+        g.sel[q] = group2_sel(so);
     }
-    const int len = ok ? (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b)) : 0;
+    g.b = b;
+    g.e = e;
+    g.len = ok ? (e - b) + (int)popc32(wide & bits_below(e) & ~bits_below(b)) : 0;
+}
+
+// The lane's value to d (its final place) through the lane's slot, placed at d's byte phase.
+__device__ __forceinline__ void g2_store(CBX_GLOBAL uint8_t* d, int smax, const G2& g, uint8_t* s_str, int lane) {
+    const uint32_t ph = (uint32_t)((uint64_t)(size_t)d & 3u);
+    const uint32_t s0 = (ph - (uint32_t)g.b) & 3u;   // character b lands at slot byte s0 + b = ph (mod 4)
+    uint8_t* slot = s_str + lane * str_lane_slot(smax, 2);
+    group2_put(smax, g.u01, g.u23, g.nb, g.sel, s0, slot);
+    utf8_store_slot(d, g.len, 2 * smax, (const uint32_t*)slot + ((s0 + (uint32_t)g.b) >> 2));
+}
+
+// The tile's payload of one element through a tile-contiguous LDS staging (the wave's string area),
+// copied out with aligned 16-byte stores: staging byte k is global byte A + k (A = D rounded down to
+// 16, D the tile's destination), so the body moves as whole 16-byte chunks -- ~2 coalesced store
+// instructions per element where each lane's own head / dword / tail stores were ~8 scattered ones.
+// Every lane ORs its composed groups into the zeroed staging at its tile-local place, the characters
+// outside its kept range [b, e) zeroed first (their bytes then land as zeros in the neighbours' bytes:
+// OR-ing zeros changes nothing), 32 guard bytes in front for lane 0's leading characters.  The two
+// partial chunks at the ends go out as byte stores (the neighbouring tiles own the bytes around).
+constexpr uint32_t kU8StageGuard = 32;
+
+__device__ __forceinline__ void lds_or32(uint32_t addr, uint32_t v) {
+    __hip_atomic_fetch_or((__attribute__((address_space(3))) uint32_t*)(size_t)addr, v, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void g2_stage_store(CBX_GLOBAL uint8_t* D, uint32_t ex, uint32_t tot, int smax, G2& g,
+                                               uint8_t* s_str, int lane) {
+    const uint32_t ph = (uint32_t)((uint64_t)(size_t)D & 15u);
+    CBX_GLOBAL uint8_t* A = D - ph;
+    const uint32_t sb = lds_addr(s_str) + kU8StageGuard;   // staging byte 0 (16-aligned)
+    const uint32_t end = ph + tot;
+    for (uint32_t q = (uint32_t)lane; 16u * q < end + 2u * (uint32_t)smax + 8u; q += kWave)
+        *(__attribute__((address_space(3))) u32x4*)(size_t)(sb + 16u * q) = u32x4{0u, 0u, 0u, 0u};
+    // the kept characters' bytes only (a leading / trailing trimmed character is one byte: zeroed)
+    const uint32_t bb = (uint32_t)g.b * 0x01010101u, eb = (uint32_t)g.e * 0x01010101u + 0x7F7F7F7Fu;
+#pragma unroll
+    for (int q = 0; q < kStrNG; q++) {
+        if (4 * q >= smax) break;
+        const uint32_t pos4 = 0x03020100u + 0x04040404u * (uint32_t)q;
+        const uint32_t km = ((((pos4 | 0x80808080u) - bb) & (eb - pos4)) >> 7) & 0x01010101u;   // 1 per kept character
+        g.u01[q] &= __builtin_amdgcn_perm(km, km, 0x01010000u) * 0xFFu;
+        g.u23[q] &= __builtin_amdgcn_perm(km, km, 0x03030202u) * 0xFFu;
+    }
+    // character b lands at staging byte ph + ex (the stream's leading b one-byte characters before it)
+    uint32_t pos = sb + ph + ex - (uint32_t)g.b, carry = 0;
+#pragma unroll
+    for (int q = 0; q < kStrNG; q++) {
+        if (4 * q >= smax) break;
+        const uint32_t lo = __builtin_amdgcn_perm(g.u23[q], g.u01[q], g.sel[q].x), hi = __builtin_amdgcn_perm(g.u23[q], g.u01[q], g.sel[q].y);
+        const uint32_t k8 = 8u * (pos & 3u);
+        const uint64_t v = (((uint64_t)hi << 32) | lo) << k8;
+        const uint32_t w0 = (uint32_t)v | carry, w1 = (uint32_t)(v >> 32);
+        const uint32_t w2 = (uint32_t)(((uint64_t)hi << k8) >> 32);
+        lds_or32(pos & ~3u, w0);
+        lds_or32((pos & ~3u) + 4u, w1);
+        const uint32_t np = pos + g.nb[q];
+        const uint32_t dd = (np >> 2) - (pos >> 2);
+        carry = dd == 0u ? w0 : dd == 1u ? w1 : w2;
+        pos = np;
+    }
+    lds_or32(pos & ~3u, carry);
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the wave's ORs landed before its reads
+    // copy out: whole chunks [q_lo, q_hi), the head bytes [ph, 16) of chunk 0 and the tail of chunk q_hi
+    const uint32_t q_lo = ph ? 1u : 0u, q_hi = end >> 4;
+    for (uint32_t q = q_lo + (uint32_t)lane; q < q_hi; q += kWave)
+        st_pay((CBX_GLOBAL u32x4*)(A + 16u * q), lds_ld<u32x4>(sb + 16u * q));
+    const uint32_t he = end < 16u ? end : 16u;
+    if (ph && (uint32_t)lane >= ph && (uint32_t)lane < he) A[lane] = lds_ld<uint8_t>(sb + (uint32_t)lane);
+    const uint32_t t0 = 16u * q_hi;
+    if (t0 >= 16u * q_lo && t0 + (uint32_t)lane < end && (t0 > 0 || !ph)) A[t0 + lane] = lds_ld<uint8_t>(sb + t0 + (uint32_t)lane);
+}
+
+__device__ __forceinline__ void str_utf8_fast2(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
+                                               const StrCall& c, const TileCtx& t, const int32_t* s_cnt,
+                                               const uint8_t* src, uint32_t rec_addr, uint8_t* s_str, int lane) {
+    bool el = t.active && (op.segment < 0 || op.segment == t.seg);
+    if (op.n_odo) el &= odo_present(opp, op.n_odo, s_cnt, lane);
+    const int o = a.start_off + op.eo;
+    const bool ok = el && o <= t.avail;
+    const int n = ok ? (op.size < t.avail - o ? op.size : t.avail - o) : 0;
+    G2 g;
+    g2_prep(op.trim, op.size, op.eo, n, ok, src, rec_addr, g);
     gp(c.validity)[t.tile] = __ballot(ok);
     uint32_t tot;
-    const uint32_t ex = wave_excl_scan32((uint32_t)len, lane, tot);
-    CBX_GLOBAL uint8_t* dst = utf8_offsets(a, c, t, utf8_tile_base(c, t), ex, len, tot, lane);
+    const uint32_t ex = wave_excl_scan32((uint32_t)g.len, lane, tot);
+    CBX_GLOBAL uint8_t* dst = utf8_offsets(a, c, t, utf8_tile_base(c, t), ex, g.len, tot, lane);
     if (!dst || (CBX_DIAG & 16)) return;
-    CBX_GLOBAL uint8_t* d = dst + ex;
-    const uint32_t ph = (uint32_t)((uint64_t)(size_t)d & 3u);
-    const uint32_t s0 = (ph - (uint32_t)b) & 3u;   // character b lands at slot byte s0 + b = ph (mod 4)
-    uint8_t* slot = s_str + lane * str_lane_slot(smax, 2);
-    group2_put(smax, u01, u23, nb, sel, s0, slot);
-    utf8_store_slot(d, len, 2 * smax, (const uint32_t*)slot + ((s0 + (uint32_t)b) >> 2));
+#ifdef CBX_U8_STAGE
+    g2_stage_store(dst, ex, tot, op.size, g, s_str, lane);
+#else
+    g2_store(dst + ex, op.size, g, s_str, lane);
+#endif
 }
 
 __device__ __forceinline__ void str_utf8_fast(const KernelArgs& a, const StrOp& op, const CBX_CONST StrOp* opp,
@@ -1272,6 +1354,48 @@ __device__ __forceinline__ void str_utf8_two(const KernelArgs& a, const StrOp& A
                  utf8_tile_base(cb, t));
 }
 
+// Two register-path Utf8 elements of mutually exclusive segment redefines (exp2's STATIC-DETAILS /
+// CONTACTS: the same record bytes read as fields of different segments) in one pass, as str_view_pair
+// does for views: each lane composes the field of its record's segment, so the tile pays one compose
+// for the pair; each column gets its validity word, its int32 offsets (a record of the other segment
+// adds 0 bytes: a null value) and the lane's bytes at its place.  One scan of 16-bit halves places both
+// columns (utf8_pair_fits).  The specialised kernel pairs them (cbx_jit.h: same kind, trim and code
+// page, no OCCURS).
+__device__ __forceinline__ void str_utf8_pair(const KernelArgs& a, const StrOp& A, const StrCall& ca, const StrOp& B,
+                                              const StrCall& cb, const TileCtx& t, const uint8_t* src, uint32_t rec_addr,
+                                              const uint32_t* s_lut, uint8_t* s_str, int lane) {
+    const bool sa = t.seg == A.segment;
+    const int eo = sa ? A.eo : B.eo, size = sa ? A.size : B.size;
+    const int smax = A.size > B.size ? A.size : B.size;
+    const int o = a.start_off + eo;
+    const bool ok = t.active && (sa || t.seg == B.segment) && o <= t.avail;
+    const int n = ok ? (size < t.avail - o ? size : t.avail - o) : 0;
+    const bool g2 = A.kind == CBX_K_STRING && A.pad == 2;
+    G2 g;
+    u32x4 q[kStrNC];
+    int len;
+    if (g2) {
+        g2_prep(A.trim, smax, eo, n, ok, src, rec_addr, g);
+        len = g.len;
+    } else {
+        const int l0 = str_lane_compose(A.kind, A.trim, A.pad, smax, eo, n, ok, src, rec_addr, s_lut, s_str, lane, q, false);
+        len = ok ? l0 : 0;
+    }
+    gp(ca.validity)[t.tile] = __ballot(ok && sa);
+    gp(cb.validity)[t.tile] = __ballot(ok && !sa);
+    const uint32_t la = sa ? (uint32_t)len : 0u, lb = sa ? 0u : (uint32_t)len;
+    uint32_t tot2;
+    const uint32_t ex2 = wave_excl_scan32(la | (lb << 16), lane, tot2);   // a tile's total < 64 KiB (utf8_pair_fits)
+    const uint32_t exa = ex2 & 0xFFFFu, exb = ex2 >> 16;
+    CBX_GLOBAL uint8_t* da = utf8_offsets(a, ca, t, utf8_tile_base(ca, t), exa, (int)la, tot2 & 0xFFFFu, lane);
+    CBX_GLOBAL uint8_t* db = utf8_offsets(a, cb, t, utf8_tile_base(cb, t), exb, (int)lb, tot2 >> 16, lane);
+    if (CBX_DIAG & 16) return;
+    CBX_GLOBAL uint8_t* d = sa ? (da ? da + exa : nullptr) : (db ? db + exb : nullptr);
+    if (!d) return;   // (a column whose region overflowed: reported by utf8_offsets)
+    if (g2) g2_store(d, smax, g, s_str, lane);
+    else utf8_store_direct(d, len, smax * A.pad, q);
+}
+
 // ---- Utf8 count pass (specialised kernels only: CBX_COUNT_LUT) ----
 // The count kernel's LDS copy of the code-page LUT keeps, per byte, only what a UTF-8 length needs:
 // the trim flag and the UTF-8 length.  A trimmed character maps to <= U+0020, one UTF-8 byte, so a
@@ -1288,6 +1412,33 @@ __device__ __forceinline__ uint8_t count_lut_byte(uint32_t e) {
 
 // UTF-8 length of the lane's value of a register-path code-page element whose n bytes are all in
 // the record (n == op.size; the caller checks), from the count LUT.
+// str_count_lane: the same for a lane whose field is `size` <= smax bytes at eo (a segment-redefine pair
+// of fields: each lane counts its record's segment's field; smax the compile-time bound).
+__device__ __forceinline__ int str_count_lane(int trim, int smax, int size, int eo, const uint8_t* src, uint32_t rec_addr, bool ok,
+                                              const uint32_t* s_lut) {
+    uint32_t w[8];
+    img_bytes32(src, rec_addr + (ok ? (uint32_t)eo : 0u), smax, w);
+    uint32_t acc = 0, tm = 0;
+    const uint32_t lut8 = lds_addr(s_lut);   // count_lut_byte entries
+#pragma unroll
+    for (int j = 0; j < kStrFastBytes; j++) {
+        if (j < smax) {
+            const uint32_t idx = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            const uint32_t e = (uint32_t)(int32_t)lds_ld<int8_t>(lut8 + idx);
+            tm = __builtin_amdgcn_alignbit(tm, e, 31);   // (tm << 1) | trim bit
+            acc += j < size ? (e & 0xFFu) : 0u;          // trim * 128 + UTF-8 length
+        }
+    }
+    const uint32_t keep = ~__builtin_bitreverse32(tm << (32 - smax)) & bits_below(size);
+    const int total = (int)(acc & 127u);
+    const bool tl = trim == CBX_TRIM_LEFT || trim == CBX_TRIM_BOTH;
+    const bool tr = trim == CBX_TRIM_RIGHT || trim == CBX_TRIM_BOTH;
+    if (!ok) return 0;
+    if (!keep) return (tl || tr) ? 0 : total;
+    const int lead = (int)ctz32(keep), trail = size - (32 - (int)clz32(keep));
+    return total - (tl ? lead : 0) - (tr ? trail : 0);
+}
+
 __device__ __forceinline__ int str_count_fast(const StrOp& op, const uint8_t* src, uint32_t rec_addr, bool ok,
                                               const uint32_t* s_lut) {
     uint32_t w[8];
@@ -1342,6 +1493,31 @@ __device__ __forceinline__ int str_count_fast(const StrOp& op, const uint8_t* sr
     if (!keep) return (tl || tr) ? 0 : total;
     const int lead = (int)ctz32(keep), trail = size - (32 - (int)clz32(keep));
     return total - (tl ? lead : 0) - (tr ? trail : 0);
+}
+
+// The Utf8 count pass over a segment-redefine pair (str_utf8_pair's counterpart): each lane counts its
+// record's segment's field with the count LUT, one scan of 16-bit halves gives both tile totals.
+// Returns false (nothing written) for a tile with a record ending inside its field or a non-code-page
+// pair: the caller counts each element on its own (str_element, mode 1).
+__device__ __forceinline__ bool str_count_pair(const KernelArgs& a, const StrOp& A, const StrOp& B, const TileCtx& t,
+                                               const uint8_t* src, uint32_t rec_addr, const uint32_t* s_lut, int lane) {
+    const bool sa = t.seg == A.segment;
+    const int eo = sa ? A.eo : B.eo, size = sa ? A.size : B.size;
+    const int smax = A.size > B.size ? A.size : B.size;
+    const int o = a.start_off + eo;
+    const bool el = t.active && (sa || t.seg == B.segment);
+    const bool ok = el && o + size <= t.avail;
+    const bool part = el && o <= t.avail && !ok;
+    if (A.kind != CBX_K_STRING || __ballot(part)) return false;
+    const int len = str_count_lane(A.trim, smax, size, eo, src, rec_addr, ok, s_lut + 256);
+    const uint32_t la = sa ? (uint32_t)len : 0u, lb = sa ? 0u : (uint32_t)len;
+    uint32_t tot2;
+    wave_excl_scan32(la | (lb << 16), lane, tot2);
+    if (lane == 0) {
+        gp(a.str_tot)[(int64_t)A.seq * a.n_tiles + t.tile] = tot2 & 0xFFFFu;
+        gp(a.str_tot)[(int64_t)B.seq * a.n_tiles + t.tile] = tot2 >> 16;
+    }
+    return true;
 }
 
 // One string element of the tile (StringDecoders.decodeEbcdicString / decodeAsciiString):

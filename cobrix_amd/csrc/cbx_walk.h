@@ -508,8 +508,8 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
 // ---- VarOccursRecordExtractor: record lengths by walking each record's dependees ----
 // extractVarOccursRecordBytes (:52-136): a walk with no decoding besides the dependees, every
 // non-redefined field advancing by its walked size; the record is the walked prefix of the stream
-// (a short read at the end is zero-filled: the record may reach past n_bytes).  Sequential in the
-// stream (a record starts where the previous one ends): one thread.
+// (a short read at the end is zero-filled: the record may reach past n_bytes).  The stream's framing
+// from these lengths is chunk-parallel (cbx_chain.h: VarOccursStep).
 __device__ int walk_length(const WalkArgs& a, const uint8_t* rec, int avail) {
     WalkFrame st[kWalkDepth];
     WalkDeps dep;
@@ -590,60 +590,6 @@ __device__ int walk_length(const WalkArgs& a, const uint8_t* rec, int avail) {
         fr.cur = ch.next;
     }
     return last_size;
-}
-
-__global__ void walk_frame_kernel(WalkArgs a, int64_t first, int64_t n_bytes, int64_t capacity, int64_t* rec_off,
-                                  int32_t* rec_len, int64_t* out /* [0] records, [1] end of the last record */) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    int64_t pos = first, k = 0;
-    while (pos < n_bytes) {   // hasNext: offset < size
-        const int64_t left = n_bytes - pos;
-        const int len = walk_length(a, a.data + pos, left < 0x7fffffff ? (int)left : 0x7fffffff);
-        if (len <= 0) { out[2] = len < 0 ? -1 : 0; break; }
-        if (k < capacity) { rec_off[k] = pos; rec_len[k] = len; }
-        k++;
-        pos += len;
-    }
-    out[0] = k;
-    out[1] = pos;
-}
-
-// ---- VRLRecordReader.fetchRecordUsingRecordLengthField (CP/reader/iterator/VRLRecordReader.scala:114-149) ----
-// A record starts where the previous one ends: its first start_offset + lfb bytes (lfb = the length
-// field's offset + size) carry the length field, decoded as extractPrimitiveField does; the record is
-// those bytes + max(0, length + adjustment - lfb + end_offset) more (fewer at the end of the stream,
-// which then ends).  Sequential by definition: one device thread walks the stream; the data never
-// leaves the GPU.  Error (the reference throws IllegalStateException): 1 a null or non-Int/Long value.
-struct LenFieldArgs {
-    const uint8_t* data;
-    int64_t n_bytes;
-    const CBX_CONST Field* field;     // the length field (decode offset relative to the record start + start_off)
-    int32_t start_off, end_off, adjustment, lfb;
-};
-
-__global__ void lenfield_frame_kernel(LenFieldArgs a, int64_t capacity, int64_t* rec_off, int32_t* rec_len,
-                                      int64_t* out /* [0] records, [1] error kind, [2] error position */) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    const Field f = ldc(a.field);
-    const int64_t head = (int64_t)a.start_off + a.lfb;
-    int64_t pos = 0, k = 0;
-    while (pos + head <= a.n_bytes) {   // dataStream.next(startOffset + lengthFieldBlock) in full
-        const uint8_t* p = a.data + pos + a.start_off + f.offset;
-        // an Integral field (ReaderParametersValidator.getLengthField): Int / Long -> toInt; a null or
-        // a BigDecimal (precision > 18) value: "must be an integral type"
-        const Val x = decode_numeric(f, p);
-        if (!x.valid || (f.out_type != CBX_O_I32 && f.out_type != CBX_O_I64)) { out[1] = 1; out[2] = pos; break; }
-        const int32_t len = (int32_t)(uint32_t)x.lo;
-        // Java int arithmetic: recordLength = value + adjustment; rest = recordLength - lfb + endOffset
-        const int32_t rest = (int32_t)((uint32_t)len + (uint32_t)a.adjustment - (uint32_t)a.lfb + (uint32_t)a.end_off);
-        const int64_t left = a.n_bytes - (pos + head);
-        const int64_t take = rest > 0 ? (rest < left ? rest : left) : 0;
-        if (k < capacity) { rec_off[k] = pos; rec_len[k] = (int32_t)(head + take); }
-        k++;
-        pos += head + take;
-        if (rest > 0 && take < rest) break;   // a short read closes the stream
-    }
-    out[0] = k;
 }
 
 #endif  // CBX_JIT_WALK

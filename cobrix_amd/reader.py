@@ -1032,8 +1032,8 @@ class VarLenNestedReader(_BaseReader):
         return fi
 
     def frame_length_field(self, d_data, n_bytes: int, stream=None):
-        """VRLRecordReader.fetchRecordUsingRecordLengthField on the GPU (one device thread walks the
-        stream) -> (rec_off, rec_len) of the records: each starts where the previous ended, its length
+        """VRLRecordReader.fetchRecordUsingRecordLengthField on the GPU (chunk-parallel framing,
+        cbx_chain.h) -> (rec_off, rec_len) of the records: each starts where the previous ended, its length
         from the field inside it (+ rdw_adjustment), record_start/end_offset included."""
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream()
@@ -1133,7 +1133,7 @@ class VarLenNestedReader(_BaseReader):
         return t
 
     def frame_var_occurs(self, d_data, n_bytes: int, stream=None):
-        """VarOccursRecordExtractor (GPU, sequential walk) -> (rec_off, rec_len, virtual_bytes): the
+        """VarOccursRecordExtractor (GPU, chunk-parallel framing: cbx_chain.h) -> (rec_off, rec_len, virtual_bytes): the
         last record may reach past n_bytes into the reference's zero fill (d_data holds zeros there)."""
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream()

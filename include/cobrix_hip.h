@@ -451,8 +451,9 @@ int cbx_plan_set_walk(cbx_plan* plan, const cbx_walk_node* nodes, int32_t n_node
 
 /* VarOccursRecordExtractor (CP/reader/extractors/raw/VarOccursRecordExtractor.scala:30-154): record
  * boundaries of a file whose record size follows from its OCCURS DEPENDING ON values (no RDW, no
- * length field), from first_offset on.  A record starts where the previous one ends, so the walk is
- * sequential (one device thread: a latency-bound path).  A short read at the end is zero-filled by
+ * length field), from first_offset on.  A record starts where the previous one ends; the stream is
+ * framed chunk-parallel (speculated chunk entries corrected until they agree with the sequential walk,
+ * cbx_chain.h), with the sequential walk's results.  A short read at the end is zero-filled by
  * the reference: the last record may reach past n_bytes, up to *virtual_bytes (the buffer must hold
  * zeros there before decoding).  Needs a plan with cbx_plan_set_walk. */
 int cbx_frame_var_occurs(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, int64_t first_offset,
@@ -467,8 +468,9 @@ int cbx_frame_var_occurs(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes,
  * record.  The field must be a primitive Integral one (ReaderParametersValidator.getLengthField); its
  * value is decoded as extractPrimitiveField does (Int / Long -> toInt) and a null or BigDecimal value
  * fails with CBX_E_STATE (the reference's IllegalStateException).  rec_off / rec_len receive
- * the record starts and lengths (decode them with cbx_decode_var at start_offset).  Sequential in the
- * stream: one device thread walks it. */
+ * the record starts and lengths (decode them with cbx_decode_var at start_offset).  Framed
+ * chunk-parallel like cbx_frame_var_occurs (cbx_chain.h); the error reported is the first one on the
+ * record chain. */
 int cbx_frame_length_field(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, int32_t field,
                            int32_t start_offset, int32_t end_offset, int32_t adjustment, int64_t* d_rec_off,
                            int32_t* d_rec_len, int64_t capacity, int64_t* n_records, void* stream);

@@ -478,6 +478,37 @@ def test_utf8_onepass_code_pages_and_trim(cp, trim, monkeypatch):
     assert not errs, errs
 
 
+@pytest.mark.parametrize("staged", [False, True])
+@pytest.mark.parametrize("trim", ["none", "left", "right", "both"])
+@pytest.mark.parametrize("cp", ["cp037", "common", "ascii"])
+def test_utf8_decode_code_pages_and_trim(cp, trim, staged, monkeypatch):
+    """The count + scan + decode Arrow Utf8 path on fields of 1..32 bytes full of trimmable bytes, every
+    trim policy, single- / two-byte code pages and ASCII; staged: the tile-staged payload store
+    (CBX_U8_STAGE: kept bytes OR-ed into a zeroed tile-contiguous LDS staging, copied out in aligned
+    16-byte chunks, byte stores at the ends).  Bit-exact against the oracle."""
+    sizes = [1, 2, 3, 4, 5, 7, 8, 9, 13, 16, 17, 20, 31, 32]
+    cb_text = "       01  R.\n" + "".join(f"          05  F{i}  PIC X({s}).\n" for i, s in enumerate(sizes))
+    rec = sum(sizes)
+    rng = np.random.default_rng(19)
+    n = 70_003
+    raw = rng.integers(0, 256, (n, rec), dtype=np.uint8)
+    pad = 0x40 if cp != "ascii" else 0x20
+    raw[rng.random((n, rec)) < 0.33] = pad
+    raw[:, ::5][rng.random((n, (rec + 4) // 5)) < 0.2] = 0x05 if cp != "ascii" else 0x09
+    data = raw.tobytes()
+    if staged:
+        monkeypatch.setenv("CBX_JIT_DEFINES", "CBX_U8_STAGE=1")
+    kw = dict(string_trimming_policy=trim, jit_min_records=1, string_utf8=True)
+    if cp == "ascii":
+        kw["is_ebcdic"] = False
+    else:
+        kw["ebcdic_code_page"] = cp
+    rd, batch = _fixed(cb_text, data, **kw)
+    assert _kernel_kind(rd) == 1
+    errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
+    assert not errs, errs
+
+
 def test_synstr200_full_size_sampled_utf8():
     """Config C3 as the bench runs it (50 M SYNSTR200 records, Arrow Utf8 layout: count pass, device
     scan, every offset and payload byte written once by the specialised decode kernel): a sample

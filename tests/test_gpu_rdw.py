@@ -208,6 +208,80 @@ def test_record_length_field_errors():
         rd2.read(_lenfield_file(rng, 5))
 
 
+LENFIELD_BIN_COPYBOOK = """
+       01  REC.
+           05  REC-LEN     PIC 9(4) COMP.
+           05  BODY        PIC X(400).
+"""
+
+
+def _lenfield_bin_file(rng, n, lo=2, hi=400, digits=False):
+    """n records of a 2-byte big-endian COMP length (the whole record's) + body.  digits: bodies of
+    cp037 digits and record-like bytes (every position a plausible-looking start); else random bytes."""
+    out, offs = bytearray(), []
+    for _ in range(n):
+        total = int(rng.integers(lo, hi + 1))
+        offs.append(len(out))
+        out += total.to_bytes(2, "big")
+        if digits:
+            body = rng.integers(0, 3, total - 2, dtype=np.uint8)   # 0x00 0x01 0x02: lengths of 1, 2 or 258+ bytes
+        else:
+            body = rng.integers(0, 256, total - 2, dtype=np.uint8)
+        out += bytes(body)
+    return bytes(out), offs
+
+
+@pytest.mark.parametrize("chunk", ["32", "96", "1024", None])
+@pytest.mark.parametrize("kind", ["display", "binary", "adversarial"])
+def test_record_length_field_chunked_framing(kind, chunk, monkeypatch):
+    """The chunk-parallel length-field framing (cbx_chain.h: speculated chunk entries, fix rounds that
+    stop where the true chain meets the speculated one, the settle pass) gives the sequential walk's
+    records for chunks from 32 bytes (chains crossing thousands of chunks) to the default, on streams
+    whose bodies look like record starts everywhere ("adversarial": 2-byte lengths of 0..2, so every
+    speculation walks a wrong chain) -- offsets / lengths equal the generator's."""
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import VarLenNestedReader
+    if chunk is not None:
+        monkeypatch.setenv("CBX_CHAIN_CHUNK", chunk)
+    rng = np.random.default_rng({"display": 5, "binary": 6, "adversarial": 7}[kind])
+    if kind == "display":
+        raw = _lenfield_file(rng, 20_000)
+        p, _ = parse_options({"record_length_field": "REC-LEN"})
+        rd = VarLenNestedReader(LENFIELD_COPYBOOK, p)
+        off = [0]
+        for _ in range(20_000 - 1):
+            off.append(off[-1] + int(raw[off[-1] + 2:off[-1] + 5].decode("cp037")))
+    else:
+        raw, off = _lenfield_bin_file(rng, 20_000, digits=kind == "adversarial")
+        p, _ = parse_options({"record_length_field": "REC-LEN", "rdw_adjustment": "0"})
+        rd = VarLenNestedReader(LENFIELD_BIN_COPYBOOK, p)
+    t = rd._device_file(raw)
+    o, ln, _ = rd.frame_file(t, len(raw))
+    assert o.cpu().tolist() == off
+    assert ln.cpu().tolist() == [b - a for a, b in zip(off, off[1:] + [len(raw)])]
+
+
+@pytest.mark.parametrize("chunk", ["32", None])
+def test_record_length_field_chunked_error_position(chunk, monkeypatch):
+    """With chunks of 32 bytes the first undecodable length ON the record chain fails the framing,
+    as the reference's walk does; undecodable bytes the speculated chains meet elsewhere do not."""
+    from cobrix_amd import native as N
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import VarLenNestedReader
+    if chunk is not None:
+        monkeypatch.setenv("CBX_CHAIN_CHUNK", chunk)
+    rng = np.random.default_rng(11)
+    raw = _lenfield_file(rng, 2000, bad_at=1500)
+    p, _ = parse_options({"record_length_field": "REC-LEN"})
+    rd = VarLenNestedReader(LENFIELD_COPYBOOK, p)
+    with pytest.raises(N.CbxError) as e:
+        rd.read(raw)
+    assert e.value.code == N.CBX_E_STATE
+    good = _lenfield_file(np.random.default_rng(11), 2000)
+    rows = rd.read(good).to_rows()
+    assert rows == RO.var_len_rows(rd.copybook, good, p)
+
+
 def _frame_async(raw: bytes, seeds=None, cap=None, max_rounds=0):
     """cbx_frame_rdw_async + cbx_frame_rdw_state -> (offsets, lengths, state) or CbxError."""
     import ctypes

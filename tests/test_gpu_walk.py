@@ -77,10 +77,14 @@ def test_walk_nested_odo_rdw_vs_oracle(var_size):
     assert not bad, (bad[:5], rows[bad[0]], exp[bad[0]])
 
 
-def test_walk_var_occurs_extractor_vs_oracle():
-    """No RDW: VarOccursRecordExtractor framing on the GPU (sequential walk), then the walk decode."""
+@pytest.mark.parametrize("chunk", [None, "32", "128"])
+def test_walk_var_occurs_extractor_vs_oracle(chunk, monkeypatch):
+    """No RDW: VarOccursRecordExtractor framing on the GPU (chunk-parallel, cbx_chain.h: chunks of 32 /
+    128 bytes make every record chain cross many speculated chunk entries), then the walk decode."""
+    if chunk is not None:
+        monkeypatch.setenv("CBX_CHAIN_CHUNK", chunk)
     rnd = random.Random(11)
-    raw = b"".join(nested_record(rnd, True) for _ in range(400))
+    raw = b"".join(nested_record(rnd, True) for _ in range(400 if chunk is None else 3000))
     rd, p = _reader(NESTED, {"variable_size_occurs": "true"})
     rows = rd.read(raw).to_rows()
     exp = RO.var_len_rows(rd.copybook, raw, p)

@@ -71,12 +71,23 @@ def _compile(src: str, lib_path: str | None = None) -> str:
     return r.stdout or f"hipRTC ({lib_path}) died: exit {r.returncode}\n{r.stderr[-2000:]}"
 
 
-def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coop: bool = False) -> str:
+def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coop: bool = False, seg_pair: bool = False) -> str:
     """The specialised record kernel's source as cbx_jit.h emits it (jit_source), for a 3-element
-    string layout; coop: the cooperative form (jit_coop: coop_lds / coop_loop, ops split on l.wid)."""
+    string layout; coop: the cooperative form (jit_coop: coop_lds / coop_loop, ops split on l.wid);
+    seg_pair: two segment-redefine elements in one pass (str_utf8_pair / str_count_pair)."""
     view = "true" if layout == 1 else "false"
     ops = [f"{{{20 * i},20,1,4,0,2,{i},0,{i},-1,{{0,0,0,0}},{{0,0,0,0}},0}}" for i in range(3)]
-    if pair:
+    if seg_pair:
+        sa = "{0,20,1,4,0,2,0,0,0,0,{0,0,0,0},{0,0,0,0},0}"
+        sb = "{0,17,1,4,0,2,1,0,1,1,{0,0,0,0},{0,0,0,0},0}"
+        if count:
+            body = (f"    {{ constexpr StrOp opa = {sa}; constexpr StrOp opb = {sb}; if (!str_count_pair(a, opa, opb, t, img, rec_addr, l.lut, lane)) {{\n"
+                    "      str_element<false>(a, opa, a.sops + 0, ldc(a.scall + 0), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane);\n"
+                    "      str_element<false>(a, opb, a.sops + 1, ldc(a.scall + 1), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane); } }\n")
+        else:
+            body = (f"    {{ constexpr StrOp opa = {sa}; constexpr StrOp opb = {sb}; str_utf8_pair(a, opa, ldc(a.scall + 0), opb, "
+                    "ldc(a.scall + 1), t, img, rec_addr, l.lut, l.str, lane); }\n")
+    elif pair:
         body = (f"    {{ constexpr StrOp opa = {ops[0]}; constexpr StrOp opb = {ops[1]}; str_utf8_two(a, opa, a.sops + 0, "
                 f"ldc(a.scall + 0), opb, a.sops + 1, ldc(a.scall + 1), t, l.cnt, img, rec_addr, l.lut, l.str, lane); }}\n")
     elif loop:
@@ -148,12 +159,14 @@ extern "C" __global__ __launch_bounds__(cbx::kWave * cbx::kListWaves) void cbx_j
                                                          (2, False, False, False, False), (2, True, False, False, False),
                                                          (0, False, True, False, False), (2, False, False, True, False),
                                                          (1, False, False, False, True), (2, False, False, False, True),
-                                                         (2, True, False, False, True)])
+                                                         (2, True, False, False, True), (2, False, False, "seg", False),
+                                                         (2, True, False, "seg", False)])
 @pytest.mark.parametrize("compiler", range(2), ids=["rocm", "torch"])
 def test_record_kernel_compiles_with_hiprtc(layout, count, loop, pair, coop, compiler):
     if compiler >= len(COMPILERS):
         pytest.skip("no second hipRTC")
-    err = _compile(_record_kernel(layout, count, loop, pair, coop), COMPILERS[compiler])
+    src = _record_kernel(layout, count, loop, pair is True, coop, seg_pair=pair == "seg")
+    err = _compile(src, COMPILERS[compiler])
     assert not err, err[:3000]
 
 
