@@ -2498,13 +2498,14 @@ namespace {
 // h: [0] records, [1] the chain's end position, [2] error kind (the step's), [3] error position.
 template <typename Step>
 int frame_chain(const Step& s, int64_t first, int64_t n_bytes, int64_t capacity, int64_t* d_rec_off, int32_t* d_rec_len,
-                hipStream_t st, int64_t h[4]) {
+                hipStream_t st, int64_t h[4], int64_t min_chunk) {
     h[0] = 0; h[1] = first; h[2] = 0; h[3] = 0;
     const int64_t span = n_bytes - first;
     if (span <= 0) return CBX_OK;
-    // chunks: ~32 k lanes of walkers for a large stream, >= 1 KiB each (env CBX_CHAIN_CHUNK: tests force
+    // chunks: ~32 k lanes of walkers for a large stream, >= min_chunk bytes each -- enough records per
+    // chunk that a speculated chain meets the true one inside it (env CBX_CHAIN_CHUNK: tests force
     // small chunks, so chains cross many of them)
-    int64_t chunk = std::min<int64_t>(65536, std::max<int64_t>(1024, span / 32768));
+    int64_t chunk = std::min<int64_t>(std::max<int64_t>(65536, min_chunk), std::max<int64_t>(min_chunk, span / 32768));
     if (const char* e = getenv("CBX_CHAIN_CHUNK")) chunk = std::max<int64_t>(32, atoll(e));
     chunk = (chunk + 31) & ~(int64_t)31;
     const int64_t K = (span + chunk - 1) / chunk;
@@ -2576,7 +2577,7 @@ extern "C" int cbx_frame_length_field(cbx_plan* P, const uint8_t* d_data, int64_
     a.lfb = hf.offset + hf.size;
     int64_t h[4];
     int r;
-    if ((r = frame_chain(LenFieldStep{a}, 0, n_bytes, capacity, d_rec_off, d_rec_len, st, h))) return r;
+    if ((r = frame_chain(LenFieldStep{a}, 0, n_bytes, capacity, d_rec_off, d_rec_len, st, h, 1024))) return r;
     *n_records = h[0];
     if (h[2] == 1)
         return fail(CBX_E_STATE, "Record length value of the field at byte " + std::to_string(h[3]) +
@@ -2605,7 +2606,9 @@ extern "C" int cbx_frame_var_occurs(cbx_plan* P, const uint8_t* d_data, int64_t 
     a.lut = P->d_lut;
     int64_t h[4];
     int r;
-    if ((r = frame_chain(VarOccursStep{a, n_bytes}, first_offset, n_bytes, capacity, d_rec_off, d_rec_len, st, h))) return r;
+    // (a record walked from a wrong start reads its counts from the wrong bytes -- often the maxima --
+    // so such chains need more records than length-field ones to land on a true start: 16 KiB chunks)
+    if ((r = frame_chain(VarOccursStep{a, n_bytes}, first_offset, n_bytes, capacity, d_rec_off, d_rec_len, st, h, 16384))) return r;
     if (h[2] == 2) return fail(CBX_E_UNSUPPORTED, "cbx_frame_var_occurs: copybook nesting deeper than the walk's frame stack");
     *n_records = h[0];
     *virtual_bytes = std::max(n_bytes, h[1]);

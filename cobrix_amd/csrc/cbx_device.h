@@ -1217,7 +1217,8 @@ __device__ __forceinline__ void g2_store(CBX_GLOBAL uint8_t* d, int smax, const 
 // The tile's payload of one element through a tile-contiguous LDS staging (the wave's string area),
 // copied out with aligned 16-byte stores: staging byte k is global byte A + k (A = D rounded down to
 // 16, D the tile's destination), so the body moves as whole 16-byte chunks -- ~2 coalesced store
-// instructions per element where each lane's own head / dword / tail stores were ~8 scattered ones.
+// instructions per element where each lane's own head / dword / tail stores were ~8 scattered ones
+// (SYNSTR200 Utf8 chain 8.08 -> 8.03 and 8.26 -> 8.03 ms, same-box A/B; CBX_U8_DIRECT: the old form).
 // Every lane ORs its composed groups into the zeroed staging at its tile-local place, the characters
 // outside its kept range [b, e) zeroed first (their bytes then land as zeros in the neighbours' bytes:
 // OR-ing zeros changes nothing), 32 guard bytes in front for lane 0's leading characters.  The two
@@ -1229,8 +1230,9 @@ __device__ __forceinline__ void lds_or32(uint32_t addr, uint32_t v) {
                           __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__device__ __forceinline__ void g2_stage_store(CBX_GLOBAL uint8_t* D, uint32_t ex, uint32_t tot, int smax, G2& g,
+__device__ __forceinline__ void g2_stage_store(CBX_GLOBAL uint8_t* D, uint32_t ex, uint32_t tot, int smax, const G2& gin, bool on,
                                                uint8_t* s_str, int lane) {
+    G2 g = gin;   // (on: the lane's value belongs to this column -- a segment-redefine pair stages one column at a time)
     const uint32_t ph = (uint32_t)((uint64_t)(size_t)D & 15u);
     CBX_GLOBAL uint8_t* A = D - ph;
     const uint32_t sb = lds_addr(s_str) + kU8StageGuard;   // staging byte 0 (16-aligned)
@@ -1238,7 +1240,7 @@ __device__ __forceinline__ void g2_stage_store(CBX_GLOBAL uint8_t* D, uint32_t e
     for (uint32_t q = (uint32_t)lane; 16u * q < end + 2u * (uint32_t)smax + 8u; q += kWave)
         *(__attribute__((address_space(3))) u32x4*)(size_t)(sb + 16u * q) = u32x4{0u, 0u, 0u, 0u};
     // the kept characters' bytes only (a leading / trailing trimmed character is one byte: zeroed)
-    const uint32_t bb = (uint32_t)g.b * 0x01010101u, eb = (uint32_t)g.e * 0x01010101u + 0x7F7F7F7Fu;
+    const uint32_t bb = (uint32_t)g.b * 0x01010101u, eb = (uint32_t)(on ? g.e : 0) * 0x01010101u + 0x7F7F7F7Fu;
 #pragma unroll
     for (int q = 0; q < kStrNG; q++) {
         if (4 * q >= smax) break;
@@ -1291,8 +1293,8 @@ __device__ __forceinline__ void str_utf8_fast2(const KernelArgs& a, const StrOp&
     const uint32_t ex = wave_excl_scan32((uint32_t)g.len, lane, tot);
     CBX_GLOBAL uint8_t* dst = utf8_offsets(a, c, t, utf8_tile_base(c, t), ex, g.len, tot, lane);
     if (!dst || (CBX_DIAG & 16)) return;
-#ifdef CBX_U8_STAGE
-    g2_stage_store(dst, ex, tot, op.size, g, s_str, lane);
+#ifndef CBX_U8_DIRECT   // (A/B: each lane's own head / dword / tail stores, g2_store)
+    g2_stage_store(dst, ex, tot, op.size, g, true, s_str, lane);
 #else
     g2_store(dst + ex, op.size, g, s_str, lane);
 #endif
@@ -1391,6 +1393,13 @@ __device__ __forceinline__ void str_utf8_pair(const KernelArgs& a, const StrOp& 
     CBX_GLOBAL uint8_t* db = utf8_offsets(a, cb, t, utf8_tile_base(cb, t), exb, (int)lb, tot2 >> 16, lane);
     if (CBX_DIAG & 16) return;
     CBX_GLOBAL uint8_t* d = sa ? (da ? da + exa : nullptr) : (db ? db + exb : nullptr);
+#ifndef CBX_U8_DIRECT
+    if (g2) {   // each column's tile staged and copied out in turn (the lanes of the other segment add nothing)
+        if (da) g2_stage_store(da, exa, tot2 & 0xFFFFu, smax, g, sa, s_str, lane);
+        if (db) g2_stage_store(db, exb, tot2 >> 16, smax, g, !sa, s_str, lane);
+        return;
+    }
+#endif
     if (!d) return;   // (a column whose region overflowed: reported by utf8_offsets)
     if (g2) g2_store(d, smax, g, s_str, lane);
     else utf8_store_direct(d, len, smax * A.pad, q);

@@ -483,9 +483,10 @@ def test_utf8_onepass_code_pages_and_trim(cp, trim, monkeypatch):
 @pytest.mark.parametrize("cp", ["cp037", "common", "ascii"])
 def test_utf8_decode_code_pages_and_trim(cp, trim, staged, monkeypatch):
     """The count + scan + decode Arrow Utf8 path on fields of 1..32 bytes full of trimmable bytes, every
-    trim policy, single- / two-byte code pages and ASCII; staged: the tile-staged payload store
-    (CBX_U8_STAGE: kept bytes OR-ed into a zeroed tile-contiguous LDS staging, copied out in aligned
-    16-byte chunks, byte stores at the ends).  Bit-exact against the oracle."""
+    trim policy, single- / two-byte code pages and ASCII; staged (the default): the tile-staged payload
+    store (kept bytes OR-ed into a zeroed tile-contiguous LDS staging, copied out in aligned 16-byte
+    chunks, byte stores at the ends), else each lane's own stores (CBX_U8_DIRECT).  Bit-exact against
+    the oracle."""
     sizes = [1, 2, 3, 4, 5, 7, 8, 9, 13, 16, 17, 20, 31, 32]
     cb_text = "       01  R.\n" + "".join(f"          05  F{i}  PIC X({s}).\n" for i, s in enumerate(sizes))
     rec = sum(sizes)
@@ -496,8 +497,8 @@ def test_utf8_decode_code_pages_and_trim(cp, trim, staged, monkeypatch):
     raw[rng.random((n, rec)) < 0.33] = pad
     raw[:, ::5][rng.random((n, (rec + 4) // 5)) < 0.2] = 0x05 if cp != "ascii" else 0x09
     data = raw.tobytes()
-    if staged:
-        monkeypatch.setenv("CBX_JIT_DEFINES", "CBX_U8_STAGE=1")
+    if not staged:
+        monkeypatch.setenv("CBX_JIT_DEFINES", "CBX_U8_DIRECT=1")
     kw = dict(string_trimming_policy=trim, jit_min_records=1, string_utf8=True)
     if cp == "ascii":
         kw["is_ebcdic"] = False
