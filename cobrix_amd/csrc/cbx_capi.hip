@@ -2350,6 +2350,61 @@ extern "C" int cbx_hier_list_offsets(const int64_t* d_parent_row, int64_t child_
     return CBX_OK;
 }
 
+// ---- string views -> Arrow Utf8 (cbx_views_to_utf8) ----
+__global__ void views_len_kernel(const u32x4* views, int64_t n, uint32_t* len) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) len[i] = views[i].x;
+    else if (i == n) len[i] = 0;
+}
+
+// One value per thread: its int32 offset and its bytes (inline in the view when <= 12, else at buffer
+// view.z, offset view.w of the slot's region), dword stores where the destination allows.
+__global__ void views_copy_kernel(const u32x4* views, int64_t n, const uint8_t* region, int64_t bb, const int64_t* offs,
+                                  int32_t* offs32, uint8_t* out, int64_t cap, int64_t* size, int32_t* status) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    const int64_t total = offs[n];
+    if (total > cap || total > 0x7fffffffll) {
+        if (i == 0) *status = 1;
+        return;
+    }
+    offs32[i] = (int32_t)offs[i];
+    if (i == n) { *size = total; return; }
+    const u32x4 v = views[i];
+    const uint32_t len = v.x;
+    const uint8_t* src = len <= 12 ? (const uint8_t*)(views + i) + 4 : region + (int64_t)v.z * bb + v.w;
+    uint8_t* dst = out + offs[i];
+    for (uint32_t k = 0; k < len; k++) dst[k] = src[k];
+}
+
+extern "C" int cbx_views_to_utf8(const uint8_t* d_views, int64_t n, const uint8_t* d_region, int64_t buffer_bytes,
+                                 int32_t* d_offsets, uint8_t* d_data, int64_t data_capacity, int64_t* d_size, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n < 0 || !d_offsets || !d_size || (n > 0 && (!d_views || !d_region || buffer_bytes <= 0)) || data_capacity < 0 ||
+        (data_capacity > 0 && !d_data) || ((uintptr_t)d_views & 15))
+        return fail(CBX_E_ARGUMENT, "cbx_views_to_utf8: invalid arguments");
+    const int64_t nsum = scan_sums_len(n + 1);
+    AsyncBlock blk(st);
+    const size_t bytes = (size_t)((n + 1) * 4 + 15) / 16 * 16 + (size_t)(n + 1) * 8 + (size_t)nsum * 8 + 16;
+    HIP_CHECK(hipMallocAsync(&blk.p, bytes, st));
+    uint32_t* len = (uint32_t*)blk.p;
+    int64_t* offs = (int64_t*)((uint8_t*)blk.p + (size_t)((n + 1) * 4 + 15) / 16 * 16);
+    int64_t* sums = offs + (n + 1);
+    int32_t* status = (int32_t*)(sums + nsum);
+    HIP_CHECK(hipMemsetAsync(status, 0, 4, st));
+    const unsigned g = (unsigned)((n + 1 + 255) / 256);
+    hipLaunchKernelGGL(views_len_kernel, dim3(g), dim3(256), 0, st, (const u32x4*)d_views, n, len);
+    device_scan(len, n + 1, offs, sums, st);
+    hipLaunchKernelGGL(views_copy_kernel, dim3(g), dim3(256), 0, st, (const u32x4*)d_views, n, d_region, buffer_bytes,
+                       (const int64_t*)offs, d_offsets, d_data, data_capacity, d_size, status);
+    HIP_CHECK(hipGetLastError());
+    int32_t h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, status, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (h) return fail(CBX_E_CAPACITY, "cbx_views_to_utf8: the payload exceeds data_capacity or an int32 offset");
+    return CBX_OK;
+}
+
 extern "C" int cbx_hier_dependee_counts(const cbx_hier_walk* walk, const cbx_hier_dependee* deps, int32_t n_deps,
                                         const cbx_hier_odo_array* arrays, int32_t n_arrays, int32_t* d_counts, int64_t pitch,
                                         int32_t* d_changed, void* stream) {

@@ -82,8 +82,8 @@ class ReaderParameters:
     string_views: bool = False
     # Arrow Utf8 layout (cbx_plan_options.string_views = 2): int32 offsets relative to each slot's
     # region, a count pass + device scan, then every offset and payload byte written once at its final
-    # place by the decode kernel (no placement pass); takes precedence over string_views except on the
-    # record walk, which writes views
+    # place by the decode kernel (no placement pass); takes precedence over string_views.  The record
+    # walk writes views and converts them (cbx_views_to_utf8)
     string_utf8: bool = False
     # record_length_field (VRLRecordReader.fetchRecordUsingRecordLengthField): records framed by a length
     # field inside them instead of RDW headers (not with is_record_sequence)
@@ -592,6 +592,30 @@ def decode_views(views: np.ndarray, data: bytes, buffer_bytes: int, region: int)
     return out
 
 
+def views_to_utf8(plan: DecodePlan, cols: List[Dict[str, Any]], n_rec: int, stream) -> None:
+    """String-view columns (16-byte views + per-slot regions) -> Arrow Utf8 columns (int32 offsets per
+    slot, payload in the slot's own region), in place in `cols`, on the device: the record walk writes
+    views (one pass with data-dependent offsets); a reader asked for string_utf8 hands out Utf8."""
+    torch = _torch()
+    L = N.load()
+    pitch = 64 * ((n_rec + 63) // 64)
+    for ci, info in enumerate(plan.columns):
+        c = cols[ci]
+        if "views" not in c:
+            continue
+        dev = c["views"].device
+        cap = int(c["capacity"])
+        offs = torch.zeros(info.n_slots * (pitch + 1), dtype=torch.int32, device=dev)
+        sizes = torch.zeros(info.n_slots, dtype=torch.int64, device=dev)
+        data = torch.empty(max(1, cap * info.n_slots), dtype=torch.uint8, device=dev)
+        for s in range(info.n_slots):
+            N.check(L.cbx_views_to_utf8(c["views"].data_ptr() + 16 * s * pitch, n_rec, c["data"].data_ptr() + s * cap,
+                                        max(1, int(c["buffer_bytes"])), offs.data_ptr() + 4 * s * (pitch + 1),
+                                        data.data_ptr() + s * cap, cap, sizes.data_ptr() + 8 * s,
+                                        ctypes.c_void_p(stream.cuda_stream)))
+        cols[ci] = {"validity": c["validity"], "offsets32": offs, "data": data, "sizes": sizes, "capacity": cap}
+
+
 def string_capacity(native_plan, n_rec: int, exact: Optional[Sequence[int]] = None) -> List[int]:
     """Per-column payload bytes per slot: the exact pre-pass result or cbx_string_bound."""
     if exact is not None:
@@ -652,6 +676,29 @@ def check_hierarchical(cb: cbk.Copybook, params: ReaderParameters, plan: DecodeP
     segs = plan.segment_groups
     if len(segs) > 16:
         raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: more than 16 segment redefines")
+    if plan.walk is not None:
+        # the record walk decodes a row from its own bytes only: an OCCURS DEPENDING ON a field that
+        # another record of the hierarchical record registers in the shared dependFields map
+        # (RecordExtractors.scala:224-245 -- a string dependee through occurs_mappings, a
+        # variable_size_occurs layout) is not seen there; reported instead of decoded differently
+        def stmts(g):
+            for c in g.children:
+                yield c
+                if isinstance(c, cbk.Group):
+                    yield from stmts(c)
+        prims = [q for q in stmts(cb.ast) if not isinstance(q, cbk.Group)]
+        root = next((i for i, g in enumerate(segs) if g.parent_segment is None), -1)
+        for st in stmts(cb.ast):
+            ai = plan.array_of_node.get(id(st))
+            if ai is None or st.depending_on is None:
+                continue
+            sa = plan.arrays[ai].segment
+            q = next((q for q in prims if q.is_dependee and q.name == st.depending_on), None)
+            fq = plan.field_of_node.get(id(q)) if q is not None else None
+            sq = plan.fields[fq].segment if fq is not None else sa
+            if sa >= 0 and sq != sa and not (sa == root and sq < 0):
+                raise N.CbxError(N.CBX_E_UNSUPPORTED, f"hierarchical records: {st.name} DEPENDING ON {st.depending_on}, "
+                                                      "a field of another segment, with the record walk")
 
 
 class HierBatch:
@@ -810,6 +857,13 @@ class _BaseReader:
     def spark_schema(self):
         return reader_schema(self.copybook, self.params, self.VARIABLE_LENGTH)
 
+    def _batch(self, n_rec: int, cols: List[Dict[str, Any]], first_record_id: int, gen_id: bool, stream) -> DecodedBatch:
+        """The decoded columns as a batch; with string_utf8 on a record-walk plan (which writes views)
+        its string columns are converted to Arrow Utf8 on the device (cbx_views_to_utf8)."""
+        if self.walk and self.params.string_utf8:
+            views_to_utf8(self.plan, cols, n_rec, stream)
+        return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, gen_id)
+
     def close(self):
         self.native.close()
 
@@ -873,7 +927,7 @@ class FixedLenNestedReader(_BaseReader):
         N.check(L.cbx_decode_fixed(self.native.handle, d_data.data_ptr(), n_rec, stride, self.params.start_offset,
                                    first_record_id, cs, ctypes.c_void_p(st.cuda_stream)))
         N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
-        return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, False)
+        return self._batch(n_rec, cols, first_record_id, False, st)
 
     def decode(self, data: bytes, first_record_id: int = 0) -> DecodedBatch:
         torch = _torch()
@@ -1097,7 +1151,7 @@ class VarLenNestedReader(_BaseReader):
         N.check(L.cbx_decode_selected(self.native.handle, d_data.data_ptr(), n_bytes, ctypes.byref(sel["struct"]),
                                       n_rec, self.params.start_offset, cs, ctypes.c_void_p(st.cuda_stream)))
         N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
-        return DecodedBatch(self.plan, n_rec, cols, 0, self.collapse_root, self.params.generate_record_id)
+        return self._batch(n_rec, cols, 0, self.params.generate_record_id, st)
 
     def decode_device(self, d_data, n_bytes: int, rec_off, rec_len, first_record_id: int = 0,
                       stream=None, exact_strings: bool = False) -> DecodedBatch:
@@ -1121,7 +1175,7 @@ class VarLenNestedReader(_BaseReader):
                                  rec_len.data_ptr(), n_rec, self.params.start_offset, first_record_id, cs,
                                  ctypes.c_void_p(st.cuda_stream)))
         N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
-        return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, self.params.generate_record_id)
+        return self._batch(n_rec, cols, first_record_id, self.params.generate_record_id, st)
 
     def _device_file(self, data: bytes):
         torch = _torch()

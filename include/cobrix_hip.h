@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 14
+#define CBX_ABI_VERSION 15
 
 /* status codes */
 #define CBX_OK 0
@@ -573,6 +573,16 @@ typedef struct {
 int cbx_hier_dependee_counts(const cbx_hier_walk* walk, const cbx_hier_dependee* deps, int32_t n_deps,
                              const cbx_hier_odo_array* arrays, int32_t n_arrays, int32_t* d_counts, int64_t pitch,
                              int32_t* d_changed, void* stream);
+
+/* One string slot in the string-view layout (Utf8View: 16-byte views, long payloads in data buffers of
+ * buffer_bytes each starting at region, cbx_string_view_geometry) -> Arrow Utf8 (int32 offsets
+ * [n + 1] + the payload written contiguously into data, data_capacity bytes).  The record walk
+ * (cbx_plan_set_walk: data-dependent offsets, one pass) writes views; this converts its columns for a
+ * consumer of the Utf8 layout the reference's StringType maps to (SC/schema/CobolSchema.scala:
+ * StringType).  Validity is unchanged (null values are empty).  *d_size (device int64) receives the
+ * payload bytes; CBX_E_CAPACITY when they exceed data_capacity or an int32 offset (Arrow's limit). */
+int cbx_views_to_utf8(const uint8_t* d_views, int64_t n, const uint8_t* d_region, int64_t buffer_bytes,
+                      int32_t* d_offsets, uint8_t* d_data, int64_t data_capacity, int64_t* d_size, void* stream);
 
 /* Text record framing (is_text = true) on the GPU: replaces TextRecordExtractor
  * (cobol-parser/.../reader/extractors/raw/TextRecordExtractor.scala:26-108, chosen by

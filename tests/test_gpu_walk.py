@@ -62,14 +62,30 @@ def _walk_kind(rd) -> int:
     return k.value
 
 
+@pytest.mark.parametrize("utf8", [False, True])
 @pytest.mark.parametrize("var_size", [True, False])
-def test_walk_nested_odo_rdw_vs_oracle(var_size):
+def test_walk_nested_odo_rdw_vs_oracle(var_size, utf8):
+    """utf8: string_utf8 on the walk, which writes views -- its string columns handed out as Arrow Utf8
+    (cbx_views_to_utf8), the same rows and a Utf8 ("u") Arrow export."""
     rnd = random.Random(5 + var_size)
     raw = rdw_file([nested_record(rnd, var_size) for _ in range(3000)])
     opts = {"is_record_sequence": "true", "variable_size_occurs": str(var_size).lower(), "generate_record_id": "true"}
-    rd, p = _reader(NESTED, opts)
+    rd, p = _reader(NESTED, opts, **({"string_utf8": True} if utf8 else {}))
     assert rd.walk
-    rows = rd.read(raw, file_id=1).to_rows()
+    batch = rd.read(raw, file_id=1)
+    if utf8:
+        strs = [c for c in batch.cols if "offsets32" in c or "views" in c]
+        assert strs and all("offsets32" in c for c in strs)
+        from cobrix_amd.arrow_device import export_device
+        _, _, nodes = export_device(batch)
+
+        def fmts(ns):
+            for n in ns:
+                yield n.fmt
+                yield from fmts(n.children)
+        f = set(fmts(nodes))
+        assert "u" in f and "vu" not in f, f
+    rows = batch.to_rows()
     assert _walk_kind(rd) == (3 if _JIT_MIN > 0 else 2)
     exp = RO.var_len_rows(rd.copybook, raw, p, file_id=1)
     assert len(rows) == len(exp) == 3000

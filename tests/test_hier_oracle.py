@@ -126,3 +126,44 @@ def test_sibling_dependees_follow_the_walk_not_the_file():
     (a,), (b,) = par["SIB_A"], par["SIB_B"]
     assert a["A_CNT"] == 3 and len(a["A_ITEMS"]) == 1
     assert b["B_CNT"] == 2 and len(b["B_ITEMS"]) == 3 and len(b["B_P"]) == 1
+
+
+STRDEP_COPYBOOK = """
+       01  REC.
+           05  SEGMENT-ID        PIC X(1).
+           05  PARENT-SEG.
+               10  P-NAME        PIC X(4).
+               10  P-CODE        PIC X(1).
+           05  CHILD-SEG REDEFINES PARENT-SEG.
+               10  C-NAME        PIC X(3).
+               10  C-CODE        PIC X(1).
+               10  C-A OCCURS 0 TO 3 TIMES DEPENDING ON {dep}.
+                   15  C-AV      PIC X(2).
+"""
+STRDEP_OPTS = {"is_record_sequence": "true", "segment_field": "SEGMENT_ID",
+               "redefine_segment_id_map:1": "PARENT-SEG => P", "redefine-segment-id-map:2": "CHILD-SEG => C",
+               "segment-children:1": "PARENT-SEG => CHILD-SEG", "occurs_mappings": '{"C_A":{"A":1,"B":2,"C":3}}'}
+
+
+def test_cross_segment_string_dependee_is_reported():
+    """A child's OCCURS DEPENDING ON a string field of its parent (occurs_mappings) needs the record walk,
+    which decodes each row from its own bytes and cannot see the parent's registration in the shared
+    dependFields map: the reader reports it (CBX_E_UNSUPPORTED) where the reference returns rows --
+    the oracle's walk resolves the parent's "B" to 2 elements -- while the same array DEPENDING ON its
+    own segment's field is accepted."""
+    from cobrix_amd import native as N
+    import cobrix_amd.reader as R
+    p, _ = parse_options(STRDEP_OPTS)
+    cb = parse_copybook_for(STRDEP_COPYBOOK.format(dep="P-CODE"), p)
+    rows = RO.var_len_rows(cb, rdw("PNAMEB") + rdw("CABCZaabbcc"), p)
+    assert len(rows[0]["REC"]["PARENT_SEG"]["CHILD_SEG"][0]["C_A"]) == 2
+    orig = R.NativePlan
+    R.NativePlan = lambda plan: None   # (the check runs before any device allocation)
+    try:
+        with pytest.raises(N.CbxError) as e:
+            R.VarLenNestedReader(STRDEP_COPYBOOK.format(dep="P-CODE"), p)
+        assert e.value.code == N.CBX_E_UNSUPPORTED and "P_CODE" in str(e.value)
+        rd = R.VarLenNestedReader(STRDEP_COPYBOOK.format(dep="C-CODE"), p)
+        assert rd.walk
+    finally:
+        R.NativePlan = orig

@@ -1,11 +1,12 @@
-"""A/B timing of the Arrow Utf8 decode variants on one 50 M-record SYNSTR200 batch (GPU).
+"""A/B timing of decode variants on one 50 M-record SYNSTR200 batch in the Arrow Utf8 layout (GPU), or
+on a SYN200 batch with --syn200.
 
 Each variant is a set of environment knobs read by the library at compile / launch time
 (CBX_JIT_DEFINES, CBX_UTF8_ONEPASS, CBX_LB_SPIN, CBX_MAX_BLOCKS_PER_CU, ...); every variant gets
 a fresh reader (plan), so its kernels are compiled with its knobs.  Prints one JSON line per variant:
 decode-chain ms per call (HIP events), kernel kind, look-back recounts.
 
-usage: python tools/u8_ab.py [records] [VAR=VAL;VAR=VAL ...]...   (a bare "-" = no knobs)
+usage: python tools/u8_ab.py [--syn200] [records] [VAR=VAL;VAR=VAL ...]...   (a bare "-" = no knobs)
 """
 import ctypes
 import json
@@ -22,9 +23,11 @@ def main():
     from cobrix_amd import synth
     from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters, _alloc_columns, string_capacity
     args = sys.argv[1:]
+    syn = "--syn200" in args
+    args = [a for a in args if a != "--syn200"]
     n = int(args[0]) if args and args[0].isdigit() else 50_000_000
     variants = [a for a in args if not a.isdigit()] or ["-"]
-    rec = synth.synstr200(n, seed=20261017, device="cuda").view(-1)
+    rec = (synth.syn200(n, seed=20261015, device="cuda") if syn else synth.synstr200(n, seed=20261017, device="cuda")).view(-1)
     torch.cuda.synchronize()
     L = N.load()
     st = torch.cuda.current_stream()
@@ -35,7 +38,8 @@ def main():
         os.environ.update(base_env)
         knobs = {} if v == "-" else dict(kv.split("=", 1) for kv in v.split(";") if kv)
         os.environ.update(knobs)
-        rd = FixedLenNestedReader(synth.SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_utf8=True))
+        rd = (FixedLenNestedReader(synth.SYN200_COPYBOOK, ReaderParameters(string_views=True)) if syn else
+              FixedLenNestedReader(synth.SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_utf8=True)))
         h = rd.native.handle
         cols, cs = _alloc_columns(rd.plan, n, string_capacity(rd.native, n), rec.device)
         N.check(L.cbx_plan_set_profiling(h, 1))
