@@ -957,7 +957,10 @@ def main():
         absent += absent_element_bytes(plan, cols, m) if has_lists else 0
     dec_avg_ms = sum(dec[: nc.value]) / max(1, args.steps)     # per step: every call of the step
     fix_avg_ms = sum(fix[: nc.value]) / max(1, args.steps)
-    achieved = alg / (dec_avg_ms * 1e-3) / 1e9
+    # the decode chain: the record kernel (+ its Utf8 count pass and scan, list kernels) and the fixup
+    # pass of the values it deferred -- all of cbx_decode_*'s device work
+    chain_ms = dec_avg_ms + fix_avg_ms
+    achieved = alg / (chain_ms * 1e-3) / 1e9
     kind = ctypes.c_int32(0)
     N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
     kname = {1: "cbx_jit_decode (copybook-specialised, hipRTC)", 2: "cbx::walk_kernel (record walk)"}.get(
@@ -967,6 +970,7 @@ def main():
     lists = any(c.list_array >= 0 for c in plan.columns)
     if lists:   # the OCCURS list elements: the element-parallel kernel launched right after the decode kernel
         kname += " + cbx::list_kernel (OCCURS lists; decode_kernel time covers both)"
+    kname += " + cbx::fixup_kernel (deferred values; post_kernels time)"
     tag = f"{args.workload}_{strings}{'' if args.occurs == 'lists' else '_slots'}_{n_rec}"
     traffic, traffic_src = measured_traffic(tag)
     kernel_ms = {"decode_kernel": round(dec_avg_ms, 4), "post_kernels": round(fix_avg_ms, 4)}
@@ -1020,12 +1024,13 @@ def main():
                          "frac_of_measured_peak": round(achieved / HBM_MEASURED_GBS, 4),
                          "algorithmic_bytes_per_launch": alg,
                          **({"absent_element_bytes": absent, "moved_bytes_per_launch": alg - absent,
-                             "frac_moved_bytes": round((alg - absent) / (dec_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "frac_moved_bytes": round((alg - absent) / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "note": "8(d) counts the input records whole (absent ODO elements included); "
                                      "frac_moved_bytes counts what the kernels must read and write"}
                             if absent else {}),
                          "layout_bytes_per_launch": lay, "layout_overhead": lay - alg,
-                         "timing": "HIP events on the launch stream (cbx_plan_kernel_times), average of the timed steps",
+                         "timing": "HIP events on the launch stream (cbx_plan_kernel_times): decode_kernel + post_kernels "
+                                   "(the fixup pass), average of the timed steps",
                          "traffic": traffic, "traffic_source": traffic_src},
         }
         if e2e is not None:
