@@ -148,14 +148,18 @@ def _lenfield_file(rng, n, bad_at=None):
     return bytes(out)
 
 
+@pytest.mark.parametrize("chunk", [None, "64"])
 @pytest.mark.parametrize("start,end,adj", [(0, 0, 0), (3, 0, 3), (0, 2, -2), (2, 1, 1)])
-def test_record_length_field_framing_vs_oracle(start, end, adj):
+def test_record_length_field_framing_vs_oracle(start, end, adj, chunk, monkeypatch):
     """record_length_field (VRLRecordReader.fetchRecordUsingRecordLengthField) on the GPU: records
     whose DISPLAY length field gives the record size (+ rdw_adjustment), record_start/end_offset
-    bytes around each record, a truncated last record -- framing and rows equal the oracle's."""
+    bytes around each record, a truncated last record -- framing and rows equal the oracle's, at the
+    default chunking and with 64-byte chunks (cbx_chain.h: every record chain crosses chunks)."""
     import dataclasses
     from cobrix_amd.options import parse_options
     from cobrix_amd.reader import VarLenNestedReader
+    if chunk is not None:
+        monkeypatch.setenv("CBX_CHAIN_CHUNK", chunk)
     rng = np.random.default_rng(start * 7 + end)
     recs = []
     for i in range(3000):
