@@ -206,7 +206,7 @@ WORKLOADS = {
     # C3 is quoted on 64 GB strong-scaled: 320 M records over the job, decoded in
     # batches whose int32 Utf8 offsets fit (an Arrow chunked array: one chunk per batch and column)
     "synstr200": dict(records=320_000_000, config="C3", strings="offsets", strong=True,
-                      batch_records=50_000_000,
+                      batch_records=50_000_000, pipeline="0,0",
                       desc="SYNSTR200: fixed-length 200-byte records, 10 x PIC X(20) cp037 -> UTF-8, trim both "
                            "-- BASELINE config C3 (64 GB strong-scaled over the job)",
                       data="synthetic (cobrix_amd/synth.py SYNSTR200: lengths 0-20, 25% accented, 10% leading "
@@ -241,7 +241,7 @@ class _Fixed:
     records (every batch its own output columns: for the Utf8 layout one Arrow array per batch and
     column -- a chunked array -- whose int32 offsets fit its slot region)."""
 
-    def __init__(self, name, n_rec, dev, rank, window, strings, batch_records=0, record_base=None):
+    def __init__(self, name, n_rec, dev, rank, window, strings, batch_records=0, record_base=None, pipeline=""):
         import torch
         from cobrix_amd.reader import FixedLenNestedReader, ReaderParameters
         from cobrix_amd import synth
@@ -257,6 +257,9 @@ class _Fixed:
             params = ReaderParameters(window_bytes=window, ebcdic_code_page="cp037", **lay)
         torch.cuda.synchronize()
         self.rd = FixedLenNestedReader(cb, params)
+        # --pipeline C,D: odd batches on a second plan and stream (cbx_plan_pipeline)
+        self.pipe = tuple(int(x) for x in pipeline.split(",")) if pipeline else None
+        self.rdB = FixedLenNestedReader(cb, params) if self.pipe and self.batch < n_rec else None
         self.n_rec, self.in_bytes, self.dev = n_rec, n_rec * self.stride, dev
         self.record_base = rank * n_rec if record_base is None else record_base
         self.shard_note = f"records [{self.record_base}, {self.record_base + n_rec}) of the job, Record_Id base static"
@@ -267,6 +270,15 @@ class _Fixed:
         from cobrix_amd import native as N
         from cobrix_amd.reader import _alloc_columns, string_capacity
         self.L, self.h, self.stream = N.load(), self.rd.native.handle, ctypes.c_void_p(stream.cuda_stream)
+        self.targets = [(self.h, self.stream)]
+        if self.rdB is not None:
+            import torch
+            self.streamB = torch.cuda.Stream(self.dev)
+            hB = self.rdB.native.handle
+            N.check(self.L.cbx_plan_pipeline(self.h, hB, self.pipe[0], self.pipe[1]))
+            self.targets.append((hB, ctypes.c_void_p(self.streamB.cuda_stream)))
+            self.shard_note += (f"; batches alternating between two plans on two streams (cbx_plan_pipeline: count pass "
+                                f"beside the other plan's decode, {self.pipe[0]} / {self.pipe[1]} workgroups per CU)")
         # parts: (first record, records, columns, cbx_column table) per batch
         self.parts = []
         for r0 in range(0, self.n_rec, self.batch):
@@ -276,14 +288,18 @@ class _Fixed:
         self.cols, self.cs = self.parts[0][2], self.parts[0][3]
 
     def calls_per_step(self) -> int:
-        return len(self.parts)
+        return (len(self.parts) + len(self.targets) - 1) // len(self.targets)   # (the profiled plan's calls)
+
+    def pipelined(self) -> bool:
+        return len(self.targets) > 1
 
     def step(self, world=1):
         from cobrix_amd import native as N
         # fixed-length shards: rank r holds records [r n, (r + 1) n) -- the Record_Id base is static
-        for r0, m, _, cs in self.parts:
-            N.check(self.L.cbx_decode_fixed(self.h, self.rec.data_ptr() + r0 * self.stride, m, self.stride, 0,
-                                            self.record_base + r0, cs, self.stream))
+        for i, (r0, m, _, cs) in enumerate(self.parts):
+            h, st = self.targets[i % len(self.targets)]
+            N.check(self.L.cbx_decode_fixed(h, self.rec.data_ptr() + r0 * self.stride, m, self.stride, 0,
+                                            self.record_base + r0, cs, st))
         return None
 
     def verify(self, world):
@@ -832,6 +848,11 @@ def main():
     ap.add_argument("--strings", default="", choices=["", "views", "offsets", "large"],
                     help="string column layout (default per workload): Arrow string views, Arrow Utf8 offsets "
                          "(in place after a count pass) or Arrow large-string offsets (placement pass)")
+    ap.add_argument("--pipeline", default="",
+                    help="C,D: a fixed-length Utf8 job's batches alternate between two plans on two streams "
+                         "(cbx_plan_pipeline), one plan's count pass beside the other's decode, the count / decode "
+                         "kernels capped at C / D resident workgroups per CU (0: default occupancy); default per "
+                         "workload (C3: 0,0 -- 53.3 -> 51.3 ms per 64 GB step; capped forms were slower), '-': off")
     ap.add_argument("--occurs", default="lists", choices=["lists", "slots"],
                     help="OCCURS DEPENDING ON layout: Arrow lists (present elements) or one slot row per element")
     ap.add_argument("--seed-mb", type=int, default=100, choices=[100, 32],
@@ -888,7 +909,9 @@ def main():
 
     progress(f"generating {n_req} records per GPU on {dev} (world {world})")
     if args.workload in ("syn200", "synstr200"):
-        job = _Fixed(args.workload, n_req, dev, rank, args.window, strings, batch, rec_base)
+        pipe = args.pipeline or W.get("pipeline", "")
+        job = _Fixed(args.workload, n_req, dev, rank, args.window, strings, batch, rec_base,
+                     pipeline=pipe if strings == "offsets" and pipe != "-" else "")
     else:
         job = _VarLen(args.workload, n_req, dev, rank, world, args.window, strings, args.occurs == "lists",
                       args.seed_mb, batch)
@@ -919,6 +942,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     N.check(L.cbx_plan_check(h, job.stream))
+    for hx, sx in getattr(job, "targets", [])[1:]:   # the pipelined second plan's calls
+        N.check(L.cbx_plan_check(hx, sx))
     calls = args.steps * (job.calls_per_step() if hasattr(job, "calls_per_step") else 1)
     dec = (ctypes.c_float * calls)()
     fix = (ctypes.c_float * calls)()
@@ -960,6 +985,9 @@ def main():
     # the decode chain: the record kernel (+ its Utf8 count pass and scan, list kernels) and the fixup
     # pass of the values it deferred -- all of cbx_decode_*'s device work
     chain_ms = dec_avg_ms + fix_avg_ms
+    piped = hasattr(job, "pipelined") and job.pipelined()
+    if piped:   # two plans' chains overlap on two streams: the step's wall time is the chain
+        chain_ms = ms_per_step
     achieved = alg / (chain_ms * 1e-3) / 1e9
     kind = ctypes.c_int32(0)
     N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
@@ -1029,8 +1057,10 @@ def main():
                                      "frac_moved_bytes counts what the kernels must read and write"}
                             if absent else {}),
                          "layout_bytes_per_launch": lay, "layout_overhead": lay - alg,
-                         "timing": "HIP events on the launch stream (cbx_plan_kernel_times): decode_kernel + post_kernels "
-                                   "(the fixup pass), average of the timed steps",
+                         "timing": ("wall time of the step: two plans' count + decode chains overlapped on two streams "
+                                    "(cbx_plan_pipeline)") if piped else
+                                   ("HIP events on the launch stream (cbx_plan_kernel_times): decode_kernel + post_kernels "
+                                    "(the fixup pass), average of the timed steps"),
                          "traffic": traffic, "traffic_source": traffic_src},
         }
         if e2e is not None:

@@ -157,6 +157,11 @@ struct cbx_plan {
     int32_t* d_wvslot = nullptr;
     int32_t n_vslots = 0;
     int32_t fid_col = -1, rid_col = -1;
+    // cbx_plan_pipeline: Utf8 batches of two plans on two streams, one plan's count pass beside the
+    // other's decode (each call waits for the peer's last count pass before its own, and marks its own)
+    cbx_plan* pipe_peer = nullptr;
+    hipEvent_t pipe_done = nullptr;
+    int pipe_count_bpc = 0, pipe_decode_bpc = 0;
     // profiling: HIP events around the decode kernel and the post passes of every call (no sync)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;     // free events
@@ -596,6 +601,8 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
     (void)hipFree(P->d_wvbase); (void)hipFree(P->d_wvcol); (void)hipFree(P->d_wvslot);
     for (auto& e : P->ev_pool) (void)hipEventDestroy(e);
     for (auto& c : P->ev_calls) for (auto& e : c.e) if (e) (void)hipEventDestroy(e);
+    if (P->pipe_peer) P->pipe_peer->pipe_peer = nullptr;
+    if (P->pipe_done) (void)hipEventDestroy(P->pipe_done);
     delete P;
 }
 
@@ -1010,10 +1017,15 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     // numerics) and the windowed C4/C5 layouts gain from every extra resident workgroup
     if (!coop && contig && S.sops.size() >= S.nops.size() && S.sops.size() > 0) blocks_per_cu = std::min(blocks_per_cu, 4);
     if (const char* e = getenv("CBX_MAX_BLOCKS_PER_CU")) blocks_per_cu = std::max(1, std::min(blocks_per_cu, atoi(e)));   // tuning
+    const bool piped = P->pipe_peer && mode == 0 && P->packed && P->n_seq > 0;
+    if (piped && P->pipe_decode_bpc > 0) blocks_per_cu = std::min(blocks_per_cu, P->pipe_decode_bpc);
     const int64_t blocks_needed = coop ? n_tiles : (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t grid = std::min<int64_t>(blocks_needed, (int64_t)P->num_cus * blocks_per_cu);
     const bool prof = P->profiling && mode == 0;
     cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};
+    // pipelined with a peer plan: this call's count pass follows the peer's last one (so it runs beside
+    // the peer's decode), before the timing starts
+    if (piped && P->pipe_peer->pipe_done) HIP_CHECK(hipStreamWaitEvent(st, P->pipe_peer->pipe_done, 0));
     if (prof) {
         for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
         HIP_CHECK(hipEventRecord(ce.e[0], st));
@@ -1042,6 +1054,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         const int kind = P->last_kind;
         if ((r = launch(P, c, columns, 1, st))) return r;
         P->last_kind = kind;
+        if (piped) HIP_CHECK(hipEventRecord(P->pipe_done, st));
     } else if (mode == 0 && P->packed && P->n_seq > 0) {
         KernelArgs ac = a;
         ac.mode = 1;
@@ -1060,6 +1073,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
         int cbpc = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / clds));
         if (ce2 == hipSuccess && cocc > 0) cbpc = std::min(cbpc, cocc);
         if (const char* e = getenv("CBX_MAX_BLOCKS_PER_CU")) cbpc = std::max(1, std::min(cbpc, atoi(e)));   // tuning
+        if (piped && P->pipe_count_bpc > 0) cbpc = std::min(cbpc, P->pipe_count_bpc);
         const int64_t cneeded = ccoop ? n_tiles : (n_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
         const int64_t cgrid = std::min<int64_t>(cneeded, (int64_t)P->num_cus * cbpc);
         if (cfn) {
@@ -1070,6 +1084,7 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
             HIP_CHECK(hipGetLastError());
         }
         if ((r = string_scan(P, n_tiles, st))) return r;
+        if (piped) HIP_CHECK(hipEventRecord(P->pipe_done, st));
     }
     if (jfn) {
         void* kargs[] = {&a};
@@ -1412,6 +1427,23 @@ extern "C" int cbx_plan_lookback_stats(cbx_plan* P, int64_t* recounts, void* str
     HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
     *recounts = s[1];
     HIP_CHECK(hipMemsetAsync(P->d_status + 1, 0, 2 * sizeof(int32_t), (hipStream_t)stream));
+    return CBX_OK;
+}
+
+extern "C" int cbx_plan_pipeline(cbx_plan* A, cbx_plan* B, int32_t count_blocks_per_cu, int32_t decode_blocks_per_cu) {
+    if (!A || A == B || count_blocks_per_cu < 0 || decode_blocks_per_cu < 0)
+        return fail(CBX_E_ARGUMENT, "cbx_plan_pipeline: invalid arguments");
+    if (A->pipe_peer) { A->pipe_peer->pipe_peer = nullptr; A->pipe_peer = nullptr; }
+    A->pipe_count_bpc = A->pipe_decode_bpc = 0;
+    if (!B) return CBX_OK;
+    if (B->pipe_peer) { B->pipe_peer->pipe_peer = nullptr; B->pipe_peer = nullptr; }
+    for (cbx_plan* P : {A, B}) {
+        if (!P->pipe_done) HIP_CHECK(hipEventCreateWithFlags(&P->pipe_done, hipEventDisableTiming));
+        P->pipe_count_bpc = count_blocks_per_cu;
+        P->pipe_decode_bpc = decode_blocks_per_cu;
+    }
+    A->pipe_peer = B;
+    B->pipe_peer = A;
     return CBX_OK;
 }
 

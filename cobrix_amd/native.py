@@ -43,8 +43,8 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
                     "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs",
                     "cbx_plan_set_record_base", "cbx_frame_length_field", "cbx_plan_set_odo_counts",
-                    "cbx_plan_lookback_stats", "cbx_hier_dependee_counts", "cbx_views_to_utf8")
-ABI_VERSION = 15
+                    "cbx_plan_lookback_stats", "cbx_hier_dependee_counts", "cbx_views_to_utf8", "cbx_plan_pipeline")
+ABI_VERSION = 16
 
 
 class NativeLibraryError(RuntimeError):
@@ -224,7 +224,8 @@ def load():
                      ("cbx_frame_length_field", [P, P, i64, i32, i32, i32, i32, P, P, i64, P, P]),
                      ("cbx_plan_set_odo_counts", [P, P, i64]),
                      ("cbx_hier_dependee_counts", [P, P, i32, P, i32, P, i64, P, P]),
-                     ("cbx_views_to_utf8", [P, i64, P, i64, P, P, i64, P, P])):
+                     ("cbx_views_to_utf8", [P, i64, P, i64, P, P, i64, P, P]),
+                     ("cbx_plan_pipeline", [P, P, i32, i32])):
         if hasattr(L, name):   # (diagnostic builds of older revisions lack the newest entry points)
             getattr(L, name).argtypes = at
     if L.cbx_abi_version() != ABI_VERSION:

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 15
+#define CBX_ABI_VERSION 16
 
 /* status codes */
 #define CBX_OK 0
@@ -224,6 +224,14 @@ typedef struct {
 typedef struct cbx_plan cbx_plan;
 
 int32_t cbx_abi_version(void);
+
+/* Pipelined Arrow Utf8 batches: two plans of the same layout decoding alternate batches on two
+ * streams.  Each cbx_decode_fixed / cbx_decode_var call of a linked plan (Utf8 layout) makes its
+ * stream wait for the peer plan's last count pass + scan before its own, and marks its own end, so
+ * one plan's count pass (HBM-read bound) runs beside the other's decode (issue bound) instead of
+ * after it; count_blocks_per_cu / decode_blocks_per_cu (0: the default occupancy) cap the resident
+ * workgroups per CU of the two kernels so both fit on a CU at once.  B = NULL unlinks A. */
+int cbx_plan_pipeline(cbx_plan* a, cbx_plan* b, int32_t count_blocks_per_cu, int32_t decode_blocks_per_cu);
 const char* cbx_last_error(void);
 
 /* Build a plan from the flattened copybook.  Copies the tables to device memory. */

@@ -760,3 +760,47 @@ def test_var_utf8_batches_vs_oracle():
         assert not errs, (r0, errs)
         rid = batch.cols[rd.plan.record_id_column]["values"][: r1 - r0].cpu().numpy()
         assert np.array_equal(rid, np.arange(r0, r1)), r0
+
+
+@pytest.mark.parametrize("caps", [(0, 0), (1, 7)])
+def test_utf8_pipelined_plans_vs_single(caps):
+    """cbx_plan_pipeline: batches alternating between two linked plans on two streams (each call's count
+    pass after the peer's, beside the peer's decode; the kernels' workgroups per CU capped) give the same
+    columns as one plan decoding the batches in turn, and as the oracle on a sample."""
+    import ctypes
+    from cobrix_amd import native as N
+    from cobrix_amd.reader import _alloc_columns, string_capacity, DecodedBatch
+    from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
+    from parity import compare_sample
+    n, nb = 2_000_000, 5
+    rec = synstr200(n, seed=31, device="cuda").view(-1)
+    prm = ReaderParameters(ebcdic_code_page="cp037", string_utf8=True)
+    A, B, S = (FixedLenNestedReader(SYNSTR200_COPYBOOK, prm) for _ in range(3))
+    L = N.load()
+    N.check(L.cbx_plan_pipeline(A.native.handle, B.native.handle, caps[0], caps[1]))
+    s1, s2 = torch.cuda.current_stream(), torch.cuda.Stream()
+    m = n // nb
+    outs, refs = [], []
+    for i in range(nb):
+        h, st = (A.native.handle, s1) if i % 2 == 0 else (B.native.handle, s2)
+        cols, cs = _alloc_columns(A.plan, m, string_capacity(A.native, m), rec.device)
+        N.check(L.cbx_decode_fixed(h, rec.data_ptr() + i * m * 200, m, 200, 0, i * m, cs, ctypes.c_void_p(st.cuda_stream)))
+        outs.append(cols)
+    torch.cuda.synchronize()
+    for rd in (A, B):
+        N.check(L.cbx_plan_check(rd.native.handle, ctypes.c_void_p(s1.cuda_stream)))
+    for i in range(nb):
+        cols, cs = _alloc_columns(S.plan, m, string_capacity(S.native, m), rec.device)
+        N.check(L.cbx_decode_fixed(S.native.handle, rec.data_ptr() + i * m * 200, m, 200, 0, i * m, cs,
+                                   ctypes.c_void_p(s1.cuda_stream)))
+        refs.append(cols)
+    torch.cuda.synchronize()
+    for i in range(nb):
+        for a, b in zip(outs[i], refs[i]):
+            assert torch.equal(a["offsets32"], b["offsets32"]) and torch.equal(a["validity"], b["validity"])
+            assert torch.equal(a["data"][: int(b["sizes"][0])], b["data"][: int(b["sizes"][0])])
+    batch = DecodedBatch(A.plan, m, outs[3], 3 * m, False, False)
+    idx = np.unique(np.random.default_rng(2).integers(0, m, 2000))
+    sample = rec.view(n, 200)[torch.as_tensor(3 * m + idx, device="cuda")].cpu().numpy().tobytes()
+    assert not compare_sample(batch, idx, O.decode_fixed(A.copybook, sample))
+    N.check(L.cbx_plan_pipeline(A.native.handle, None, 0, 0))
