@@ -815,6 +815,7 @@ class _BaseReader:
 
     def __init__(self, copybook_contents: str, params: ReaderParameters):
         self.params = params
+        self.copybook_contents = copybook_contents
         self.copybook = parse_copybook_for(copybook_contents, params)
         var = self.VARIABLE_LENGTH
         # the fixed-length reader only uses the redefine map (FixedLenNestedRowIterator.scala:50-70);
@@ -865,6 +866,11 @@ class _BaseReader:
         return DecodedBatch(self.plan, n_rec, cols, first_record_id, self.collapse_root, gen_id)
 
     def close(self):
+        peer = getattr(self, "_peer", None)
+        if peer is not None:   # (the pipelined second plan of decode_batches)
+            N.check(N.load().cbx_plan_pipeline(self.native.handle, None, 0, 0))
+            peer.close()
+            self._peer = None
         self.native.close()
 
 
@@ -928,6 +934,42 @@ class FixedLenNestedReader(_BaseReader):
                                    first_record_id, cs, ctypes.c_void_p(st.cuda_stream)))
         N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
         return self._batch(n_rec, cols, first_record_id, False, st)
+
+    def decode_batches(self, d_data, n_bytes: int, batch_records: int, first_record_id: int = 0) -> List[DecodedBatch]:
+        """A split resident in HBM decoded as consecutive batches of <= batch_records records (the
+        Arrow Utf8 layout's int32 offsets cap a batch; a consumer takes one Arrow array per batch --
+        a chunked array).  In the Utf8 layout the batches alternate between this plan and a second
+        one on a second stream, linked by cbx_plan_pipeline: a batch's count pass runs beside the
+        previous batch's decode (C3: 53.3 -> 51.3 ms per 64 GB).  Other layouts decode in turn."""
+        torch = _torch()
+        stride = self.get_record_size()
+        n_rec = n_bytes // stride
+        if n_rec == 0:
+            return [self.decode_device(d_data, 0, first_record_id)]
+        bs = batch_records if batch_records > 0 else n_rec
+        L = N.load()
+        s0 = torch.cuda.current_stream()
+        targets = [(self, s0)]
+        if self.params.string_utf8 and not self.walk and n_rec > bs:
+            if getattr(self, "_peer", None) is None:
+                self._peer = FixedLenNestedReader(self.copybook_contents, self.params)
+                N.check(L.cbx_plan_pipeline(self.native.handle, self._peer.native.handle, 0, 0))
+            targets.append((self._peer, torch.cuda.Stream(d_data.device)))
+            targets[1][1].wait_stream(s0)   # (the data and any earlier work on the first stream)
+        out, pending = [], []
+        for k, r0 in enumerate(range(0, n_rec, bs)):
+            rd, st = targets[k % len(targets)]
+            m = min(bs, n_rec - r0)
+            cols, cs = _alloc_columns(rd.plan, m, string_capacity(rd.native, m), d_data.device)
+            N.check(L.cbx_decode_fixed(rd.native.handle, d_data.data_ptr() + r0 * stride, m, stride, self.params.start_offset,
+                                       first_record_id + r0, cs, ctypes.c_void_p(st.cuda_stream)))
+            pending.append((cols, cs))   # (the column table lives until the calls are checked)
+            out.append((m, cols, first_record_id + r0, st))
+        for rd, st in targets:
+            N.check(L.cbx_plan_check(rd.native.handle, ctypes.c_void_p(st.cuda_stream)))
+        if len(targets) > 1:
+            s0.wait_stream(targets[1][1])
+        return [self._batch(m, cols, fid, False, st) for m, cols, fid, st in out]
 
     def decode(self, data: bytes, first_record_id: int = 0) -> DecodedBatch:
         torch = _torch()

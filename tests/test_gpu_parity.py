@@ -804,3 +804,26 @@ def test_utf8_pipelined_plans_vs_single(caps):
     sample = rec.view(n, 200)[torch.as_tensor(3 * m + idx, device="cuda")].cpu().numpy().tobytes()
     assert not compare_sample(batch, idx, O.decode_fixed(A.copybook, sample))
     N.check(L.cbx_plan_pipeline(A.native.handle, None, 0, 0))
+
+
+def test_decode_batches_pipelined_utf8():
+    """FixedLenNestedReader.decode_batches in the Utf8 layout: batches alternate between the reader's
+    plan and a pipelined peer (cbx_plan_pipeline) on two streams; every batch equals decode_device of
+    the same records, and the views layout decodes the same batches in turn."""
+    from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
+    n, bs = 700_003, 150_000
+    rec = synstr200(n, seed=41, device="cuda").view(-1)
+    rd = FixedLenNestedReader(SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_utf8=True))
+    batches = rd.decode_batches(rec, n * 200, bs, first_record_id=10)
+    assert [b.n_rec for b in batches] == [bs] * 4 + [n - 4 * bs]
+    ref = FixedLenNestedReader(SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_utf8=True))
+    for k, b in enumerate(batches):
+        r = ref.decode_device(rec[k * bs * 200: min(n, (k + 1) * bs) * 200], b.n_rec * 200, first_record_id=10 + k * bs)
+        for x, y in zip(b.cols, r.cols):
+            assert torch.equal(x["offsets32"], y["offsets32"]) and torch.equal(x["validity"], y["validity"])
+            assert torch.equal(x["data"][: int(y["sizes"][0])], y["data"][: int(y["sizes"][0])])
+    assert batches[4].to_rows()[:50] == ref.decode_device(rec[4 * bs * 200:], (n - 4 * bs) * 200).to_rows()[:50]
+    rd.close()
+    vw = FixedLenNestedReader(SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_views=True))
+    vb = vw.decode_batches(rec, n * 200, bs)
+    assert sum(b.n_rec for b in vb) == n and vb[1].to_rows()[:20] == batches[1].to_rows()[:20]
