@@ -405,7 +405,8 @@ class _VarLen:
     RDW framing of the run seeded by its entries + (N > 1) one device all-gather of the run's record
     count, whose exclusive prefix is the run's Record_Id base + decode."""
 
-    def __init__(self, name, n_rec, dev, rank, world, window, strings, lists=True, seed_mb=100, batch_records=0):
+    def __init__(self, name, n_rec, dev, rank, world, window, strings, lists=True, seed_mb=100, batch_records=0,
+                 pieces=1):
         import torch
         import torch.distributed as dist
         from cobrix_amd import native as N
@@ -422,6 +423,8 @@ class _VarLen:
             cb, segs = synth.WIDE_ODO_COPYBOOK, synth.WIDE_ODO_SEGMENTS
         self.dev, self.world, self.rank = dev, world, rank
         self.batch = batch_records
+        self.n_pieces = pieces
+        self.seed_recs = None   # records of the run before each seed (the setup framing), for pieces
         L = N.load()
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         opts = dict(is_record_sequence=True, segment_field="SEGMENT-ID", segment_id_redefine_map=segs,
@@ -508,6 +511,8 @@ class _VarLen:
         self.raw = full[lo:hi].clone() if world > 1 else full
         self.in_bytes = hi - lo
         self.seeds = [e.offset_from - lo for e in entries[k0:k1]] or [0]
+        sd_abs = torch.tensor([lo + x for x in self.seeds], dtype=hdr_off.dtype, device=dev)
+        self.seed_recs = [int(v) - self.expected_base for v in torch.searchsorted(hdr_off, sd_abs).tolist()]
         self.n_entries_file, self.entry_run = len(entries), (k0, k1)
         self.setup_bytes_held = int(self.raw.numel())
         del full, off, ln, hdr_off, idx_rd
@@ -531,13 +536,44 @@ class _VarLen:
         # decodes the run in batches whose int32 offsets fit (one Arrow array per batch and column)
         self.batch = self.batch if 0 < self.batch < self.n_rec else max(1, self.n_rec)
         self.parts = []
-        for r0 in range(0, max(1, self.n_rec), self.batch):
-            m = min(self.batch, self.n_rec - r0)
-            cols, cs = _alloc_columns(self.rd.plan, m, string_capacity(self.rd.native, m), self.dev)
-            self.parts.append((r0, m, cols, cs))
+        self.pieces = []
+        if self.n_pieces > 1 and self.seed_recs is not None and len(self.seeds) > 1:
+            # pieces: runs of whole index entries, each framed from its own entries and decoded as its
+            # own batch (as the reference reads one partition per index entry), the framing of the
+            # next pieces on a second stream beside the decode of this one
+            # consecutive entries to a piece while it stays within n_rec / pieces records (and the batch)
+            target = min(self.batch, -(-self.n_rec // self.n_pieces))
+            ends = self.seed_recs[1:] + [self.n_rec]
+            cuts = [0]
+            for j in range(1, len(self.seeds)):
+                if ends[j] - self.seed_recs[cuts[-1]] > target:
+                    cuts.append(j)
+            cuts.append(len(self.seeds))
+            for i in range(len(cuts) - 1):
+                a = self.seeds[cuts[i]]
+                b = self.seeds[cuts[i + 1]] if cuts[i + 1] < len(self.seeds) else self.in_bytes
+                r0 = self.seed_recs[cuts[i]]
+                r1 = self.seed_recs[cuts[i + 1]] if cuts[i + 1] < len(self.seeds) else self.n_rec
+                if r1 - r0 > self.batch and self.batch < self.n_rec:
+                    raise RuntimeError(f"piece of {r1 - r0} records exceeds the batch of {self.batch}")
+                sd = (ctypes.c_int64 * (cuts[i + 1] - cuts[i]))(*[x - a for x in self.seeds[cuts[i]:cuts[i + 1]]])
+                cols, cs = _alloc_columns(self.rd.plan, r1 - r0, string_capacity(self.rd.native, r1 - r0), self.dev)
+                self.parts.append((r0, r1 - r0, cols, cs))
+                self.pieces.append(dict(a=a, b=b, sd=sd, r0=r0, m=r1 - r0,
+                                        state=torch.zeros(3, dtype=torch.int64, device=self.dev),
+                                        framed=torch.cuda.Event(), decoded=torch.cuda.Event()))
+            self.fstream = torch.cuda.Stream(self.dev)
+            self.fstream_p = ctypes.c_void_p(self.fstream.cuda_stream)
+            self.shard_note += (f"; {len(self.pieces)} pieces of whole index entries, each framed (second stream) "
+                                f"and decoded as its own batch, the framing beside the previous piece's decode")
+        else:
+            for r0 in range(0, max(1, self.n_rec), self.batch):
+                m = min(self.batch, self.n_rec - r0)
+                cols, cs = _alloc_columns(self.rd.plan, m, string_capacity(self.rd.native, m), self.dev)
+                self.parts.append((r0, m, cols, cs))
+            if len(self.parts) > 1:
+                self.shard_note += f"; decoded in {len(self.parts)} batches of <= {self.batch} records"
         self.cols, self.cs = self.parts[0][2], self.parts[0][3]
-        if len(self.parts) > 1:
-            self.shard_note += f"; decoded in {len(self.parts)} batches of <= {self.batch} records"
         self.fr0, self.fr1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # the run's Record_Id base lives on the device: the decode kernels read it (cbx_plan_set_record_base)
         self.base = torch.zeros(1, dtype=torch.int64, device=self.dev)
@@ -550,6 +586,8 @@ class _VarLen:
         # no host wait inside the step: the framing's count stays on the device (cbx_frame_rdw_async),
         # is all-gathered there, and the decode runs over the count the index run predicts (checked
         # against the framing's after the timed steps, cbx_frame_rdw_state)
+        if self.pieces:
+            return self._step_pieces()
         self.fr0.record()
         N.check(self.L.cbx_frame_rdw_async(self.raw.data_ptr(), self.in_bytes, self.sd, len(self.seeds),
                                            ctypes.byref(self.prm), self.off.data_ptr(), self.ln.data_ptr(), self.cap,
@@ -562,6 +600,40 @@ class _VarLen:
             N.check(self.L.cbx_decode_var(self.h, self.raw.data_ptr(), self.in_bytes, self.off.data_ptr() + 8 * r0,
                                           self.ln.data_ptr() + 4 * r0, m, 0, r0, cs, self.stream))
         return (self.fr0, self.fr1)
+
+    def _step_pieces(self):
+        """The run as pieces of index entries: piece k's framing on the second stream (after the previous
+        step's decode of piece k read its offsets), piece k's decode on the launch stream after it."""
+        import torch
+        from cobrix_amd import native as N
+        cur = torch.cuda.current_stream()
+        base = self.raw.data_ptr()
+        for i, pc in enumerate(self.pieces):
+            self.fstream.wait_event(pc["decoded"])
+            if i == 0:
+                self.fr0.record(self.fstream)
+            N.check(self.L.cbx_frame_rdw_async(base + pc["a"], pc["b"] - pc["a"], pc["sd"], len(pc["sd"]),
+                                               ctypes.byref(self.prm), self.off.data_ptr() + 8 * pc["r0"],
+                                               self.ln.data_ptr() + 4 * pc["r0"], pc["m"], pc["state"].data_ptr(), 0,
+                                               self.fstream_p))
+            pc["framed"].record(self.fstream)
+        self.fr1.record(self.fstream)
+        for pc, (r0, m, _, cs) in zip(self.pieces, self.parts):
+            cur.wait_event(pc["framed"])
+            N.check(self.L.cbx_decode_var(self.h, base + pc["a"], pc["b"] - pc["a"], self.off.data_ptr() + 8 * r0,
+                                          self.ln.data_ptr() + 4 * r0, m, 0, r0, cs, self.stream))
+            pc["decoded"].record(cur)
+        return (self.fr0, self.fr1)
+
+    def pieces_check(self) -> bool:
+        """After timing: every piece's framing found the records the index run puts in it."""
+        from cobrix_amd import native as N
+        nfr = ctypes.c_int64(0)
+        for pc in self.pieces:
+            N.check(self.L.cbx_frame_rdw_state(pc["state"].data_ptr(), ctypes.byref(nfr), self.stream))
+            if nfr.value != pc["m"]:
+                raise RuntimeError(f"piece framing found {nfr.value} records, the index run holds {pc['m']}")
+        return True
 
     def calls_per_step(self) -> int:
         return len(self.parts)
@@ -579,9 +651,12 @@ class _VarLen:
         import torch
         from cobrix_amd import native as N
         nfr = ctypes.c_int64(0)
-        N.check(self.L.cbx_frame_rdw_state(self.state.data_ptr(), ctypes.byref(nfr), self.stream))
-        if nfr.value != self.n_expected:
-            raise RuntimeError(f"framing found {nfr.value} records, the index run holds {self.n_expected}")
+        if self.pieces:
+            self.pieces_check()
+        else:
+            N.check(self.L.cbx_frame_rdw_state(self.state.data_ptr(), ctypes.byref(nfr), self.stream))
+            if nfr.value != self.n_expected:
+                raise RuntimeError(f"framing found {nfr.value} records, the index run holds {self.n_expected}")
         got = int(self.base.item()) if world > 1 else 0
         rid0 = self.parts[0][2][self.rd.plan.record_id_column]["values"]
         r0, m, cols, _ = self.parts[-1]
@@ -604,8 +679,11 @@ class _VarLen:
         pieces = [(bounds[i], bounds[i + 1], [s - bounds[i] for s in self.seeds if bounds[i] <= s < bounds[i + 1]])
                   for i in range(len(bounds) - 1)]
         # records per piece from the timed framing (the same seeds give the same boundaries)
-        offs = self.off[: self.n_rec] - 4
-        cnt = [int(torch.searchsorted(offs, torch.tensor([b], device=self.dev)).item()) for b in bounds]
+        if self.seed_recs is not None:   # (pieces leave piece-relative offsets in self.off)
+            cnt = self.seed_recs[::entries_per_piece] + [self.n_rec]
+        else:
+            offs = self.off[: self.n_rec] - 4
+            cnt = [int(torch.searchsorted(offs, torch.tensor([b], device=self.dev)).item()) for b in bounds]
         max_rec = max(cnt[i + 1] - cnt[i] for i in range(len(pieces)))
         max_bytes = max(b - a for a, b, _ in pieces)
         bufs = [torch.empty(max_bytes, dtype=torch.uint8, device=self.dev) for _ in range(2)]
@@ -853,6 +931,10 @@ def main():
                          "(cbx_plan_pipeline), one plan's count pass beside the other's decode, the count / decode "
                          "kernels capped at C / D resident workgroups per CU (0: default occupancy); default per "
                          "workload (C3: 0,0 -- 53.3 -> 51.3 ms per 64 GB step; capped forms were slower), '-': off")
+    ap.add_argument("--pieces", type=int, default=0,
+                    help="rdw_narrow / wide_odo on one GPU: the run framed and decoded as this many pieces of "
+                         "whole index entries, a piece's framing beside the previous piece's decode (0 = workload "
+                         "default, 1 = one framing + one decode)")
     ap.add_argument("--occurs", default="lists", choices=["lists", "slots"],
                     help="OCCURS DEPENDING ON layout: Arrow lists (present elements) or one slot row per element")
     ap.add_argument("--seed-mb", type=int, default=100, choices=[100, 32],
@@ -913,8 +995,9 @@ def main():
         job = _Fixed(args.workload, n_req, dev, rank, args.window, strings, batch, rec_base,
                      pipeline=pipe if strings == "offsets" and pipe != "-" else "")
     else:
+        pieces = args.pieces if args.pieces > 0 else W.get("pieces", 1)
         job = _VarLen(args.workload, n_req, dev, rank, world, args.window, strings, args.occurs == "lists",
-                      args.seed_mb, batch)
+                      args.seed_mb, batch, pieces=pieces if world == 1 else 1)
     st = torch.cuda.current_stream()
     progress(f"{job.in_bytes / 1e9:.2f} GB on this rank; allocating columns")
     job.prepare(st)

@@ -1219,6 +1219,59 @@ class VarLenNestedReader(_BaseReader):
         N.check(L.cbx_plan_check(self.native.handle, ctypes.c_void_p(st.cuda_stream)))
         return self._batch(n_rec, cols, first_record_id, self.params.generate_record_id, st)
 
+    def read_entries(self, d_data, n_bytes: int, entries: Sequence[SparseIndexEntry], entries_per_piece: int = 1,
+                     file_id: int = 0, input_file_name: Optional[str] = None) -> List[DecodedBatch]:
+        """An RDW file as the reference reads it -- a partition per sparse-index entry
+        (CobolScanners.buildScanForVarLenIndex, SC/source/scanners/CobolScanners.scala:40-75), each with
+        its own VarLenNestedIterator from the entry's offset and record index -- `entries_per_piece`
+        consecutive entries to a batch: a piece's records framed from its entries' offsets (the RDW walk
+        seeded at them, cbx_frame_rdw) on a second stream while the previous piece is selected and
+        decoded on the current one.  The batches, in file order, hold the rows `read` returns.
+        input_file_name: as in `read`."""
+        torch = _torch()
+        self._file_column(None, input_file_name, check_only=True)
+        if not self.params.is_record_sequence or self.params.is_text or self.hierarchical:
+            raise N.CbxError(N.CBX_E_UNSUPPORTED, "read_entries: RDW record sequences only (flat plans)")
+        if entries_per_piece < 1:
+            raise ValueError("entries_per_piece must be >= 1")
+        ents = list(entries) or [SparseIndexEntry(0, -1, file_id, 0)]
+        main = torch.cuda.current_stream()
+        side = torch.cuda.Stream(d_data.device)
+        side.wait_stream(main)   # (d_data written on the current stream)
+        L = N.load()
+        out: List[DecodedBatch] = []
+        for k in range(0, len(ents), entries_per_piece):
+            group = ents[k:k + entries_per_piece]
+            a = group[0].offset_from
+            known = k + entries_per_piece < len(ents)
+            b = ents[k + entries_per_piece].offset_from if known else n_bytes   # (entries tile the file)
+            # records of the piece: the next piece's record index minus this one's (the last: a bound)
+            cap = (ents[k + entries_per_piece].record_index - group[0].record_index + 1) if known else (b - a) // 5 + 1
+            with torch.cuda.stream(side):
+                off = torch.empty(max(1, cap), dtype=torch.int64, device=d_data.device)
+                ln = torch.empty(max(1, cap), dtype=torch.int32, device=d_data.device)
+            sd = (ctypes.c_int64 * len(group))(*[e.offset_from - a for e in group])
+            # the file header record lies at the file's start, the footer before its end: a piece elsewhere
+            # frames neither (the selection still drops the records within file_end_offset of each entry's
+            # offset_to, as the reference's entry-bounded streams do: cbx_select.h sel_footer)
+            prm = self.rdw_params()
+            if a > 0:
+                prm.file_header_bytes = 0
+            if known:
+                prm.file_footer_bytes = 0
+            n = ctypes.c_int64(0)
+            N.check(L.cbx_frame_rdw(d_data.data_ptr() + a, b - a, sd, len(group), ctypes.byref(prm), off.data_ptr(),
+                                    ln.data_ptr(), max(1, cap), ctypes.byref(n), ctypes.c_void_p(side.cuda_stream)))
+            off.record_stream(main)
+            ln.record_stream(main)
+            main.wait_stream(side)
+            piece = d_data[a:b]
+            rebased = [SparseIndexEntry(e.offset_from - a, e.offset_to - a if e.offset_to >= 0 else -1, e.file_id,
+                                        e.record_index) for e in group]
+            sel = self.select(piece, b - a, off[: n.value], ln[: n.value], rebased, file_id, stream=main)
+            out.append(self._file_column(self.decode_selected(piece, b - a, sel, stream=main), input_file_name))
+        return out
+
     def _device_file(self, data: bytes):
         torch = _torch()
         # zero fill past the data: text windows and VarOccursRecordExtractor's short last record

@@ -164,6 +164,41 @@ def test_gpu_selection_vs_oracle(extra, views):
         assert not bad, (jit, bad[:5], rows[bad[0]], exp[bad[0]])
 
 
+@pytest.mark.parametrize("per", [1, 3])
+@pytest.mark.parametrize("extra", [
+    {"segment_id_root": "C", "input_split_records": "700", "generate_record_id": "true"},
+    {"segment_id_level0": "C", "segment_id_level1": "P", "segment_id_prefix": "XYZ", "input_split_records": "1000",
+     "generate_record_id": "true"},
+    {"segment_id_root": "C", "segment_filter": "P", "input_split_records": "250", "generate_record_id": "true",
+     "redefine_segment_id_map:0": "STATIC-DETAILS => C", "redefine-segment-id-map:1": "CONTACTS => P"},
+    {"segment_id_level0": "P", "segment_id_level1": "C", "input_split_records": "900",
+     "file_start_offset": "100", "file_end_offset": "120", "generate_record_id": "true"},
+])
+def test_gpu_read_entries_pieces_vs_oracle(extra, per):
+    """read_entries: the file as pieces of index entries (each framed from its entries on a second
+    stream, selected and decoded as its own batch) -> the rows of the whole-file oracle, in order."""
+    from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow
+    raw = rdw_narrow(20_000, seed=12)[0].numpy().tobytes()
+    if "file_start_offset" in extra:
+        raw = bytes(range(100)) + raw + bytes(120)
+    rd, p = _var_reader(RDW_NARROW_COPYBOOK, {**_SYN_OPTS, **extra})
+    t = rd._device_file(raw)
+    off, ln, _ = rd.frame_file(t, len(raw))
+    ents = rd.generate_index(t, len(raw), off, ln, file_id=2)
+    assert len(ents) > 4
+    exp_ents = [(e.offset_from, e.offset_to, e.record_index) for e in RO.sparse_index(rd.copybook, raw, p, 2)]
+    assert [(e.offset_from, e.offset_to, e.record_index) for e in ents] == exp_ents
+    whole = rd.read(raw, file_id=2).to_rows()
+    batches = rd.read_entries(t, len(raw), ents, entries_per_piece=per, file_id=2)
+    assert len(batches) == -(-len(ents) // per)
+    rows = [r for b in batches for r in b.to_rows()]
+    exp = RO.var_len_rows(rd.copybook, raw, p, file_id=2)
+    assert len(whole) == len(exp)
+    assert len(rows) == len(exp), (len(rows), len(exp), [len(b.to_rows()) for b in batches][:6], ents[:3])
+    bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
+    assert not bad, (bad[:5], rows[bad[0]], exp[bad[0]])
+
+
 def _norm(v):
     if isinstance(v, dict):
         return {k: _norm(x) for k, x in v.items()}
