@@ -606,6 +606,32 @@ def test_two_byte_page_compose_vs_oracle(views, trim, jit):
     assert not errs, errs[:10]
 
 
+@pytest.mark.parametrize("views", ["views", "utf8"])
+@pytest.mark.parametrize("trim", ["none", "both", "left"])
+@pytest.mark.parametrize("jit", [-1, 1])
+def test_one_byte_waves_compose_vs_oracle(views, trim, jit):
+    """cp037 fields whose characters all map to 1-byte UTF-8 (letters, digits, EBCDIC spaces and
+    trimmable controls) in most tiles, every third tile with one accented character in one record:
+    the 2-byte group compose on waves of (almost) only 1-byte characters, fields of 1-32 bytes at
+    every dword phase, against the oracle."""
+    from cobrix_amd.synth import _CP037_ALNUM, _CP037_ACCENTED
+    cb = cbk.parse_copybook(COMPOSE_COPYBOOK, code_page="cp037", string_trimming=trim)
+    n, size = 64 * 97 + 13, cb.record_size
+    rng = np.random.default_rng(len(trim) + 3 * (jit + 2))
+    narrow = np.array(_CP037_ALNUM + [0x40] * 12 + [0x05, 0x25, 0x4B, 0x6B], dtype=np.uint8)
+    out = narrow[rng.integers(0, len(narrow), (n, size))]
+    lead = rng.random(n) < 0.2
+    out[lead, : size // 3] = 0x40
+    for t in range(0, (n + 63) // 64, 3):   # one accented character in every third tile
+        r = min(n - 1, 64 * t + int(rng.integers(0, 64)))
+        out[r, int(rng.integers(0, size))] = _CP037_ACCENTED[t % len(_CP037_ACCENTED)]
+    data = out.tobytes()
+    rd, batch = _fixed(COMPOSE_COPYBOOK, data, ebcdic_code_page="cp037", string_trimming_policy=trim,
+                       jit_min_records=jit, **_layout(views))
+    errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
+    assert not errs, errs[:10]
+
+
 def _wide_odo_forced(n_roots: int, seed: int):
     """C5 records (wide_odo) with the NUM-STRAT dependee forced, root by root, to 0, 1, 2000, out of
     range (2001, 65535) or random, and a share of C records cut before NUM-STRAT (a null dependee:
