@@ -931,6 +931,8 @@ def main():
                          "(cbx_plan_pipeline), one plan's count pass beside the other's decode, the count / decode "
                          "kernels capped at C / D resident workgroups per CU (0: default occupancy); default per "
                          "workload (C3: 0,0 -- 53.3 -> 51.3 ms per 64 GB step; capped forms were slower), '-': off")
+    ap.add_argument("--batch-records", type=int, default=0,
+                    help="Utf8 layout: records per decode call (0 = the workload's batch; int32 offsets must fit)")
     ap.add_argument("--pieces", type=int, default=0,
                     help="rdw_narrow / wide_odo on one GPU: the run framed and decoded as this many pieces of "
                          "whole index entries, a piece's framing beside the previous piece's decode (0 = workload "
@@ -983,7 +985,7 @@ def main():
         rec_base = n_req * rank // world
         n_req = n_req * (rank + 1) // world - rec_base
     # a batch per call: Utf8 int32 offsets must fit each slot region (<= 40 UTF-8 bytes per X(20) value)
-    batch = W.get("batch_records", 0) if strings == "offsets" else 0
+    batch = (args.batch_records or W.get("batch_records", 0)) if strings == "offsets" else 0
 
     def progress(msg):
         if rank == 0:
