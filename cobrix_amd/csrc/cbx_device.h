@@ -2139,6 +2139,13 @@ __device__ __forceinline__ void coop_loop(const KernelArgs& a, const WaveLds& l,
     uint4 buf[KH];
     const int wid = l.wid;
     body.wid = wid;
+#ifndef CBX_NO_COOP_PRIO
+    // the tile's second wave at issue priority 1 for the whole loop (no per-segment flips): the
+    // younger wave of a pair otherwise loses every VALU arbitration to the older one and the tile's
+    // barriers wait on it (MI355X_MICROARCH.md, two waves per SIMD, item 4).  SYN200 decode 3.83 ->
+    // 3.72 ms, three same-box pairs (profiles/r05_ab/coop_prio.log)
+    if (wid == 1) __builtin_amdgcn_s_setprio(1);
+#endif
     tile = first_tile<Body>(tile);   // (the workgroup's tiles: runs of kVRun with run-gathered words)
     if (tile < a.n_tiles) coop_issue<KP>(a, contig_span(a, tile), wid, lane, buf);
     Stamps st;
