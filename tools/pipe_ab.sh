@@ -1,4 +1,4 @@
-# A/B of the pipelined fixed-length Utf8 job (bench.py --pipeline C,D) on C3; usage: bash tools/r05_pipe_ab.sh TAG "" "0,0" ...
+# A/B of the pipelined fixed-length Utf8 job (bench.py --pipeline C,D) on C3; usage: bash tools/pipe_ab.sh TAG "" "0,0" ...
 set -u
 OUT=gpurun_out/$1; shift; mkdir -p $OUT
 for P in "$@"; do
