@@ -26,7 +26,6 @@
 #include "cbx_hier.h"
 #include "cbx_walk.h"
 #include "cbx_chain.h"
-#include "cbx_utf8.h"
 
 using namespace cbx;
 
@@ -122,14 +121,6 @@ struct cbx_plan {
     // the cooperative-tile decision each specialised kernel was compiled with (jit_coop_of reads env
     // knobs: launches reuse the compile-time answer, never re-derive it)
     bool jit_coop[4 * kPre + 5] = {};
-    // the one-pass Arrow Utf8 kernel (cbx_utf8.h) by prefetch depth, with its staging bytes
-    bool u8_tried[kPre + 1] = {};
-    hipFunction_t u8_fn[kPre + 1] = {};
-    int u8_need[kPre + 1] = {};
-    // its look-back granules (never cleared: every launch has its own tag) and the last tag
-    uint64_t* d_lb_tile = nullptr; int64_t lb_tile_cap = 0;
-    uint64_t* d_lb_blk = nullptr;  int64_t lb_blk_cap = 0;
-    uint32_t lb_epoch = 0;
     int rec_extent = 0;          // bytes past the decode base that any field (any OCCURS element) reaches
     std::string jit_error;
     int last_kind = 0;
@@ -594,7 +585,6 @@ extern "C" void cbx_plan_destroy(cbx_plan* P) {
     (void)hipFree(P->d_segmap); (void)hipFree(P->d_lut); (void)hipFree(P->d_cols);
     (void)hipFree(P->d_seqcall); (void)hipFree(P->d_str_tot); (void)hipFree(P->d_str_excl); (void)hipFree(P->d_block_sums);
     (void)hipFree(P->d_local); (void)hipFree(P->d_scratch); (void)hipFree(P->d_status); (void)hipFree(P->d_stamps);
-    (void)hipFree(P->d_lb_tile); (void)hipFree(P->d_lb_blk);
     (void)hipFree(P->d_lops); (void)hipFree(P->d_list_len); (void)hipFree(P->d_list_flag);
     (void)hipFree(P->d_wnodes); (void)hipFree(P->d_warr); (void)hipFree(P->d_whand); (void)hipFree(P->d_wslot_base);
     (void)hipFree(P->d_wtile_bytes); (void)hipFree(P->d_wcursor);
@@ -902,79 +892,6 @@ static int launch(cbx_plan* P, const CallShape& c, const cbx_column* columns, in
     a.defer_bits = P->d_defer_bits;
     const size_t lds_own = kLutLds + (size_t)kWavesPerBlock * a.lds_wave;
     if (lds_own > 160 * 1024) return fail(CBX_E_UNSUPPORTED, "record window does not fit in LDS");
-    // the one-pass Arrow Utf8 kernel (cbx_utf8.h): tile totals, look-back and decode in ONE launch
-    // over the input (no count pass re-reading it, no scan kernel)
-    if (!span && contig && mode == 0 && P->packed && P->n_seq > 0 && P->jit_min >= 0 && c.n_rec >= P->jit_min) {
-        const int k = contig_kp(sdw);
-        if (!P->u8_tried[k]) {
-            P->u8_tried[k] = true;
-            const U8Plan u = jit_utf8_plan(true, false, jit_pro(P), 2, S.win, S.nops, S.batches, S.sops);
-            if (u.ok && jit_utf8_ring(u, a.lds_rows, 2) > 0) {   // at least 2 workgroups per CU
-                std::string err;
-                P->u8_fn[k] = jit_get(jit_utf8_source(k, u, S.win, S.nops, S.batches, S.sops), &err, "cbx_jit_utf8");
-                P->u8_need[k] = u.max_need;
-                if (!P->u8_fn[k]) P->jit_error = err;
-            }
-        }
-        // workgroups per CU: as many as leave each wave a ring of two of the largest entries (4 on
-        // SYNSTR200: 6.6 KB rings); env CBX_U8_WGS caps it (tuning)
-        int wgs = 4;
-        if (const char* e = getenv("CBX_U8_WGS")) wgs = std::max(2, std::min(4, atoi(e)));
-        U8Plan uq;
-        uq.max_need = P->u8_need[k];
-        while (wgs > 2 && jit_utf8_ring(uq, a.lds_rows, wgs) == 0) wgs--;
-        const int ring = jit_utf8_ring(uq, a.lds_rows, wgs);
-        if (hipFunction_t ufn = ring > 0 ? P->u8_fn[k] : nullptr) {
-            const size_t lds = (size_t)kU8LutLds + (size_t)a.lds_rows + (size_t)kU8Waves * ring;
-            a.lb_ring = ring;
-            const int64_t nblk = (n_tiles + kLbBlock - 1) / kLbBlock;
-            const int64_t cap0 = P->lb_tile_cap, cap1 = P->lb_blk_cap;
-            if ((r = grow(&P->d_lb_tile, &P->lb_tile_cap, (int64_t)P->n_seq * n_tiles, st)) ||
-                (r = grow(&P->d_lb_blk, &P->lb_blk_cap, (int64_t)P->n_seq * nblk * 2, st)))
-                return r;
-            // fresh (or reused) memory holds no granule of this plan's tags: zero it once
-            if (++P->lb_epoch == 0 || P->lb_tile_cap != cap0 || P->lb_blk_cap != cap1 || P->lb_epoch == 1) {
-                HIP_CHECK(hipMemsetAsync(P->d_lb_tile, 0, sizeof(uint64_t) * P->lb_tile_cap, st));
-                HIP_CHECK(hipMemsetAsync(P->d_lb_blk, 0, sizeof(uint64_t) * P->lb_blk_cap, st));
-                if (P->lb_epoch == 0) P->lb_epoch = 1;
-            }
-            a.lb_tile = P->d_lb_tile;
-            a.lb_blk = P->d_lb_blk;
-            a.lb_nblk = nblk;
-            a.lb_tag = P->lb_epoch;
-            const char* es = getenv("CBX_LB_SPIN");      // polls before a missing total is recounted
-            const char* ef = getenv("CBX_LB_FORCE");     // tests: force the recount paths
-            a.lb_spin = es ? std::max(0, atoi(es)) : 20000;
-            a.lb_force = ef ? atoi(ef) : 0;
-            int bpc = std::min(wgs, (int)((160 * 1024) / lds));
-            int occ = 0;
-            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ufn, kWave * kU8Waves, lds) == hipSuccess && occ > 0)
-                bpc = std::min(bpc, occ);
-            if (const char* e = getenv("CBX_MAX_BLOCKS_PER_CU")) bpc = std::max(1, std::min(bpc, atoi(e)));   // tuning
-            const int64_t grid = std::min<int64_t>(n_tiles, (int64_t)P->num_cus * bpc);
-            const bool prof = P->profiling;
-            cbx_plan::CallEvents ce{{nullptr, nullptr, nullptr}};
-            if (prof) {
-                for (auto& e : ce.e) if (!(e = take_event(P))) return fail(CBX_E_HIP, "hipEventCreate failed");
-                HIP_CHECK(hipEventRecord(ce.e[0], st));
-            }
-            P->last_kind = 4;
-            void* kargs[] = {&a};
-            HIP_CHECK(hipModuleLaunchKernel(ufn, (unsigned)grid, 1, 1, kWave * kU8Waves, 1, 1, (unsigned)lds, st, kargs, nullptr));
-            if (prof) HIP_CHECK(hipEventRecord(ce.e[1], st));
-            if (n_defer_seq > 0) {
-                const unsigned gy = (unsigned)std::min<int64_t>(n_defer_seq, 65535);
-                hipLaunchKernelGGL(fixup_kernel, dim3((unsigned)((n_tiles + 4 * kWave - 1) / (4 * kWave)), gy), dim3(4 * kWave), 0, st,
-                                   a, (const CBX_CONST DeferSeq*)P->d_defer, n_defer_seq);
-                HIP_CHECK(hipGetLastError());
-            }
-            if (prof) {
-                HIP_CHECK(hipEventRecord(ce.e[2], st));
-                P->ev_calls.push_back(ce);
-            }
-            return CBX_OK;
-        }
-    }
     // resident blocks per CU: the LDS bound and the runtime's occupancy (registers)
     // copybook-specialised kernel for large contiguous batches (cbx_jit.h)
     hipFunction_t jfn = span_fn;
@@ -1417,16 +1334,6 @@ extern "C" int cbx_plan_set_odo_counts(cbx_plan* P, const int32_t* d_counts, int
     if (d_counts && P->walk) return fail(CBX_E_UNSUPPORTED, "cbx_plan_set_odo_counts: the record walk reads its counts itself");
     P->d_odo = d_counts;
     P->odo_pitch = d_counts ? pitch : 0;
-    return CBX_OK;
-}
-
-extern "C" int cbx_plan_lookback_stats(cbx_plan* P, int64_t* recounts, void* stream) {
-    if (!P || !recounts) return fail(CBX_E_ARGUMENT, "cbx_plan_lookback_stats: invalid arguments");
-    int32_t s[3] = {0, 0, 0};
-    HIP_CHECK(hipMemcpyAsync(s, P->d_status, sizeof(s), hipMemcpyDeviceToHost, (hipStream_t)stream));
-    HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
-    *recounts = s[1];
-    HIP_CHECK(hipMemsetAsync(P->d_status + 1, 0, 2 * sizeof(int32_t), (hipStream_t)stream));
     return CBX_OK;
 }
 

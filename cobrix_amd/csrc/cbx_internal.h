@@ -174,16 +174,6 @@ struct KernelArgs {
     int32_t lds_wave;          // total per wave
     int32_t dump_stride;       // bytes between the lanes' string dump slots (4, or 0 = one shared slot)
     uint64_t* stamps;          // diagnostic build (CBX_STAMPS) only: per-segment wave-cycle sums
-    // one-pass Arrow Utf8 decode (cbx_utf8.h): look-back granules {value, tag} of every (sequence,
-    // tile) total and (sequence, block of 64 tiles) total / inclusive prefix, the launch's tag, the
-    // poll budget before a missing total is recounted from the input, test switches forcing recounts
-    uint64_t* lb_tile;         // [n_seq][n_tiles]
-    uint64_t* lb_blk;          // [n_seq][lb_nblk][2]: B, P
-    int64_t lb_nblk;
-    uint32_t lb_tag;
-    int32_t lb_spin;
-    int32_t lb_force;          // bit 0: recount every in-block total, bit 1: every block total
-    int32_t lb_ring;           // bytes of each wave's LDS ring of staged elements
 };
 
 }  // namespace cbx

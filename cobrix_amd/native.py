@@ -43,8 +43,8 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
                     "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs",
                     "cbx_plan_set_record_base", "cbx_frame_length_field", "cbx_plan_set_odo_counts",
-                    "cbx_plan_lookback_stats", "cbx_hier_dependee_counts", "cbx_views_to_utf8", "cbx_plan_pipeline")
-ABI_VERSION = 16
+                    "cbx_hier_dependee_counts", "cbx_views_to_utf8", "cbx_plan_pipeline")
+ABI_VERSION = 17
 
 
 class NativeLibraryError(RuntimeError):
@@ -211,7 +211,6 @@ def load():
     L.cbx_plan_set_profiling.argtypes = [P, i32]
     L.cbx_plan_kernel_times.argtypes = [P, P, P, i32, P]
     L.cbx_plan_kernel_kind.argtypes = [P, P]
-    L.cbx_plan_lookback_stats.argtypes = [P, P, P]
     L.cbx_plan_specialize.argtypes = [P, P, i64, P, i32]
     L.cbx_sparse_index.argtypes = [P, P, i64, P, P, i64, P, P, i64, P, P]
     L.cbx_select_records.argtypes = [P, P, i64, P, P, i64, i32, P, i32, P, P, P]

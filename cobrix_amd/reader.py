@@ -488,6 +488,16 @@ def _file_name_array(name: str, n: int):
     return pa.DictionaryArray.from_arrays(pa.array(np.zeros(n, dtype=np.int32)), pa.array([name], pa.string()))
 
 
+def _record_stream(cols: Sequence[Dict[str, Any]], stream) -> None:
+    """Mark every tensor of a column table as used on `stream` (the caching allocator then keeps
+    its memory until that stream's queued work is done)."""
+    torch = _torch()
+    for c in cols:
+        for v in c.values():
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                v.record_stream(stream)
+
+
 def _alloc_columns(plan: DecodePlan, n_rec: int, slot_capacity: Sequence[int], device) -> Tuple[List[Dict[str, Any]], ctypes.Array]:
     """Caller-owned output buffers (cobrix_hip.h cbx_column): slot-major values, validity
     bitmaps, and for strings one Arrow large-string array per slot (regions of slot_capacity)."""
@@ -605,9 +615,13 @@ def views_to_utf8(plan: DecodePlan, cols: List[Dict[str, Any]], n_rec: int, stre
             continue
         dev = c["views"].device
         cap = int(c["capacity"])
-        offs = torch.zeros(info.n_slots * (pitch + 1), dtype=torch.int32, device=dev)
-        sizes = torch.zeros(info.n_slots, dtype=torch.int64, device=dev)
-        data = torch.empty(max(1, cap * info.n_slots), dtype=torch.uint8, device=dev)
+        with torch.cuda.stream(stream):
+            # allocated and zero-filled on the stream the conversion runs on (ordered before its writes)
+            offs = torch.zeros(info.n_slots * (pitch + 1), dtype=torch.int32, device=dev)
+            sizes = torch.zeros(info.n_slots, dtype=torch.int64, device=dev)
+            data = torch.empty(max(1, cap * info.n_slots), dtype=torch.uint8, device=dev)
+        if stream != torch.cuda.current_stream():
+            _record_stream([{"o": offs, "s": sizes, "d": data}], torch.cuda.current_stream())
         for s in range(info.n_slots):
             N.check(L.cbx_views_to_utf8(c["views"].data_ptr() + 16 * s * pitch, n_rec, c["data"].data_ptr() + s * cap,
                                         max(1, int(c["buffer_bytes"])), offs.data_ptr() + 4 * s * (pitch + 1),
@@ -960,7 +974,12 @@ class FixedLenNestedReader(_BaseReader):
         for k, r0 in enumerate(range(0, n_rec, bs)):
             rd, st = targets[k % len(targets)]
             m = min(bs, n_rec - r0)
-            cols, cs = _alloc_columns(rd.plan, m, string_capacity(rd.native, m), d_data.device)
+            with torch.cuda.stream(st):
+                # zero-filled on the stream that decodes the batch: a fill queued on s0 behind the
+                # previous batch's decode is not ordered before the side stream's count and decode
+                cols, cs = _alloc_columns(rd.plan, m, string_capacity(rd.native, m), d_data.device)
+            if st is not s0:
+                _record_stream(cols, s0)   # (consumed on s0 after the final wait)
             N.check(L.cbx_decode_fixed(rd.native.handle, d_data.data_ptr() + r0 * stride, m, stride, self.params.start_offset,
                                        first_record_id + r0, cs, ctypes.c_void_p(st.cuda_stream)))
             pending.append((cols, cs))   # (the column table lives until the calls are checked)
@@ -1225,8 +1244,9 @@ class VarLenNestedReader(_BaseReader):
         (CobolScanners.buildScanForVarLenIndex, SC/source/scanners/CobolScanners.scala:40-75), each with
         its own VarLenNestedIterator from the entry's offset and record index -- `entries_per_piece`
         consecutive entries to a batch: a piece's records framed from its entries' offsets (the RDW walk
-        seeded at them, cbx_frame_rdw) on a second stream while the previous piece is selected and
-        decoded on the current one.  The batches, in file order, hold the rows `read` returns.
+        seeded at them, cbx_frame_rdw), then selected and decoded, one piece after another on the
+        current stream (framing returns the piece's record count to the host, so pieces do not
+        overlap).  The batches, in file order, hold the rows `read` returns.
         input_file_name: as in `read`."""
         torch = _torch()
         self._file_column(None, input_file_name, check_only=True)
@@ -1236,8 +1256,6 @@ class VarLenNestedReader(_BaseReader):
             raise ValueError("entries_per_piece must be >= 1")
         ents = list(entries) or [SparseIndexEntry(0, -1, file_id, 0)]
         main = torch.cuda.current_stream()
-        side = torch.cuda.Stream(d_data.device)
-        side.wait_stream(main)   # (d_data written on the current stream)
         L = N.load()
         out: List[DecodedBatch] = []
         for k in range(0, len(ents), entries_per_piece):
@@ -1247,9 +1265,8 @@ class VarLenNestedReader(_BaseReader):
             b = ents[k + entries_per_piece].offset_from if known else n_bytes   # (entries tile the file)
             # records of the piece: the next piece's record index minus this one's (the last: a bound)
             cap = (ents[k + entries_per_piece].record_index - group[0].record_index + 1) if known else (b - a) // 5 + 1
-            with torch.cuda.stream(side):
-                off = torch.empty(max(1, cap), dtype=torch.int64, device=d_data.device)
-                ln = torch.empty(max(1, cap), dtype=torch.int32, device=d_data.device)
+            off = torch.empty(max(1, cap), dtype=torch.int64, device=d_data.device)
+            ln = torch.empty(max(1, cap), dtype=torch.int32, device=d_data.device)
             sd = (ctypes.c_int64 * len(group))(*[e.offset_from - a for e in group])
             # the file header record lies at the file's start, the footer before its end: a piece elsewhere
             # frames neither (the selection still drops the records within file_end_offset of each entry's
@@ -1261,10 +1278,7 @@ class VarLenNestedReader(_BaseReader):
                 prm.file_footer_bytes = 0
             n = ctypes.c_int64(0)
             N.check(L.cbx_frame_rdw(d_data.data_ptr() + a, b - a, sd, len(group), ctypes.byref(prm), off.data_ptr(),
-                                    ln.data_ptr(), max(1, cap), ctypes.byref(n), ctypes.c_void_p(side.cuda_stream)))
-            off.record_stream(main)
-            ln.record_stream(main)
-            main.wait_stream(side)
+                                    ln.data_ptr(), max(1, cap), ctypes.byref(n), ctypes.c_void_p(main.cuda_stream)))
             piece = d_data[a:b]
             rebased = [SparseIndexEntry(e.offset_from - a, e.offset_to - a if e.offset_to >= 0 else -1, e.file_id,
                                         e.record_index) for e in group]

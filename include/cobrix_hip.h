@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 16
+#define CBX_ABI_VERSION 17
 
 /* status codes */
 #define CBX_OK 0
@@ -301,15 +301,9 @@ int cbx_plan_check(cbx_plan* plan, void* stream);
 int cbx_plan_set_profiling(cbx_plan* plan, int32_t enable);
 int cbx_plan_kernel_times(cbx_plan* plan, float* decode_ms, float* post_ms, int32_t max_calls, int32_t* n_calls);
 
-/* One-pass Arrow Utf8 kernel (kind 4): the number of tile totals its look-back had to recount from
- * the input since the last call (a total left unpublished past the poll budget -- a workgroup that
- * was not resident, or a test forcing the fallback); then reset.  Synchronises the stream. */
-int cbx_plan_lookback_stats(cbx_plan* plan, int64_t* recounts, void* stream);
-
 /* Which decode kernel the plan's last decode call ran: *kind = 0 the table-driven kernel,
  * 2 the record walk (cbx_plan_set_walk), 3 its copybook-specialised form,
- * 1 the copybook-specialised kernel, 4 the one-pass Arrow Utf8 kernel (the specialised decode with
- * its tile totals resolved by a look-back inside the launch: no count pass, no scan).  If specialisation was attempted and failed, *kind = 0 and
+ * 1 the copybook-specialised kernel.  If specialisation was attempted and failed, *kind = 0 and
  * the reason is in cbx_last_error() (the call itself succeeded on the table-driven kernel). */
 int cbx_plan_kernel_kind(cbx_plan* plan, int32_t* kind);
 

@@ -220,7 +220,7 @@ def test_specialised_kernel_vs_oracle(case, views):
     in the three string layouts (Arrow large-string offsets / string views / Utf8)."""
     cb_text, data, kw, okw = _jit_cases()[case]
     rd, batch = _fixed(cb_text, data, jit_min_records=1, **_layout(views), **kw)
-    assert _kernel_kind(rd) in (1, 4), "specialised kernel did not run"
+    assert _kernel_kind(rd) == 1, "specialised kernel did not run"
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data, **okw))
     assert not errs, errs
     # the table-driven kernel on the same plan layout agrees as well
@@ -239,7 +239,7 @@ def test_specialised_kernel_segments_and_offsets():
     seg_map = {"C": "STATIC-DETAILS", "P": "CONTACTS"}
     rd, batch = _fixed(cb_text, recs, segment_field="SEGMENT-ID", segment_id_redefine_map=seg_map,
                        start_offset=3, end_offset=1, jit_min_records=1)
-    assert _kernel_kind(rd) in (1, 4)
+    assert _kernel_kind(rd) == 1
     res = O.decode_fixed(rd.copybook, recs, segment_field="SEGMENT-ID", segment_redefine_map=seg_map,
                          record_size=L, start_offset=3, end_offset=1)
     assert not compare_batch(batch, res)
@@ -255,7 +255,7 @@ def test_synstr200_vs_oracle(n, jit, views):
     data = synstr200(n, seed=3 + n).numpy().tobytes()
     rd, batch = _fixed(SYNSTR200_COPYBOOK, data, ebcdic_code_page="cp037", jit_min_records=jit, **_layout(views))
     if n >= 262_144 or jit == 1:
-        assert _kernel_kind(rd) in (1, 4)
+        assert _kernel_kind(rd) == 1
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
     assert not errs, errs
 
@@ -337,7 +337,7 @@ def test_syn200_full_size_sampled_parity(views):
     rec = syn200(n, seed=20261015, device="cuda")
     rd = FixedLenNestedReader(SYN200_COPYBOOK, ReaderParameters(**_layout(views)))
     batch = rd.decode_device(rec.view(-1), n * 200)
-    assert _kernel_kind(rd) in (1, 4)
+    assert _kernel_kind(rd) == 1
     rng = np.random.default_rng(2)
     idx = np.unique(np.concatenate([np.arange(128), n - 128 + np.arange(128), rng.integers(0, n, 5744)]))
     sample = rec[torch.as_tensor(idx, device="cuda")].cpu().numpy().tobytes()
@@ -361,7 +361,7 @@ def test_synstr200_full_size_sampled_views():
     rec = synstr200(n, seed=20261017, device="cuda")
     rd = FixedLenNestedReader(SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_views=True))
     batch = rd.decode_device(rec.view(-1), n * 200)
-    assert _kernel_kind(rd) in (1, 4)
+    assert _kernel_kind(rd) == 1
     rng = np.random.default_rng(5)
     idx = np.unique(np.concatenate([np.arange(128), n - 128 + np.arange(128), rng.integers(0, n, 3744)]))
     sample = rec[torch.as_tensor(idx, device="cuda")].cpu().numpy().tobytes()
@@ -412,7 +412,7 @@ def test_var_span_kernel_vs_oracle(views):
     from cobrix_amd.synth import rdw_narrow
     raw = rdw_narrow(20_000, seed=21)[0].numpy().tobytes()
     rd, errs = _var_decode_vs_oracle(raw, views, jit_min_records=1)
-    assert _kernel_kind(rd) in (1, 4) and not errs, errs
+    assert _kernel_kind(rd) == 1 and not errs, errs
     rng = np.random.default_rng(4)
     body = bytearray()
     for i in range(5000):
@@ -423,34 +423,26 @@ def test_var_span_kernel_vs_oracle(views):
         payload = payload[:ln]
         body += bytes([0, 0, ln & 0xFF, ln >> 8]) + bytes(payload)
     rd, errs = _var_decode_vs_oracle(bytes(body), views, jit_min_records=1)
-    assert _kernel_kind(rd) in (1, 4) and not errs, errs
+    assert _kernel_kind(rd) == 1 and not errs, errs
 
 
-@pytest.mark.parametrize("force", [0, 1, 3])
 @pytest.mark.parametrize("n", [1, 63, 4097, 20_011, 300_001])
-def test_utf8_onepass_vs_oracle(n, force, monkeypatch):
-    """The one-pass Arrow Utf8 kernel (cbx_utf8.h, kernel kind 4): tile totals published and the
-    tiles' places resolved by the look-back inside the decode launch.  Bit-exact against the oracle
-    across block boundaries (64 tiles) and rounds of the grid; force = 1 / 3 make every in-block total
-    (1) and also every block total (3) come from the look-back's recount of the input instead of the
-    published granules (the forward-progress fallback), which must give the same bytes."""
+def test_utf8_chain_vs_oracle(n):
+    """The Arrow Utf8 chain of the specialised kernels (count pass, scan of the tile totals, decode
+    writing every payload byte at its final place): bit-exact against the oracle across tile and grid
+    round boundaries."""
     from cobrix_amd.synth import SYNSTR200_COPYBOOK, synstr200
-    if force == 3 and n > 20_011:
-        pytest.skip("forced block recounts are quadratic in the block count")
-    monkeypatch.setenv("CBX_UTF8_ONEPASS", "1")
-    if force:
-        monkeypatch.setenv("CBX_LB_FORCE", str(force))
     data = synstr200(n, seed=5 + n).numpy().tobytes()
     rd, batch = _fixed(SYNSTR200_COPYBOOK, data, ebcdic_code_page="cp037", jit_min_records=1, string_utf8=True)
-    assert _kernel_kind(rd) == 4, "one-pass Utf8 kernel did not run"
+    assert _kernel_kind(rd) == 1, "specialised kernel did not run"
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
     assert not errs, errs
 
 
 @pytest.mark.parametrize("trim", ["none", "left", "right", "both"])
 @pytest.mark.parametrize("cp", ["cp037", "common", "ascii"])
-def test_utf8_onepass_code_pages_and_trim(cp, trim, monkeypatch):
-    """The one-pass kernel's width-pattern compose (characters of 0 / 1 / 2 UTF-8 bytes, those outside
+def test_utf8_code_pages_and_trim(cp, trim):
+    """The Utf8 decode's width-pattern compose (characters of 0 / 1 / 2 UTF-8 bytes, those outside
     the trimmed range dropped) on every trim policy, single- and two-byte code pages and ASCII, with
     fields of 1..32 bytes (groups of 4 characters cut at every phase) and values full of trimmable
     bytes: bit-exact against the oracle."""
@@ -466,14 +458,13 @@ def test_utf8_onepass_code_pages_and_trim(cp, trim, monkeypatch):
     raw[sp] = pad
     raw[:, ::5][rng.random((n, (rec + 4) // 5)) < 0.2] = 0x05 if cp != "ascii" else 0x09
     data = raw.tobytes()
-    monkeypatch.setenv("CBX_UTF8_ONEPASS", "1")
     kw = dict(string_trimming_policy=trim, jit_min_records=1, string_utf8=True)
     if cp == "ascii":
         kw["is_ebcdic"] = False
     else:
         kw["ebcdic_code_page"] = cp
     rd, batch = _fixed(cb_text, data, **kw)
-    assert _kernel_kind(rd) == 4
+    assert _kernel_kind(rd) == 1
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
     assert not errs, errs
 
@@ -521,7 +512,7 @@ def test_synstr200_full_size_sampled_utf8():
     rec = synstr200(n, seed=20261017, device="cuda")
     rd = FixedLenNestedReader(SYNSTR200_COPYBOOK, ReaderParameters(ebcdic_code_page="cp037", string_utf8=True))
     batch = rd.decode_device(rec.view(-1), n * 200)
-    assert _kernel_kind(rd) in (1, 4)
+    assert _kernel_kind(rd) == 1
     rng = np.random.default_rng(6)
     idx = np.unique(np.concatenate([np.arange(128), n - 128 + np.arange(128), rng.integers(0, n, 3744)]))
     sample = rec[torch.as_tensor(idx, device="cuda")].cpu().numpy().tobytes()
@@ -601,7 +592,7 @@ def test_two_byte_page_compose_vs_oracle(views, trim, jit):
     rd, batch = _fixed(COMPOSE_COPYBOOK, data, ebcdic_code_page="cp037", string_trimming_policy=trim,
                        jit_min_records=jit, **_layout(views))
     if jit == 1:
-        assert _kernel_kind(rd) in (1, 4)
+        assert _kernel_kind(rd) == 1
     errs = compare_batch(batch, O.decode_fixed(rd.copybook, data))
     assert not errs, errs[:10]
 
@@ -805,11 +796,13 @@ def test_utf8_pipelined_plans_vs_single(caps):
     L = N.load()
     N.check(L.cbx_plan_pipeline(A.native.handle, B.native.handle, caps[0], caps[1]))
     s1, s2 = torch.cuda.current_stream(), torch.cuda.Stream()
+    s2.wait_stream(s1)   # (the generated input)
     m = n // nb
     outs, refs = [], []
     for i in range(nb):
         h, st = (A.native.handle, s1) if i % 2 == 0 else (B.native.handle, s2)
-        cols, cs = _alloc_columns(A.plan, m, string_capacity(A.native, m), rec.device)
+        with torch.cuda.stream(st):   # (zero-filled on the stream that decodes the batch)
+            cols, cs = _alloc_columns(A.plan, m, string_capacity(A.native, m), rec.device)
         N.check(L.cbx_decode_fixed(h, rec.data_ptr() + i * m * 200, m, 200, 0, i * m, cs, ctypes.c_void_p(st.cuda_stream)))
         outs.append(cols)
     torch.cuda.synchronize()

@@ -23,7 +23,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "cobrix_amd", "csrc")
 HEADERS = [("cobrix_hip.h", os.path.join(ROOT, "include", "cobrix_hip.h"))] + [
-    (n, os.path.join(CSRC, n)) for n in ("cbx_decode.h", "cbx_internal.h", "cbx_device.h", "cbx_list.h", "cbx_walk.h", "cbx_utf8.h")]
+    (n, os.path.join(CSRC, n)) for n in ("cbx_decode.h", "cbx_internal.h", "cbx_device.h", "cbx_list.h", "cbx_walk.h")]
 
 
 def _torch_hiprtc() -> str | None:
@@ -239,55 +239,4 @@ def test_walk_kernel_compiles_with_hiprtc(compiler):
     if compiler >= len(COMPILERS):
         pytest.skip("no second hipRTC")
     err = _compile(WALK_KERNEL, COMPILERS[compiler])
-    assert not err, err[:3000]
-
-
-def _utf8_onepass_kernel(n_str: int = 10, numerics: bool = False) -> str:
-    """The one-pass Arrow Utf8 kernel as jit_utf8_source emits it (cbx_jit.h): SYNSTR200's shape
-    (n_str x PIC X(20), cp037 pad 2, trim both) split over the 4 waves of a workgroup -- composes into
-    the wave's ring, numerics, flushes of earlier tiles' entries -- optionally with a COMP-3 group on
-    the last wave."""
-    ops = [f"{{{20 * i},20,1,4,0,2,{i},0,{i},-1,{{0,0,0,0}},{{0,0,0,0}},0}}" for i in range(n_str)]
-    per = [(w * n_str // 4, (w + 1) * n_str // 4) for w in range(4)]
-    rng = "".join(f"    {'else ' if w else ''}if (wid == {w}) {{ lo = {lo}; hi = {hi}; }}\n" for w, (lo, hi) in enumerate(per))
-    comp = ""
-    for w, (lo, hi) in enumerate(per):
-        comp += ("      if (l.wid == 0) {\n" if w == 0 else f"      }} else if (l.wid == {w}) {{\n")
-        for i in range(lo, hi):
-            comp += (f"        if (todo & {1 << (i - lo)}u) {{ constexpr StrOp op = {ops[i]}; if (u8_compose(a, op, {i}, "
-                     f"ldc(a.scall + {i}), t, img, rec_addr, ring, lane)) todo &= ~{1 << (i - lo)}u; }}\n")
-    nums = ""
-    for w in range(4):
-        nums += ("        if (l.wid == 0) {\n" if w == 0 else f"        }} else if (l.wid == {w}) {{\n")
-        if numerics and w == 3:
-            nums += ("      { constexpr NumOp g[1] = {{" + str(20 * n_str) + ",0,8,2,0,0,0,0,0,10,0,-1,-1,0,0xffffffffffffffffull,0x0ull,"
-                     "0x1ull,0x0ull,0x0ull,0x0ull,{0,0,0,0},{0,0,0,0}}}; num_group<0,8,false,1>(a, g, 0, t, img, rec_addr, l.cnt, lane, vw); }\n")
-    body = ("    uint32_t todo = 0;\n    if (cur >= 0) { int lo = 0, hi = 0; range(l.wid, lo, hi); todo = (1u << (hi - lo)) - 1u; }\n"
-            "    bool num = cur < 0;\n    for (;;) {\n" + comp + "      }\n      st.mark(2);\n"
-            "      if (!todo && !num) {\n        num = true;\n" + nums + "        }\n      }\n"
-            "      if (!todo && (ring.np == 0 || u8_oldest_tile(ring) == cur)) break;\n"
-            "      if (todo && ring.np == 0) { if (lane == 0) atomicOr(a.status, 1); break; }\n"
-            "      u8_flush_oldest(a, ring, lane, cur);\n      st.mark(3);\n    }\n")
-    return ("#define CBX_STR_LAYOUT 2\n#define CBX_MODE 0\n#include \"cbx_utf8.h\"\nnamespace cbx {\nstruct JitU8Body {\n"
-            "  __device__ __forceinline__ void range(int wid, int& lo, int& hi) const {\n" + rng + "  }\n"
-            "  __device__ __forceinline__ void run(const KernelArgs& a, const TileCtx& t, const uint8_t* img, uint32_t rec_addr,\n"
-            "                                      const U8Lds& l, int lane, U8Ring& ring, int64_t cur, Stamps& st) {\n    DirectSink vw;\n"
-            "    (void)img; (void)rec_addr;\n" + body + "  }\n};\n}  // namespace cbx\n"
-            "extern \"C\" __global__ __launch_bounds__(cbx::kWave * cbx::kU8Waves) __attribute__((amdgpu_waves_per_eu(4))) "
-            "void cbx_jit_utf8(cbx::KernelArgs a) {\n"
-            "  using namespace cbx;\n  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
-            "  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);\n  const int lane = threadIdx.x % kWave;\n"
-            "  if (!lds_base_ok(smem)) { if (threadIdx.x == 0) atomicOr(a.status, 4); return; }\n"
-            "  const U8Lds l = u8_lds(a, smem, wid);\n  u8_lut_fill(a, (uint32_t*)smem);\n  __syncthreads();\n"
-            "  u8_loop<13, kU8Waves>(a, l, lane, JitU8Body{});\n}\n")
-
-
-@pytest.mark.parametrize("numerics", [False, True])
-@pytest.mark.parametrize("compiler", range(2), ids=["rocm", "torch"])
-def test_utf8_onepass_kernel_compiles_with_hiprtc(numerics, compiler):
-    """The one-pass Arrow Utf8 kernel (cbx_utf8.h: compose into LDS staging, look-back over the tiles'
-    totals, one copy-out) compiles against the bundled headers with both compilers."""
-    if compiler >= len(COMPILERS):
-        pytest.skip("no second hipRTC")
-    err = _compile(_utf8_onepass_kernel(numerics=numerics), COMPILERS[compiler])
     assert not err, err[:3000]

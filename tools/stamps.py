@@ -5,9 +5,8 @@ specialised kernels then compile with -DCBX_STAMPS too).  Prints each segment's 
 wave time.  Shares only: the stamps' waits forbid overlaps the product kernel has, so the diagnostic
 build's run time is not quoted anywhere.
 
-usage: python tools/stamps.py [--workload syn200|synstr200] [--records N] [--onepass]
-  syn200 / synstr200 (views or Utf8 count + decode): the contiguous decode loop's segments;
-  synstr200 --onepass: the one-pass Utf8 kernel's (cbx_utf8.h u8_loop)."""
+usage: python tools/stamps.py [--workload syn200|synstr200] [--records N] [--views]
+  syn200 / synstr200 (views or Utf8 count + decode): the contiguous decode loop's segments."""
 import argparse
 import ctypes
 import os
@@ -17,19 +16,14 @@ os.environ["CBX_LIB_VARIANT"] = "stamps"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SEG = ["stage (prefetched loads -> LDS)", "prefetch issue", "prologue", "strings", "numerics", "tile end sync"]
-SEG_U8 = ["stage (prefetched loads -> LDS)", "barrier + prefetch issue", "compose", "flush (look-back + copy)",
-          "block totals", "tile end barrier"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="syn200", choices=["syn200", "synstr200"])
     ap.add_argument("--records", type=int, default=10_000_000)
-    ap.add_argument("--onepass", action="store_true")
     ap.add_argument("--views", action="store_true")
     a = ap.parse_args()
-    if a.onepass:
-        os.environ["CBX_UTF8_ONEPASS"] = "1"
     import torch
     from cobrix_amd import native as N
     from cobrix_amd import synth
@@ -56,7 +50,7 @@ def main():
     d = list(out)
     kind = ctypes.c_int32()
     N.check(L.cbx_plan_kernel_kind(h, ctypes.byref(kind)))
-    names = SEG_U8 if kind.value == 4 else SEG
+    names = SEG
     tot = sum(d[:6])
     print(f"workload={a.workload} kind={kind.value} waves={d[7]} total_wave_clk={tot}")
     for k, name in enumerate(names):
