@@ -270,17 +270,31 @@ struct VWords {
     __device__ __forceinline__ void svalid(const StrCall&, int i, int64_t, uint64_t m) { put(NNUM + NDEF + i, m); }
     // the run starting at tile t0: lanes 8k..8k+7 of pair r store word 8r + k of its tiles (64 B)
     // own: the words this wave gathered (a cooperative tile's waves each flush their own ops' words)
+    // The 8 word pointers of a pair come from scalar loads (the word index is a compile-time constant
+    // per k) and are selected per lane: a per-lane load of the pointer table was a vector load whose
+    // wait (vmcnt(0), in issue order) also waited for every value store of the tile before it.
+    __device__ __forceinline__ static uint64_t* word_ptr(const KernelArgs& a, int w) {
+        return w < NNUM ? ldc(a.ncall + w).validity
+             : w < NNUM + NDEF ? a.defer_bits + (int64_t)(w - NNUM) * a.n_tiles
+                               : ldc(a.scall + (w - NNUM - NDEF)).validity;
+    }
     __device__ __forceinline__ void flush(const KernelArgs& a, int n_words, int64_t t0, int lane, uint64_t own = ~0ull) {
         const int jj = lane & 7;
+        const int kk = lane >> 3;
 #pragma unroll
         for (int r = 0; r < NV; r++) {
-            const int w = 8 * r + (lane >> 3);
-            if (w < n_words && ((own >> (w & 63)) & 1) && t0 + jj < a.n_tiles) {
-                uint64_t* p = w < NNUM ? a.ncall[w].validity
-                            : w < NNUM + NDEF ? a.defer_bits + (int64_t)(w - NNUM) * a.n_tiles
-                                              : a.scall[w - NNUM - NDEF].validity;
-                gp(p)[t0 + jj] = ((uint64_t)hi[r] << 32) | lo[r];
+            uint64_t* p = nullptr;
+            bool mine = false;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int w = 8 * r + k;
+                if (w < n_words && ((own >> (w & 63)) & 1)) {
+                    uint64_t* q = word_ptr(a, w);
+                    p = kk == k ? q : p;
+                    mine |= kk == k;
+                }
             }
+            if (mine && t0 + jj < a.n_tiles) gp(p)[t0 + jj] = ((uint64_t)hi[r] << 32) | lo[r];
         }
     }
 };
@@ -1029,7 +1043,13 @@ __device__ __forceinline__ int utf8_compose(const KernelArgs& a, const StrOp& op
 // The tile's place in the element's slot region (the count pass's exclusive scan).  The
 // specialised kernel loads it for all of a tile's elements before the first is decoded (one wait
 // for the tile instead of a dependent scalar load in front of every element's stores).
-__device__ __forceinline__ int64_t utf8_tile_base(const StrCall& c, const TileCtx& t) { return c.excl[t.tile] - c.excl[0]; }
+// (scalar loads through the constant address space: with the generic pointer they were flat loads,
+// which count in vmcnt AND lgkmcnt out of order -- every element then waited vmcnt(0), draining the
+// wave's value stores and the next tile's prefetched loads, 5 times per SYNSTR200 tile and wave)
+__device__ __forceinline__ int64_t utf8_tile_base(const StrCall& c, const TileCtx& t) {
+    const CBX_CONST int64_t* x = (const CBX_CONST int64_t*)c.excl;
+    return x[t.tile] - x[0];
+}
 
 // The element's int32 offsets (from the tile's place, base) and the slot's size; returns the tile's
 // destination, or null when the region (or an int32 offset) overflows.
@@ -1598,7 +1618,7 @@ __device__ __forceinline__ void str_element(const KernelArgs& a, const StrOp& op
     const bool packed = str_layout(a) == 2;
     CBX_GLOBAL uint8_t* dst;
     if (packed) {
-        const int64_t base = c.excl[t.tile] - c.excl[0];   // the tile's place in the slot's region
+        const int64_t base = utf8_tile_base(c, t);   // the tile's place in the slot's region
         const int64_t end = base + tot;
         CBX_GLOBAL int32_t* offs = gp((int32_t*)c.local);
         st_out(offs + t.tile * kWave + lane, (int32_t)(base + ex));
@@ -2132,12 +2152,34 @@ __device__ __forceinline__ void coop_issue(const KernelArgs& a, const ContigSpan
     }
 }
 
-template <int KP, typename Body>
+// Chunk rows of the wave's share (coop_issue's buf) into the workgroup's image; waits for the loads.
+template <int KP>
+__device__ __forceinline__ void coop_put(const KernelArgs& a, const ContigSpan& sp, int wid, int lane,
+                                         const uint4 (&buf)[(KP + kWavesPerBlock - 1) / kWavesPerBlock], uint8_t* s_img) {
+    constexpr int KH = (KP + kWavesPerBlock - 1) / kWavesPerBlock;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));   // (contig_store: no LDS addresses held across the decode)
+#pragma unroll
+    for (int v = 0; v < KH; v++) {
+        const int c = (v * kWavesPerBlock + wid) * kWave + ln;
+        if (c < sp.nch) contig_put(a, sp, c, buf[v], s_img);
+    }
+}
+
+// The next tile's image is written at the END of a tile (after the barrier that retires the image),
+// not at the top of the next one: its loads, issued at the top, are then followed in the same
+// iteration by the tile's value stores, and the wait for them is a counted vmcnt(N) that leaves those
+// stores in flight.  (At the loop top the wait merged the loop entry -- loads with nothing behind
+// them -- and became vmcnt(6..0): every tile waited for all of the previous tile's stores to be
+// acknowledged, in issue order, before staging.)  The first tile is loaded and staged before the loop.
+// kW: the wave (the kernel runs one instantiation per wave), so the wave's part of the tile
+// (body.part<kW>) is straight-line code between the loads and the wait for them.
+template <int KP, int kW, typename Body>
 __device__ __forceinline__ void coop_loop(const KernelArgs& a, const WaveLds& l, int64_t tile, int64_t tstep,
                                           int lane, Body body) {
     constexpr int KH = (KP + kWavesPerBlock - 1) / kWavesPerBlock;
     uint4 buf[KH];
-    const int wid = l.wid;
+    constexpr int wid = kW;
     body.wid = wid;
 #ifndef CBX_NO_COOP_PRIO
     // the tile's second wave at issue priority 1 for the whole loop (no per-segment flips): the
@@ -2147,35 +2189,30 @@ __device__ __forceinline__ void coop_loop(const KernelArgs& a, const WaveLds& l,
     if (wid == 1) __builtin_amdgcn_s_setprio(1);
 #endif
     tile = first_tile<Body>(tile);   // (the workgroup's tiles: runs of kVRun with run-gathered words)
-    if (tile < a.n_tiles) coop_issue<KP>(a, contig_span(a, tile), wid, lane, buf);
+    if (tile >= a.n_tiles) return;
+    coop_issue<KP>(a, contig_span(a, tile), wid, lane, buf);
+    coop_put<KP>(a, contig_span(a, tile), wid, lane, buf, l.img);
     Stamps st;
     st.init();
-    while (tile < a.n_tiles) {
-        const ContigSpan sp = contig_span(a, tile);
-        {
-            int ln = lane;
-            asm volatile("" : "+v"(ln));   // (contig_store: no LDS addresses held across the decode)
-#pragma unroll
-            for (int v = 0; v < KH; v++) {
-                const int c = (v * kWavesPerBlock + wid) * kWave + ln;
-                if (c < sp.nch) contig_put(a, sp, c, buf[v], l.img);
-            }
-        }
+    while (true) {
         __syncthreads();   // the tile's image complete
         st.mark(0);
+        const ContigSpan sp = contig_span(a, tile);
         const int64_t next = next_tile<Body>(tile, tstep);
         body.begin(tile);
+        // issued even past the last tile (a span of no chunks: every offset out of range, no access)
         coop_issue<KP>(a, contig_span(a, next), wid, lane, buf);
         st.mark(1);
         TileCtx t = tile_ctx<false>(a, tile, lane);
         const uint32_t rec0 = (uint32_t)(lane * a.cpitch + 4 * sp.mis_dw);
         st.mark(2);
-        body.pre(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
-        body.post(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
+        body.template part<kW>(a, t, (const uint8_t*)l.img, rec0 + (uint32_t)a.start_off, l, lane, st);
         run_end(a, body, tile, lane);
         __syncthreads();   // every wave done with the image
         st.mark(5);
         tile = next;
+        if (tile >= a.n_tiles) break;
+        coop_put<KP>(a, contig_span(a, tile), wid, lane, buf, l.img);
     }
     st.flush(a, lane);
 }

@@ -73,7 +73,7 @@ def _compile(src: str, lib_path: str | None = None) -> str:
 
 def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coop: bool = False, seg_pair: bool = False) -> str:
     """The specialised record kernel's source as cbx_jit.h emits it (jit_source), for a 3-element
-    string layout; coop: the cooperative form (jit_coop: coop_lds / coop_loop, ops split on l.wid);
+    string layout; coop: the cooperative form (jit_coop: coop_lds / coop_loop<KP, kW>, ops split on the wave, part<kW>);
     seg_pair: two segment-redefine elements in one pass (str_utf8_pair / str_count_pair)."""
     view = "true" if layout == 1 else "false"
     ops = [f"{{{20 * i},20,1,4,0,2,{i},0,{i},-1,{{0,0,0,0}},{{0,0,0,0}},0}}" for i in range(3)]
@@ -96,13 +96,14 @@ def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coo
         body = "".join(f"    {{ constexpr StrOp op = {o}; str_element<{view}>(a, op, a.sops + {i}, ldc(a.scall + {i}), t, l.cnt, img, rec_addr, false, l.lut, l.str, lane); }}\n"
                        + ("    } else {\n" if coop and i == 0 else "") for i, o in enumerate(ops))
         if coop:
-            body = "    if (l.wid == 0) {\n" + body + "    }\n"
+            body = "    if constexpr (kW == 0) {\n" + body + "    }\n"
     lds = "coop_lds" if coop else "wave_lds"
     lut = (f"  WaveLds l = {lds}(a, smem + 1024, wid);\n  l.lut = (uint32_t*)smem;\n"
            "  for (int i = threadIdx.x; i < 256; i += blockDim.x) { const uint32_t e = a.lut[i]; l.lut[i] = e; ((uint8_t*)(l.lut + 256))[i] = count_lut_byte(e); }\n"
            if count else
            f"  const WaveLds l = {lds}(a, smem, wid);\n  lut_lds_fill(a, l.lut);\n")
-    loop_call = ("  coop_loop<13>(a, l, (int64_t)blockIdx.x, (int64_t)gridDim.x, lane, JitBody{});\n}\n" if coop else
+    loop_call = ("  if (wid == 0) coop_loop<13, 0>(a, l, (int64_t)blockIdx.x, (int64_t)gridDim.x, lane, JitBody{});\n"
+                 "  else coop_loop<13, 1>(a, l, (int64_t)blockIdx.x, (int64_t)gridDim.x, lane, JitBody{});\n}\n" if coop else
                  "  int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid;\n"
                  "  const int64_t tstep = (int64_t)gridDim.x * kWavesPerBlock;\n"
                  "  contig_loop<13, 0, false>(a, l, tile, tstep, lane, JitBody{});\n}\n")
@@ -112,7 +113,9 @@ def _record_kernel(layout: int, count: bool, loop: bool, pair: bool = False, coo
             "#include \"cbx_device.h\"\nnamespace cbx {\nstruct JitBody {\n  static constexpr int kWords = 0;\n  int wid = 0;\n  DirectSink vw;\n"
             "  __device__ __forceinline__ void begin(int64_t) {}\n"
             "  __device__ __forceinline__ void flush(const KernelArgs&, int64_t, int) {}\n"
-            "  __device__ __forceinline__ void pre" + sig + body + "  }\n"
+            + ("  template <int kW>\n  __device__ __forceinline__ void part" + sig + body + "  }\n"
+               "  __device__ __forceinline__ void pre" + sig + "  }\n" if coop else
+               "  __device__ __forceinline__ void pre" + sig + body + "  }\n") +
             "  __device__ __forceinline__ void post" + sig + "  }\n};\n}  // namespace cbx\n"
             "extern \"C\" __global__ __launch_bounds__(cbx::kWave * cbx::kWavesPerBlock) void k(cbx::KernelArgs a) {\n"
             "  using namespace cbx;\n  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"

@@ -27,10 +27,9 @@ def main():
             subprocess.run(["tar", "-x", "-C", d], input=arch, check=True)
         csrc = os.path.join(d, "cobrix_amd", "csrc")
         inc = os.path.join(d, "include")
-        G.JIT_HEADERS = (("cobrix_hip.h", os.path.join(inc, "cobrix_hip.h")),
-                         ("cbx_decode.h", os.path.join(csrc, "cbx_decode.h")),
-                         ("cbx_internal.h", os.path.join(csrc, "cbx_internal.h")),
-                         ("cbx_device.h", os.path.join(csrc, "cbx_device.h")))
+        # the bundle's header set as __graft_entry__ lists it, taken from the revision's tree
+        G.JIT_HEADERS = tuple((n, os.path.join(inc if n == "cobrix_hip.h" else csrc, n)) for n, _ in G.JIT_HEADERS
+                              if os.path.exists(os.path.join(inc if n == "cobrix_hip.h" else csrc, n)))
         G.CSRC = csrc
         G._write_jit_bundle()
         out = os.path.join(ROOT, "cobrix_amd", f"libcobrix_hip_{name}.so")
