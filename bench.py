@@ -438,12 +438,13 @@ class _VarLen:
         self.prm = self.rd.rdw_params()
         self.seed_mb = seed_mb
         t0 = time.perf_counter()
-        if world > 1 and seed_mb == 100:
+        if world > 1:
             # O(shard) setup: rank r generates block r only (its size first, then in place behind a
             # room for one index entry of tail), and the file's index is built as a chain over the
-            # ranks (shard.index_chain: the 100 MB default resets at every cut) -- each rank holds its
-            # block + the tail of the file before it that its run starts in
-            S = 100 * 1024 * 1024
+            # ranks (shard.index_chain: the 100 MB default resets at every cut; a 32 MB block size is
+            # subtracted, and the link carries the residual) -- each rank holds its block + the tail of
+            # the file before it that its run starts in
+            S = seed_mb * 1024 * 1024
             room = (S + (16 << 20) + 255) & ~255
             blen = size(rank)
             buf = torch.empty(room + blen, dtype=torch.uint8, device=dev)
@@ -451,14 +452,14 @@ class _VarLen:
             n_block = int(hdr.numel())
             del hdr
 
-            def index_fn(region):
+            def index_fn(region, start_bytes):
                 n = int(region.numel())
                 off, ln, nf = _frame_rdw(L, region, n, [0], self.prm, n_block + (n - blen) // 8 + 2, dev, st)
-                ents = idx_rd.generate_index(region, n, off[:nf], ln[:nf])
+                ents = idx_rd.generate_index(region, n, off[:nf], ln[:nf], start_bytes=start_bytes)
                 del off, ln
                 return [(e.offset_from, e.record_index) for e in ents], nf
 
-            res = index_chain(buf, room, index_fn)
+            res = index_chain(buf, room, index_fn, split_bytes=idx_rd.split_residual_bytes())
             torch.cuda.synchronize()
             self.index_ms = (time.perf_counter() - t0) * 1e3
             self.raw = res["run"]
@@ -473,27 +474,16 @@ class _VarLen:
             self.setup_bytes_held = int(buf.numel())
             torch.cuda.empty_cache()
             self.shard_note = (f"entries [{k0}, {k0 + len(res['entries'])}) of the file's {self.n_entries_file} "
-                               f"(100 MB index built as a chain over the ranks, shard.index_chain), bytes "
+                               f"({seed_mb} MB index built as a chain over the ranks, shard.index_chain), bytes "
                                f"[{lo}, {lo + self.in_bytes}) of {total_bytes}; this rank generated and holds "
                                f"only its block + {room} bytes of room for the tail before it "
                                f"({self.setup_bytes_held / max(1, self.in_bytes):.3f} x its run); Record_Id base "
                                f"from a device all-gather of record counts")
             return
-        # one GPU (or the subtracting 32 MB split, whose cuts carry a residual and are not a chain):
-        # the whole file of `world` blocks, framed and indexed here
-        if world == 1:
-            full, hdr = gen(0)
-            starts, n_total = [0], int(hdr.numel())
-            del hdr
-        else:
-            sizes = [size(b) for b in range(world)]
-            starts = [sum(sizes[:b]) for b in range(world)]
-            full = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
-            n_total = 0
-            for b in range(world):
-                _, h = gen(b, out=full[starts[b]:starts[b] + sizes[b]])
-                n_total += int(h.numel())
-                del h
+        # one GPU: the whole file, framed and indexed here
+        full, hdr = gen(0)
+        starts, n_total = [0], int(hdr.numel())
+        del hdr
         torch.cuda.synchronize()
         total_bytes = int(full.numel())
         off, ln, nf = _frame_rdw(L, full, total_bytes, starts, self.prm, n_total + 1, dev, st)

@@ -1999,8 +1999,9 @@ extern "C" int cbx_sparse_index(cbx_plan* P, const uint8_t* d_data, int64_t n_by
     hipStream_t st = (hipStream_t)stream;
     if (!P || !prm || !n_entries || capacity < 0 || (capacity > 0 && !entries) || n_rec < 0 ||
         (n_rec > 0 && (!d_rec_off || !d_rec_len || !d_data)) || (prm->header_bytes != 0 && prm->header_bytes != 4) ||
-        prm->records_per_entry < 0 || (prm->records_per_entry == 0 && prm->bytes_per_entry <= 0))
+        prm->records_per_entry < 0 || (prm->records_per_entry == 0 && prm->bytes_per_entry <= 0) || prm->start_bytes < 0)
         return fail(CBX_E_ARGUMENT, "cbx_sparse_index: invalid arguments");
+    const int64_t rho = prm->start_bytes;   // bytesInChunk at the first record (an entry already cut)
     *n_entries = 0;
     bool root_keys = false;   // level-0 keys: segment_id_level0 / segment_id_root, or a hierarchical file's root ids
     for (int k = 0; P->opts.has_segments && k < P->opts.segments.n_keys; k++) root_keys |= P->opts.segments.key_level[k] == 0;
@@ -2064,11 +2065,12 @@ extern "C" int cbx_sparse_index(cbx_plan* P, const uint8_t* d_data, int64_t n_by
                 HIP_CHECK(hipMemcpyAsync(&last_off, d_rec_off + last, sizeof(int64_t), hipMemcpyDeviceToHost, st));
                 HIP_CHECK(hipMemcpyAsync(&first_cand, cand, sizeof(int64_t), hipMemcpyDeviceToHost, st));
                 HIP_CHECK(hipStreamSynchronize(st));
-                const int64_t K = (last_off - prm->header_bytes) / S + 1;
+                // thresholds j S - rho (bytesInChunk = prefix + rho - cuts S), j = 1..K
+                const int64_t K = (last_off - prm->header_bytes + rho) / S + 1;
                 HIP_CHECK(hipMallocAsync(&blk2.p, sizeof(int64_t) * (2 * K + 2), st));
                 int64_t* rj = (int64_t*)blk2.p;
                 hipLaunchKernelGGL(idx_size_kernel, dim3(blocks_for(K, 256)), dim3(256), 0, st, ia, (const int64_t*)cand, n_cand,
-                                   S, K, rj);
+                                   S, K, rho, rj);
                 HIP_CHECK(hipGetLastError());
                 std::vector<int64_t> h(K);
                 HIP_CHECK(hipMemcpyAsync(h.data(), rj, sizeof(int64_t) * K, hipMemcpyDeviceToHost, st));
@@ -2096,7 +2098,7 @@ extern "C" int cbx_sparse_index(cbx_plan* P, const uint8_t* d_data, int64_t n_by
                 HIP_CHECK(hipMallocAsync(&blk2.p, sizeof(int64_t) * (n_cand + 2), st));
                 d_split = (int64_t*)blk2.p + 1;
                 hipLaunchKernelGGL(idx_walk_kernel, dim3(1), dim3(64), 0, st, ia, (const int64_t*)cand, n_cand, N > 0 ? 0 : 2, N,
-                                   S, d_split, n_cand, (int64_t*)blk2.p);
+                                   S, N > 0 ? 0 : rho, d_split, n_cand, (int64_t*)blk2.p);
                 HIP_CHECK(hipGetLastError());
                 HIP_CHECK(hipMemcpyAsync(&n_split, blk2.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
                 HIP_CHECK(hipStreamSynchronize(st));

@@ -367,11 +367,13 @@ __global__ void idx_compact_kernel(IdxArgs a, const uint32_t* flag, const int64_
 
 __device__ __forceinline__ int64_t idx_prefix(const IdxArgs& a, int64_t i) { return a.rec_off[i] - a.header_bytes; }
 
-// subtract mode: r_j = first candidate rank with prefix >= j*S, for j = 1..K (binary search)
-__global__ void idx_size_kernel(IdxArgs a, const int64_t* cand, int64_t n_cand, int64_t S, int64_t K, int64_t* rj) {
+// subtract mode: r_j = first candidate rank with prefix >= j*S - rho, for j = 1..K (binary search);
+// rho: bytesInChunk at the first record (IndexGenerator.scala:88-127, a piece of a file that starts at
+// one of its entries carries that entry's residual)
+__global__ void idx_size_kernel(IdxArgs a, const int64_t* cand, int64_t n_cand, int64_t S, int64_t K, int64_t rho, int64_t* rj) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
     if (j > K) return;
-    const int64_t target = j * S;
+    const int64_t target = j * S - rho;
     int64_t lo = 0, hi = n_cand;
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
@@ -382,14 +384,14 @@ __global__ void idx_size_kernel(IdxArgs a, const int64_t* cand, int64_t n_cand, 
 
 // One wave walks the split chain over the candidate list: from rank `cur`, the next split is the
 // first rank whose candidate satisfies the target; probes of 64 ranks, galloping then 64-ary search.
-// mode 0: records (target index s + N);  mode 2: size-reset (target prefix(s) + S).
-// out[k] = framed index of split k (k >= 1); *n_out = number of splits.
+// mode 0: records (target index s + N);  mode 2: size-reset (target prefix(s) + S; the first entry's
+// bytesInChunk starts at rho).  out[k] = framed index of split k (k >= 1); *n_out = number of splits.
 __global__ __launch_bounds__(64) void idx_walk_kernel(IdxArgs a, const int64_t* cand, int64_t n_cand, int mode,
-                                                      int64_t N, int64_t S, int64_t* out, int64_t cap, int64_t* n_out) {
+                                                      int64_t N, int64_t S, int64_t rho, int64_t* out, int64_t cap, int64_t* n_out) {
     const int lane = threadIdx.x;
     // entry 0 starts at record 0 (numbering position 0); its "position" for the targets:
     int64_t pos_num = 0;                       // record number of the current split
-    int64_t pos_prefix = 0;                    // its header offset
+    int64_t pos_prefix = -rho;                 // its header offset (less the bytes it starts with)
     int64_t cur = -1;                          // candidate rank of the current split (-1: entry 0)
     int64_t k = 0;
     auto ok = [&](int64_t r) -> bool {         // candidate r satisfies the target (monotone in r)

@@ -109,7 +109,7 @@ class CbxRdwParams(ctypes.Structure):
 
 class CbxIndexEntry(ctypes.Structure):
     _fields_ = [("offset_from", ctypes.c_int64), ("offset_to", ctypes.c_int64), ("record_index", ctypes.c_int64),
-                ("file_id", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("file_id", ctypes.c_int32), ("reserved", ctypes.c_int32), ("start_bytes", ctypes.c_int64)]
 
 
 class CbxIndexParams(ctypes.Structure):

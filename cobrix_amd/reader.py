@@ -1102,11 +1102,14 @@ class VarLenNestedReader(_BaseReader):
         return prm
 
     def generate_index(self, d_data, n_bytes: int, rec_off, rec_len, file_id: int = 0,
-                       stream=None) -> List[SparseIndexEntry]:
-        """GPU sparse index over the framed file (IndexGenerator.sparseIndexGenerator)."""
+                       stream=None, start_bytes: int = 0) -> List[SparseIndexEntry]:
+        """GPU sparse index over the framed file (IndexGenerator.sparseIndexGenerator).  start_bytes:
+        bytesInChunk at the first record, for a piece of a file starting at one of its entries
+        (cobrix_hip.h cbx_index_params; shard.index_chain)."""
         torch = _torch()
         st = stream if stream is not None else torch.cuda.current_stream()
         prm = self.index_params(file_id)
+        prm.start_bytes = int(start_bytes)
         L = N.load()
         n = ctypes.c_int64(0)
         cap = 1024
@@ -1121,6 +1124,13 @@ class VarLenNestedReader(_BaseReader):
             N.check(rc)
             break
         return [SparseIndexEntry(e.offset_from, e.offset_to, e.file_id, e.record_index) for e in ents[: n.value]]
+
+    def split_residual_bytes(self) -> Optional[int]:
+        """The split size when IndexGenerator subtracts it at every cut (isSplitBySize: an explicit
+        input_split_size_mb / the HDFS block size), else None (records, or the 100 MB default that resets)."""
+        p = self.params
+        split_mb = p.input_split_size_mb if p.input_split_size_mb is not None else p.hdfs_default_block_size_mb
+        return split_mb * 1024 * 1024 if p.input_split_records is None and split_mb is not None else None
 
     def index_generation_needed(self) -> bool:
         """VarLenNestedReader.isIndexGenerationNeeded (:85)."""

@@ -88,7 +88,7 @@ def entry_shards(entries, n_bytes: int, world: int) -> List[Tuple[int, int]]:
     return out
 
 
-def index_chain(buf, tail_room: int, index_fn, group=None) -> dict:
+def index_chain(buf, tail_room: int, index_fn, group=None, split_bytes: Optional[int] = None) -> dict:
     """Sparse index of ONE variable-length file whose blocks are spread over the ranks (rank r holds
     block r, the blocks in rank order, each starting at a record header), with every rank holding
     only its own block plus, in front of it, the tail of the file before it that belongs to its run.
@@ -98,12 +98,15 @@ def index_chain(buf, tail_room: int, index_fn, group=None) -> dict:
     only on the records from that start on: the file's index is a chain.  Rank r receives from rank
     r - 1 the start of the last entry found so far (file offset, record index) and the bytes from
     there to the end of block r - 1 (at most one entry), indexes that tail + its block as a file of
-    its own -- index_fn(region) -> ([(offset_from, record_index)] region-relative, the first (0, 0);
-    record count) -- keeps every entry but the last, and sends the last one on.  The last rank keeps
-    all of its entries.  Rank r's run = its entries: a contiguous, balanced (one block, give or take
-    an entry) share of the file in file order; the union over the ranks is the whole file's index.
-    (The subtracting split-size rule carries a residual across cuts and is not a chain of this form:
-    callers index such files whole.)
+    its own -- index_fn(region, start_bytes) -> ([(offset_from, record_index)] region-relative, the
+    first (0, 0); record count) -- keeps every entry but the last, and sends the last one on.  The last
+    rank keeps all of its entries.  Rank r's run = its entries: a contiguous, balanced (one block, give
+    or take an entry) share of the file in file order; the union over the ranks is the whole file's index.
+    The subtracting split-size rule (split_bytes: an explicit input_split_size_mb or the HDFS block size,
+    VarLenNestedReader.scala:237-243) does not reset the byte count at a cut, it subtracts the split size:
+    the count at entry k is its offset minus k split sizes, so the link also carries that residual of
+    the entry it hands on, and the next rank indexes its region starting from it (start_bytes; 0 with
+    the resetting default, whose count is 0 at every entry).
 
     buf: uint8 tensor [tail_room + block bytes], the block at buf[tail_room:]; the received tail
     lands right in front of it.  Point-to-point send/recv of int64[3] + the tail bytes (device
@@ -128,19 +131,19 @@ def index_chain(buf, tail_room: int, index_fn, group=None) -> dict:
         else:
             dist.recv(t, src=src, group=group)
 
-    meta = torch.zeros(3, dtype=torch.int64, device=cdev)   # file offset, record index, tail bytes
+    meta = torch.zeros(4, dtype=torch.int64, device=cdev)   # file offset, record index, tail bytes, residual
     if rank > 0:
         dist.recv(meta, src=rank - 1, group=group)
-    r_off, r_rec, tail = (int(x) for x in meta.tolist())
+    r_off, r_rec, tail, r_res = (int(x) for x in meta.tolist())
     if tail < 0:
         raise RuntimeError(f"index_chain: rank {rank - 1} had a tail larger than the {tail_room}-byte room")
     if tail > 0:
         recv_into(buf[tail_room - tail:tail_room], rank - 1)
-    res, fwd = chain_step(buf[tail_room - tail:], index_fn, r_off, r_rec, rank == world - 1)
+    res, fwd = chain_step(buf[tail_room - tail:], index_fn, r_off, r_rec, rank == world - 1, r_res, split_bytes)
     if fwd is not None:
-        f_off, f_rec, f_bytes = fwd
+        f_off, f_rec, f_bytes, f_res = fwd
         ok = f_bytes.numel() <= tail_room
-        out = torch.tensor([f_off, f_rec, f_bytes.numel() if ok else -1], dtype=torch.int64, device=cdev)
+        out = torch.tensor([f_off, f_rec, f_bytes.numel() if ok else -1, f_res], dtype=torch.int64, device=cdev)
         dist.send(out, dst=rank + 1, group=group)
         if not ok:
             raise RuntimeError(f"index_chain: {f_bytes.numel()}-byte tail for rank {rank + 1} exceeds the "
@@ -150,18 +153,21 @@ def index_chain(buf, tail_room: int, index_fn, group=None) -> dict:
     return res
 
 
-def chain_step(region, index_fn, r_off: int, r_rec: int, last: bool):
+def chain_step(region, index_fn, r_off: int, r_rec: int, last: bool, r_res: int = 0,
+               split_bytes: Optional[int] = None):
     """One link of index_chain: `region` starts at the file offset r_off (record index r_rec) at an
-    entry start and runs to the end of this rank's block.  Returns (result, forward): the result dict
-    of index_chain, and (file offset, record index, bytes) of the entry handed to the next rank (None
-    for the last rank)."""
-    ents, n_rec = index_fn(region)
+    entry start, whose byte count is r_res (subtracting split), and runs to the end of this rank's
+    block.  Returns (result, forward): the result dict of index_chain, and (file offset, record index,
+    bytes, residual) of the entry handed to the next rank (None for the last rank)."""
+    ents, n_rec = index_fn(region, r_res)
     if not ents or ents[0][0] != 0:
         raise RuntimeError("index_chain: index_fn must return the region's entries, the first at offset 0")
     fwd = None
     if not last:
         last_off, last_rec = ents[-1]
-        fwd = (r_off + last_off, r_rec + last_rec, region[last_off:])
+        # IndexGenerator.scala:110-116: the count at the region's k-th entry = r_res + its offset - k S
+        res_last = r_res + last_off - (len(ents) - 1) * split_bytes if split_bytes else 0
+        fwd = (r_off + last_off, r_rec + last_rec, region[last_off:], res_last)
         keep, run_end, n_run = ents[:-1], last_off, last_rec
     else:
         keep, run_end, n_run = ents, int(region.numel()), n_rec

@@ -354,7 +354,11 @@ int cbx_frame_rdw_state(const int64_t* d_state, int64_t* n_records, void* stream
  * subtract_size != 0 (input_split_size_mb / HDFS block size: the split size is subtracted, not
  * reset), or the 100 MB default (reset); with `hierarchical` only at records whose segment id is
  * a level-0 key of the plan's segment map.  The first entry is (0, -1, file_id, 0); the last
- * entry's offset_to is -1.  record_index counts every header read (the file header record too). */
+ * entry's offset_to is -1.  record_index counts every header read (the file header record too).
+ * start_bytes: IndexGenerator's bytesInChunk as of the first framed record, which is taken as an entry
+ * already cut -- 0 for a whole file; for a piece of a file that starts at one of the file's entries, that
+ * entry's residual under the subtracting size split (its header offset minus the split size times the
+ * cuts up to it): the piece's entries are then the file's (shard.index_chain). */
 typedef struct {
     int64_t offset_from, offset_to;
     int64_t record_index;
@@ -371,6 +375,7 @@ typedef struct {
     int32_t hierarchical;       /* cut only at level-0 segment records (segment levels given) */
     int32_t file_id;
     int32_t reserved;
+    int64_t start_bytes;        /* bytesInChunk at the first framed record (0: a whole file) */
 } cbx_index_params;
 
 int cbx_sparse_index(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,

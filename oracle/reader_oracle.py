@@ -171,10 +171,14 @@ class Entry:
 
 
 def sparse_index(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
-                 default_entry_bytes: Optional[int] = None) -> List[Entry]:
+                 default_entry_bytes: Optional[int] = None, split_bytes: Optional[int] = None,
+                 start_bytes: int = 0) -> List[Entry]:
     """VarLenNestedReader.generateIndex (:125-180) -> IndexGenerator.sparseIndexGenerator (:33-157).
     default_entry_bytes replaces Constants.defaultIndexEntrySizeMB (tests of the reset rule on
-    small files)."""
+    small files); split_bytes replaces split_mb * MEGABYTE of an explicit (subtracted) split size (tests
+    of the subtract rule on small files).  start_bytes: bytesInChunk as of the first record, taken as an
+    entry already cut (a piece of a file that starts at one of its entries; 0 for a whole file -- where
+    the first record is never cut either)."""
     rp = header_parser(cb, p)
     split_records = p.input_split_records
     split_mb = p.input_split_size_mb if p.input_split_size_mb is not None else p.hdfs_default_block_size_mb
@@ -192,13 +196,16 @@ def sparse_index(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
     really_hier = seg_reader is not None and is_hier
     split_by_size = split_records is None and split_mb is not None
     bytes_per = split_mb * MEGABYTE if split_mb is not None else (default_entry_bytes or DEFAULT_ENTRY_MB * MEGABYTE)
+    if split_bytes is not None:
+        split_by_size, bytes_per = split_records is None, split_bytes
 
     def need_split(records: int, size: int) -> bool:
         return records >= split_records if split_records is not None else size >= bytes_per
 
     s = Stream(data)
     index = [Entry(0, -1, file_id, 0)]
-    byte_index = records_in_chunk = bytes_in_chunk = record_index = 0
+    byte_index = records_in_chunk = record_index = 0
+    bytes_in_chunk = start_bytes
     root_record_id = ""
     while True:
         hdr = s.next(rp.header_length)
@@ -212,13 +219,13 @@ def sparse_index(cb: cbk.Copybook, data: bytes, p, file_id: int = 0,
                 cur = _trim(seg_reader.segment_id(record))
                 if (cur != "" and not root_ids) or cur in root_ids:
                     root_record_id = cur
-            if need_split(records_in_chunk, bytes_in_chunk):
+            if record_index > 0 and need_split(records_in_chunk, bytes_in_chunk):
                 if not really_hier or _trim(seg_reader.segment_id(record)) in root_ids:
                     index[-1].offset_to = byte_index
                     index.append(Entry(byte_index, -1, file_id, record_index))
                     records_in_chunk = 0
                     if split_by_size:
-                        bytes_in_chunk -= split_mb * MEGABYTE
+                        bytes_in_chunk -= bytes_per
                     else:
                         bytes_in_chunk = 0
         record_index += 1

@@ -355,10 +355,12 @@ def test_async_framing_reports_errors_on_the_device(monkeypatch):
         assert np.array_equal(off, eo) and np.array_equal(ln, el) and s == [len(eo), -1, 0]
 
 
-def test_index_chain_on_the_device_equals_whole_file_index():
+@pytest.mark.parametrize("subtract", [0, 1])
+def test_index_chain_on_the_device_equals_whole_file_index(subtract):
     """shard.chain_step links run in sequence on the GPU (framing + cbx_sparse_index of each rank's
-    tail + block, 64 kB entries at roots): the union of the runs' entries is the GPU index of the
-    whole file, the runs tile it, and the record bases are the counts before each run."""
+    tail + block, 64 kB entries at roots; resetting or subtracting the split size, the subtracting links
+    starting from the residual the previous link hands on): the union of the runs' entries is the GPU
+    index of the whole file, the runs tile it, and the record bases are the counts before each run."""
     import ctypes
     from cobrix_amd import native as N
     from cobrix_amd.shard import chain_step
@@ -368,11 +370,11 @@ def test_index_chain_on_the_device_equals_whole_file_index():
         is_record_sequence=True, segment_field="SEGMENT-ID", segment_id_levels=["C"]))
     S = 64 * 1024
 
-    def index_fn(region):
+    def index_fn(region, start_bytes=0):
         n = int(region.numel())
         off, ln = rd.frame(region, n)
         prm = rd.index_params()
-        prm.bytes_per_entry, prm.subtract_size = S, 0
+        prm.bytes_per_entry, prm.subtract_size, prm.start_bytes = S, subtract, start_bytes
         arr = (N.CbxIndexEntry * 4096)()
         ne = ctypes.c_int64(0)
         N.check(N.load().cbx_sparse_index(rd.native.handle, region.data_ptr(), n, off.data_ptr(), ln.data_ptr(),
@@ -381,15 +383,17 @@ def test_index_chain_on_the_device_equals_whole_file_index():
 
     whole = torch.cat(blocks)
     exp, n_all = index_fn(whole)
-    got, runs, r_off, r_rec, tail = [], [], 0, 0, None
+    got, runs, r_off, r_rec, r_res, tail = [], [], 0, 0, 0, None
     for b, blk in enumerate(blocks):
         region = blk if tail is None else torch.cat([tail, blk])
-        res, fwd = chain_step(region, index_fn, r_off, r_rec, b == len(blocks) - 1)
+        res, fwd = chain_step(region, index_fn, r_off, r_rec, b == len(blocks) - 1, r_res, S if subtract else None)
         assert res["record_base"] == sum(r["n_records"] for r in runs)
         got += res["entries"]
         runs.append(res)
         if fwd is not None:
-            r_off, r_rec, tail = fwd[0], fwd[1], fwd[2].clone()
+            r_off, r_rec, tail, r_res = fwd[0], fwd[1], fwd[2].clone(), fwd[3]
+            # the residual is the whole file's bytesInChunk at that entry: its offset minus the cuts so far
+            assert not subtract or r_res == r_off - len(got) * S
     assert len(exp) > 8 and got == exp
     assert torch.equal(torch.cat([r["run"] for r in runs]), whole)
     assert sum(r["n_records"] for r in runs) == n_all

@@ -157,7 +157,7 @@ def test_bench_rejects_world_mismatch():
     assert r.returncode == 2 and "WORLD_SIZE 1 != --gpus 2" in r.stderr
 
 
-def _chain_worker(rank, world, port, q, entry_bytes):
+def _chain_worker(rank, world, port, q, entry_bytes, subtract=False):
     """One rank of a chained index (shard.index_chain): it holds only its own block of the file and
     the tail the rank before it sends; index_fn = the oracle restatement of IndexGenerator."""
     import torch.distributed as dist
@@ -177,12 +177,13 @@ def _chain_worker(rank, world, port, q, entry_bytes):
     p, _ = parse_options({**_CHAIN_OPTS})
     cb = parse_copybook_for(RDW_NARROW_COPYBOOK, p)
 
-    def index_fn(region):
+    def index_fn(region, start_bytes):
         raw = region.numpy().tobytes()
-        ents = RO.sparse_index(cb, raw, p, 0, entry_bytes)
+        ents = (RO.sparse_index(cb, raw, p, 0, split_bytes=entry_bytes, start_bytes=start_bytes) if subtract
+                else RO.sparse_index(cb, raw, p, 0, entry_bytes))
         return [(e.offset_from, e.record_index) for e in ents], len(O.frame_rdw(raw)[0])
 
-    r = index_chain(buf, room, index_fn)
+    r = index_chain(buf, room, index_fn, split_bytes=entry_bytes if subtract else None)
     q.put((rank, r["entries"], r["record_base"], r["n_records"], r["run_start"], r["seeds"],
            r["run"].numpy().tobytes()))
     dist.destroy_process_group()
@@ -191,12 +192,14 @@ def _chain_worker(rank, world, port, q, entry_bytes):
 _CHAIN_OPTS = {"is_record_sequence": "true", "segment_field": "SEGMENT_ID", "segment_id_root": "C"}
 
 
+@pytest.mark.parametrize("subtract", [False, True], ids=["reset", "subtract"])
 @pytest.mark.parametrize("world,entry_bytes", [(2, 20_000), (3, 7_000), (3, 100_000)])
-def test_index_chain_equals_whole_file_index_gloo(world, entry_bytes):
+def test_index_chain_equals_whole_file_index_gloo(world, entry_bytes, subtract):
     """A file's index computed as a chain over ranks that each hold one block (+ one entry of tail)
     equals the oracle's index of the whole file: same entries, the runs tile the file in order, the
     record bases are the record counts before each run.  At 100 kB entries over ~200 kB blocks
-    some ranks get one entry or none."""
+    some ranks get one entry or none.  subtract: the split size subtracted at each cut (an explicit
+    split size / the HDFS block size, IndexGenerator.scala:110-116), the links carrying the residual."""
     from cobrix_amd.options import parse_options
     from cobrix_amd.reader import parse_copybook_for
     from cobrix_amd.synth import RDW_NARROW_COPYBOOK, rdw_narrow
@@ -205,7 +208,7 @@ def test_index_chain_equals_whole_file_index_gloo(world, entry_bytes):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_chain_worker, args=(r, world, port, q, entry_bytes)) for r in range(world)]
+    procs = [ctx.Process(target=_chain_worker, args=(r, world, port, q, entry_bytes, subtract)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = sorted(q.get(timeout=180) for _ in range(world))
@@ -215,7 +218,9 @@ def test_index_chain_equals_whole_file_index_gloo(world, entry_bytes):
     whole = b"".join(rdw_narrow(2500 + 700 * b, seed=40 + b)[0].numpy().tobytes() for b in range(world))
     p, _ = parse_options({**_CHAIN_OPTS})
     cb = parse_copybook_for(RDW_NARROW_COPYBOOK, p)
-    exp = [(e.offset_from, e.record_index) for e in RO.sparse_index(cb, whole, p, 0, entry_bytes)]
+    ents = (RO.sparse_index(cb, whole, p, 0, split_bytes=entry_bytes) if subtract
+            else RO.sparse_index(cb, whole, p, 0, entry_bytes))
+    exp = [(e.offset_from, e.record_index) for e in ents]
     assert len(exp) > world
     assert [e for r in res for e in r[1]] == exp
     assert b"".join(r[6] for r in res) == whole
