@@ -2346,6 +2346,25 @@ extern "C" int cbx_views_to_utf8(const uint8_t* d_views, int64_t n, const uint8_
     return CBX_OK;
 }
 
+extern "C" int cbx_hier_dependee_values(cbx_plan* P, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                                        const int32_t* d_rec_len, int64_t n_rows, int32_t start_offset, int32_t field,
+                                        int64_t* d_values, uint64_t* d_validity, void* stream) {
+    if (!P || n_rows < 0 || n_bytes < 0 || start_offset < 0 || field < 0 || field >= (int32_t)P->hfields.size() ||
+        (n_rows > 0 && (!d_data || !d_rec_off || !d_rec_len || !d_values || !d_validity)))
+        return fail(CBX_E_ARGUMENT, "cbx_hier_dependee_values: invalid arguments");
+    const Field f = P->dfields_h[field];
+    if (!(f.kind == CBX_K_BCD || f.kind == CBX_K_BINARY || f.kind == CBX_K_ASCII_NUM || f.kind == CBX_K_ZONED) ||
+        f.n_dims != 0)
+        return fail(CBX_E_UNSUPPORTED, "cbx_hier_dependee_values: the field is not an integral DEPENDING ON field");
+    if (n_rows > 0) {
+        hipLaunchKernelGGL(hier_dep_values_kernel, dim3(blocks_for(n_rows, 64)), dim3(64), 0, (hipStream_t)stream, d_data,
+                           n_bytes, d_rec_off, d_rec_len, n_rows, start_offset, (const CBX_CONST Field*)P->d_fields + field,
+                           d_values, d_validity);
+        HIP_CHECK(hipGetLastError());
+    }
+    return CBX_OK;
+}
+
 extern "C" int cbx_hier_dependee_counts(const cbx_hier_walk* walk, const cbx_hier_dependee* deps, int32_t n_deps,
                                         const cbx_hier_odo_array* arrays, int32_t n_arrays, int32_t* d_counts, int64_t pitch,
                                         int32_t* d_changed, void* stream) {

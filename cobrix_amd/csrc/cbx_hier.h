@@ -329,6 +329,33 @@ __global__ void hier_root_pos_kernel(HierArgs a, const int64_t* excl, int64_t* r
     if (i < a.n && a.type[i] == a.root) root_pos[excl[i]] = i;
 }
 
+// ---- dependee values of the rows (cbx_hier_dependee_values) ----
+// One thread per row: the field decoded from the row's bytes as Primitive.decodeTypeValue does
+// (RecordExtractors.extractValue, :276-292) -- null past the row's end or when malformed -- as the
+// integer its registration keeps (Number.intValue).  Independent of the row's segment: the root record
+// decodes every segment group from its own bytes (getGroupValues over the record group, :365-372).
+// Validity: one ballot word per 64 rows.
+__global__ __launch_bounds__(64) void hier_dep_values_kernel(const uint8_t* data, int64_t n_bytes, const int64_t* rec_off,
+                                                            const int32_t* rec_len, int64_t n, int32_t start_off,
+                                                            const CBX_CONST Field* fp, int64_t* values, uint64_t* validity) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const Field f = ldc(fp);
+    bool ok = false;
+    int64_t v = 0;
+    if (x < n) {
+        const int64_t base = rec_off[x];
+        const int64_t o = base + start_off + f.offset;
+        if (f.offset + start_off + f.size <= rec_len[x] && o >= 0 && o + f.size <= n_bytes) {
+            const Val dv = decode_count_int(f, data + o);
+            ok = dv.valid;
+            v = (int64_t)dv.lo;
+        }
+        values[x] = v;
+    }
+    const uint64_t m = __ballot(ok);
+    if (threadIdx.x == 0 && x < n) validity[x >> 6] = m;
+}
+
 // ---- the shared dependFields map (cbx_hier_dependee_counts) ----
 // One thread per hierarchical record (root row r): the reference's recursive walk as an explicit
 // stack of (row, segment, child-type cursor, child-row range), each row's events replayed in field
@@ -362,8 +389,8 @@ __device__ __forceinline__ void hier_dep_events(const HierDepArgs& a, int ev_row
             const int dd = A.dependee;
             const int32_t v = regv[dd];
             const int32_t c = ((regok >> dd) & 1u) && v >= A.min_count && v <= A.max_count ? v : A.max_count;
-            counts[(int64_t)A.out_row * pitch + x] = root ? -1 : c;
-            if (!root && A.first_counts && A.first_counts[x] != c) *changed = 1;
+            counts[(int64_t)A.out_row * pitch + x] = c;
+            if (A.first_counts && A.first_counts[x] != c) *changed = 1;
         }
     }
 }

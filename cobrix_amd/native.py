@@ -43,8 +43,8 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
                     "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs",
                     "cbx_plan_set_record_base", "cbx_frame_length_field", "cbx_plan_set_odo_counts",
-                    "cbx_hier_dependee_counts", "cbx_views_to_utf8", "cbx_plan_pipeline")
-ABI_VERSION = 17
+                    "cbx_hier_dependee_counts", "cbx_hier_dependee_values", "cbx_views_to_utf8", "cbx_plan_pipeline")
+ABI_VERSION = 18
 
 
 class NativeLibraryError(RuntimeError):
@@ -109,14 +109,14 @@ class CbxRdwParams(ctypes.Structure):
 
 class CbxIndexEntry(ctypes.Structure):
     _fields_ = [("offset_from", ctypes.c_int64), ("offset_to", ctypes.c_int64), ("record_index", ctypes.c_int64),
-                ("file_id", ctypes.c_int32), ("reserved", ctypes.c_int32), ("start_bytes", ctypes.c_int64)]
+                ("file_id", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class CbxIndexParams(ctypes.Structure):
     _fields_ = [("records_per_entry", ctypes.c_int64), ("bytes_per_entry", ctypes.c_int64),
                 ("subtract_size", ctypes.c_int32), ("header_bytes", ctypes.c_int32),
                 ("has_file_header", ctypes.c_int32), ("hierarchical", ctypes.c_int32),
-                ("file_id", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("file_id", ctypes.c_int32), ("reserved", ctypes.c_int32), ("start_bytes", ctypes.c_int64)]
 
 
 class CbxSelection(ctypes.Structure):
@@ -223,6 +223,7 @@ def load():
                      ("cbx_frame_length_field", [P, P, i64, i32, i32, i32, i32, P, P, i64, P, P]),
                      ("cbx_plan_set_odo_counts", [P, P, i64]),
                      ("cbx_hier_dependee_counts", [P, P, i32, P, i32, P, i64, P, P]),
+                     ("cbx_hier_dependee_values", [P, P, i64, P, P, i64, i32, i32, P, P, P]),
                      ("cbx_views_to_utf8", [P, i64, P, i64, P, P, i64, P, P]),
                      ("cbx_plan_pipeline", [P, P, i32, i32])):
         if hasattr(L, name):   # (diagnostic builds of older revisions lack the newest entry points)

@@ -721,17 +721,25 @@ class HierBatch:
     1 + s the records of segment s placed in the tree -- and `offsets[s]` the Arrow list offsets of
     segment s's children over its parent table (cbx_hier_list_offsets)."""
 
-    def __init__(self, flat: DecodedBatch, table_rows: List[int], offsets: Dict[int, np.ndarray],
+    def __init__(self, flat: DecodedBatch, table_rows: List[int], offsets: Dict[int, Any],
                  collapse_root: bool, generate_record_id: bool):
         self.flat, self.plan = flat, flat.plan
         self.table_rows = table_rows
         self.table_base = [int(x) for x in np.concatenate([[0], np.cumsum(table_rows)])]
-        self.offsets = offsets
+        self.d_offsets = offsets          # int32 list offsets per child segment, on the device
+        self._h_offsets: Optional[Dict[int, np.ndarray]] = None
         self.collapse_root, self.generate_record_id = collapse_root, generate_record_id
         self.input_file: Optional[Tuple[str, str]] = None
         self.n_rec = table_rows[0]
         self.children = {id(g): [c for c in self.plan.segment_groups if c.parent_segment is g]
                          for g in self.plan.segment_groups}
+
+    @property
+    def offsets(self) -> Dict[int, np.ndarray]:
+        """Host copies of the list offsets (made on first use by the row / pyarrow builders)."""
+        if self._h_offsets is None:
+            self._h_offsets = {s: (o.cpu().numpy() if hasattr(o, "cpu") else np.asarray(o)) for s, o in self.d_offsets.items()}
+        return self._h_offsets
 
     def _seg(self, g) -> int:
         return self.plan.segment_groups.index(g)
@@ -1394,11 +1402,14 @@ class VarLenNestedReader(_BaseReader):
             # lands on the child's first byte and its bound on the child's own length
             kid_off = sel["rec_off"][table_rows[0]:n_rows.value]
             if int(kid_off.min().item()) < s0:
-                raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a child segment record starts within "
-                                                      "record_start_offset bytes of the data")
-            kid_off -= s0
+                # a child within s0 bytes of the data's start (a root shorter than the start offset): the
+                # rows are decoded from a copy with s0 bytes in front, which no row reads
+                d_data = torch.cat([torch.zeros(s0, dtype=torch.uint8, device=dev), d_data[:n_bytes]])
+                n_bytes += s0
+                sel["rec_off"][: table_rows[0]] += s0
+            else:
+                kid_off -= s0
             sel["rec_len"][table_rows[0]:n_rows.value] += s0
-        flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
         # every child segment's list offsets over its parent table (device)
         base = np.concatenate([[0], np.cumsum(table_rows)]).astype(np.int64)
         d_offsets: Dict[int, Any] = {}
@@ -1410,17 +1421,17 @@ class VarLenNestedReader(_BaseReader):
             o = torch.empty(pn + 1, dtype=torch.int32, device=dev)
             N.check(L.cbx_hier_list_offsets(parent_row.data_ptr(), int(base[1 + s]), table_rows[1 + s], pb, pn, o.data_ptr(), sp))
             d_offsets[s] = o
-        odo = self._hier_dependee_counts(flat, table_rows, d_offsets, prm.root_segment, st)
+        # the counts of arrays whose DEPENDING ON field another record of the hierarchical record
+        # registers, resolved before the decode (one decode of the rows)
+        odo = self._hier_dependee_counts(d_data, n_bytes, sel, table_rows, d_offsets, prm.root_segment, st)
         if odo is not None:
-            # arrays whose count comes from a dependee another segment of the hierarchical record
-            # registered: decode again with those counts
             N.check(L.cbx_plan_set_odo_counts(self.native.handle, odo.data_ptr(), int(odo.shape[1])))
-            try:
-                flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
-            finally:
+        try:
+            flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
+        finally:
+            if odo is not None:
                 N.check(L.cbx_plan_set_odo_counts(self.native.handle, None, 0))
-        offsets = {s: o.cpu().numpy() for s, o in d_offsets.items()}
-        return HierBatch(flat, table_rows, offsets, self.collapse_root, self.params.generate_record_id)
+        return HierBatch(flat, table_rows, d_offsets, self.collapse_root, self.params.generate_record_id)
 
     def _file_column(self, batch, input_file_name: Optional[str], check_only: bool = False):
         """with_input_file_name_col: the batch's file-name column (SimpleStream.inputFileName).  The
@@ -1435,18 +1446,22 @@ class VarLenNestedReader(_BaseReader):
             batch.input_file = (self.params.input_file_name_column, input_file_name)
         return batch
 
-    def _hier_dependee_counts(self, flat: DecodedBatch, table_rows: List[int], child_offsets, root_seg: int, stream):
+    def _hier_dependee_counts(self, d_data, n_bytes: int, sel: Dict[str, Any], table_rows: List[int], child_offsets,
+                              root_seg: int, stream):
         """extractHierarchicalRecord shares ONE dependFields map between the segments of a hierarchical
         record (RecordExtractors.scala:224-245): a DEPENDING ON field registers its value when a record's
         group holding it is decoded, and an array reads the value registered last -- in the walk's
-        order (:324-370): the root record's groups, then per child segment in copybook order each child
-        record followed by its own subtree.  The records' own bytes give the same count when the
-        dependee sits in the array's own segment and is not null there; otherwise (a dependee of the
-        parent segment, of a sibling segment walked earlier, of the common header, or a null one) the
-        count is the value registered last in the walk.  Resolved on the device
-        (cbx_hier_dependee_counts: one thread per hierarchical record replays the walk's events);
-        returns the counts (int32 [n_arrays, rows], -1 where the first decode's own count stands)
-        when some differ from the first decode, else None."""
+        order (:324-372): the root record's groups -- the common header and every segment group, from the
+        root's own bytes, with the root segment's children walked where its group ends -- then per child
+        segment in copybook order each child record followed by its own subtree.  The records' own bytes
+        give the same count when the dependee sits in the array's own segment and is not null there;
+        otherwise (a dependee of the parent segment, of a sibling segment walked earlier, of the common
+        header, of a segment group placed before the root's, or a null one) the count is the value
+        registered last in the walk.  Resolved on the device BEFORE the rows are decoded: the dependee
+        fields decoded from every row's bytes (cbx_hier_dependee_values), then one thread per
+        hierarchical record replays the walk's events (cbx_hier_dependee_counts).  Returns the counts
+        (int32 [n_arrays, rows], -1 for arrays the decode resolves from the row's own bytes), or None
+        when no array depends on a numeric field of a segment."""
         torch = _torch()
         plan = self.plan
         arrays = [(ai, ar) for ai, ar in enumerate(plan.arrays) if ar.dependee >= 0 and ar.segment >= 0]
@@ -1462,6 +1477,7 @@ class VarLenNestedReader(_BaseReader):
         dfs(self.copybook.ast)
         segs = plan.segment_groups
         root_pos = order[id(segs[root_seg])]
+        has_kids = {sgi for sgi, g in enumerate(segs) if any(h.parent_segment is g for h in segs)}
         deps: List[int] = []               # dependee field indices, in the device table's order
         events: Dict[int, List[Tuple[int, int]]] = {}   # event row -> [(field order, event)]
         odo: List[Tuple[int, Any]] = []
@@ -1474,24 +1490,27 @@ class VarLenNestedReader(_BaseReader):
                     raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a string DEPENDING ON field "
                                                           "outside the array's segment")
                 continue
-            if any(order[id(g)] < root_pos for g in segs if g is not segs[root_seg]) and df.segment != ar.segment:
-                # the root record decodes a segment group placed before the root's from its own bytes,
-                # ahead of the children -- registrations this walk does not model
-                raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a segment group before the root "
-                                                      "segment's with a cross-segment DEPENDING ON")
             if dcol.out_type not in (N.O_I32, N.O_I64, N.O_DEC128):
                 raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a DEPENDING ON field decoded as "
                                                       "floating point")
             if ar.dependee not in deps:
                 deps.append(ar.dependee)
                 e = deps.index(ar.dependee)
-                if df.segment < 0:
-                    # the common header: only the root record decodes it, ahead of the children when
-                    # it precedes the root's segment group (after it: once the children are walked)
-                    if order[id(dcol.node)] < root_pos:
-                        events.setdefault(N.CBX_HIER_MAX_SEG, []).append((order[id(dcol.node)], e))
-                else:
-                    events.setdefault(df.segment, []).append((order[id(dcol.node)], e))
+                pos = order[id(dcol.node)]
+                if df.segment < 0 or df.segment != root_seg and order[id(segs[df.segment])] < root_pos:
+                    # decoded from the root's bytes ahead of the root segment's group: the common header,
+                    # or a segment group placed before the root's (registered before the children walk;
+                    # after the root's group, once the children are walked -- no array of theirs sees it)
+                    if df.segment >= 0 and df.segment in has_kids:
+                        # the root's walk also extracts that group's own children over the record's rows
+                        # (getGroupValues of any segment redefine, :361-369) -- registrations not modelled
+                        raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a DEPENDING ON field in a "
+                                                              "segment group with children placed before the root "
+                                                              "segment's")
+                    if pos < root_pos:
+                        events.setdefault(N.CBX_HIER_MAX_SEG, []).append((pos, e))
+                if df.segment >= 0:
+                    events.setdefault(df.segment, []).append((pos, e))
             odo.append((ai, ar))
             events.setdefault(ar.segment, []).append((order[id(anode)], -len(odo)))
         if not odo:
@@ -1500,6 +1519,9 @@ class VarLenNestedReader(_BaseReader):
                 any(len(v) > N.CBX_HIER_MAX_EVENTS for v in events.values()):
             raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: more DEPENDING ON fields / arrays than "
                                                   "cbx_hier_dependee_counts takes")
+        L = N.load()
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        dev = sel["rec_off"].device
         w = N.CbxHierWalk()
         w.n_segments, w.root_segment = len(segs), root_seg
         base = np.concatenate([[0], np.cumsum(table_rows)]).astype(np.int64)
@@ -1521,23 +1543,26 @@ class VarLenNestedReader(_BaseReader):
         for row, evs in events.items():
             for k, (_, e) in enumerate(sorted(evs)):
                 w.events[row][k] = e
+        # every dependee decoded from every row's own bytes (the rows' registrations)
+        vals = torch.empty((max(1, len(deps)), n), dtype=torch.int64, device=dev)
+        valid = torch.empty((max(1, len(deps)), (n + 63) // 64), dtype=torch.int64, device=dev)
         dt = (N.CbxHierDependee * max(1, len(deps)))()
         for e, fi in enumerate(deps):
-            ci = plan.fields[fi].column
-            dt[e].values = flat.cols[ci]["values"].data_ptr()
-            dt[e].validity = flat.cols[ci]["validity"].data_ptr()
-            dt[e].out_type = plan.columns[ci].out_type
+            N.check(L.cbx_hier_dependee_values(self.native.handle, d_data.data_ptr(), n_bytes, sel["rec_off"].data_ptr(),
+                                               sel["rec_len"].data_ptr(), n, self.params.start_offset, fi,
+                                               vals[e].data_ptr(), valid[e].data_ptr(), sp))
+            dt[e].values, dt[e].validity, dt[e].out_type = vals[e].data_ptr(), valid[e].data_ptr(), N.O_I64
         at = (N.CbxHierOdoArray * len(odo))()
         for k, (ai, ar) in enumerate(odo):
             at[k].dependee, at[k].out_row = deps.index(ar.dependee), ai
             at[k].min_count, at[k].max_count = ar.min_count, ar.max_count
-            at[k].first_counts = flat.cols[ar.count_column]["values"].data_ptr()
-        dev = flat.cols[0]["validity"].device
+            at[k].first_counts = None
         out = torch.full((len(plan.arrays), n), -1, dtype=torch.int32, device=dev)
         changed = torch.zeros(1, dtype=torch.int32, device=dev)
-        N.check(N.load().cbx_hier_dependee_counts(ctypes.byref(w), dt, len(deps), at, len(odo), out.data_ptr(), n,
-                                                  changed.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
-        return out if int(changed.item()) else None
+        N.check(L.cbx_hier_dependee_counts(ctypes.byref(w), dt, len(deps), at, len(odo), out.data_ptr(), n,
+                                           changed.data_ptr(), sp))
+        out._cbx_keep = (vals, valid)   # (the value columns live until the resolution has run)
+        return out
 
     def read(self, data: bytes, file_id: int = 0, input_file_name: Optional[str] = None) -> DecodedBatch:
         """A whole file, as the reference reads it: sparse-index entries (when index generation

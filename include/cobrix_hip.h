@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 17
+#define CBX_ABI_VERSION 18
 
 /* status codes */
 #define CBX_OK 0
@@ -510,9 +510,12 @@ int cbx_frame_length_field(cbx_plan* plan, const uint8_t* d_data, int64_t n_byte
  * is resolved on the device by cbx_hier_dependee_counts and applied with cbx_plan_set_odo_counts.
  * Several segment ids mapped to one segment that has children: flags bit 0 (the general walk: one
  * thread per hierarchical record runs extractChildren's recursion with its id-based break rule).
- * Not covered (reported by the host, CBX_E_UNSUPPORTED, never decoded differently): a cross-segment
- * DEPENDING ON when a segment group precedes the root segment's in the copybook; a string DEPENDING
- * ON field outside the array's segment. */
+ * The counts are resolved BEFORE the decode (one decode): cbx_hier_dependee_values decodes each
+ * DEPENDING ON field from every row's bytes, cbx_hier_dependee_counts replays the walk.
+ * Not covered (reported by the host, CBX_E_UNSUPPORTED, never decoded differently): a segment group
+ * placed before the root segment's that has child segments, with a cross-segment DEPENDING ON (the
+ * root's record walk extracts that group's children too); a DEPENDING ON field outside the array's
+ * segment on a record-walk plan (string dependees through occurs_mappings, variable_size_occurs). */
 typedef struct {
     int32_t n_segments;               /* segment redefines (cbx_field.segment / key_segment indices) */
     int32_t root_segment;             /* the segment without a parent */
@@ -536,6 +539,16 @@ int cbx_hier_select(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, cons
 int cbx_hier_list_offsets(const int64_t* d_parent_row, int64_t child_begin, int64_t n_child, int64_t parent_begin,
                           int64_t n_parent, int32_t* d_offsets, void* stream);
 
+/* A DEPENDING ON field (plan field `field`: integral COMP-3 / binary / DISPLAY) decoded from each of
+ * n_rows rows' own bytes -- at rec_off + start_offset + its offset, null past rec_len or when malformed,
+ * whatever the row's segment (the root record decodes every segment group from its own bytes,
+ * RecordExtractors.scala:365-372) -- into d_values (int64 Number.intValue) and d_validity (one bit per
+ * row, a word per 64 rows).  The dependee columns of cbx_hier_dependee_counts (out_type CBX_O_I64),
+ * so the counts exist before the rows are decoded.  Asynchronous on `stream`. */
+int cbx_hier_dependee_values(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, const int64_t* d_rec_off,
+                             const int32_t* d_rec_len, int64_t n_rows, int32_t start_offset, int32_t field,
+                             int64_t* d_values, uint64_t* d_validity, void* stream);
+
 /* The dependFields map extractHierarchicalRecord shares between the segments of one hierarchical
  * record (RecordExtractors.scala:224-245, walk order :324-370), on the device: one thread per
  * hierarchical record walks its rows as the reference does -- the root, then per child segment in
@@ -543,10 +556,11 @@ int cbx_hier_list_offsets(const int64_t* d_parent_row, int64_t child_begin, int6
  * its own subtree -- replaying at every row its segment's events in field order: a numeric DEPENDING
  * ON field registers its value (Number.intValue) when the row decodes it non-null; an array takes the
  * value registered last (its maximum when none is, or the value is outside [min, max]).
- * counts (device, [n_arrays_out][pitch] int32) receives the count of every array event's rows --
- * -1 for root rows, whose own decode resolves them -- and *d_changed (device int32) is set to 1
- * when some count differs from the first decode's (first_counts); apply with
- * cbx_plan_set_odo_counts and decode again.  Rows as cbx_hier_select emits them. */
+ * counts (device, [n_arrays_out][pitch] int32) receives the count of every array event's rows, root
+ * rows included, and *d_changed (device int32) is set to 1 when some count differs from first_counts
+ * (when given); apply with cbx_plan_set_odo_counts to the decode.  Rows as cbx_hier_select emits them.
+ * Root-record registrations that precede the root segment's group (the common header, a segment group
+ * placed before it, decoded from the root's bytes) are events[CBX_HIER_MAX_SEG]. */
 #define CBX_HIER_MAX_SEG 16       /* segments of a hierarchical layout (cbx_hier_select's limit) */
 #define CBX_HIER_MAX_EVENTS 32    /* events per segment */
 #define CBX_HIER_MAX_DEPS 16      /* dependees and arrays of one cbx_hier_dependee_counts call */

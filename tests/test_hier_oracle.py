@@ -167,3 +167,42 @@ def test_cross_segment_string_dependee_is_reported():
         assert rd.walk
     finally:
         R.NativePlan = orig
+
+
+BEFORE_ROOT_COPYBOOK = """
+       01  REC.
+           05  SEGMENT-ID        PIC X(1).
+           05  SIB-A.
+               10  A-CNT         PIC 9(1).
+               10  A-ITEMS OCCURS 0 TO 5 TIMES DEPENDING ON A-CNT.
+                   15  A-V       PIC X(2).
+           05  PARENT-SEG REDEFINES SIB-A.
+               10  P-CNT         PIC 9(1).
+               10  P-NAME        PIC X(3).
+               10  P-ITEMS OCCURS 0 TO 5 TIMES DEPENDING ON A-CNT.
+                   15  P-V       PIC X(1).
+           05  SIB-B REDEFINES SIB-A.
+               10  B-CNT         PIC 9(1).
+               10  B-ITEMS OCCURS 0 TO 5 TIMES DEPENDING ON A-CNT.
+                   15  B-V       PIC X(1).
+"""
+
+BEFORE_ROOT_OPTS = {"is_record_sequence": "true", "segment_field": "SEGMENT_ID",
+                    "redefine_segment_id_map:1": "PARENT-SEG => P", "redefine-segment-id-map:2": "SIB-A => A",
+                    "redefine-segment-id-map:3": "SIB-B => B", "segment-children:1": "PARENT-SEG => SIB-A,SIB-B"}
+
+
+def test_group_before_the_root_registers_from_the_root_bytes():
+    """A child segment's group placed before the root segment's: the root record's walk decodes it from
+    the ROOT's bytes first (getGroupValues over the record group, RecordExtractors.scala:365-372), so
+    A-CNT is registered with the root's byte at that offset (its P-CNT digit) before the root's own
+    P-ITEMS reads it; the A children then register their own A-CNT for B's B-ITEMS."""
+    p, _ = parse_options(BEFORE_ROOT_OPTS)
+    cb = parse_copybook_for(BEFORE_ROOT_COPYBOOK, p)
+    data = rdw("P2ABCxyzw") + rdw("B4wxyz") + rdw("A3aabbcc") + rdw("B1qrst")
+    r = RO.var_len_rows(cb, data, p)[0]["REC"]["PARENT_SEG"]
+    # P-ITEMS: A-CNT from the root's bytes = '2'; the A child: A-ITEMS on its own A-CNT = 3
+    assert r["P_CNT"] == 2 and len(r["P_ITEMS"]) == 2
+    assert len(r["SIB_A"]) == 1 and len(r["SIB_A"][0]["A_ITEMS"]) == 3
+    # the B children are walked after the A children (copybook order): A-CNT = 3 from the A record
+    assert [len(b["B_ITEMS"]) for b in r["SIB_B"]] == [3, 3]
