@@ -141,6 +141,9 @@ struct cbx_plan {
     const int64_t* d_rec_base = nullptr;   // caller's device Record_Id base (cbx_plan_set_record_base)
     const int32_t* d_odo = nullptr;        // caller's OCCURS DEPENDING ON counts (cbx_plan_set_odo_counts)
     int64_t odo_pitch = 0;
+    const int64_t* d_dep_seed = nullptr;   // the record walk's per-row dependFields seeds (cbx_plan_set_dep_seed)
+    int64_t seed_pitch = 0;
+    int32_t seed_root = -1;
     int64_t n_str_slots = 0;
     uint32_t* d_wcursor = nullptr; int64_t wcursor_cap = 0;
     int64_t* d_wvbase = nullptr;        // per column: first validity-word index among all column slots
@@ -1167,7 +1170,7 @@ static std::string jit_walk_source(const cbx_plan* P) {
            "  template <typename RP>\n"
            "  __device__ __forceinline__ void operator()(const WalkArgs& a, const WalkLds& wl, uint8_t* area, RP rec,\n"
            "      int avail, int seg, int64_t r, int64_t tile, int lane, bool act) const {\n"
-           "    WalkDeps dep;\n    dep.clear();\n    int off0 = 0;\n";
+           "    WalkDeps dep;\n    walk_seed(a, dep, r, act, seg);\n    int off0 = 0;\n";
     g.body(P->walk_root, "off0", "0", "act", 2, 0);
     g.o << "  }\n};\n}  // namespace cbx\n"
            "extern \"C\" __global__ __launch_bounds__(256) void cbx_jit_walk(cbx::WalkArgs a) {\n"
@@ -1203,6 +1206,7 @@ static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hip
     a.stride = c.stride; a.start_off = c.start_off; a.first_record_id = c.first_record_id; a.rec_id_base = P->d_rec_base;
     a.rec_id = c.rec_id; a.rec_seg = c.rec_seg; a.file_id = c.file_id >= 0 ? c.file_id : P->opts.file_id;
     a.var_occurs = P->walk_var; a.n_tiles = n_tiles; a.pitch = n_tiles * kWave;
+    a.dep_seed = P->d_dep_seed; a.seed_pitch = P->seed_pitch; a.hier_root = P->seed_root;
     a.nodes = (const CBX_CONST cbx_walk_node*)P->d_wnodes; a.root = P->walk_root;
     a.warr = (const CBX_CONST cbx_walk_array*)P->d_warr;
     a.handlers = (const CBX_CONST cbx_walk_handler*)P->d_whand; a.n_handlers = P->walk_n_handlers;
@@ -1326,6 +1330,16 @@ extern "C" int cbx_plan_check(cbx_plan* P, void* stream) {
 extern "C" int cbx_plan_set_record_base(cbx_plan* P, const int64_t* d_base) {
     if (!P) return fail(CBX_E_ARGUMENT, "cbx_plan_set_record_base: invalid plan");
     P->d_rec_base = d_base;
+    return CBX_OK;
+}
+
+extern "C" int cbx_plan_set_dep_seed(cbx_plan* P, const int64_t* d_seed, int64_t pitch, int32_t root_segment) {
+    if (!P || pitch < 0 || (d_seed && (pitch == 0 || root_segment < 0)))
+        return fail(CBX_E_ARGUMENT, "cbx_plan_set_dep_seed: invalid arguments");
+    if (d_seed && !P->walk) return fail(CBX_E_STATE, "cbx_plan_set_dep_seed: the plan has no record walk (cbx_plan_set_walk)");
+    P->d_dep_seed = d_seed;
+    P->seed_pitch = d_seed ? pitch : 0;
+    P->seed_root = d_seed ? root_segment : -1;
     return CBX_OK;
 }
 
@@ -2353,10 +2367,17 @@ extern "C" int cbx_hier_dependee_values(cbx_plan* P, const uint8_t* d_data, int6
         (n_rows > 0 && (!d_data || !d_rec_off || !d_rec_len || !d_values || !d_validity)))
         return fail(CBX_E_ARGUMENT, "cbx_hier_dependee_values: invalid arguments");
     const Field f = P->dfields_h[field];
-    if (!(f.kind == CBX_K_BCD || f.kind == CBX_K_BINARY || f.kind == CBX_K_ASCII_NUM || f.kind == CBX_K_ZONED) ||
+    const bool str = f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII;
+    if (!(str || f.kind == CBX_K_BCD || f.kind == CBX_K_BINARY || f.kind == CBX_K_ASCII_NUM || f.kind == CBX_K_ZONED) ||
         f.n_dims != 0)
-        return fail(CBX_E_UNSUPPORTED, "cbx_hier_dependee_values: the field is not an integral DEPENDING ON field");
-    if (n_rows > 0) {
+        return fail(CBX_E_UNSUPPORTED, "cbx_hier_dependee_values: the field is not an integral or string DEPENDING ON field");
+    if (n_rows > 0 && str) {   // Right(s): the occurs_mappings key it equals (the plan's walk handlers)
+        hipLaunchKernelGGL(hier_dep_str_kernel, dim3(blocks_for(n_rows, 64)), dim3(64), 0, (hipStream_t)stream, d_data,
+                           n_bytes, d_rec_off, d_rec_len, n_rows, start_offset, (const CBX_CONST Field*)P->d_fields + field,
+                           (const uint32_t*)P->d_lut, (const CBX_CONST cbx_walk_handler*)P->d_whand,
+                           P->d_whand ? P->walk_n_handlers : 0, d_values, d_validity);
+        HIP_CHECK(hipGetLastError());
+    } else if (n_rows > 0) {
         hipLaunchKernelGGL(hier_dep_values_kernel, dim3(blocks_for(n_rows, 64)), dim3(64), 0, (hipStream_t)stream, d_data,
                            n_bytes, d_rec_off, d_rec_len, n_rows, start_offset, (const CBX_CONST Field*)P->d_fields + field,
                            d_values, d_validity);
@@ -2379,8 +2400,9 @@ extern "C" int cbx_hier_dependee_counts(const cbx_hier_walk* walk, const cbx_hie
     a.n_arrays = n_arrays;
     for (int i = 0; i < n_deps; i++) {
         const int ot = deps[i].out_type;
-        if (!deps[i].values || !deps[i].validity || (ot != CBX_O_I32 && ot != CBX_O_I64 && ot != CBX_O_DEC128))
-            return fail(CBX_E_ARGUMENT, "cbx_hier_dependee_counts: a dependee column must be I32, I64 or DEC128");
+        if (!deps[i].values || !deps[i].validity || (ot != CBX_O_I32 && ot != CBX_O_I64 && ot != CBX_O_DEC128 && ot != CBX_O_STRING) ||
+            deps[i].walk_slot >= 8)
+            return fail(CBX_E_ARGUMENT, "cbx_hier_dependee_counts: a dependee column must be I32, I64, DEC128 or string keys");
         a.dep[i] = deps[i];
     }
     for (int i = 0; i < n_arrays; i++) {
@@ -2614,6 +2636,7 @@ extern "C" int cbx_frame_var_occurs(cbx_plan* P, const uint8_t* d_data, int64_t 
     if (first_offset >= n_bytes) return CBX_OK;
     WalkArgs a{};
     a.data = d_data;
+    a.hier_root = -1;
     a.nodes = (const CBX_CONST cbx_walk_node*)P->d_wnodes; a.root = P->walk_root;
     a.warr = (const CBX_CONST cbx_walk_array*)P->d_warr;
     a.handlers = (const CBX_CONST cbx_walk_handler*)P->d_whand; a.n_handlers = P->walk_n_handlers;

@@ -370,8 +370,15 @@ struct HierDepArgs {
     int32_t n_deps, n_arrays;
 };
 
+// The record walk's dependee slots (cbx_hier_walk.seeds): kind << 32 | value per slot.
+constexpr int kHierWalkSlots = 8;
+struct HierSlots {
+    int64_t s[kHierWalkSlots];
+};
+
 __device__ __forceinline__ void hier_dep_events(const HierDepArgs& a, int ev_row, int64_t x, bool root, int32_t* regv,
-                                                uint32_t& regok, int32_t* counts, int64_t pitch, int32_t* changed) {
+                                                uint32_t& regok, int32_t* counts, int64_t pitch, int32_t* changed,
+                                                HierSlots& sl) {
     for (int k = 0; k < CBX_HIER_MAX_EVENTS; k++) {
         const int e = a.w.events[ev_row][k];
         if (e == -32768) break;
@@ -380,10 +387,12 @@ __device__ __forceinline__ void hier_dep_events(const HierDepArgs& a, int ev_row
             if (!((d.validity[x >> 6] >> (x & 63)) & 1ull)) continue;   // a null value registers nothing
             int32_t v;
             if (d.out_type == CBX_O_I32) v = ((const int32_t*)d.values)[x];
-            else if (d.out_type == CBX_O_I64) v = (int32_t)((const int64_t*)d.values)[x];
+            else if (d.out_type == CBX_O_I64 || d.out_type == CBX_O_STRING) v = (int32_t)((const int64_t*)d.values)[x];
             else v = (int32_t)((const int64_t*)d.values)[2 * x];   // DEC128: the low 64 bits (intValue)
             regv[e] = v;
             regok |= 1u << e;
+            if (d.walk_slot >= 0 && d.walk_slot < kHierWalkSlots)   // Left(int) / Right(key id + 1)
+                sl.s[d.walk_slot] = (int64_t)(d.out_type == CBX_O_STRING ? 2 : 1) << 32 | (uint32_t)v;
         } else {
             const cbx_hier_odo_array& A = a.arr[-e - 1];
             const int dd = A.dependee;
@@ -395,25 +404,35 @@ __device__ __forceinline__ void hier_dep_events(const HierDepArgs& a, int ev_row
     }
 }
 
+__device__ __forceinline__ void hier_put_seed(const HierDepArgs& a, int64_t x, int64_t pitch, const HierSlots& sl) {
+    if (!a.w.seeds) return;
+#pragma unroll
+    for (int i = 0; i < kHierWalkSlots; i++) a.w.seeds[(int64_t)i * pitch + x] = sl.s[i];
+}
+
 __global__ void hier_dep_kernel(HierDepArgs a, int32_t* counts, int64_t pitch, int32_t* changed) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= a.w.table_rows[0]) return;
     int32_t regv[CBX_HIER_MAX_DEPS];
     uint32_t regok = 0;
     for (int k = 0; k < CBX_HIER_MAX_DEPS; k++) regv[k] = 0;
+    HierSlots sl;
+    for (int k = 0; k < kHierWalkSlots; k++) sl.s[k] = 0;
     // stack frames: row, segment, next child type (index into children[seg]), child rows [lo, hi)
     int64_t f_row[kHierMaxSeg + 1], f_lo[kHierMaxSeg + 1], f_hi[kHierMaxSeg + 1];
     int f_seg[kHierMaxSeg + 1], f_ci[kHierMaxSeg + 1];
     const int root = a.w.root_segment;
-    hier_dep_events(a, CBX_HIER_MAX_SEG, r, true, regv, regok, counts, pitch, changed);
-    hier_dep_events(a, root, r, true, regv, regok, counts, pitch, changed);
+    hier_dep_events(a, CBX_HIER_MAX_SEG, r, true, regv, regok, counts, pitch, changed, sl);
+    hier_put_seed(a, r, pitch, sl);   // (the root's walk registers its own groups' dependees itself)
+    hier_dep_events(a, root, r, true, regv, regok, counts, pitch, changed, sl);
     int d = 0;
     f_row[0] = r; f_seg[0] = root; f_ci[0] = -1; f_lo[0] = f_hi[0] = 0;
     while (d >= 0) {
         if (f_lo[d] < f_hi[d]) {   // the next child row of the current type: visit it, then its subtree
             const int c = a.w.children[f_seg[d]][f_ci[d]];
             const int64_t x = a.w.table_base[1 + c] + f_lo[d]++;
-            hier_dep_events(a, c, x, false, regv, regok, counts, pitch, changed);
+            hier_put_seed(a, x, pitch, sl);
+            hier_dep_events(a, c, x, false, regv, regok, counts, pitch, changed, sl);
             if (d + 1 <= kHierMaxSeg) {
                 d++;
                 f_row[d] = x; f_seg[d] = c; f_ci[d] = -1; f_lo[d] = f_hi[d] = 0;

@@ -65,6 +65,13 @@ struct WalkArgs {
     const int64_t* vslot_base;        // per column: index of its slot 0 among all column slots
     const int32_t* vslot_col;         // per validity word: its column and slot
     const int32_t* vslot_slot;
+    // hierarchical records (cbx_plan_set_dep_seed): each row's dependFields as the rows before it in
+    // extractHierarchicalRecord's walk left the map -- [kWalkDeps][seed_pitch] int64, kind << 32 | value
+    // (kind 0 unseen) -- and the root segment: a child row decodes its own group only (:300-322), so
+    // its walk registers no common-header dependee (hier_root < 0: not hierarchical)
+    const int64_t* dep_seed;
+    int64_t seed_pitch;
+    int32_t hier_root;
 };
 
 // The wave's LDS area of the tile being walked (vlds): validity words, then string cursors.
@@ -97,9 +104,11 @@ struct WalkDep { int32_t kind, v; };
 // dep_slot), unrolled into selects so the table never goes to scratch.
 struct WalkDeps {
     int32_t kind[kWalkDeps], v[kWalkDeps];
+    bool common_ok;   // the row registers common-header dependees (not a hierarchical child row)
     __device__ __forceinline__ void clear() {
 #pragma unroll
         for (int i = 0; i < kWalkDeps; i++) { kind[i] = 0; v[i] = 0; }
+        common_ok = true;
     }
     __device__ __forceinline__ WalkDep get(int s) const {
         WalkDep d{0, 0};
@@ -114,6 +123,20 @@ struct WalkDeps {
             if (i == s && on) { kind[i] = d.kind; v[i] = d.v; }
     }
 };
+
+// A row's map at its start: empty, or the hierarchical walk's state before the row (dep_seed).
+__device__ __forceinline__ void walk_seed(const WalkArgs& a, WalkDeps& dep, int64_t r, bool act, int seg) {
+    dep.clear();
+    if (a.hier_root >= 0) dep.common_ok = seg == a.hier_root;
+    if (a.dep_seed && act && r < a.seed_pitch) {
+#pragma unroll
+        for (int i = 0; i < kWalkDeps; i++) {
+            const int64_t x = a.dep_seed[(int64_t)i * a.seed_pitch + r];
+            dep.kind[i] = (int32_t)(x >> 32);
+            dep.v[i] = (int32_t)x;
+        }
+    }
+}
 
 __device__ __forceinline__ uint32_t walk_lut(const WalkArgs& a, const WalkLds& wl, int kind, uint32_t b) {
     return kind == CBX_K_STRING_ASCII ? ascii_lut(b) : wl.lut[b];
@@ -223,7 +246,7 @@ __device__ __forceinline__ void walk_prim_f(const WalkArgs& a, const WalkLds& wl
                     if (eq) key = hd.key_id + 1;
                 }
             }
-            dep.set(dep_slot, ok, WalkDep{2, key});
+            dep.set(dep_slot, ok && (f.segment >= 0 || dep.common_ok), WalkDep{2, key});
         }
         return;
     }
@@ -242,7 +265,7 @@ __device__ __forceinline__ void walk_prim_f(const WalkArgs& a, const WalkLds& wl
     if (dep_slot >= 0 && !element) {   // Left(Number.intValue)
         Val dv{0, 0, false};
         if (ok) dv = decode_count_int(f, p);
-        dep.set(dep_slot, ok && dv.valid, WalkDep{1, (int32_t)dv.lo});
+        dep.set(dep_slot, ok && dv.valid && (f.segment >= 0 || dep.common_ok), WalkDep{1, (int32_t)dv.lo});
     }
 }
 
@@ -288,7 +311,7 @@ __device__ void walk_tile(const WalkArgs& a, const WalkLds& wl, uint8_t* stk, co
     int32_t* VO = VS + a.depth * kWave;       // [depth][64] running offset
     int32_t* VC = VO + a.depth * kWave;       // [depth][64] element count (array frames)
     WalkDeps dep;
-    dep.clear();
+    walk_seed(a, dep, r, act, seg);
     int sp = 0;
     U[0] = WalkU{a.root, 0, ldc(a.nodes + a.root).child, 0, 0, 0, __ballot(act)};
     VS[lane] = 0;
@@ -503,6 +526,49 @@ struct TableWalk {
 __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
     walk_tiles(a, wsm, TableWalk{});
+}
+
+// ---- hierarchical records: a string DEPENDING ON field's registration per row ----
+// extractValue's Right(s) (RecordExtractors.scala:285-292) as the walk keeps it (walk_prim_f): the
+// occurs_mappings key id + 1 the decoded string equals (0: no handler lists it), registered whenever
+// the field starts within the row (a null string -- offset past the end -- registers nothing).  One
+// thread per row; validity one ballot word per 64 rows (cbx_hier_dependee_values).
+__global__ __launch_bounds__(64) void hier_dep_str_kernel(const uint8_t* data, int64_t n_bytes, const int64_t* rec_off,
+                                                         const int32_t* rec_len, int64_t n, int32_t start_off,
+                                                         const CBX_CONST Field* fp, const uint32_t* lut,
+                                                         const CBX_CONST cbx_walk_handler* handlers, int32_t n_handlers,
+                                                         int64_t* values, uint64_t* validity) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const Field f = ldc(fp);
+    bool ok = false;
+    int key = 0;
+    if (x < n) {
+        const int64_t base = rec_off[x];
+        const int avail = rec_len[x];
+        const int o = start_off + f.offset;
+        ok = o <= avail && base + o <= n_bytes;
+        if (ok) {
+            int m = o + f.size <= avail ? f.size : avail - o;
+            if (base + o + m > n_bytes) m = (int)(n_bytes - base - o);
+            const uint8_t* p = data + base + o;
+            auto lutf = [&](uint32_t b) { return f.kind == CBX_K_STRING_ASCII ? ascii_lut(b) : lut[b]; };
+            const StrSpan sp = string_span(f.kind, f.trim, p, m, lutf);
+            const int len = sp.utf8_len;
+            if (len <= 64) {
+                uint8_t buf[64];
+                string_write(f.kind, p, sp, buf, lutf);
+                for (int h = 0; h < n_handlers && key == 0; h++) {
+                    const cbx_walk_handler hd = ldc(handlers + h);
+                    bool eq = hd.key_len == len;
+                    for (int i = 0; eq && i < len; i++) eq = hd.key[i] == buf[i];
+                    if (eq) key = hd.key_id + 1;
+                }
+            }
+        }
+        values[x] = key;
+    }
+    const uint64_t mm = __ballot(ok);
+    if (threadIdx.x == 0 && x < n) validity[x >> 6] = mm;
 }
 
 // ---- VarOccursRecordExtractor: record lengths by walking each record's dependees ----

@@ -43,8 +43,8 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
                     "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs",
                     "cbx_plan_set_record_base", "cbx_frame_length_field", "cbx_plan_set_odo_counts",
-                    "cbx_hier_dependee_counts", "cbx_hier_dependee_values", "cbx_views_to_utf8", "cbx_plan_pipeline")
-ABI_VERSION = 18
+                    "cbx_hier_dependee_counts", "cbx_hier_dependee_values", "cbx_plan_set_dep_seed", "cbx_views_to_utf8", "cbx_plan_pipeline")
+ABI_VERSION = 19
 
 
 class NativeLibraryError(RuntimeError):
@@ -156,7 +156,7 @@ HIER_EVENT_END = -32768
 
 class CbxHierDependee(ctypes.Structure):
     _fields_ = [("values", ctypes.c_void_p), ("validity", ctypes.c_void_p), ("out_type", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("walk_slot", ctypes.c_int32)]
 
 
 class CbxHierOdoArray(ctypes.Structure):
@@ -170,7 +170,8 @@ class CbxHierWalk(ctypes.Structure):
                 ("table_rows", ctypes.c_int64 * (CBX_HIER_MAX_SEG + 1)),
                 ("child_offsets", ctypes.c_void_p * CBX_HIER_MAX_SEG),
                 ("children", (ctypes.c_int8 * CBX_HIER_MAX_SEG) * CBX_HIER_MAX_SEG),
-                ("events", (ctypes.c_int16 * CBX_HIER_MAX_EVENTS) * (CBX_HIER_MAX_SEG + 1))]
+                ("events", (ctypes.c_int16 * CBX_HIER_MAX_EVENTS) * (CBX_HIER_MAX_SEG + 1)),
+                ("seeds", ctypes.c_void_p)]
 
 
 _lib = None
@@ -224,11 +225,14 @@ def load():
                      ("cbx_plan_set_odo_counts", [P, P, i64]),
                      ("cbx_hier_dependee_counts", [P, P, i32, P, i32, P, i64, P, P]),
                      ("cbx_hier_dependee_values", [P, P, i64, P, P, i64, i32, i32, P, P, P]),
+                     ("cbx_plan_set_dep_seed", [P, P, i64, i32]),
                      ("cbx_views_to_utf8", [P, i64, P, i64, P, P, i64, P, P]),
                      ("cbx_plan_pipeline", [P, P, i32, i32])):
         if hasattr(L, name):   # (diagnostic builds of older revisions lack the newest entry points)
             getattr(L, name).argtypes = at
-    if L.cbx_abi_version() != ABI_VERSION:
+    if L.cbx_abi_version() != ABI_VERSION and not os.environ.get("CBX_LIB_VARIANT"):
+        # (a diagnostic variant built from an older revision -- tools/build_variant.py -- is timed on the
+        # entry points both revisions share)
         raise NativeLibraryError(f"{LIB_PATH}: ABI {L.cbx_abi_version()} != {ABI_VERSION}; rebuild it")
     _lib = L
     return L

@@ -682,37 +682,59 @@ def hier_general_walk(params: ReaderParameters, plan: DecodePlan) -> bool:
     return any(g.name in parents and len(ids.get(g.name, [])) > 1 for g in plan.segment_groups)
 
 
-def check_hierarchical(cb: cbk.Copybook, params: ReaderParameters, plan: DecodePlan) -> None:
+def check_hierarchical(cb: cbk.Copybook, params: ReaderParameters, plan: DecodePlan) -> bool:
     """What the GPU hierarchical path assumes (cobrix_hip.h cbx_hier_select); anything else is
-    reported, never decoded differently."""
+    reported, never decoded differently.  Returns whether a record-walk plan needs its rows' dependee
+    maps seeded (cbx_plan_set_dep_seed): an OCCURS DEPENDING ON a field that another record of the
+    hierarchical record registers in the shared dependFields map (RecordExtractors.scala:224-245)."""
     if not params.segment_field or not params.segment_id_redefine_map:
         raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records need segment_field and redefine-segment-id-map")
     segs = plan.segment_groups
     if len(segs) > 16:
         raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: more than 16 segment redefines")
-    if plan.walk is not None:
-        # the record walk decodes a row from its own bytes only: an OCCURS DEPENDING ON a field that
-        # another record of the hierarchical record registers in the shared dependFields map
-        # (RecordExtractors.scala:224-245 -- a string dependee through occurs_mappings, a
-        # variable_size_occurs layout) is not seen there; reported instead of decoded differently
-        def stmts(g):
-            for c in g.children:
-                yield c
-                if isinstance(c, cbk.Group):
-                    yield from stmts(c)
-        prims = [q for q in stmts(cb.ast) if not isinstance(q, cbk.Group)]
-        root = next((i for i, g in enumerate(segs) if g.parent_segment is None), -1)
-        for st in stmts(cb.ast):
-            ai = plan.array_of_node.get(id(st))
-            if ai is None or st.depending_on is None:
-                continue
-            sa = plan.arrays[ai].segment
-            q = next((q for q in prims if q.is_dependee and q.name == st.depending_on), None)
-            fq = plan.field_of_node.get(id(q)) if q is not None else None
-            sq = plan.fields[fq].segment if fq is not None else sa
-            if sa >= 0 and sq != sa and not (sa == root and sq < 0):
-                raise N.CbxError(N.CBX_E_UNSUPPORTED, f"hierarchical records: {st.name} DEPENDING ON {st.depending_on}, "
-                                                      "a field of another segment, with the record walk")
+    if plan.walk is None:
+        return False
+
+    def stmts(g):
+        for c in g.children:
+            yield c
+            if isinstance(c, cbk.Group):
+                yield from stmts(c)
+    order = list(stmts(cb.ast))
+    prims = [q for q in order if not isinstance(q, cbk.Group)]
+    root = next((i for i, g in enumerate(segs) if g.parent_segment is None), -1)
+    cross = seg_odo = False
+    for st in order:
+        ai = plan.array_of_node.get(id(st))
+        if ai is None or st.depending_on is None:
+            continue
+        sa = plan.arrays[ai].segment
+        q = next((q for q in prims if q.is_dependee and q.name == st.depending_on), None)
+        fq = plan.field_of_node.get(id(q)) if q is not None else None
+        sq = plan.fields[fq].segment if fq is not None else sa
+        cross |= sa >= 0 and sq != sa and not (sa == root and sq < 0)
+        seg_odo |= sa >= 0
+    if not seg_odo:
+        return False
+    # An array of a segment reads the map another record may have filled: its dependee in another
+    # segment, or its own dependee null in this row (the registration before it stays).  The seeds come
+    # from the dependee fields decoded from each row's bytes at their copybook offsets
+    # (cbx_hier_dependee_values): a dependee inside an OCCURS, or placed after a variable-size OCCURS
+    # (variable_size_occurs: a data-dependent offset), registers what that decode cannot see -- reported
+    # when the array depends on another segment, else the row's own map (a null own dependee then counts
+    # the maximum instead of the earlier registration)
+    first_odo = next((k for k, st in enumerate(order) if st.depending_on is not None and st.is_array), len(order))
+    for k, st in enumerate(order):
+        if isinstance(st, cbk.Group) or not st.is_dependee:
+            continue
+        fi = plan.field_of_node.get(id(st))
+        if fi is None or plan.fields[fi].n_dims != 0 or (plan.walk.variable_size_occurs and k > first_odo):
+            if cross:
+                raise N.CbxError(N.CBX_E_UNSUPPORTED, f"hierarchical records: {st.name}, a DEPENDING ON field of "
+                                                      "another segment's array, inside an OCCURS or behind a "
+                                                      "variable-size one")
+            return False
+    return True
 
 
 class HierBatch:
@@ -869,8 +891,9 @@ class _BaseReader:
         if walk:
             self.plan = plan(True)
         self.walk = walk
+        self.walk_seeds = False
         if self.hierarchical:
-            check_hierarchical(self.copybook, params, self.plan)
+            self.walk_seeds = check_hierarchical(self.copybook, params, self.plan)
         self.native = NativePlan(self.plan)
 
     @property
@@ -1422,15 +1445,24 @@ class VarLenNestedReader(_BaseReader):
             N.check(L.cbx_hier_list_offsets(parent_row.data_ptr(), int(base[1 + s]), table_rows[1 + s], pb, pn, o.data_ptr(), sp))
             d_offsets[s] = o
         # the counts of arrays whose DEPENDING ON field another record of the hierarchical record
-        # registers, resolved before the decode (one decode of the rows)
-        odo = self._hier_dependee_counts(d_data, n_bytes, sel, table_rows, d_offsets, prm.root_segment, st)
+        # registers, resolved before the decode (one decode of the rows); on a record-walk plan each
+        # row's dependee map as the hierarchical walk leaves it before the row (the walk counts itself)
+        odo = seeds = None
+        if self.walk_seeds:
+            seeds = self._hier_walk_seeds(d_data, n_bytes, sel, table_rows, d_offsets, prm.root_segment, st)
+        elif self.plan.walk is None:
+            odo = self._hier_dependee_counts(d_data, n_bytes, sel, table_rows, d_offsets, prm.root_segment, st)
         if odo is not None:
             N.check(L.cbx_plan_set_odo_counts(self.native.handle, odo.data_ptr(), int(odo.shape[1])))
+        if seeds is not None:
+            N.check(L.cbx_plan_set_dep_seed(self.native.handle, seeds.data_ptr(), int(seeds.shape[1]), prm.root_segment))
         try:
             flat = self.decode_selected(d_data, n_bytes, sel, stream=st)
         finally:
             if odo is not None:
                 N.check(L.cbx_plan_set_odo_counts(self.native.handle, None, 0))
+            if seeds is not None:
+                N.check(L.cbx_plan_set_dep_seed(self.native.handle, None, 0, 0))
         return HierBatch(flat, table_rows, d_offsets, self.collapse_root, self.params.generate_record_id)
 
     def _file_column(self, batch, input_file_name: Optional[str], check_only: bool = False):
@@ -1522,6 +1554,24 @@ class VarLenNestedReader(_BaseReader):
         L = N.load()
         sp = ctypes.c_void_p(stream.cuda_stream)
         dev = sel["rec_off"].device
+        w = self._hier_walk_struct(table_rows, child_offsets, root_seg, order, events)
+        vals, valid, dt = self._hier_dependee_columns(d_data, n_bytes, sel, deps, n, stream)
+        at = (N.CbxHierOdoArray * len(odo))()
+        for k, (ai, ar) in enumerate(odo):
+            at[k].dependee, at[k].out_row = deps.index(ar.dependee), ai
+            at[k].min_count, at[k].max_count = ar.min_count, ar.max_count
+            at[k].first_counts = None
+        out = torch.full((len(plan.arrays), n), -1, dtype=torch.int32, device=dev)
+        changed = torch.zeros(1, dtype=torch.int32, device=dev)
+        N.check(L.cbx_hier_dependee_counts(ctypes.byref(w), dt, len(deps), at, len(odo), out.data_ptr(), n,
+                                           changed.data_ptr(), sp))
+        out._cbx_keep = (vals, valid)   # (the value columns live until the resolution has run)
+        return out
+
+    def _hier_walk_struct(self, table_rows: List[int], child_offsets, root_seg: int, order: Dict[int, int],
+                          events: Dict[int, List[Tuple[int, int]]]):
+        """cbx_hier_walk: tables, child segments in copybook order, their list offsets, events in field order."""
+        segs = self.plan.segment_groups
         w = N.CbxHierWalk()
         w.n_segments, w.root_segment = len(segs), root_seg
         base = np.concatenate([[0], np.cumsum(table_rows)]).astype(np.int64)
@@ -1543,7 +1593,17 @@ class VarLenNestedReader(_BaseReader):
         for row, evs in events.items():
             for k, (_, e) in enumerate(sorted(evs)):
                 w.events[row][k] = e
-        # every dependee decoded from every row's own bytes (the rows' registrations)
+        w.seeds = None
+        return w
+
+    def _hier_dependee_columns(self, d_data, n_bytes: int, sel: Dict[str, Any], deps: List[int], n: int, stream,
+                               slots: Optional[List[int]] = None):
+        """Every dependee field decoded from every row's own bytes (the rows' registrations,
+        cbx_hier_dependee_values): (values, validity, the cbx_hier_dependee table)."""
+        torch = _torch()
+        L = N.load()
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        dev = sel["rec_off"].device
         vals = torch.empty((max(1, len(deps)), n), dtype=torch.int64, device=dev)
         valid = torch.empty((max(1, len(deps)), (n + 63) // 64), dtype=torch.int64, device=dev)
         dt = (N.CbxHierDependee * max(1, len(deps)))()
@@ -1551,18 +1611,68 @@ class VarLenNestedReader(_BaseReader):
             N.check(L.cbx_hier_dependee_values(self.native.handle, d_data.data_ptr(), n_bytes, sel["rec_off"].data_ptr(),
                                                sel["rec_len"].data_ptr(), n, self.params.start_offset, fi,
                                                vals[e].data_ptr(), valid[e].data_ptr(), sp))
-            dt[e].values, dt[e].validity, dt[e].out_type = vals[e].data_ptr(), valid[e].data_ptr(), N.O_I64
-        at = (N.CbxHierOdoArray * len(odo))()
-        for k, (ai, ar) in enumerate(odo):
-            at[k].dependee, at[k].out_row = deps.index(ar.dependee), ai
-            at[k].min_count, at[k].max_count = ar.min_count, ar.max_count
-            at[k].first_counts = None
-        out = torch.full((len(plan.arrays), n), -1, dtype=torch.int32, device=dev)
+            is_str = self.plan.columns[self.plan.fields[fi].column].out_type in (N.O_STRING, N.O_BINARY)
+            dt[e].values, dt[e].validity = vals[e].data_ptr(), valid[e].data_ptr()
+            dt[e].out_type = N.O_STRING if is_str else N.O_I64
+            dt[e].walk_slot = slots[e] if slots is not None else -1
+        return vals, valid, dt
+
+    def _hier_walk_seeds(self, d_data, n_bytes: int, sel: Dict[str, Any], table_rows: List[int], child_offsets,
+                         root_seg: int, stream):
+        """Record-walk plans: each row's dependFields map at the row's start, as extractHierarchicalRecord's
+        walk leaves it (RecordExtractors.scala:224-245, walk order :324-372) -- the registrations of the
+        rows before it in the walk, and for a root row those of the root's groups ahead of the root
+        segment's (the common header, segment groups placed before it, from the root's bytes).  The walk
+        kernel then resolves every count itself, registering the row's own dependees as it goes (a child
+        row: its segment group's only).  Returns int64 [8, rows] (cbx_plan_set_dep_seed)."""
+        torch = _torch()
+        plan, walk = self.plan, self.plan.walk
+        n = int(sum(table_rows))
+        dev = sel["rec_off"].device
+        seeds = torch.zeros((8, max(1, n)), dtype=torch.int64, device=dev)
+        if n == 0:
+            return seeds
+        order: Dict[int, int] = {}
+
+        def dfs(st):
+            order[id(st)] = len(order)
+            for c in getattr(st, "children", []) or []:
+                dfs(c)
+        dfs(self.copybook.ast)
+        segs = plan.segment_groups
+        root_pos = order[id(segs[root_seg])]
+        has_kids = {sgi for sgi, g in enumerate(segs) if any(h.parent_segment is g for h in segs)}
+        deps: List[int] = []
+        slots: List[int] = []
+        events: Dict[int, List[Tuple[int, int]]] = {}
+        for nd in walk.nodes:
+            if nd.dep_slot < 0 or nd.field < 0 or nd.field in deps:
+                continue
+            fi = nd.field
+            df = plan.fields[fi]
+            pos = order[id(plan.columns[df.column].node)]
+            e = len(deps)
+            deps.append(fi)
+            slots.append(nd.dep_slot)
+            if df.segment < 0 or df.segment != root_seg and order[id(segs[df.segment])] < root_pos:
+                if df.segment >= 0 and df.segment in has_kids:
+                    raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: a DEPENDING ON field in a segment "
+                                                          "group with children placed before the root segment's")
+                if pos < root_pos:
+                    events.setdefault(N.CBX_HIER_MAX_SEG, []).append((pos, e))
+            if df.segment >= 0:
+                events.setdefault(df.segment, []).append((pos, e))
+        if len(deps) > N.CBX_HIER_MAX_DEPS or any(len(v) > N.CBX_HIER_MAX_EVENTS for v in events.values()):
+            raise N.CbxError(N.CBX_E_UNSUPPORTED, "hierarchical records: more DEPENDING ON fields than "
+                                                  "cbx_hier_dependee_counts takes")
+        w = self._hier_walk_struct(table_rows, child_offsets, root_seg, order, events)
+        w.seeds = seeds.data_ptr()
+        vals, valid, dt = self._hier_dependee_columns(d_data, n_bytes, sel, deps, n, stream, slots)
         changed = torch.zeros(1, dtype=torch.int32, device=dev)
-        N.check(L.cbx_hier_dependee_counts(ctypes.byref(w), dt, len(deps), at, len(odo), out.data_ptr(), n,
-                                           changed.data_ptr(), sp))
-        out._cbx_keep = (vals, valid)   # (the value columns live until the resolution has run)
-        return out
+        N.check(N.load().cbx_hier_dependee_counts(ctypes.byref(w), dt, len(deps), None, 0, None, n, changed.data_ptr(),
+                                                  ctypes.c_void_p(stream.cuda_stream)))
+        seeds._cbx_keep = (vals, valid)
+        return seeds
 
     def read(self, data: bytes, file_id: int = 0, input_file_name: Optional[str] = None) -> DecodedBatch:
         """A whole file, as the reference reads it: sparse-index entries (when index generation

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 18
+#define CBX_ABI_VERSION 19
 
 /* status codes */
 #define CBX_OK 0
@@ -567,8 +567,9 @@ int cbx_hier_dependee_values(cbx_plan* plan, const uint8_t* d_data, int64_t n_by
 typedef struct {
     const void* values;               /* device: the dependee column's values, slot 0 (row-indexed) */
     const uint64_t* validity;         /* device: its validity words, slot 0 */
-    int32_t out_type;                 /* CBX_O_I32 / CBX_O_I64 / CBX_O_DEC128 */
-    int32_t reserved;
+    int32_t out_type;                 /* CBX_O_I32 / CBX_O_I64 / CBX_O_DEC128; CBX_O_STRING: int64 values are the
+                                       * occurs_mappings key id + 1 of a string dependee (cbx_hier_dependee_values) */
+    int32_t walk_slot;                /* its dependee slot in the plan's record walk (seeds), -1 none */
 } cbx_hier_dependee;
 
 typedef struct {
@@ -589,7 +590,18 @@ typedef struct {
      * registrations before the root segment's group): e >= 0 registers dependee e, e < 0 resolves
      * array -e - 1; -32768 ends */
     int16_t events[CBX_HIER_MAX_SEG + 1][CBX_HIER_MAX_EVENTS];
+    /* device, or NULL: [8][pitch] int64, each row's record-walk dependee slots as the walk leaves the map
+     * before the row (after the root's registrations that precede the root segment's group, for a root
+     * row): kind << 32 | value, kind 0 unseen, 1 Left(int), 2 Right(key id + 1) -- cbx_plan_set_dep_seed */
+    int64_t* seeds;
 } cbx_hier_walk;
+
+/* Record-walk plans (cbx_plan_set_walk: variable_size_occurs, string dependees through occurs_mappings,
+ * DEPENDING ON inside an OCCURS): the walk resolves a row's counts itself from its dependFields map; for
+ * hierarchical rows that map starts as the walk of the hierarchical record left it (cbx_hier_walk.seeds),
+ * and a child row registers no common-header dependee (it decodes its own segment group only,
+ * RecordExtractors.scala:300-322).  d_seed = NULL clears it.  Asynchronous use by later decode calls. */
+int cbx_plan_set_dep_seed(cbx_plan* plan, const int64_t* d_seed, int64_t pitch, int32_t root_segment);
 
 int cbx_hier_dependee_counts(const cbx_hier_walk* walk, const cbx_hier_dependee* deps, int32_t n_deps,
                              const cbx_hier_odo_array* arrays, int32_t n_arrays, int32_t* d_counts, int64_t pitch,

@@ -371,3 +371,52 @@ def test_hier_child_within_record_start_offset():
     for r in rows:
         r.pop("Record_Id", None), r.pop("File_Id", None)
     assert rows == exp and len(rows) == 1 and len(rows[0]["REC"]["PARENT_SEG"]["CHILD_SEG"]) == 1
+
+
+def _strdep_stream(n: int, seed: int) -> bytes:
+    """Records of tests/test_hier_oracle.py's STRDEP layout: parents with a code A / B / C (listed by
+    occurs_mappings) or another letter, children with their own code and up to three items, strays
+    and records cut short."""
+    rnd = random.Random(seed)
+    out = bytearray()
+    for _ in range(n):
+        kind = rnd.choice("PCCCZ")
+        if kind == "P":
+            body = "P" + "NAME" + rnd.choice("ABCXB")
+        elif kind == "C":
+            body = "C" + "ABC" + rnd.choice("ABCQ") + "".join(rnd.choice(["aa", "bb", "cc"]) for _ in range(3))
+        else:
+            body = "Z" + "9" * 6
+        if rnd.random() < 0.1:
+            body = body[:rnd.randint(1, len(body))]
+        b = body.encode("cp037")
+        out += bytes([0, 0, len(b) & 0xFF, len(b) >> 8]) + b
+    return bytes(out)
+
+
+@pytest.mark.parametrize("dep", ["P-CODE", "C-CODE"])
+@pytest.mark.parametrize("var_size", [False, True])
+def test_hier_walk_cross_segment_dependee_vs_oracle(dep, var_size):
+    """Record-walk plans (a string DEPENDING ON through occurs_mappings; variable_size_occurs) whose
+    child array depends on its PARENT's field: each row's walk starts from the dependee map the
+    hierarchical walk left before it (cbx_hier_dependee_values decodes the registrations, the resolver
+    emits per-row seeds, cbx_plan_set_dep_seed hands them to the walk), and a child registers no common
+    field -- round 5 reported these layouts as unsupported.  The own-segment dependee (C-CODE) is
+    seeded too: a child whose own code is null (cut short) counts with the code an earlier child
+    registered.  Rows equal the oracle's ora_extract_hier walk, both walks (table / specialised)."""
+    import dataclasses
+    from cobrix_amd.options import parse_options
+    from cobrix_amd.reader import VarLenNestedReader
+    from test_hier_oracle import STRDEP_COPYBOOK, STRDEP_OPTS
+    raw = _strdep_stream(5000, 31 + var_size)
+    for jit in (-1, 1):
+        opts = {**STRDEP_OPTS, "generate_record_id": "true", "variable_size_occurs": str(var_size).lower()}
+        p, _ = parse_options(opts)
+        p = dataclasses.replace(p, jit_min_records=jit)
+        rd = VarLenNestedReader(STRDEP_COPYBOOK.format(dep=dep), p)
+        assert rd.walk and rd.walk_seeds
+        rows = rd.read(raw).to_rows()
+        exp = RO.var_len_rows(rd.copybook, raw, p)
+        assert len(rows) == len(exp) > 100
+        bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
+        assert not bad, (jit, bad[:5], rows[bad[0]], exp[bad[0]])

@@ -145,13 +145,12 @@ STRDEP_OPTS = {"is_record_sequence": "true", "segment_field": "SEGMENT_ID",
                "segment-children:1": "PARENT-SEG => CHILD-SEG", "occurs_mappings": '{"C_A":{"A":1,"B":2,"C":3}}'}
 
 
-def test_cross_segment_string_dependee_is_reported():
+def test_cross_segment_string_dependee_seeds_the_walk():
     """A child's OCCURS DEPENDING ON a string field of its parent (occurs_mappings) needs the record walk,
-    which decodes each row from its own bytes and cannot see the parent's registration in the shared
-    dependFields map: the reader reports it (CBX_E_UNSUPPORTED) where the reference returns rows --
-    the oracle's walk resolves the parent's "B" to 2 elements -- while the same array DEPENDING ON its
-    own segment's field is accepted."""
-    from cobrix_amd import native as N
+    which decodes each row from its own bytes: the reader seeds each row's dependee map with the
+    hierarchical walk's state before it (check_hierarchical -> walk_seeds, cbx_plan_set_dep_seed) -- the
+    oracle's walk resolves the parent's "B" to 2 elements.  The same array DEPENDING ON its own segment's
+    field is seeded as well (a null own code leaves the earlier registration in force)."""
     import cobrix_amd.reader as R
     p, _ = parse_options(STRDEP_OPTS)
     cb = parse_copybook_for(STRDEP_COPYBOOK.format(dep="P-CODE"), p)
@@ -160,11 +159,10 @@ def test_cross_segment_string_dependee_is_reported():
     orig = R.NativePlan
     R.NativePlan = lambda plan: None   # (the check runs before any device allocation)
     try:
-        with pytest.raises(N.CbxError) as e:
-            R.VarLenNestedReader(STRDEP_COPYBOOK.format(dep="P-CODE"), p)
-        assert e.value.code == N.CBX_E_UNSUPPORTED and "P_CODE" in str(e.value)
+        rd = R.VarLenNestedReader(STRDEP_COPYBOOK.format(dep="P-CODE"), p)
+        assert rd.walk and rd.walk_seeds
         rd = R.VarLenNestedReader(STRDEP_COPYBOOK.format(dep="C-CODE"), p)
-        assert rd.walk
+        assert rd.walk and rd.walk_seeds
     finally:
         R.NativePlan = orig
 
