@@ -134,6 +134,9 @@ struct cbx_plan {
     std::vector<cbx_walk_array> h_warr;
     bool walk_jit_tried = false;
     hipFunction_t walk_jit_fn = nullptr;
+    bool chain_jit_tried = false;            // the specialised var-occurs framing (jit_chain_source)
+    hipFunction_t chain_jit_fn[5] = {};      // sample, spec, fix, settle, write
+    bool last_chain_jit = false;             // the last cbx_frame_var_occurs used them
     cbx_walk_array* d_warr = nullptr;
     cbx_walk_handler* d_whand = nullptr;
     int64_t* d_wslot_base = nullptr;    // per column: first string-slot index
@@ -1179,6 +1182,142 @@ static std::string jit_walk_source(const cbx_plan* P) {
     return g.ok ? g.o.str() : std::string();
 }
 
+// ---- the copybook-specialised var-occurs framing (cbx_frame_var_occurs) ----
+// walk_length (cbx_walk.h: VarOccursRecordExtractor.extractVarOccursRecordBytes, :52-136) unrolled like
+// cbx_jit_walk: a group's children in sequence, an OCCURS of groups a loop over its elements, every
+// dependee decoded with its Field as a constant from the zero-filled record bytes; subtrees without
+// OCCURS or dependees fold to their static walked size.  One lane per record (the chain's step), so no
+// ballots: the lanes of a wave walk different records of different chunks.  The five chain passes
+// (cbx_chain.h) are wrapped as extern "C" kernels of one module around that step.
+struct LenGen {
+    const cbx_plan* P;
+    std::ostringstream o;
+    int uid = 0, prims = 0;
+    bool ok = true;
+
+    void line(int ind, const std::string& t) { o << std::string(2 * ind, ' ') << t << "\n"; }
+
+    // the walked size of group g's children when it depends on no data (no OCCURS, no dependee), else -1
+    int static_size(int g, int depth) const {
+        if (depth > 64) return -1;
+        const std::vector<cbx_walk_node>& N = P->h_wnodes;
+        int sum = 0;
+        for (int c = N[g].child, guard = 0; c >= 0 && guard < (int)N.size(); c = N[c].next, guard++) {
+            const cbx_walk_node& n = N[c];
+            if (n.array >= 0) return -1;
+            int w = n.actual_size;
+            if (n.kind == CBX_W_GROUP) {
+                if ((w = static_size(c, depth + 1)) < 0) return -1;
+            } else if (n.dep_slot >= 0 && n.field >= 0) {
+                return -1;
+            }
+            if (!(n.flags & CBX_W_REDEFINED)) sum += w;
+        }
+        return sum;
+    }
+
+    // walk_length's frames: the table walk fails (-1) past kWalkDepth frames; the unrolled form is only
+    // generated for copybooks that never get there (sp = the frame index of group g's children)
+    void body(int g, const std::string& off, int ind, int sp) {
+        if (sp >= 48) { ok = false; return; }
+        const std::vector<cbx_walk_node>& N = P->h_wnodes;
+        for (int c = N[g].child, guard = 0; c >= 0 && ok && guard < (int)N.size(); c = N[c].next, guard++) {
+            const cbx_walk_node& n = N[c];
+            const std::string K = std::to_string(uid++);
+            const bool adv = !(n.flags & CBX_W_REDEFINED);
+            if (n.array >= 0) {   // an OCCURS: its present elements, walked (:109-113)
+                if (sp + 1 >= kWalkDepth) { ok = false; return; }
+                line(ind, "{   // OCCURS (node " + std::to_string(c) + ")");
+                line(ind + 1, "const int cnt" + K + " = walk_count(a, " + std::to_string(n.array) + ", dep);");
+                if (n.kind == CBX_W_GROUP) {
+                    if (sp + 2 >= kWalkDepth) { ok = false; return; }
+                    const int S = static_size(c, 0);
+                    if (S >= 0) {
+                        line(ind + 1, "const int w" + K + " = cnt" + K + " * " + std::to_string(S) + ";");
+                    } else {
+                        line(ind + 1, "int eo" + K + " = " + off + ";");
+                        line(ind + 1, "for (int e" + K + " = 0; e" + K + " < cnt" + K + "; e" + K + "++) {");
+                        body(c, "eo" + K, ind + 2, sp + 2);
+                        line(ind + 1, "}");
+                        line(ind + 1, "const int w" + K + " = eo" + K + " - " + off + ";");
+                    }
+                } else {
+                    line(ind + 1, "const int w" + K + " = cnt" + K + " * " + std::to_string(n.data_size) + ";");
+                }
+                if (adv) line(ind + 1, off + " += w" + K + ";");
+                line(ind, "}");
+                continue;
+            }
+            if (n.kind == CBX_W_GROUP) {   // every non-redefined field advances by its walked size (:111-131)
+                if (sp + 1 >= kWalkDepth) { ok = false; return; }
+                const int S = static_size(c, 0);
+                if (S >= 0) {
+                    if (adv && S) line(ind, off + " += " + std::to_string(S) + ";");
+                    continue;
+                }
+                line(ind, "{   // group (node " + std::to_string(c) + ")");
+                line(ind + 1, "int go" + K + " = " + off + ";");
+                body(c, "go" + K, ind + 1, sp + 1);
+                if (adv) line(ind + 1, off + " = go" + K + ";");
+                line(ind, "}");
+                continue;
+            }
+            if (n.dep_slot >= 0 && n.field >= 0) {   // a dependee: decoded from the (zero-filled) bytes
+                if (++prims > kJitMaxOps) { ok = false; return; }
+                const Field& f = P->dfields_h[n.field];
+                const int size = std::min(n.actual_size, 64);
+                const bool str = f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII;
+                line(ind, "{   // dependee (node " + std::to_string(c) + ")");
+                line(ind + 1, "constexpr Field f = " + field_literal(f) + ";");
+                line(ind + 1, "uint8_t zb[64];");
+                line(ind + 1, "if (" + off + " + " + std::to_string(size) + " <= avail) {");
+                line(ind + 2, "for (int i = 0; i < " + std::to_string(size) + "; i++) zb[i] = rec[" + off + " + i];");
+                line(ind + 1, "} else {");
+                line(ind + 2, "for (int i = 0; i < " + std::to_string(size) + "; i++) zb[i] = " + off + " + i < avail ? rec[" + off +
+                                  " + i] : 0;");
+                line(ind + 1, "}");
+                if (str) line(ind + 1, "walk_len_str_dep(a, f, zb, " + std::to_string(size) + ", " + std::to_string(n.dep_slot) + ", dep);");
+                else line(ind + 1, "{ const Val dv = decode_count_int(f, zb); dep.set(" + std::to_string(n.dep_slot) +
+                                       ", dv.valid, WalkDep{1, (int32_t)dv.lo}); }");
+                line(ind, "}");
+            }
+            if (adv && n.actual_size) line(ind, off + " += " + std::to_string(n.actual_size) + ";");
+        }
+    }
+};
+
+// The specialised framing's source, or "" when the copybook is beyond the unrolled form's limits.
+static std::string jit_chain_source(const cbx_plan* P) {
+    LenGen g{P};
+    g.o << "#define CBX_STR_LAYOUT 1\n#define CBX_MODE 0\n#define CBX_JIT_WALK 1\n#include \"cbx_device.h\"\n"
+           "#include \"cbx_walk.h\"\n#include \"cbx_chain.h\"\n"
+           "namespace cbx {\n"
+           "__device__ __forceinline__ int jit_walk_length(const WalkArgs& a, const CBX_GLOBAL uint8_t* rec, int avail) {\n"
+           "  WalkDeps dep;\n  dep.clear();\n  int off0 = 0;\n";
+    g.body(P->walk_root, "off0", 1, 0);
+    g.o << "  return off0;\n}\n"
+           "struct JitVarOccursStep {   // VarOccursStep's layout and semantics\n"
+           "  WalkArgs a;\n  int64_t n_bytes;\n"
+           "  __device__ __forceinline__ ChainStep at(int64_t pos) const {\n"
+           "    ChainStep s{kChainStop, 0, 0};\n"
+           "    if (pos >= n_bytes) return s;\n"
+           "    const int64_t left = n_bytes - pos;\n"
+           "    const int len = jit_walk_length(a, gp(a.data) + pos, left < 0x7fffffff ? (int)left : 0x7fffffff);\n"
+           "    if (len <= 0) return s;\n"
+           "    s.len = len;\n    s.next = pos + len;\n    return s;\n  }\n};\n"
+           "}  // namespace cbx\n"
+           "using cbx::JitVarOccursStep;\nusing cbx::ChainArgs;\n"
+           "extern \"C\" __global__ void cbx_jit_chain_sample(JitVarOccursStep s, ChainArgs c, int n_max) { cbx::chain_sample_run(s, c, n_max); }\n"
+           "extern \"C\" __global__ __launch_bounds__(256) void cbx_jit_chain_spec(JitVarOccursStep s, ChainArgs c) { cbx::chain_spec_run(s, c); }\n"
+           "extern \"C\" __global__ __launch_bounds__(256) void cbx_jit_chain_fix(JitVarOccursStep s, ChainArgs c, const int64_t* ex_in, int64_t* ex_out) {\n"
+           "  cbx::chain_fix_run(s, c, ex_in, ex_out);\n}\n"
+           "extern \"C\" __global__ void cbx_jit_chain_settle(JitVarOccursStep s, ChainArgs c, int64_t* ex) { cbx::chain_settle_run(s, c, ex); }\n"
+           "extern \"C\" __global__ __launch_bounds__(256) void cbx_jit_chain_write(JitVarOccursStep s, ChainArgs c, const int64_t* base, int64_t capacity,\n"
+           "                                                  int64_t* rec_off, int32_t* rec_len) {\n"
+           "  cbx::chain_write_run(s, c, base, capacity, rec_off, rec_len);\n}\n";
+    return g.ok ? g.o.str() : std::string();
+}
+
 // The record walk (cbx_walk.h): one lane per record, data-dependent offsets.
 static int walk_launch(cbx_plan* P, const CallShape& c, cbx_column* columns, hipStream_t st) {
     const int64_t n_tiles = (c.n_rec + kWave - 1) / kWave;
@@ -1412,6 +1551,12 @@ extern "C" int cbx_plan_kernel_kind(cbx_plan* P, int32_t* kind) {
     if (!P || !kind) return fail(CBX_E_ARGUMENT, "cbx_plan_kernel_kind: invalid arguments");
     *kind = P->last_kind;
     if (!P->last_kind && !P->jit_error.empty()) g_err = P->jit_error;
+    return CBX_OK;
+}
+
+extern "C" int cbx_plan_frame_kind(cbx_plan* P, int32_t* kind) {
+    if (!P || !kind) return fail(CBX_E_ARGUMENT, "cbx_plan_frame_kind: invalid arguments");
+    *kind = P->last_chain_jit ? 1 : 0;
     return CBX_OK;
 }
 
@@ -2533,9 +2678,11 @@ extern "C" int cbx_plan_set_walk(cbx_plan* P, const cbx_walk_node* nodes, int32_
 namespace {
 // Chunk-parallel framing of a record chain (cbx_chain.h) from `first` over [first, n_bytes).
 // h: [0] records, [1] the chain's end position, [2] error kind (the step's), [3] error position.
+// jf: the specialised passes (sample, spec, fix, settle, write: jit_chain_source's kernels, Step's layout),
+// nullptr: the library's templates.
 template <typename Step>
 int frame_chain(const Step& s, int64_t first, int64_t n_bytes, int64_t capacity, int64_t* d_rec_off, int32_t* d_rec_len,
-                hipStream_t st, int64_t h[4], int64_t min_chunk) {
+                hipStream_t st, int64_t h[4], int64_t min_chunk, const hipFunction_t* jf = nullptr) {
     h[0] = 0; h[1] = first; h[2] = 0; h[3] = 0;
     const int64_t span = n_bytes - first;
     if (span <= 0) return CBX_OK;
@@ -2568,26 +2715,59 @@ int frame_chain(const Step& s, int64_t first, int64_t n_bytes, int64_t capacity,
     HIP_CHECK(hipMemsetAsync(c.bits, 0, (size_t)nw * 4, st));
     HIP_CHECK(hipMemsetAsync(c.out, 0, 16 * 8, st));
     const unsigned g = (unsigned)((K + 255) / 256);
-    hipLaunchKernelGGL(chain_sample<Step>, dim3(1), dim3(1), 0, st, s, c, 256);
-    hipLaunchKernelGGL(chain_spec<Step>, dim3(g), dim3(256), 0, st, s, c);
-    HIP_CHECK(hipGetLastError());
+    Step sa = s;   // (addressable kernel arguments for the module launches)
+    auto mlaunch = [&](hipFunction_t f, unsigned grid, unsigned block, void** args) {
+        return hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, 0, st, args, nullptr);
+    };
+    int n_sample = 256;
+    if (jf) {
+        void* a0[] = {&sa, &c, &n_sample};
+        HIP_CHECK(mlaunch(jf[0], 1, 1, a0));
+        void* a1[] = {&sa, &c};
+        HIP_CHECK(mlaunch(jf[1], g, 256, a1));
+    } else {
+        hipLaunchKernelGGL(chain_sample<Step>, dim3(1), dim3(1), 0, st, s, c, n_sample);
+        hipLaunchKernelGGL(chain_spec<Step>, dim3(g), dim3(256), 0, st, s, c);
+        HIP_CHECK(hipGetLastError());
+    }
     HIP_CHECK(hipMemcpyAsync(ex[0], c.spec_exit, (size_t)K * 8, hipMemcpyDeviceToDevice, st));
     int cur = 0;
     bool changed = K > 1;
     for (int r = 0; r < kChainRounds && changed; r++) {
         HIP_CHECK(hipMemsetAsync(c.out + 4, 0, 8, st));
-        hipLaunchKernelGGL(chain_fix<Step>, dim3(g), dim3(256), 0, st, s, c, (const int64_t*)ex[cur], ex[cur ^ 1]);
-        HIP_CHECK(hipGetLastError());
+        if (jf) {
+            const int64_t* ein = ex[cur];
+            int64_t* eout = ex[cur ^ 1];
+            void* a2[] = {&sa, &c, &ein, &eout};
+            HIP_CHECK(mlaunch(jf[2], g, 256, a2));
+        } else {
+            hipLaunchKernelGGL(chain_fix<Step>, dim3(g), dim3(256), 0, st, s, c, (const int64_t*)ex[cur], ex[cur ^ 1]);
+            HIP_CHECK(hipGetLastError());
+        }
         cur ^= 1;
         int64_t flag = 0;
         HIP_CHECK(hipMemcpyAsync(&flag, c.out + 4, 8, hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
         changed = flag != 0;
     }
-    if (changed) hipLaunchKernelGGL(chain_settle<Step>, dim3(1), dim3(1), 0, st, s, c, ex[cur]);
+    if (changed) {
+        if (jf) {
+            int64_t* e = ex[cur];
+            void* a3[] = {&sa, &c, &e};
+            HIP_CHECK(mlaunch(jf[3], 1, 1, a3));
+        } else {
+            hipLaunchKernelGGL(chain_settle<Step>, dim3(1), dim3(1), 0, st, s, c, ex[cur]);
+        }
+    }
     device_scan(c.cnt, K, base, sums, st);
-    hipLaunchKernelGGL(chain_write<Step>, dim3(g), dim3(256), 0, st, s, c, (const int64_t*)base, capacity, d_rec_off, d_rec_len);
-    HIP_CHECK(hipGetLastError());
+    if (jf) {
+        const int64_t* b = base;
+        void* a4[] = {&sa, &c, &b, &capacity, &d_rec_off, &d_rec_len};
+        HIP_CHECK(mlaunch(jf[4], g, 256, a4));
+    } else {
+        hipLaunchKernelGGL(chain_write<Step>, dim3(g), dim3(256), 0, st, s, c, (const int64_t*)base, capacity, d_rec_off, d_rec_len);
+        HIP_CHECK(hipGetLastError());
+    }
     HIP_CHECK(hipMemcpyAsync(h, c.out, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     return CBX_OK;
@@ -2642,11 +2822,28 @@ extern "C" int cbx_frame_var_occurs(cbx_plan* P, const uint8_t* d_data, int64_t 
     a.handlers = (const CBX_CONST cbx_walk_handler*)P->d_whand; a.n_handlers = P->walk_n_handlers;
     a.arrays = (const CBX_CONST cbx_array*)P->d_arrays; a.fields = (const CBX_CONST Field*)P->d_fields;
     a.lut = P->d_lut;
+    // the copybook-specialised step for large streams (records estimated at the copybook's largest
+    // form; cbx_plan_options.jit_min_records, CBX_NO_JIT_WALK as for the walk), else the table walk
+    const hipFunction_t* jf = nullptr;
+    if (P->jit_min >= 0 && (n_bytes - first_offset) / std::max<int64_t>(1, P->walk_max_rec) >= P->jit_min &&
+        !getenv("CBX_NO_JIT_WALK")) {
+        if (!P->chain_jit_tried) {
+            P->chain_jit_tried = true;
+            const std::string src = jit_chain_source(P);
+            static const char* const names[5] = {"cbx_jit_chain_sample", "cbx_jit_chain_spec", "cbx_jit_chain_fix",
+                                                 "cbx_jit_chain_settle", "cbx_jit_chain_write"};
+            bool all = !src.empty();
+            for (int i = 0; i < 5 && all; i++) all = (P->chain_jit_fn[i] = jit_get(src, &P->jit_error, names[i])) != nullptr;
+            if (!all) for (auto& f : P->chain_jit_fn) f = nullptr;
+        }
+        if (P->chain_jit_fn[0]) jf = P->chain_jit_fn;
+    }
+    P->last_chain_jit = jf != nullptr;
     int64_t h[4];
     int r;
     // (a record walked from a wrong start reads its counts from the wrong bytes -- often the maxima --
     // so such chains need more records than length-field ones to land on a true start: 16 KiB chunks)
-    if ((r = frame_chain(VarOccursStep{a, n_bytes}, first_offset, n_bytes, capacity, d_rec_off, d_rec_len, st, h, 16384))) return r;
+    if ((r = frame_chain(VarOccursStep{a, n_bytes}, first_offset, n_bytes, capacity, d_rec_off, d_rec_len, st, h, 16384, jf))) return r;
     if (h[2] == 2) return fail(CBX_E_UNSUPPORTED, "cbx_frame_var_occurs: copybook nesting deeper than the walk's frame stack");
     *n_records = h[0];
     *virtual_bytes = std::max(n_bytes, h[1]);

@@ -83,6 +83,7 @@ struct LenFieldStep {
 // ---- VarOccursRecordExtractor: a record's length walked over its dependees ----
 // hasNext while offset < size; a record may reach past n_bytes (zero-filled, the virtual length).
 // walk_length: > 0 the record's length, 0 nothing to walk, -1 the copybook nests deeper than the walk.
+#ifndef CBX_JIT_WALK
 struct VarOccursStep {
     WalkArgs a;
     int64_t n_bytes;
@@ -97,6 +98,7 @@ struct VarOccursStep {
         return s;
     }
 };
+#endif
 
 // Chunk state (device, one entry per chunk).  out: [0] records (the write pass), [1] the chain's end
 // position, [2] error kind, [3] error position, [4] the fix rounds' changed flag, [5] lo, [6] hi.
@@ -132,7 +134,7 @@ __device__ __forceinline__ int64_t chain_rank(const ChainArgs& c, int64_t k, int
 
 // The true chain's first records: the plausible length range [lo, hi] for the speculation.
 template <typename Step>
-__global__ void chain_sample(Step s, ChainArgs c, int n_max) {
+__device__ __forceinline__ void chain_sample_run(const Step& s, const ChainArgs& c, int n_max) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     int64_t pos = c.first;
     int64_t lo = 0x7fffffff, hi = 0;
@@ -161,7 +163,7 @@ __device__ __forceinline__ bool chain_plausible(const Step& s, int64_t pos, int6
 }
 
 template <typename Step>
-__global__ void chain_spec(Step s, ChainArgs c) {
+__device__ __forceinline__ void chain_spec_run(const Step& s, const ChainArgs& c) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c.n_chunks) return;
     const int64_t b = chunk_begin(c, k), e = chunk_end(c, k);
@@ -213,7 +215,7 @@ __device__ __forceinline__ int64_t chain_refit(const Step& s, const ChainArgs& c
 
 // One fix round: exits read from ex_in (the previous round's), written to ex_out.
 template <typename Step>
-__global__ void chain_fix(Step s, ChainArgs c, const int64_t* ex_in, int64_t* ex_out) {
+__device__ __forceinline__ void chain_fix_run(const Step& s, const ChainArgs& c, const int64_t* ex_in, int64_t* ex_out) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c.n_chunks) return;
     const int64_t old = ex_in[k];
@@ -230,7 +232,7 @@ __global__ void chain_fix(Step s, ChainArgs c, const int64_t* ex_in, int64_t* ex
 
 // The settle pass: chunks in order, one lane (what the fix rounds left: a ripple longer than them).
 template <typename Step>
-__global__ void chain_settle(Step s, ChainArgs c, int64_t* ex) {
+__device__ __forceinline__ void chain_settle_run(const Step& s, const ChainArgs& c, int64_t* ex) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     for (int64_t k = 1; k < c.n_chunks; k++) {
         const int64_t in = ex[k - 1];
@@ -245,7 +247,8 @@ __global__ void chain_settle(Step s, ChainArgs c, int64_t* ex) {
 // Records of chunk k at base[k] (exclusive scan of cnt), at most capacity of them; the chunk where the
 // chain ends records its end position and error.
 template <typename Step>
-__global__ void chain_write(Step s, ChainArgs c, const int64_t* base, int64_t capacity, int64_t* rec_off, int32_t* rec_len) {
+__device__ __forceinline__ void chain_write_run(const Step& s, const ChainArgs& c, const int64_t* base, int64_t capacity,
+                                                int64_t* rec_off, int32_t* rec_len) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c.n_chunks) return;
     const int64_t e = chunk_end(c, k);
@@ -263,6 +266,21 @@ __global__ void chain_write(Step s, ChainArgs c, const int64_t* base, int64_t ca
         pos = r.next;
     }
     if (k == c.n_chunks - 1) c.out[0] = base[k] + c.cnt[k];
+}
+
+// The passes as kernels of the library (the specialised var-occurs framing wraps the same bodies in
+// its own extern "C" kernels, cbx_capi.hip: jit_chain_source).
+template <typename Step>
+__global__ void chain_sample(Step s, ChainArgs c, int n_max) { chain_sample_run(s, c, n_max); }
+template <typename Step>
+__global__ void chain_spec(Step s, ChainArgs c) { chain_spec_run(s, c); }
+template <typename Step>
+__global__ void chain_fix(Step s, ChainArgs c, const int64_t* ex_in, int64_t* ex_out) { chain_fix_run(s, c, ex_in, ex_out); }
+template <typename Step>
+__global__ void chain_settle(Step s, ChainArgs c, int64_t* ex) { chain_settle_run(s, c, ex); }
+template <typename Step>
+__global__ void chain_write(Step s, ChainArgs c, const int64_t* base, int64_t capacity, int64_t* rec_off, int32_t* rec_len) {
+    chain_write_run(s, c, base, capacity, rec_off, rec_len);
 }
 
 }  // namespace cbx

@@ -513,6 +513,27 @@ __device__ __forceinline__ void walk_tiles(const WalkArgs& a, uint8_t* wsm, cons
     }
 }
 
+// VarOccursRecordExtractor's string dependee (extractVarOccursRecordBytes, :88-101): the zero-filled
+// bytes decoded as a string, registered as the occurs_mappings key id + 1 it equals (0: none) --
+// walk_length's and the specialised framing's (jit_chain_source) step.
+__device__ __forceinline__ void walk_len_str_dep(const WalkArgs& a, const Field& f, const uint8_t* zb, int size, int slot,
+                                                 WalkDeps& dep) {
+    auto lutf = [&](uint32_t b) { return f.kind == CBX_K_STRING_ASCII ? ascii_lut(b) : a.lut[b]; };
+    const StrSpan s = string_span(f.kind, f.trim, zb, size, lutf);
+    uint8_t buf[64];
+    int key = 0;
+    if (s.utf8_len <= 64) {
+        string_write(f.kind, zb, s, buf, lutf);
+        for (int h = 0; h < a.n_handlers && key == 0; h++) {
+            const cbx_walk_handler hd = ldc(a.handlers + h);
+            bool eq = hd.key_len == s.utf8_len;
+            for (int i = 0; eq && i < s.utf8_len; i++) eq = hd.key[i] == buf[i];
+            if (eq) key = hd.key_id + 1;
+        }
+    }
+    dep.set(slot, true, WalkDep{2, key});
+}
+
 #ifndef CBX_JIT_WALK
 struct TableWalk {
     static constexpr bool kTyped = false;   // one instantiation, generic record pointer
@@ -633,20 +654,7 @@ __device__ int walk_length(const WalkArgs& a, const uint8_t* rec, int avail) {
             const int size = ch.actual_size < 64 ? ch.actual_size : 64;
             for (int i = 0; i < size; i++) zb[i] = fr.off + i < avail ? rec[fr.off + i] : 0;
             if (f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII) {
-                auto lutf = [&](uint32_t b) { return f.kind == CBX_K_STRING_ASCII ? ascii_lut(b) : a.lut[b]; };
-                const StrSpan s = string_span(f.kind, f.trim, zb, size, lutf);
-                uint8_t buf[64];
-                int key = 0;
-                if (s.utf8_len <= 64) {
-                    string_write(f.kind, zb, s, buf, lutf);
-                    for (int h = 0; h < a.n_handlers && key == 0; h++) {
-                        const cbx_walk_handler hd = ldc(a.handlers + h);
-                        bool eq = hd.key_len == s.utf8_len;
-                        for (int i = 0; eq && i < s.utf8_len; i++) eq = hd.key[i] == buf[i];
-                        if (eq) key = hd.key_id + 1;
-                    }
-                }
-                dep.set(ch.dep_slot, true, WalkDep{2, key});
+                walk_len_str_dep(a, f, zb, size, ch.dep_slot, dep);
             } else {
                 const Val dv = decode_count_int(f, zb);
                 dep.set(ch.dep_slot, dv.valid, WalkDep{1, (int32_t)dv.lo});

@@ -39,12 +39,12 @@ EXPORTED_SYMBOLS = ("cbx_abi_version", "cbx_last_error", "cbx_plan_create", "cbx
                     "cbx_string_bound", "cbx_string_view_geometry", "cbx_string_sizes_fixed", "cbx_decode_fixed", "cbx_decode_var",
                     "cbx_string_sizes_var", "cbx_plan_check", "cbx_frame_rdw", "cbx_frame_rdw_async", "cbx_frame_rdw_state",
                     "cbx_plan_set_profiling",
-                    "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_specialize", "cbx_frame_text",
+                    "cbx_plan_kernel_times", "cbx_plan_kernel_kind", "cbx_plan_frame_kind", "cbx_plan_specialize", "cbx_frame_text",
                     "cbx_sparse_index", "cbx_select_records", "cbx_decode_selected", "cbx_hier_select",
                     "cbx_hier_list_offsets", "cbx_plan_set_walk", "cbx_frame_var_occurs",
                     "cbx_plan_set_record_base", "cbx_frame_length_field", "cbx_plan_set_odo_counts",
                     "cbx_hier_dependee_counts", "cbx_hier_dependee_values", "cbx_plan_set_dep_seed", "cbx_views_to_utf8", "cbx_plan_pipeline")
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 
 class NativeLibraryError(RuntimeError):
@@ -212,6 +212,7 @@ def load():
     L.cbx_plan_set_profiling.argtypes = [P, i32]
     L.cbx_plan_kernel_times.argtypes = [P, P, P, i32, P]
     L.cbx_plan_kernel_kind.argtypes = [P, P]
+    L.cbx_plan_frame_kind.argtypes = [P, P]
     L.cbx_plan_specialize.argtypes = [P, P, i64, P, i32]
     L.cbx_sparse_index.argtypes = [P, P, i64, P, P, i64, P, P, i64, P, P]
     L.cbx_select_records.argtypes = [P, P, i64, P, P, i64, i32, P, i32, P, P, P]

@@ -43,7 +43,7 @@ typedef __hip_internal::uint64_t uint64_t;
 extern "C" {
 #endif
 
-#define CBX_ABI_VERSION 19
+#define CBX_ABI_VERSION 20
 
 /* status codes */
 #define CBX_OK 0
@@ -306,6 +306,11 @@ int cbx_plan_kernel_times(cbx_plan* plan, float* decode_ms, float* post_ms, int3
  * 1 the copybook-specialised kernel.  If specialisation was attempted and failed, *kind = 0 and
  * the reason is in cbx_last_error() (the call itself succeeded on the table-driven kernel). */
 int cbx_plan_kernel_kind(cbx_plan* plan, int32_t* kind);
+
+/* Which step the plan's last cbx_frame_var_occurs call walked records with: *kind = 0 the
+ * table-driven walk_length, 1 its copybook-specialised form (hipRTC, from jit_min_records records
+ * estimated at the copybook's largest record; same records, tested on both). */
+int cbx_plan_frame_kind(cbx_plan* plan, int32_t* kind);
 
 /* The copybook-specialised kernel of a plan (its contiguous fixed-length variant when the layout
  * has one, else the windowed variant): writes its HIP source

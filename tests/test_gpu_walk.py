@@ -62,6 +62,15 @@ def _walk_kind(rd) -> int:
     return k.value
 
 
+def _frame_kind(rd) -> int:
+    """1: the last var-occurs framing ran its copybook-specialised step (jit_chain_source), 0: walk_length."""
+    import ctypes
+    from cobrix_amd import native as N
+    k = ctypes.c_int32()
+    N.check(N.load().cbx_plan_frame_kind(rd.native.handle, ctypes.byref(k)))
+    return k.value
+
+
 @pytest.mark.parametrize("utf8", [False, True])
 @pytest.mark.parametrize("var_size", [True, False])
 def test_walk_nested_odo_rdw_vs_oracle(var_size, utf8):
@@ -103,14 +112,20 @@ def test_walk_var_occurs_extractor_vs_oracle(chunk, monkeypatch):
     raw = b"".join(nested_record(rnd, True) for _ in range(400 if chunk is None else 3000))
     rd, p = _reader(NESTED, {"variable_size_occurs": "true"})
     rows = rd.read(raw).to_rows()
+    assert _frame_kind(rd) == (1 if _JIT_MIN > 0 else 0)
     exp = RO.var_len_rows(rd.copybook, raw, p)
     assert len(rows) == len(exp) > 200
     bad = [i for i, (a, b) in enumerate(zip(rows, exp)) if a != b]
     assert not bad, (bad[:5], rows[bad[0]], exp[bad[0]])
 
 
-@pytest.mark.parametrize("var_size", [True, False])
-def test_walk_string_dependee_occurs_mappings(var_size):
+@pytest.mark.parametrize("var_size,rdw", [(True, True), (False, True), (True, False)])
+def test_walk_string_dependee_occurs_mappings(var_size, rdw, monkeypatch):
+    """rdw False: the records back to back, framed by VarOccursRecordExtractor -- a string dependee
+    through occurs_mappings decides each record's length (both framing steps; 64-byte chunks so the
+    chains cross many speculated entries)."""
+    if not rdw:
+        monkeypatch.setenv("CBX_CHAIN_CHUNK", "64")
     rnd = random.Random(3)
     recs = []
     for i in range(2000):
@@ -118,13 +133,17 @@ def test_walk_string_dependee_occurs_mappings(var_size):
         n = {"A ": 0, "B ": 1, "C ": 3}.get(code, 3)
         body = f"{i % 100:02d}{code}" + "".join(rnd.choice(["abc", "XYZ", "   "]) for _ in range(n if var_size else 3)) + f"{i % 1000:03d}"
         recs.append(body.encode("cp037"))
-    raw = rdw_file(recs)
-    opts = {"is_record_sequence": "true", "variable_size_occurs": str(var_size).lower(),
-            "occurs_mappings": '{"ITEMS":{"A":0,"B":1,"C":3}}'}
+    raw = rdw_file(recs) if rdw else b"".join(recs)
+    opts = {"variable_size_occurs": str(var_size).lower(), "occurs_mappings": '{"ITEMS":{"A":0,"B":1,"C":3}}'}
+    if rdw:
+        opts["is_record_sequence"] = "true"
     rd, p = _reader(MAPPED, opts)
     assert rd.walk
     rows = rd.read(raw).to_rows()
+    if not rdw:
+        assert _frame_kind(rd) == (1 if _JIT_MIN > 0 else 0)
     exp = RO.var_len_rows(rd.copybook, raw, p)
+    assert len(rows) == len(exp) == 2000
     assert rows == exp
 
 

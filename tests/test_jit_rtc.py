@@ -23,7 +23,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "cobrix_amd", "csrc")
 HEADERS = [("cobrix_hip.h", os.path.join(ROOT, "include", "cobrix_hip.h"))] + [
-    (n, os.path.join(CSRC, n)) for n in ("cbx_decode.h", "cbx_internal.h", "cbx_device.h", "cbx_list.h", "cbx_walk.h")]
+    (n, os.path.join(CSRC, n)) for n in ("cbx_decode.h", "cbx_internal.h", "cbx_device.h", "cbx_list.h", "cbx_walk.h",
+                                          "cbx_chain.h")]
 
 
 def _torch_hiprtc() -> str | None:
@@ -242,4 +243,94 @@ def test_walk_kernel_compiles_with_hiprtc(compiler):
     if compiler >= len(COMPILERS):
         pytest.skip("no second hipRTC")
     err = _compile(WALK_KERNEL, COMPILERS[compiler])
+    assert not err, err[:3000]
+
+
+CHAIN_KERNELS = """#define CBX_STR_LAYOUT 1
+#define CBX_MODE 0
+#define CBX_JIT_WALK 1
+#include "cbx_device.h"
+#include "cbx_walk.h"
+#include "cbx_chain.h"
+namespace cbx {
+__device__ __forceinline__ int jit_walk_length(const WalkArgs& a, const CBX_GLOBAL uint8_t* rec, int avail) {
+  WalkDeps dep;
+  dep.clear();
+  int off0 = 0;
+  {   // dependee (node 2)
+    constexpr Field f = {7,1,1,1,1,0,0,0,0,72,4,0,{0,0,0,0},{0,0,0,0},{0,0,0,0},-1,1,1,4,-1,1,0,0,0,0,0,1ull,0ull};
+    uint8_t zb[64];
+    if (off0 + 1 <= avail) {
+      for (int i = 0; i < 1; i++) zb[i] = rec[off0 + i];
+    } else {
+      for (int i = 0; i < 1; i++) zb[i] = off0 + i < avail ? rec[off0 + i] : 0;
+    }
+    { const Val dv = decode_count_int(f, zb); dep.set(0, dv.valid, WalkDep{1, (int32_t)dv.lo}); }
+  }
+  off0 += 1;
+  {   // OCCURS (node 3)
+    const int cnt1 = walk_count(a, 0, dep);
+    int eo1 = off0;
+    for (int e1 = 0; e1 < cnt1; e1++) {
+      {   // dependee (node 4)
+        constexpr Field f = {1,7,8,3,0,0,0,0,0,0,4,0,{0,0,0,0},{0,0,0,0},{0,0,0,0},-1,3,1,6,0,1,-1,0,0,0,0,1ull,0ull};
+        uint8_t zb[64];
+        if (eo1 + 3 <= avail) {
+          for (int i = 0; i < 3; i++) zb[i] = rec[eo1 + i];
+        } else {
+          for (int i = 0; i < 3; i++) zb[i] = eo1 + i < avail ? rec[eo1 + i] : 0;
+        }
+        walk_len_str_dep(a, f, zb, 3, 1, dep);
+      }
+      eo1 += 3;
+      {   // OCCURS (node 5)
+        const int cnt2 = walk_count(a, 1, dep);
+        const int w2 = cnt2 * 5;
+        eo1 += w2;
+      }
+    }
+    const int w1 = eo1 - off0;
+    off0 += w1;
+  }
+  off0 += 3;
+  return off0;
+}
+struct JitVarOccursStep {   // VarOccursStep's layout and semantics
+  WalkArgs a;
+  int64_t n_bytes;
+  __device__ __forceinline__ ChainStep at(int64_t pos) const {
+    ChainStep s{kChainStop, 0, 0};
+    if (pos >= n_bytes) return s;
+    const int64_t left = n_bytes - pos;
+    const int len = jit_walk_length(a, gp(a.data) + pos, left < 0x7fffffff ? (int)left : 0x7fffffff);
+    if (len <= 0) return s;
+    s.len = len;
+    s.next = pos + len;
+    return s;
+  }
+};
+}  // namespace cbx
+using cbx::JitVarOccursStep;
+using cbx::ChainArgs;
+extern "C" __global__ void cbx_jit_chain_sample(JitVarOccursStep s, ChainArgs c, int n_max) { cbx::chain_sample_run(s, c, n_max); }
+extern "C" __global__ __launch_bounds__(256) void cbx_jit_chain_spec(JitVarOccursStep s, ChainArgs c) { cbx::chain_spec_run(s, c); }
+extern "C" __global__ __launch_bounds__(256) void cbx_jit_chain_fix(JitVarOccursStep s, ChainArgs c, const int64_t* ex_in, int64_t* ex_out) {
+  cbx::chain_fix_run(s, c, ex_in, ex_out);
+}
+extern "C" __global__ void cbx_jit_chain_settle(JitVarOccursStep s, ChainArgs c, int64_t* ex) { cbx::chain_settle_run(s, c, ex); }
+extern "C" __global__ __launch_bounds__(256) void cbx_jit_chain_write(JitVarOccursStep s, ChainArgs c, const int64_t* base, int64_t capacity,
+                                                  int64_t* rec_off, int32_t* rec_len) {
+  cbx::chain_write_run(s, c, base, capacity, rec_off, rec_len);
+}
+"""
+
+
+@pytest.mark.parametrize("compiler", range(2), ids=["rocm", "torch"])
+def test_var_occurs_framing_compiles_with_hiprtc(compiler):
+    """The copybook-specialised var-occurs framing (jit_chain_source: a numeric dependee, an OCCURS of
+    groups each with a string dependee and a nested OCCURS, the five chain passes) compiles against the
+    bundled headers with both compilers."""
+    if compiler >= len(COMPILERS):
+        pytest.skip("no second hipRTC")
+    err = _compile(CHAIN_KERNELS, COMPILERS[compiler])
     assert not err, err[:3000]

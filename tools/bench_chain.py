@@ -96,26 +96,60 @@ def main():
         size += len(r)
     p2, _ = parse_options({"variable_size_occurs": "true"})
     rd2 = VarLenNestedReader(synth.WALK_NESTED_COPYBOOK, p2)
+    import dataclasses
+    rd_jit = VarLenNestedReader(synth.WALK_NESTED_COPYBOOK, dataclasses.replace(p2, jit_min_records=1))
     big, reps = repeated(b"".join(recs), int(a.gb * 1e9))
-    # (the generator's records are not all walked at their generated size: the check is the chunked
-    # framing against the sequential one on the same prefix)
-    seq = None
-    for label, chunk, n in (("one chunk (sequential)", str(1 << 40), int(a.seq_mb * 1e6)), ("chunked, same prefix", None, int(a.seq_mb * 1e6)),
-                            ("chunked", None, big.numel())):
+    # forms: the step is walk_length (the node-table walk) or its copybook-specialised form
+    # (jit_chain_source, the default from jit_min_records records).  Checks: every prefix form against
+    # the sequential walk, the whole stream's specialised framing against the table step's.
+    seq = full = None
+    pre = int(a.seq_mb * 1e6)
+    forms = (("one chunk (sequential), table step", str(1 << 40), pre, rd2, True),
+             ("chunked, same prefix, table step", None, pre, rd2, True),
+             ("chunked, same prefix, specialised step", None, pre, rd_jit, False),
+             ("chunked, table step", None, big.numel(), rd2, True),
+             ("chunked", None, big.numel(), rd2, False))
+    for label, chunk, n, rd, table in forms:
         if chunk:
             os.environ["CBX_CHAIN_CHUNK"] = chunk
         else:
             os.environ.pop("CBX_CHAIN_CHUNK", None)
+        if table:
+            os.environ["CBX_NO_JIT_WALK"] = "1"
+        else:
+            os.environ.pop("CBX_NO_JIT_WALK", None)
         n = min(n, big.numel())
-        dt, res = _time(lambda: rd2.frame_var_occurs(big, n), reps=3 if chunk is None else 1)
+        dt, res = _time(lambda: rd.frame_var_occurs(big, n), reps=3 if chunk is None else 1)
         rec = int(res[0].numel())
-        if seq is None:
-            seq = (res[0].cpu(), res[1].cpu(), res[2])
-        elif n == int(a.seq_mb * 1e6):
-            assert torch.equal(res[0].cpu(), seq[0]) and torch.equal(res[1].cpu(), seq[1]) and res[2] == seq[2]
+        kind = _frame_kind(rd)
+        assert kind == (0 if table else 1), (label, kind)
+        got = (res[0].cpu(), res[1].cpu(), res[2])
+        ref = None
+        if n == pre:
+            if seq is None:
+                seq = got
+            else:
+                ref = seq
+        elif full is None:
+            full = got
+        else:
+            ref = full
+        if ref is not None:
+            assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]) and got[2] == ref[2], label
         print(json.dumps({"framing": "variable_size_occurs", "form": label, "bytes": n, "records": rec,
-                          "ms": round(dt * 1e3, 3), "GB_s": round(n / dt / 1e9, 2), "Mrec_s": round(rec / dt / 1e6, 2)}),
+                          "ms": round(dt * 1e3, 3), "GB_s": round(n / dt / 1e9, 2), "Mrec_s": round(rec / dt / 1e6, 2),
+                          "checked": ref is not None}),
               flush=True)
+        del res
+    os.environ.pop("CBX_NO_JIT_WALK", None)
+
+
+def _frame_kind(rd) -> int:
+    import ctypes
+    from cobrix_amd import native as N
+    k = ctypes.c_int32()
+    N.check(N.load().cbx_plan_frame_kind(rd.native.handle, ctypes.byref(k)))
+    return k.value
 
 
 if __name__ == "__main__":
