@@ -1756,6 +1756,12 @@ static int frame_rdw_impl(const uint8_t* d_data, int64_t n_bytes, const int64_t*
     const unsigned wblocks = (unsigned)((n + kRdwWaves - 1) / kRdwWaves);
     hipLaunchKernelGGL(rdw_wave_kernel<false>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, 0);
     HIP_CHECK(hipGetLastError());
+    std::vector<int64_t> dbg_spec;   // env CBX_RDW_DEBUG: speculated vs settled entries (diagnostic)
+    if (!async && getenv("CBX_RDW_DEBUG")) {
+        dbg_spec.resize(n);
+        HIP_CHECK(hipMemcpyAsync(dbg_spec.data(), c.entry, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
     // fix rounds until one changes no entry (each round validates at least the next chunk of every
     // range: bounded by the chunk count).  The first kAsyncRounds (async: max_rounds) go out without
     // waiting: a round after one that changed nothing returns at once on the device.
@@ -1777,6 +1783,18 @@ static int frame_rdw_impl(const uint8_t* d_data, int64_t n_bytes, const int64_t*
             HIP_CHECK(hipMemcpyAsync(&last_changed, c.changed + round, sizeof(int32_t), hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
         }
+    }
+    if (!dbg_spec.empty()) {
+        std::vector<int64_t> fin(n);
+        HIP_CHECK(hipMemcpyAsync(fin.data(), c.entry, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        int64_t bad = 0;
+        for (int64_t k = 0; k < n; k++)
+            if (fin[k] != dbg_spec[k] && bad++ < 5)
+                fprintf(stderr, "cbx rdw debug: chunk %lld speculated %lld settled %lld\n", (long long)k, (long long)dbg_spec[k],
+                        (long long)fin[k]);
+        fprintf(stderr, "cbx rdw debug: %lld of %lld speculated entries wrong, %lld rounds\n", (long long)bad, (long long)n,
+                (long long)round);
     }
     // record counts -> bases: device exclusive scan of the chunk counts
     hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, (const uint32_t*)c.count, n,
