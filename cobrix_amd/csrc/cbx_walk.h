@@ -22,6 +22,7 @@ namespace cbx {
 
 constexpr int kWalkDepth = 16;     // group / OCCURS nesting levels
 constexpr int kWalkDeps = 8;       // DEPENDING ON names (dependee slots)
+constexpr int kWalkShortStr = 12;  // string fields of at most this many bytes: walk_prim_f's register path
 // the waves' LDS areas start past LDS address 0: the compiler the specialised walk is built with
 // (torch's hipRTC) takes a pointer to LDS address 0 for a null one
 constexpr int kWalkLdsBase = 16;
@@ -185,6 +186,53 @@ __device__ __forceinline__ void walk_prim_f(const WalkArgs& a, const WalkLds& wl
     const bool is_str = f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII || f.kind == CBX_K_HEX ||
                         f.kind == CBX_K_RAW || f.kind == CBX_K_UTF16_BE || f.kind == CBX_K_UTF16_LE;
     const DevColumn c = ldc(a.cols + f.column);
+    if (is_str && (f.kind == CBX_K_STRING || f.kind == CBX_K_STRING_ASCII) && size <= kWalkShortStr &&
+        (dep_slot < 0 || element)) {
+        // Short single-byte-page strings (every value <= 12 UTF-8 bytes of one wave: an inline view):
+        // the bytes' LUT entries once, trim and UTF-8 length as bit operations over per-byte masks, the
+        // value composed in three registers -- no byte loops, no private array (the generic path below
+        // went through scratch for the inline bytes).  A wave holding a longer value takes that path.
+        const bool on = la && o <= avail;
+        const int n = on ? (o + size <= avail ? size : avail - o) : 0;
+        uint32_t ent[kWalkShortStr];
+        uint32_t keep = 0;
+#pragma unroll
+        for (int i = 0; i < kWalkShortStr; i++) {
+            ent[i] = 0;
+            if (i < size && i < n) {
+                ent[i] = walk_lut(a, wl, f.kind, p[i]);
+                if (!(ent[i] >> 31)) keep |= 1u << i;
+            }
+        }
+        const bool tl = f.trim == CBX_TRIM_LEFT || f.trim == CBX_TRIM_BOTH;
+        const bool tr = f.trim == CBX_TRIM_RIGHT || f.trim == CBX_TRIM_BOTH;
+        // string_span: [b, e) after the left then the right trim (all trimmed: empty)
+        const int b = tl ? (keep ? __builtin_ctz(keep) : n) : 0;
+        const int e = tr ? (keep ? 32 - __builtin_clz(keep) : b) : n;
+        int len = 0;
+#pragma unroll
+        for (int i = 0; i < kWalkShortStr; i++)
+            if (i >= b && i < e) len += (int)((ent[i] >> 24) & 3u);
+        if (!__ballot(on && len > 12)) {
+            uint64_t lo = 0;
+            uint32_t hi = 0;
+            int at = 0;
+#pragma unroll
+            for (int i = 0; i < kWalkShortStr; i++) {
+                if (i >= b && i < e) {
+                    const uint32_t l = (ent[i] >> 24) & 3u;
+                    const uint32_t v = ent[i] & (l >= 3 ? 0xFFFFFFu : l == 2 ? 0xFFFFu : 0xFFu);
+                    if (at < 8) lo |= (uint64_t)v << (8 * at);
+                    if (at >= 8) hi |= v << (8 * (at - 8));
+                    else if (at > 5) hi |= v >> (8 * (8 - at));
+                    at += (int)l;
+                }
+            }
+            if (on) *gp((u32x4*)c.values + (int64_t)slot * a.pitch + r) = u32x4{(uint32_t)len, (uint32_t)lo, (uint32_t)(lo >> 32), hi};
+            walk_valid(a, wl, c.validity, f.column, slot, tile, lane, on);
+            return;
+        }
+    }
     if (is_str) {
         // Primitive.decodeTypeValue (:102-128): offset past the end -> null, else truncated
         bool ok = la && o <= avail;
