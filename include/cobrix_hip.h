@@ -467,7 +467,11 @@ int cbx_plan_set_walk(cbx_plan* plan, const cbx_walk_node* nodes, int32_t n_node
  * framed chunk-parallel (speculated chunk entries corrected until they agree with the sequential walk,
  * cbx_chain.h), with the sequential walk's results.  A short read at the end is zero-filled by
  * the reference: the last record may reach past n_bytes, up to *virtual_bytes (the buffer must hold
- * zeros there before decoding).  Needs a plan with cbx_plan_set_walk. */
+ * zeros there before decoding).  Needs a plan with cbx_plan_set_walk.  From jit_min_records records
+ * (estimated at the copybook's largest record) the step is the copybook-specialised walk_length
+ * (hipRTC; cbx_plan_frame_kind).  Device scratch, stream-ordered (hipMallocAsync, freed by the call):
+ * a bitmap of one bit per byte of [first_offset, n_bytes) -- n_bytes / 8, 125 MB per GB framed --
+ * plus ~60 bytes per chunk of >= 16 KiB; cbx_frame_length_field takes the same (chunks >= 1 KiB). */
 int cbx_frame_var_occurs(cbx_plan* plan, const uint8_t* d_data, int64_t n_bytes, int64_t first_offset,
                          int64_t* d_rec_off, int32_t* d_rec_len, int64_t capacity, int64_t* n_records,
                          int64_t* virtual_bytes, void* stream);
@@ -517,10 +521,12 @@ int cbx_frame_length_field(cbx_plan* plan, const uint8_t* d_data, int64_t n_byte
  * thread per hierarchical record runs extractChildren's recursion with its id-based break rule).
  * The counts are resolved BEFORE the decode (one decode): cbx_hier_dependee_values decodes each
  * DEPENDING ON field from every row's bytes, cbx_hier_dependee_counts replays the walk.
+ * Record-walk plans (string dependees through occurs_mappings, variable_size_occurs) take the map per
+ * row instead of counts (cbx_hier_walk.seeds -> cbx_plan_set_dep_seed).
  * Not covered (reported by the host, CBX_E_UNSUPPORTED, never decoded differently): a segment group
  * placed before the root segment's that has child segments, with a cross-segment DEPENDING ON (the
- * root's record walk extracts that group's children too); a DEPENDING ON field outside the array's
- * segment on a record-walk plan (string dependees through occurs_mappings, variable_size_occurs). */
+ * root's record walk extracts that group's children too); on a record-walk plan, a cross-segment
+ * DEPENDING ON field inside an OCCURS or behind a variable-size one. */
 typedef struct {
     int32_t n_segments;               /* segment redefines (cbx_field.segment / key_segment indices) */
     int32_t root_segment;             /* the segment without a parent */
