@@ -1134,8 +1134,13 @@ __device__ __forceinline__ RdwStream rdw_stream(const RdwArgs& a, uint8_t* ring)
     return s;
 }
 
-// kFix false: speculate every chunk's entry and walk it; true: one fix round (changed[round - 1] == 0
-// ends the loop: every thread returns).
+// A chunk the lane walk (rdw_lane_walk_kernel) hands back to the wave walk: its count word.
+constexpr uint32_t kRdwToWave = 0xFFFFFFFFu;
+
+// kFix false: `round` is the phase -- 0 speculate every chunk's entry and walk it; 1 speculate only
+// (the entries for rdw_lane_walk_kernel); 2 walk, from its entry, every chunk the lane walk handed
+// back (count == kRdwToWave).  kFix true: one fix round (changed[round - 1] == 0 ends the loop: every
+// thread returns).
 template <bool kFix>
 __global__ __launch_bounds__(kWave * kRdwWaves) void rdw_wave_kernel(RdwArgs a, RdwChunkArgs c, int32_t round) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kRdwWaves * kRdwWaveLds];
@@ -1151,9 +1156,13 @@ __global__ __launch_bounds__(kWave * kRdwWaves) void rdw_wave_kernel(RdwArgs a, 
             entry = c.exit_out[k - 1];   // in place: the predecessor's exit of this round or the last
             if (entry == c.entry[k]) continue;
             if (lane == 0) { c.entry[k] = entry; c.changed[round] = 1; }
+        } else if (round == 2) {
+            if (__builtin_amdgcn_readfirstlane((int)c.count[k]) != (int)kRdwToWave) continue;
+            entry = uni64(c.entry[k]);
         } else {
             entry = ch.known ? ch.start : rdw_entry_wave(a, s, ch.start, ch.end, ch.range_end, lane);
             if (lane == 0) c.entry[k] = entry;
+            if (round == 1) continue;
         }
         const RdwWalk w = rdw_walk_lanes(a, s, entry, ch.end, c.stage_off + k * c.stage_cap, c.stage_len + k * c.stage_cap,
                                          c.stage_cap, lane);
@@ -1163,6 +1172,50 @@ __global__ __launch_bounds__(kWave * kRdwWaves) void rdw_wave_kernel(RdwArgs a, 
             c.err[k] = w.err;
         }
     }
+}
+
+// The walk of chunks of long records, one lane per chunk (phase 1's entries): headers read straight
+// from HBM, so a wave has 64 chains in flight where the wave walk has one -- a chunk of 16 KB records
+// is ~16 dependent header loads, which the wave walk pays as 16 DMA round trips of one wave (C5).  A
+// chunk that turns out dense -- its first kRdwLaneProbe records span less than kRdwLaneProbe x 1 KiB, or
+// it holds more than kRdwLaneMax records -- is handed to the wave walk (phase 2) untouched.  Results as
+// rdw_walk_lanes': exit (or -2 after an error), valid-record count, first error, records staged as
+// (payload offset relative to the entry, length).
+constexpr int kRdwLaneProbe = 8;
+constexpr uint32_t kRdwLaneMax = 256;
+
+__global__ __launch_bounds__(256) void rdw_lane_walk_kernel(RdwArgs a, RdwChunkArgs c) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= c.n) return;
+    const RdwChunk ch = rdw_chunk(c, k);
+    const int64_t entry = c.entry[k];
+    uint32_t* so = c.stage_off + k * c.stage_cap;
+    int32_t* sl = c.stage_len + k * c.stage_cap;
+    int64_t pos = entry;
+    uint32_t count = 0, steps = 0;
+    int64_t err = -1;
+    while (pos < ch.end) {
+        const RdwStep st = rdw_step(a, pos);
+        if (st.err) {
+            err = ((pos + 4) << 2) | (st.err == -2 ? 2 : 3);   // reported at the payload offset
+            pos = -2;
+            break;
+        }
+        if (st.stop) { pos = st.next; break; }
+        if (st.valid) {
+            if ((int64_t)count < c.stage_cap) { so[count] = (uint32_t)(st.off - entry); sl[count] = st.len; }
+            count++;
+        }
+        pos = st.next;
+        steps++;
+        if ((steps == kRdwLaneProbe && pos - entry < (int64_t)kRdwLaneProbe * 1024) || count > kRdwLaneMax) {
+            c.count[k] = kRdwToWave;   // dense: the wave walk's
+            return;
+        }
+    }
+    c.exit_out[k] = pos;
+    c.count[k] = count;
+    c.err[k] = err;
 }
 
 // Settles the walk on the device after the parallel fix rounds (cbx_frame_rdw_async, no host check
