@@ -567,6 +567,10 @@ constexpr int kRdwRingWins = 8;                // windows in the wave's ring (re
 constexpr int kRdwRing = kRdwWin * kRdwRingWins;
 constexpr int kRdwWaveLds = kRdwRing;
 constexpr int kRdwWaves = 4;                   // waves per workgroup
+#ifndef CBX_RDW_SPEC_GROUP
+#define CBX_RDW_SPEC_GROUP 4
+#endif
+constexpr int kRdwSpecGroup = CBX_RDW_SPEC_GROUP;   // speculation windows loaded together
 
 // The ring is filled by LDS-DMA (buffer_load_dwordx4 ... lds: one instruction per window, 16 bytes
 // per lane straight into the window's slot, no registers).  The loads are issued as inline asm so
@@ -1085,31 +1089,44 @@ __device__ RdwWalk rdw_walk_lanes(const RdwArgs& a, RdwStream& s, int64_t pos, i
 // plausible chain at all (the chunk's start when none: the fix rounds correct it).
 __device__ int64_t rdw_entry_wave(const RdwArgs& a, RdwStream& s, int64_t s0, int64_t e, int64_t re, int lane) {
     const int64_t off = a.p.big_endian ? 2 : 0;   // position of the zero pair inside a header
-    for (int64_t w = (s.shift + s0 + off) >> 10; ; w++) {
-        const int64_t wa = w * kRdwWin - s.shift;   // window start relative to data
-        if (wa >= e + off || wa >= a.n_bytes) break;
-        // the lane's 16 bytes + the next one (from the following lane's slice, or the next window)
-        const uint4 v = rdw_win_load(s, w, lane);
-        const uint32_t nb_in = __shfl_down(v.x, 1, kWave) & 0xFFu;
-        uint32_t next_byte = nb_in;
-        if (lane == kWave - 1) {
-            const int64_t q = wa + kRdwWin;
-            next_byte = q < a.n_bytes ? a.data[q] : 1u;
+    // windows in groups of kRdwSpecGroup, all of a group's loads issued before the first is scanned: the
+    // first header of a chunk of 16 KB records lies ~8 windows in (C5), one load latency per group
+    // instead of one per window (C5 framing -7 %, C4 unchanged; 8 windows: C4 +1.5 %)
+    for (int64_t w0 = (s.shift + s0 + off) >> 10; ; w0 += kRdwSpecGroup) {
+        if (w0 * kRdwWin - s.shift >= e + off || w0 * kRdwWin - s.shift >= a.n_bytes) break;
+        uint4 vg[kRdwSpecGroup];
+#pragma unroll
+        for (int g = 0; g < kRdwSpecGroup; g++) {
+            const int64_t wa = (w0 + g) * kRdwWin - s.shift;
+            vg[g] = (wa < e + off && wa < a.n_bytes) ? rdw_win_load(s, w0 + g, lane) : make_uint4(0u, 0u, 0u, 0u);
         }
-        const uint32_t zb = zero_bytes4(v.x) | zero_bytes4(v.y) << 4 | zero_bytes4(v.z) << 8 | zero_bytes4(v.w) << 12 |
-                            (next_byte == 0 ? 1u << 16 : 0u);
-        uint32_t pairs = zb & (zb >> 1) & 0xFFFFu;   // bit i: bytes i, i + 1 of the slice are zero
-        int64_t found = -1;
-        while (pairs) {
-            const int i = __builtin_ctz(pairs);
-            pairs &= pairs - 1;
-            const int64_t p = wa + 16 * lane + i;   // pair position (relative to data)
-            const int64_t q = p - off;              // header position
-            if (p < s0 + off || q >= e || p < 0) continue;
-            if (rdw_plausible(a, q, re, true)) { found = q; break; }
+#pragma unroll
+        for (int g = 0; g < kRdwSpecGroup; g++) {
+            const int64_t wa = (w0 + g) * kRdwWin - s.shift;   // window start relative to data
+            if (wa >= e + off || wa >= a.n_bytes) break;
+            // the lane's 16 bytes + the next one (from the following lane's slice, or the next window)
+            const uint4 v = vg[g];
+            const uint32_t nb_in = __shfl_down(v.x, 1, kWave) & 0xFFu;
+            uint32_t next_byte = nb_in;
+            if (lane == kWave - 1) {
+                const int64_t q = wa + kRdwWin;
+                next_byte = q < a.n_bytes ? a.data[q] : 1u;
+            }
+            const uint32_t zb = zero_bytes4(v.x) | zero_bytes4(v.y) << 4 | zero_bytes4(v.z) << 8 | zero_bytes4(v.w) << 12 |
+                                (next_byte == 0 ? 1u << 16 : 0u);
+            uint32_t pairs = zb & (zb >> 1) & 0xFFFFu;   // bit i: bytes i, i + 1 of the slice are zero
+            int64_t found = -1;
+            while (pairs) {
+                const int i = __builtin_ctz(pairs);
+                pairs &= pairs - 1;
+                const int64_t p = wa + 16 * lane + i;   // pair position (relative to data)
+                const int64_t q = p - off;              // header position
+                if (p < s0 + off || q >= e || p < 0) continue;
+                if (rdw_plausible(a, q, re, true)) { found = q; break; }
+            }
+            const uint64_t m = __ballot(found >= 0);
+            if (m) return __shfl(found, __builtin_ctzll(m), kWave);
         }
-        const uint64_t m = __ballot(found >= 0);
-        if (m) return __shfl(found, __builtin_ctzll(m), kWave);
     }
     // no strict candidate: any plausible chain (lanes over consecutive positions)
     for (int64_t p0 = s0; p0 < e; p0 += kWave) {
