@@ -1777,6 +1777,7 @@ static int frame_rdw_impl(const uint8_t* d_data, int64_t n_bytes, const int64_t*
     // waiting: a round after one that changed nothing returns at once on the device.
     const int64_t async_rounds = std::min<int64_t>(async && max_rounds > 0 ? max_rounds : 3, n + 1);
     int64_t round = 0;
+    hipLaunchKernelGGL(rdw_check_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, c);
     for (; round < async_rounds && round <= n; round++)
         hipLaunchKernelGGL(rdw_wave_kernel<true>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, (int32_t)round);
     HIP_CHECK(hipGetLastError());

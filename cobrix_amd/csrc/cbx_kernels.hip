@@ -1164,6 +1164,7 @@ __global__ __launch_bounds__(kWave * kRdwWaves) void rdw_wave_kernel(RdwArgs a, 
     const int lane = threadIdx.x % kWave;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     if (kFix && round > 0 && c.changed[round - 1] == 0) return;
+    if (kFix && round == 0 && c.changed[c.n + 1] == 0) return;   // rdw_check_kernel found every entry right
     RdwStream s = rdw_stream(a, smem + wid * kRdwWaveLds);
     for (int64_t k = (int64_t)blockIdx.x * kRdwWaves + wid; k < c.n; k += (int64_t)gridDim.x * kRdwWaves) {
         const RdwChunk ch = rdw_chunk(c, k);
@@ -1233,6 +1234,14 @@ __global__ __launch_bounds__(256) void rdw_lane_walk_kernel(RdwArgs a, RdwChunkA
     c.exit_out[k] = pos;
     c.count[k] = count;
     c.err[k] = err;
+}
+
+// Before the fix rounds: does any chunk's entry differ from its predecessor's exit?  (changed[n + 1]; a
+// lane per chunk -- the first fix round's wave per chunk spent ~40-80 us finding that out on C5.)
+__global__ __launch_bounds__(256) void rdw_check_kernel(RdwChunkArgs c) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= c.n || k == 0) return;
+    if (!rdw_chunk(c, k).known && c.exit_out[k - 1] != c.entry[k]) c.changed[c.n + 1] = 1;
 }
 
 // Settles the walk on the device after the parallel fix rounds (cbx_frame_rdw_async, no host check
