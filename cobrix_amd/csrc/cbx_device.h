@@ -931,8 +931,9 @@ __device__ __forceinline__ void str_view_pair(const KernelArgs& a, const StrOp& 
                : u32x4{(uint32_t)len, q[0].x, view_buf(t.tile, cb), view_pos(t.tile, cb, ex)};
     }
     const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-    (gp((u32x4*)ca.views) + t.tile * kWave)[lane] = sa ? v : z;
-    (gp((u32x4*)cb.views) + t.tile * kWave)[lane] = sa ? z : v;
+    // whole 1 KiB rows per column, written once: nontemporal like every other view row (st_out)
+    st_out(gp((u32x4*)ca.views) + t.tile * kWave + lane, sa ? v : z);
+    st_out(gp((u32x4*)cb.views) + t.tile * kWave + lane, sa ? z : v);
 }
 
 // n bytes from the 16-byte aligned LDS staging s to global d at any alignment: the bytes up to d's
