@@ -1757,7 +1757,8 @@ static int frame_rdw_impl(const uint8_t* d_data, int64_t n_bytes, const int64_t*
     // speculation, then the lane-per-chunk walk of chunks of long records (C5's 16 KB roots: 64 chains
     // in flight per wave), then the wave walk of the chunks it hands back (dense ones: C4); env
     // CBX_RDW_LANE_WALK=0: speculation and wave walk in one pass (A/B)
-    static const bool lane_walk = !getenv("CBX_RDW_LANE_WALK") || atoi(getenv("CBX_RDW_LANE_WALK")) != 0;
+    const char* lw = getenv("CBX_RDW_LANE_WALK");
+    const bool lane_walk = !lw || atoi(lw) != 0;
     if (lane_walk) {
         hipLaunchKernelGGL(rdw_wave_kernel<false>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, 1);
         hipLaunchKernelGGL(rdw_lane_walk_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, c);

@@ -39,12 +39,12 @@ def _oracle(raw: bytes, **kw):
     return O.frame_rdw(raw, **kw)
 
 
-def _adversarial(n: int, seed: int, big_endian=False, adjust=0, max_len=3000) -> bytes:
+def _adversarial(n: int, seed: int, big_endian=False, adjust=0, max_len=3000, p_long=0.3) -> bytes:
     """Records of 1..max_len bytes whose payloads are full of zeros and fake plausible headers."""
     rng = np.random.default_rng(seed)
     out = bytearray()
     for _ in range(n):
-        ln = int(rng.integers(1, max_len)) if rng.random() < 0.3 else int(rng.integers(1, 80))
+        ln = int(rng.integers(1, max_len)) if rng.random() < p_long else int(rng.integers(1, 80))
         hl = ln - adjust
         h = bytes([hl >> 8, hl & 0xFF, 0, 0]) if big_endian else bytes([0, 0, hl & 0xFF, hl >> 8])
         body = bytearray(rng.integers(0, 256, ln, dtype=np.uint8).tobytes())
@@ -86,6 +86,55 @@ def test_adversarial_payloads(monkeypatch, chunk, case):
     off, ln = _frame(raw, **kw)
     assert len(off) == len(eo)
     assert np.array_equal(off, eo) and np.array_equal(ln, el)
+
+
+@pytest.mark.parametrize("lane_walk", ["1", "0"])
+@pytest.mark.parametrize("chunk", [4096, 65536, None])
+@pytest.mark.parametrize("case", [dict(), dict(big_endian=True), dict(adjust=-4), dict(header=10, footer=7)])
+def test_long_records_lane_walk(monkeypatch, lane_walk, chunk, case):
+    """Records of ~1-20 KB (C5-like) with fake headers in their payloads: chunks of long records are
+    walked one lane per chunk (rdw_lane_walk_kernel) after the speculation pass, dense stretches handed
+    back to the wave walk -- the same offsets as the sequential walk, with (1) and without (0) the lane
+    walk; small chunks make most speculated entries wrong."""
+    monkeypatch.setenv("CBX_RDW_LANE_WALK", lane_walk)
+    if chunk:
+        monkeypatch.setenv("CBX_RDW_CHUNK_BYTES", str(chunk))
+    be, adj = case.get("big_endian", False), case.get("adjust", 0)
+    body = _adversarial(600, seed=(chunk or 1) + 11 * len(case), big_endian=be, adjust=adj, max_len=20000, p_long=0.8)
+    hb, fb = case.get("header", 0), case.get("footer", 0)
+    raw = (bytes([0, 0, 0, 0]) + b"\x11" * (hb - 4) if hb else b"") + body + b"\x22" * fb
+    eo, el = _oracle(raw, big_endian=be, adjustment=adj, file_header_bytes=hb, file_footer_bytes=fb)
+    kw = dict(is_rdw_big_endian=be, rdw_adjustment=adj, file_start_offset=hb, file_end_offset=fb)
+    off, ln = _frame(raw, **kw)
+    assert len(off) == len(eo)
+    assert np.array_equal(off, eo) and np.array_equal(ln, el)
+    seeds = [e[0] for e in O.sparse_index(raw, big_endian=be, records_per_entry=97, adjustment=adj,
+                                          file_header_bytes=hb, file_footer_bytes=fb)]
+    off2, ln2 = _frame(raw, seeds=seeds, **kw)
+    assert np.array_equal(off2, eo) and np.array_equal(ln2, el)
+
+
+@pytest.mark.parametrize("lane_walk", ["1", "0"])
+def test_long_records_error_position(monkeypatch, lane_walk):
+    """A zero-length header among long records: the first one on the chain is reported, lane walk or not."""
+    monkeypatch.setenv("CBX_RDW_LANE_WALK", lane_walk)
+    monkeypatch.setenv("CBX_RDW_CHUNK_BYTES", "65536")
+    rng = np.random.default_rng(4)
+    raw = bytearray()
+    hdrs = []
+    for _ in range(300):
+        ln = int(rng.integers(4000, 16000))
+        hdrs.append(len(raw))
+        raw += bytes([0, 0, ln & 0xFF, ln >> 8]) + bytes(rng.integers(0, 256, ln, dtype=np.uint8).tobytes())
+    for k in (150, 250):
+        raw[hdrs[k]:hdrs[k] + 4] = bytes(4)
+    raw = bytes(raw)
+    with pytest.raises(RuntimeError) as oe:
+        _oracle(raw)
+    with pytest.raises(CbxError) as ge:
+        _frame(raw)
+    want = int(re.search(r"offset (\d+)", str(oe.value)).group(1))
+    assert f"at {want}." in str(ge.value), (str(ge.value), want)
 
 
 def test_record_spanning_many_chunks(monkeypatch):
