@@ -1760,7 +1760,8 @@ static int frame_rdw_impl(const uint8_t* d_data, int64_t n_bytes, const int64_t*
     const char* lw = getenv("CBX_RDW_LANE_WALK");
     const bool lane_walk = !lw || atoi(lw) != 0;
     if (lane_walk) {
-        hipLaunchKernelGGL(rdw_wave_kernel<false>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, 1);
+        if (getenv("CBX_RDW_SPEC_IN_WAVE")) hipLaunchKernelGGL(rdw_wave_kernel<false>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, 1);
+        else hipLaunchKernelGGL(rdw_spec_kernel, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c);
         hipLaunchKernelGGL(rdw_lane_walk_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, c);
         hipLaunchKernelGGL(rdw_wave_kernel<false>, dim3(wblocks), dim3(kWave * kRdwWaves), 0, st, a, c, 2);
     } else {

@@ -1192,6 +1192,19 @@ __global__ __launch_bounds__(kWave * kRdwWaves) void rdw_wave_kernel(RdwArgs a, 
     }
 }
 
+// Phase 1 as a kernel of its own: the speculation reads its windows into registers, so without the
+// walk's LDS ring (8 KiB a wave) more waves are resident per CU.
+__global__ __launch_bounds__(kWave * kRdwWaves) void rdw_spec_kernel(RdwArgs a, RdwChunkArgs c) {
+    const int lane = threadIdx.x % kWave;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    RdwStream s = rdw_stream(a, nullptr);
+    for (int64_t k = (int64_t)blockIdx.x * kRdwWaves + wid; k < c.n; k += (int64_t)gridDim.x * kRdwWaves) {
+        const RdwChunk ch = rdw_chunk(c, k);
+        const int64_t entry = ch.known ? ch.start : rdw_entry_wave(a, s, ch.start, ch.end, ch.range_end, lane);
+        if (lane == 0) c.entry[k] = entry;
+    }
+}
+
 // The walk of chunks of long records, one lane per chunk (phase 1's entries): headers read straight
 // from HBM, so a wave has 64 chains in flight where the wave walk has one -- a chunk of 16 KB records
 // is ~16 dependent header loads, which the wave walk pays as 16 DMA round trips of one wave (C5).  A
