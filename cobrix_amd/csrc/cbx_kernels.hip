@@ -1194,7 +1194,8 @@ __global__ __launch_bounds__(kWave * kRdwWaves) void rdw_wave_kernel(RdwArgs a, 
 
 // Phase 1 as a kernel of its own: the speculation reads its windows into registers, so without the
 // walk's LDS ring (8 KiB a wave) more waves are resident per CU.
-__global__ __launch_bounds__(kWave * kRdwWaves) void rdw_spec_kernel(RdwArgs a, RdwChunkArgs c) {
+__global__ __launch_bounds__(kWave * kRdwWaves) __attribute__((amdgpu_waves_per_eu(8))) void rdw_spec_kernel(RdwArgs a,
+                                                                                                         RdwChunkArgs c) {
     const int lane = threadIdx.x % kWave;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     RdwStream s = rdw_stream(a, nullptr);
