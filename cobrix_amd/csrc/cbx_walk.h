@@ -171,6 +171,41 @@ __device__ __forceinline__ int walk_count(const WalkArgs& a, int ai, const WalkD
     return (v >= ar.min_count && v <= ar.max_count) ? v : ar.max_count;
 }
 
+// A numeric value for the walk: COMP-3 of <= 8 bytes and binary of 1 / 2 / 4 / 8 bytes through the
+// record kernels' packed-nibble / byte-swap fast decoders (bcd8_raw, bin8_raw: the same Field-derived
+// typing as make_numop, folded to constants in cbx_jit_walk), everything else through the byte-loop
+// decoder; both give decode_numeric's value (the fast variants are exact for these fields).
+template <typename RP>
+__device__ __forceinline__ Val walk_numeric(const Field& f, RP p) {
+    const bool bcd = f.kind == CBX_K_BCD && f.variant == V_BCD8;
+    const bool bin = f.kind == CBX_K_BINARY && f.variant == V_BIN8;
+    if (!bcd && !bin) return decode_numeric(f, p);
+    NumOp op{};
+    op.variant = (uint8_t)f.variant;
+    op.size = (uint8_t)f.size;
+    uint32_t fl = 0;
+    if (f.flags & CBX_F_SIGNED) fl |= NF_SIGNED;
+    if (f.flags & CBX_F_BIG_ENDIAN) fl |= NF_BIG_ENDIAN;
+    if (f.fin == 0) fl |= NF_INT;
+    op.flags = (uint8_t)fl;
+    op.shift = (uint8_t)(64 - 8 * f.size);
+    op.mask = low_bytes_mask(f.size);
+    uint64_t mul = 1;
+    for (int i = 0; i < f.e_mul; i++) mul *= 10u;   // (constants in cbx_jit_walk: the loops fold)
+    op.mul = mul;
+    U128 lim = u128(1);
+    for (int i = 0; i < f.e_lim; i++) (void)u128_muladd(lim, 10, 0);
+    op.lim_lo = lim.lo;
+    op.lim_hi = lim.hi;
+    op.lim64 = lim.hi ? ~0ull : lim.lo;
+    // the 8 bytes ending at the field's end, little-endian (the field in the top bytes, zeros below)
+    uint64_t r1 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (i < f.size) r1 |= (uint64_t)(uint8_t)p[i] << (8 * (8 - f.size + i));
+    return bcd ? bcd8_raw<0>(op, r1) : bin8_raw<0>(op, r1);
+}
+
 // One primitive element at record offset `off` (relative to the decode base) for the lanes with
 // `la` (wave-uniform call: the node, its field and slot are the wave's).  `element`: an element of a
 // primitive OCCURS -- extractArray decodes those with decodeTypeValue, which never touches
@@ -300,7 +335,7 @@ __device__ __forceinline__ void walk_prim_f(const WalkArgs& a, const WalkLds& wl
     }
     bool ok = la && o + size <= avail;   // numeric past the end -> null
     Val x{0, 0, false};
-    if (ok) x = decode_numeric(f, p);
+    if (ok) x = walk_numeric(f, p);
     ok = ok && x.valid;                  // null: dependFields keeps its previous entry (:126-134)
     if (ok) {
         const int w = f.out_type == CBX_O_I32 || f.out_type == CBX_O_F32 ? 4 : f.out_type == CBX_O_DEC128 ? 16 : 8;
