@@ -22,7 +22,8 @@ namespace cbx {
 
 constexpr int kWalkDepth = 16;     // group / OCCURS nesting levels
 constexpr int kWalkDeps = 8;       // DEPENDING ON names (dependee slots)
-constexpr int kWalkShortStr = 12;  // string fields of at most this many bytes: walk_prim_f's register path
+constexpr int kWalkShortStr = 12;
+constexpr int kWalkStageChunks = 8;   // 16-byte chunks a lane stages per tile (stage_cap <= 8 KiB)  // string fields of at most this many bytes: walk_prim_f's register path
 // the waves' LDS areas start past LDS address 0: the compiler the specialised walk is built with
 // (torch's hipRTC) takes a pointer to LDS address 0 for a null one
 constexpr int kWalkLdsBase = 16;
@@ -546,8 +547,19 @@ __device__ __forceinline__ void walk_tiles(const WalkArgs& a, uint8_t* wsm, cons
                 const int mis = (int)(g0 & 15);
                 const int64_t span = hi - lo + mis;
                 if (span <= a.stage_cap) {
-                    const u32x4* src = (const u32x4*)(size_t)(g0 - mis);
-                    for (int q = lane; 16 * q < span; q += kWave) ((u32x4*)stage)[q] = src[q];
+                    // every 16-byte chunk's global load issued before the first LDS store (one latency per
+                    // tile; the stage is at most 8 KiB: 8 chunks a lane), typed pointers -- generic ones made
+                    // each chunk a flat load waited for before its flat store
+                    const CBX_GLOBAL u32x4* src = (const CBX_GLOBAL u32x4*)(size_t)(g0 - mis);
+                    __attribute__((address_space(3))) u32x4* dst = (__attribute__((address_space(3))) u32x4*)stage_l;
+                    const int nq = (int)((span + 15) >> 4);
+                    u32x4 v[kWalkStageChunks];
+#pragma unroll
+                    for (int j = 0; j < kWalkStageChunks; j++)
+                        if (lane + kWave * j < nq) v[j] = src[lane + kWave * j];
+#pragma unroll
+                    for (int j = 0; j < kWalkStageChunks; j++)
+                        if (lane + kWave * j < nq) dst[lane + kWave * j] = v[j];
                     wave_sync_lds();
                     stage_at = act ? mis + (int)(base - lo) : 0;
                     rec = stage + stage_at;
